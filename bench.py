@@ -1,0 +1,188 @@
+#!/usr/bin/env python3
+"""Benchmark: Gaussian-splats/sec, forward + backward, 1M Gaussians @ 1920x1080, SH degree 3.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 1m_1080p_sh3]
+    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+
+One step = ``_C.rasterize_gaussians`` + ``_C.rasterize_gaussians_backward`` for one
+view (+ the RCCL all-reduce of the flat 59-float-per-Gaussian gradient arena when
+N > 1), on synthetic inputs already resident in HBM.  Rank r
+renders view r (camera yawed by 5*r degrees), so per-GPU work is fixed as N grows
+("weak" scaling) and value = N * P * K / (max over ranks of the K-step time).
+
+Rank 0 prints one JSON line.  It carries the roofline of the dominant kernel (its
+algorithmic bytes per launch / its mean duration from HIP events on the launch
+stream) and the CPU baseline: the oracle (C restatement of the reference,
+oracle/) timed on this host's cores on the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from gaussian_splatting_amd import _C, _lib  # noqa: E402
+from gaussian_splatting_amd import synthetic as syn  # noqa: E402
+from gaussian_splatting_amd.distributed import GradArena  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def algorithmic_bytes(stage: str, P: int, I: int, W: int, H: int, K: int) -> float:
+    """Algorithmic HBM bytes of one launch of each stage (DESIGN.md "Roofline"; SURVEY.md section 8d itemisation)."""
+    N = W * H
+    table = {
+        # reads means 12, scale 12, rot 16, opacity 4, SH 12K; writes radii 4, means2D 8, depth 4, conic+opacity 16,
+        # rgb 12, tiles_touched 4
+        "preprocess": (44 + 12 * K + 48) * P,
+        "depth_sort": 4 * 8 * P,  # 4 key bytes + 4 value bytes, read + write, one pass
+        "scan": 8 * P,
+        "duplicate": 20 * P + 12 * I,
+        "tile_sort": 24 * I,
+        "finalize": 8 * I,
+        # gather 44 B per instance (xy 8, conic+opacity 16, rgb 12, depth 4, index 4); write 24 B per pixel
+        "render_fwd": 44 * I + 24 * N,
+        # gather 44 B per instance; read 24 B per pixel; write the per-Gaussian accumulators (10 floats)
+        "render_bwd": 44 * I + 24 * N + 40 * P,
+        # read accumulators 40 + preprocess inputs 48 + 12K; write grads 56 + 12K
+        "gauss_bwd": (40 + 48 + 12 * K + 56 + 12 * K) * P,
+    }
+    return float(table.get(stage, 0))
+
+
+def step_algorithmic_bytes(P, I, W, H, K):
+    """B_alg of SURVEY.md section 8d for one forward + backward."""
+    return (304 + 36 * K) * P + 132 * I + 48 * W * H
+
+
+def cpu_baseline(cfg_name: str, P: int, W: int, H: int, threads: int):
+    """Oracle (C restatement of the reference) forward + backward on the host, full frame, 1 rep."""
+    from oracle import oracle
+
+    scene, cam = syn.config_scene(cfg_name, seed=0, P=P)
+    gc, gd = syn.upstream_grads(H, W)
+    t0 = time.perf_counter()
+    r = oracle.forward(scene.means3D, scene.opacities, cam.viewmatrix, cam.projmatrix, cam.campos, cam.tanfovx,
+                       cam.tanfovy, H, W, shs=scene.shs, sh_degree=scene.sh_degree, scales=scene.scales,
+                       rotations=scene.rotations, nthreads=threads)
+    r.handle.backward(gc, gd, nthreads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": P / dt, "unit": "Gaussian-splats/s", "cores": threads, "kind": "port",
+            "sample": f"full {cfg_name} frame ({P} Gaussians, {W}x{H}), forward+backward, 1 rep, "
+                      f"{dt:.2f} s on {threads} OpenMP threads (oracle/gsr_oracle.c, float32)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="1m_1080p_sh3", choices=sorted(syn.CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    cfg = syn.CONFIGS[args.config]
+    P, W, H, Kdeg = cfg["P"], cfg["width"], cfg["height"], cfg["sh_degree"]
+    K = (Kdeg + 1) ** 2
+    scene, cam = syn.config_scene(args.config, seed=0, yaw_deg=5.0 * rank)
+    scene, cam = scene.to(dev), cam.to(dev)
+    gc, gd = syn.upstream_grads(H, W, seed=1 + rank)
+    gc, gd = gc.to(dev), gd.to(dev)
+    bg = torch.zeros(3, device=dev)
+    empty = torch.empty(0, device=dev)
+    arena = GradArena(P, scene.shs.shape[1], dev)
+
+    def step():
+        fwd = _C.rasterize_gaussians(bg, scene.means3D, empty, scene.opacities, scene.scales, scene.rotations, 1.0,
+                                     empty, cam.viewmatrix, cam.projmatrix, cam.tanfovx, cam.tanfovy, H, W, scene.shs,
+                                     Kdeg, cam.campos, False, False, False)
+        nr, color, radii, geom, binning, img, invd = fwd
+        _C.rasterize_gaussians_backward(bg, scene.means3D, radii, empty, scene.opacities, scene.scales,
+                                        scene.rotations, 1.0, empty, cam.viewmatrix, cam.projmatrix, cam.tanfovx,
+                                        cam.tanfovy, gc, gd, scene.shs, Kdeg, cam.campos, geom, nr, binning, img,
+                                        False, False, out=arena.views())
+        if world > 1:
+            arena.all_reduce()
+        return nr
+
+    for _ in range(args.warmup):
+        nr = step()
+    torch.cuda.synchronize()
+    _lib.profile_reset()
+    _lib.profile_enable(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        nr = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    _lib.profile_enable(False)
+    stages = _lib.profile_collect()
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    if rank == 0:
+        ms_per_step = elapsed / args.steps * 1e3
+        value = world * P * args.steps / elapsed
+        per_stage = {k: (v[0] / v[1] if v[1] else 0.0) for k, v in stages.items()}
+        dom = max(per_stage, key=per_stage.get)
+        dom_ms = per_stage[dom]
+        alg = algorithmic_bytes(dom, P, nr, W, H, K)
+        achieved = alg / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
+        line = {
+            "metric": "Gaussian-splats/sec fwd+bwd @1080p, 1M Gaussians",
+            "value": value,
+            "unit": "Gaussian-splats/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic (frustum-uniform Gaussians, SURVEY.md 8d; seed 0)",
+            "config": {"workload": args.config, "gaussians": P, "width": W, "height": H, "sh_degree": Kdeg,
+                       "num_rendered": nr, "views": "one per GPU, yaw 5 deg x rank",
+                       "parallelism": f"view-sharded x{world}" + (" + RCCL all-reduce" if world > 1 else "")},
+            "roofline": {"kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "algorithmic_bytes_per_launch": alg, "mean_launch_ms": dom_ms},
+            "stage_ms": {k: round(v, 4) for k, v in per_stage.items()},
+            "step_algorithmic_GBs": step_algorithmic_bytes(P, nr, W, H, K) / (ms_per_step * 1e-3) / 1e9,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+            line["cpu_baseline"] = cpu_baseline(args.config, P, W, H, threads)
+        else:
+            line["cpu_baseline"] = None
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,207 @@
+"""Drop-in replacement of the reference's ``diff_gaussian_rasterization._C`` module.
+
+Same three functions, same positional arguments, same return tuples as the
+pybind11 module of the reference (``ext.cpp:15-19``; tensor handling in
+``rasterize_points.cu:45-274``), implemented over the C ABI of libgsr.so
+(include/gsr.h).  Only HIP-device tensors are accepted: there is no CPU path.
+
+Error behaviour follows the reference: a malformed ``means3D`` raises
+``RuntimeError("means3D must have dimensions (num_points, 3)")``
+(rasterize_points.cu:69-71) and any failure inside the native library raises
+``RuntimeError`` with the library's message.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Tuple
+
+import torch
+
+from . import _lib
+
+__all__ = ["rasterize_gaussians", "rasterize_gaussians_backward", "mark_visible"]
+
+
+def _stream_handle(device: torch.device) -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _require_device(t: torch.Tensor, name: str) -> None:
+    if t.device.type != "cuda":
+        raise RuntimeError(f"{name}: the MI355X rasterizer needs HIP device tensors, got a {t.device.type} tensor "
+                           "(there is no CPU implementation)")
+
+
+class _Inputs:
+    """Keeps contiguous fp32 views alive for the duration of a native call."""
+
+    def __init__(self, device: torch.device):
+        self.device = device
+        self.keep = []
+
+    def opt(self, t: Optional[torch.Tensor], name: str, align16: bool = False) -> Optional[int]:
+        """Device pointer of an optional input; an empty tensor means 'absent' (data_ptr()==nullptr)."""
+        if t is None or t.numel() == 0:
+            return None
+        return self.req(t, name, align16)
+
+    def req(self, t: torch.Tensor, name: str, align16: bool = False, small: bool = False) -> int:
+        if small and t.device.type != "cuda":
+            t = t.to(self.device)  # bg / matrices / campos: 3-16 floats
+        _require_device(t, name)
+        if t.dtype != torch.float32:
+            raise RuntimeError(f"{name}: expected a float32 tensor, got {t.dtype}")
+        if t.device != self.device:
+            raise RuntimeError(f"{name}: tensor on {t.device}, expected {self.device}")
+        t = t.contiguous()
+        if align16 and t.data_ptr() % 16:
+            t = t.clone()
+        self.keep.append(t)
+        return t.data_ptr()
+
+
+class _Resizer:
+    """The reference's resizeFunctional (rasterize_points.cu:29-43) as a C callback."""
+
+    def __init__(self, tensor: torch.Tensor):
+        self.tensor = tensor
+        self.cb = _lib.ALLOC_FN(self._resize)
+
+    def _resize(self, _ctx, nbytes):
+        try:
+            self.tensor.resize_(int(nbytes))
+            return self.tensor.data_ptr()
+        except Exception:  # e.g. out of memory: the library reports GSR_ERR_ALLOC
+            return None
+
+
+def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
+                        viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
+                        prefiltered, antialiasing, debug) -> Tuple[int, torch.Tensor, torch.Tensor, torch.Tensor,
+                                                                   torch.Tensor, torch.Tensor, torch.Tensor]:
+    """RasterizeGaussiansCUDA (rasterize_points.cu:45-146).
+
+    Returns ``(num_rendered, color[3,H,W], radii[P] int32, geomBuffer, binningBuffer, imgBuffer, invdepth[1,H,W])``.
+    """
+    if means3D.ndimension() != 2 or means3D.size(1) != 3:
+        raise RuntimeError("means3D must have dimensions (num_points, 3)")
+    _require_device(means3D, "means3D")
+    device = means3D.device
+    lib = _lib.load()
+    P = means3D.size(0)
+    H, W = int(image_height), int(image_width)
+    f32 = dict(dtype=torch.float32, device=device)
+    alloc = torch.empty if P > 0 else torch.zeros  # every pixel / Gaussian is written when P > 0
+    out_color = alloc((3, H, W), **f32)
+    out_invdepth = alloc((1, H, W), **f32)
+    radii = alloc((P,), dtype=torch.int32, device=device)
+    geom = torch.empty(0, dtype=torch.uint8, device=device)
+    binning = torch.empty(0, dtype=torch.uint8, device=device)
+    img = torch.empty(0, dtype=torch.uint8, device=device)
+    if P == 0:
+        return 0, out_color, radii, geom, binning, img, out_invdepth
+
+    M = sh.size(1) if (sh is not None and sh.numel() != 0 and sh.size(0) != 0) else 0
+    ins = _Inputs(device)
+    rg, rb, ri = _Resizer(geom), _Resizer(binning), _Resizer(img)
+    nr = ctypes.c_int(0)
+    with torch.cuda.device(device):
+        rc = lib.gsr_rasterize_forward(
+            rg.cb, None, rb.cb, None, ri.cb, None, P, int(degree), M,
+            ins.req(background, "bg", small=True), W, H,
+            ins.req(means3D, "means3D"), ins.opt(sh, "sh", align16=True), ins.opt(colors, "colors_precomp"),
+            ins.req(opacity, "opacities"), ins.opt(scales, "scales"), float(scale_modifier),
+            ins.opt(rotations, "rotations", align16=True), ins.opt(cov3D_precomp, "cov3D_precomp"),
+            ins.req(viewmatrix, "viewmatrix", small=True), ins.req(projmatrix, "projmatrix", small=True),
+            ins.opt(campos if campos is not None and campos.device.type == "cuda" else
+                    (campos.to(device) if campos is not None else None), "campos"),
+            float(tan_fovx), float(tan_fovy), int(bool(prefiltered)), out_color.data_ptr(), out_invdepth.data_ptr(),
+            int(bool(antialiasing)), radii.data_ptr(), int(bool(debug)), _stream_handle(device), ctypes.byref(nr))
+    _lib.check(rc, "rasterize_gaussians")
+    return int(nr.value), out_color, radii, geom, binning, img, out_invdepth
+
+
+def rasterize_gaussians_backward(background, means3D, radii, colors, opacities, scales, rotations, scale_modifier,
+                                 cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color,
+                                 dL_dout_invdepth, sh, degree, campos, geomBuffer, R, binningBuffer, imageBuffer,
+                                 antialiasing, debug, out=None):
+    """RasterizeGaussiansBackwardCUDA (rasterize_points.cu:149-248).
+
+    Returns ``(dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations)``.
+    ``out`` (an extension, not in the reference) may map any of the names
+    ``dL_dmeans3D, dL_dsh, dL_dopacity, dL_dscales, dL_drotations`` to preallocated
+    contiguous float32 tensors of the right shape -- e.g. views of one flat
+    gradient arena that is then all-reduced without a copy.
+    """
+    _require_device(means3D, "means3D")
+    device = means3D.device
+    lib = _lib.load()
+    P = means3D.size(0)
+    H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))
+    M = sh.size(1) if (sh is not None and sh.numel() != 0 and sh.size(0) != 0) else 0
+    f32 = dict(dtype=torch.float32, device=device)
+    alloc = torch.empty if P > 0 else torch.zeros
+    out = dict(out or {})
+
+    def buf(name, shape):
+        t = out.get(name)
+        if t is None:
+            return alloc(shape, **f32)
+        if tuple(t.shape) != tuple(shape) or t.dtype != torch.float32 or not t.is_contiguous() or t.device != device:
+            raise RuntimeError(f"out[{name}] must be a contiguous float32 {tuple(shape)} tensor on {device}")
+        return t
+
+    dL_dmeans2D = alloc((P, 3), **f32)
+    dL_dcolors = alloc((P, 3), **f32)
+    dL_dopacity = buf("dL_dopacity", (P, 1))
+    dL_dmeans3D = buf("dL_dmeans3D", (P, 3))
+    dL_dcov3D = alloc((P, 6), **f32)
+    dL_dsh = buf("dL_dsh", (P, M, 3))
+    dL_dscales = buf("dL_dscales", (P, 3))
+    dL_drotations = buf("dL_drotations", (P, 4))
+    has_inv = dL_dout_invdepth is not None and dL_dout_invdepth.numel() != 0 and dL_dout_invdepth.size(0) != 0
+    dL_dinvdepths = alloc((P, 1), **f32) if has_inv else None
+    result = (dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations)
+    if P == 0:
+        return result
+
+    ins = _Inputs(device)
+    scratch = torch.empty(0, dtype=torch.uint8, device=device)
+    rs = _Resizer(scratch)
+    with torch.cuda.device(device):
+        rc = lib.gsr_rasterize_backward(
+            P, int(degree), M, int(R), ins.req(background, "bg", small=True), W, H,
+            ins.req(means3D, "means3D"), ins.opt(sh, "sh"), ins.opt(colors, "colors_precomp"),
+            ins.req(opacities, "opacities"), ins.opt(scales, "scales"), float(scale_modifier),
+            ins.opt(rotations, "rotations", align16=True), ins.opt(cov3D_precomp, "cov3D_precomp"),
+            ins.req(viewmatrix, "viewmatrix", small=True), ins.req(projmatrix, "projmatrix", small=True),
+            ins.opt(campos if campos is not None and campos.device.type == "cuda" else
+                    (campos.to(device) if campos is not None else None), "campos"),
+            float(tan_fovx), float(tan_fovy), radii.contiguous().data_ptr(), geomBuffer.data_ptr(),
+            binningBuffer.data_ptr() if binningBuffer.numel() else None, imageBuffer.data_ptr(),
+            ins.req(dL_dout_color, "dL_dout_color"),
+            ins.req(dL_dout_invdepth, "dL_dout_invdepth") if has_inv else None,
+            dL_dmeans2D.data_ptr(), None, dL_dopacity.data_ptr(), dL_dcolors.data_ptr(),
+            dL_dinvdepths.data_ptr() if has_inv else None, dL_dmeans3D.data_ptr(), dL_dcov3D.data_ptr(),
+            dL_dsh.data_ptr() if M > 0 else None, dL_dscales.data_ptr(), dL_drotations.data_ptr(),
+            int(bool(antialiasing)), int(bool(debug)), rs.cb, None, _stream_handle(device))
+    _lib.check(rc, "rasterize_gaussians_backward")
+    return result
+
+
+def mark_visible(means3D, viewmatrix, projmatrix) -> torch.Tensor:
+    """markVisible (rasterize_points.cu:250-274): bool[P], view-space z > 0.2."""
+    _require_device(means3D, "means3D")
+    device = means3D.device
+    lib = _lib.load()
+    P = means3D.size(0)
+    present = torch.zeros(P, dtype=torch.bool, device=device)
+    if P == 0:
+        return present
+    ins = _Inputs(device)
+    with torch.cuda.device(device):
+        rc = lib.gsr_mark_visible(P, ins.req(means3D, "means3D"), ins.req(viewmatrix, "viewmatrix", small=True),
+                                  ins.req(projmatrix, "projmatrix", small=True), present.data_ptr(),
+                                  _stream_handle(device))
+    _lib.check(rc, "mark_visible")
+    return present

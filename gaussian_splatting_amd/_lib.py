@@ -1,0 +1,102 @@
+"""ctypes binding of libgsr.so (the C ABI in include/gsr.h).
+
+The library is built in-tree (``python -m gaussian_splatting_amd.build``) and
+loaded from ``gaussian_splatting_amd/lib/libgsr.so``.  There is no fallback: if
+the library is missing or cannot be loaded, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+import threading
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("GSR_LIBRARY", os.path.join(_PKG, "lib", "libgsr.so"))
+HEADER_PATH = os.path.join(os.path.dirname(_PKG), "include", "gsr.h")
+
+ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
+
+_vp = ctypes.c_void_p
+_i = ctypes.c_int
+_f = ctypes.c_float
+
+# argument lists, in include/gsr.h order
+SIGNATURES = {
+    "gsr_rasterize_forward": (_i, [ALLOC_FN, _vp, ALLOC_FN, _vp, ALLOC_FN, _vp, _i, _i, _i, _vp, _i, _i, _vp, _vp,
+                                   _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp, _f, _f, _i, _vp, _vp, _i, _vp, _i,
+                                   _vp, ctypes.POINTER(_i)]),
+    "gsr_rasterize_backward": (_i, [_i, _i, _i, _i, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp,
+                                    _vp, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                    _vp, _vp, _vp, _i, _i, ALLOC_FN, _vp, _vp]),
+    "gsr_mark_visible": (_i, [_i, _vp, _vp, _vp, _vp, _vp]),
+    "gsr_last_error": (ctypes.c_char_p, []),
+    "gsr_version": (ctypes.c_char_p, []),
+    "gsr_profile_enable": (_i, [_i]),
+    "gsr_profile_collect": (_i, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong), _i]),
+    "gsr_profile_reset": (None, []),
+    "gsr_profile_stage_name": (ctypes.c_char_p, [_i]),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+class GsrError(RuntimeError):
+    """A failure reported by libgsr (the reference raises RuntimeError / AT_ERROR too)."""
+
+
+def header_symbols(path: str = HEADER_PATH) -> list:
+    """Function names declared in include/gsr.h."""
+    with open(path) as f:
+        text = f.read()
+    return sorted(set(re.findall(r"\b(gsr_[a-z_]+)\s*\(", text)) - {"gsr_alloc_fn"})
+
+
+def load():
+    """Load libgsr.so once; raises GsrError if it is missing (no CPU fallback exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise GsrError(f"libgsr.so not found at {LIB_PATH}; build it with "
+                           "`python -m gaussian_splatting_amd.build` (hipcc, gfx950)")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load().gsr_last_error().decode(errors="replace")
+        raise GsrError(f"{what} failed (code {rc}): {msg}")
+
+
+def version() -> str:
+    return load().gsr_version().decode()
+
+
+# ---- stage profiler ---------------------------------------------------------------
+def profile_enable(on: bool = True) -> None:
+    load().gsr_profile_enable(1 if on else 0)
+
+
+def profile_reset() -> None:
+    load().gsr_profile_reset()
+
+
+def profile_collect() -> dict:
+    """Per-stage (total_ms, calls) accumulated since the last reset."""
+    lib = load()
+    n = 32
+    ms = (ctypes.c_double * n)()
+    calls = (ctypes.c_longlong * n)()
+    k = lib.gsr_profile_collect(ms, calls, n)
+    return {lib.gsr_profile_stage_name(i).decode(): (ms[i], calls[i]) for i in range(k)}

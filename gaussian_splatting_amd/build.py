@@ -1,0 +1,73 @@
+"""Build libgsr.so (HIP, gfx950) in-tree with hipcc.
+
+    python -m gaussian_splatting_amd.build [--force] [--jobs N]
+
+Each .hip translation unit is compiled to an object in parallel, then linked
+into ``gaussian_splatting_amd/lib/libgsr.so``.  No torch headers are involved:
+the library is a plain C ABI (include/gsr.h).
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+OBJ = os.path.join(PKG, "build")
+LIB_DIR = os.path.join(PKG, "lib")
+LIB = os.path.join(LIB_DIR, "libgsr.so")
+SOURCES = ["api.hip", "preprocess.hip", "binning.hip", "render.hip", "backward.hip"]
+HEADERS = ["gsr_common.h", "kernels.h"]
+ARCH = os.environ.get("GSR_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-result",
+            "-I", os.path.join(ROOT, "include"), "-I", CSRC]
+
+
+def _newest_input_mtime() -> float:
+    files = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(ROOT, "include", "gsr.h"), __file__]
+    return max(os.path.getmtime(f) for f in files)
+
+
+def _compile(src: str) -> str:
+    obj = os.path.join(OBJ, src.replace(".hip", ".o"))
+    cmd = [HIPCC, *CXXFLAGS, "-c", os.path.join(CSRC, src), "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src}:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return obj
+
+
+def build(force: bool = False, jobs: int = 5, verbose: bool = True) -> str:
+    """Compile every HIP source for gfx950 and link libgsr.so; returns the library path."""
+    if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= _newest_input_mtime():
+        return LIB
+    os.makedirs(OBJ, exist_ok=True)
+    os.makedirs(LIB_DIR, exist_ok=True)
+    with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        objs = list(ex.map(_compile, SOURCES))
+    tmp = LIB + ".tmp"
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    os.replace(tmp, LIB)
+    if verbose:
+        print(f"[gsr] built {LIB}")
+    return LIB
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--jobs", type=int, default=5)
+    args = ap.parse_args()
+    try:
+        build(force=args.force, jobs=args.jobs)
+    except RuntimeError as e:
+        print(e, file=sys.stderr)
+        sys.exit(1)

@@ -1,0 +1,438 @@
+// api.hip -- host orchestration and the extern "C" boundary (include/gsr.h).
+//
+// Forward stage order mirrors CudaRasterizer::Rasterizer::forward
+// (CR/rasterizer_impl.cu:227-370); the stages themselves are this project's
+// (depth pre-sort + 16-bit tile sort instead of one 64-bit sort, footprint
+// culling in the blender, atomic-free backward).
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "../../include/gsr.h"
+#include "kernels.h"
+
+namespace {
+
+thread_local char g_err[1024] = "";
+
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+#define HIP_TRY(expr, stage)                                                                                    \
+    do {                                                                                                        \
+        hipError_t _e = (expr);                                                                                 \
+        if (_e != hipSuccess) return fail(GSR_ERR_HIP, "%s: %s", stage, hipGetErrorString(_e));                 \
+    } while (0)
+
+// ---- stage profiler -----------------------------------------------------------
+enum Stage {
+    ST_PREPROCESS = 0,
+    ST_DEPTH_SORT,
+    ST_SCAN,
+    ST_DUPLICATE,
+    ST_TILE_SORT,
+    ST_FINALIZE,
+    ST_RENDER_FWD,
+    ST_RENDER_BWD,
+    ST_GAUSS_BWD,
+    ST_COUNT
+};
+const char* kStageNames[ST_COUNT] = {"preprocess", "depth_sort", "scan",       "duplicate", "tile_sort",
+                                     "finalize",   "render_fwd", "render_bwd", "gauss_bwd"};
+
+struct Profiler {
+    bool on = false;
+    std::mutex mu;
+    struct Pending {
+        int stage;
+        hipEvent_t a, b;
+    };
+    std::vector<Pending> pending;
+    std::vector<hipEvent_t> pool;
+    double total_ms[ST_COUNT] = {};
+    long long calls[ST_COUNT] = {};
+    hipEvent_t get() {
+        if (!pool.empty()) {
+            hipEvent_t e = pool.back();
+            pool.pop_back();
+            return e;
+        }
+        hipEvent_t e;
+        (void)hipEventCreate(&e);
+        return e;
+    }
+};
+Profiler g_prof;
+
+struct StageScope {
+    int stage;
+    hipStream_t stream;
+    hipEvent_t a = nullptr;
+    StageScope(int s, hipStream_t st) : stage(s), stream(st) {
+        if (g_prof.on) {
+            std::lock_guard<std::mutex> lk(g_prof.mu);
+            a = g_prof.get();
+            (void)hipEventRecord(a, stream);
+        }
+    }
+    ~StageScope() {
+        if (a) {
+            std::lock_guard<std::mutex> lk(g_prof.mu);
+            hipEvent_t b = g_prof.get();
+            (void)hipEventRecord(b, stream);
+            g_prof.pending.push_back({stage, a, b});
+        }
+    }
+};
+
+int check_debug(int debug, hipStream_t stream, const char* stage) {
+    if (!debug) return GSR_OK;
+    hipError_t e = hipStreamSynchronize(stream);
+    if (e == hipSuccess) e = hipGetLastError();
+    if (e != hipSuccess) return fail(GSR_ERR_HIP, "%s: %s", stage, hipGetErrorString(e));
+    return GSR_OK;
+}
+
+unsigned bit_length(uint32_t n) {  // getHigherMsb (CR/rasterizer_impl.cu:36-51)
+    unsigned b = 0;
+    while (b < 32 && (n >> b)) b++;
+    return b;
+}
+
+gsr::GeomState carve_geom(char* base, int P, size_t* total) {
+    using namespace gsr;
+    Carver c{base, 0};
+    GeomState g{};
+    g.rec0 = c.take<float4>(P);
+    g.rec1 = c.take<float4>(P);
+    g.rec2 = c.take<float4>(P);
+    g.depth_key = c.take<uint32_t>(P);
+    g.depth_key_sorted = c.take<uint32_t>(P);
+    g.gid_by_rank = c.take<uint32_t>(P);
+    g.rank_of = c.take<uint32_t>(P);
+    g.tiles_touched = c.take<uint32_t>(P);
+    g.tiles_ranked = c.take<uint32_t>(P);
+    g.offsets = c.take<unsigned long long>(P);
+    g.clamped = c.take<uint8_t>(P);
+    g.status = c.take<uint32_t>(4);
+    g.sort_temp_bytes = depth_sort_temp_bytes(P);
+    g.sort_temp = c.take<char>(g.sort_temp_bytes);
+    g.scan_temp_bytes = scan_temp_bytes(P);
+    g.scan_temp = c.take<char>(g.scan_temp_bytes);
+    *total = align_up(c.off);
+    return g;
+}
+
+gsr::ImageState carve_image(char* base, int W, int H, uint32_t tiles, size_t* total) {
+    using namespace gsr;
+    Carver c{base, 0};
+    ImageState im{};
+    const size_t N = (size_t)W * H;
+    im.final_T = c.take<float>(N);
+    im.n_contrib = c.take<uint32_t>(N);
+    im.accum = c.take<float>(4 * N);
+    im.ranges = c.take<uint2>(tiles);
+    *total = align_up(c.off);
+    return im;
+}
+
+gsr::BinningState carve_binning(char* base, size_t R, bool key16, size_t* total) {
+    using namespace gsr;
+    Carver c{base, 0};
+    BinningState b{};
+    const size_t ks = key16 ? 2 : 4;
+    b.keys = c.take<char>(R * ks);
+    b.keys_sorted = c.take<char>(R * ks);
+    b.emit_gid = c.take<uint32_t>(R);
+    b.e_sorted = c.take<uint32_t>(R);
+    b.sorted_gid = c.take<uint32_t>(R);
+    b.sort_temp_bytes = R ? tile_sort_temp_bytes(R, key16) : 0;
+    b.sort_temp = c.take<char>(b.sort_temp_bytes);
+    *total = align_up(c.off);
+    return b;
+}
+
+gsr::GradRecs carve_recs(char* base, size_t R, size_t* total) {
+    using namespace gsr;
+    Carver c{base, 0};
+    GradRecs r{};
+    r.a = c.take<float4>(R);
+    r.b = c.take<float4>(R);
+    r.c = c.take<float2>(R);
+    *total = align_up(c.off);
+    return r;
+}
+
+void* call_alloc(gsr_alloc_fn fn, void* ctx, size_t bytes) {
+    if (!fn) return nullptr;
+    return fn(ctx, bytes ? bytes : 1);
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* gsr_last_error(void) { return g_err; }
+
+const char* gsr_version(void) { return "gsr 0.1.0 gfx950"; }
+
+int gsr_profile_enable(int enable) {
+    std::lock_guard<std::mutex> lk(g_prof.mu);
+    g_prof.on = enable != 0;
+    return GSR_OK;
+}
+
+void gsr_profile_reset(void) {
+    std::lock_guard<std::mutex> lk(g_prof.mu);
+    for (auto& p : g_prof.pending) {
+        g_prof.pool.push_back(p.a);
+        g_prof.pool.push_back(p.b);
+    }
+    g_prof.pending.clear();
+    for (int i = 0; i < ST_COUNT; i++) {
+        g_prof.total_ms[i] = 0;
+        g_prof.calls[i] = 0;
+    }
+}
+
+int gsr_profile_collect(double* total_ms, long long* calls, int max_stages) {
+    std::lock_guard<std::mutex> lk(g_prof.mu);
+    for (auto& p : g_prof.pending) {
+        (void)hipEventSynchronize(p.b);
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+            g_prof.total_ms[p.stage] += ms;
+            g_prof.calls[p.stage] += 1;
+        }
+        g_prof.pool.push_back(p.a);
+        g_prof.pool.push_back(p.b);
+    }
+    g_prof.pending.clear();
+    for (int i = 0; i < ST_COUNT && i < max_stages; i++) {
+        if (total_ms) total_ms[i] = g_prof.total_ms[i];
+        if (calls) calls[i] = g_prof.calls[i];
+    }
+    return ST_COUNT;
+}
+
+const char* gsr_profile_stage_name(int stage) {
+    return (stage >= 0 && stage < ST_COUNT) ? kStageNames[stage] : "";
+}
+
+int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
+                     unsigned char* present, void* stream) {
+    (void)projmatrix;  // checkFrustum computes the projection but only tests view-space z
+    g_err[0] = 0;
+    if (P < 0) return fail(GSR_ERR_ARGUMENT, "mark_visible: P must be >= 0");
+    if (P == 0) return GSR_OK;
+    if (!means3D || !viewmatrix || !present) return fail(GSR_ERR_ARGUMENT, "mark_visible: null pointer");
+    HIP_TRY(gsr::launch_mark_visible(P, means3D, viewmatrix, reinterpret_cast<bool*>(present), (hipStream_t)stream),
+            "mark_visible");
+    return GSR_OK;
+}
+
+int gsr_rasterize_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_alloc, void* binning_ctx,
+                          gsr_alloc_fn image_alloc, void* image_ctx, int P, int D, int M, const float* background,
+                          int width, int height, const float* means3D, const float* shs, const float* colors_precomp,
+                          const float* opacities, const float* scales, float scale_modifier, const float* rotations,
+                          const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix,
+                          const float* cam_pos, float tan_fovx, float tan_fovy, int prefiltered, float* out_color,
+                          float* out_invdepth, int antialiasing, int* radii, int debug, void* stream_,
+                          int* num_rendered) {
+    using namespace gsr;
+    g_err[0] = 0;
+    hipStream_t stream = (hipStream_t)stream_;
+    if (num_rendered) *num_rendered = 0;
+    if (P < 0 || width <= 0 || height <= 0)
+        return fail(GSR_ERR_ARGUMENT, "rasterize_forward: invalid sizes P=%d W=%d H=%d", P, width, height);
+    if (P == 0) return GSR_OK;  // RI/rasterize_points.cu:108: nothing is launched
+    if (!means3D || !opacities || !viewmatrix || !projmatrix || !background || !out_color || !out_invdepth || !radii)
+        return fail(GSR_ERR_ARGUMENT, "rasterize_forward: missing required input");
+    if (!colors_precomp && !shs)
+        return fail(GSR_ERR_ARGUMENT, "rasterize_forward: provide either SHs or precomputed colours");
+    if (!cov3D_precomp && (!scales || !rotations))
+        return fail(GSR_ERR_ARGUMENT, "rasterize_forward: provide scales+rotations or a precomputed covariance");
+    if (!colors_precomp && (D < 0 || D > 3 || (D + 1) * (D + 1) > M))
+        return fail(GSR_ERR_ARGUMENT, "rasterize_forward: SH degree %d needs %d coefficients, got %d", D,
+                    (D + 1) * (D + 1), M);
+    if (!colors_precomp && !cam_pos) return fail(GSR_ERR_ARGUMENT, "rasterize_forward: campos required for SHs");
+
+    const float focal_y = height / (2.0f * tan_fovy);  // CR/rasterizer_impl.cu:253-254
+    const float focal_x = width / (2.0f * tan_fovx);
+    const uint32_t gx = (width + kTile - 1) / kTile, gy = (height + kTile - 1) / kTile;
+    const uint32_t tiles = gx * gy;
+    const bool key16 = tiles <= 65536u;
+    const unsigned bit = bit_length(tiles);
+
+    size_t geom_bytes = 0, img_bytes = 0;
+    carve_geom(nullptr, P, &geom_bytes);
+    char* gbase = (char*)call_alloc(geom_alloc, geom_ctx, geom_bytes);
+    if (!gbase) return fail(GSR_ERR_ALLOC, "rasterize_forward: geometry buffer allocation failed");
+    GeomState geom = carve_geom(gbase, P, &geom_bytes);
+    carve_image(nullptr, width, height, tiles, &img_bytes);
+    char* ibase = (char*)call_alloc(image_alloc, image_ctx, img_bytes);
+    if (!ibase) return fail(GSR_ERR_ALLOC, "rasterize_forward: image buffer allocation failed");
+    ImageState img = carve_image(ibase, width, height, tiles, &img_bytes);
+
+    HIP_TRY(hipMemsetAsync(geom.status, 0, 4 * sizeof(uint32_t), stream), "status init");
+    {
+        StageScope sc(ST_PREPROCESS, stream);
+        PreprocessArgs pa{};
+        pa.P = P; pa.D = D; pa.M = M; pa.W = width; pa.H = height;
+        pa.means3D = means3D; pa.scales = scales; pa.scale_modifier = scale_modifier; pa.rotations = rotations;
+        pa.opacities = opacities; pa.shs = colors_precomp ? nullptr : shs; pa.cov3D_precomp = cov3D_precomp;
+        pa.colors_precomp = colors_precomp; pa.viewmatrix = viewmatrix; pa.projmatrix = projmatrix;
+        pa.campos = cam_pos; pa.tan_fovx = tan_fovx; pa.tan_fovy = tan_fovy; pa.focal_x = focal_x;
+        pa.focal_y = focal_y; pa.gx = gx; pa.gy = gy; pa.prefiltered = prefiltered; pa.antialiasing = antialiasing;
+        pa.footprint_cull = (width < 32000 && height < 32000) ? 1 : 0;
+        pa.radii = radii; pa.geom = geom;
+        HIP_TRY(launch_preprocess(pa, stream), "preprocess");
+    }
+    if (int rc = check_debug(debug, stream, "preprocess")) return rc;
+    if (prefiltered) {
+        uint32_t st = 0;
+        HIP_TRY(hipMemcpyAsync(&st, geom.status, sizeof(uint32_t), hipMemcpyDeviceToHost, stream), "status copy");
+        HIP_TRY(hipStreamSynchronize(stream), "status sync");
+        if (st & 1u)
+            return fail(GSR_ERR_PREFILTERED,
+                        "Point is filtered although prefiltered is set. This shouldn't happen! (CR/auxiliary.h:184)");
+    }
+    {
+        StageScope sc(ST_DEPTH_SORT, stream);
+        HIP_TRY(depth_sort(geom, P, stream), "depth_sort");
+    }
+    if (int rc = check_debug(debug, stream, "depth_sort")) return rc;
+    {
+        StageScope sc(ST_SCAN, stream);
+        HIP_TRY(rank_and_scan(geom, P, stream), "scan");
+    }
+    if (int rc = check_debug(debug, stream, "scan")) return rc;
+
+    // The one host synchronisation of the forward (CR/rasterizer_impl.cu:313).
+    unsigned long long total = 0;
+    HIP_TRY(hipMemcpyAsync(&total, geom.offsets + (P - 1), sizeof(total), hipMemcpyDeviceToHost, stream),
+            "num_rendered copy");
+    HIP_TRY(hipStreamSynchronize(stream), "num_rendered sync");
+    if (total > (unsigned long long)INT_MAX)
+        return fail(GSR_ERR_OVERFLOW, "rasterize_forward: %llu tile instances exceed INT_MAX", total);
+    const size_t R = (size_t)total;
+
+    size_t bin_bytes = 0;
+    carve_binning(nullptr, R, key16, &bin_bytes);
+    char* bbase = (char*)call_alloc(binning_alloc, binning_ctx, bin_bytes);
+    if (!bbase) return fail(GSR_ERR_ALLOC, "rasterize_forward: binning buffer allocation failed");
+    BinningState bin = carve_binning(bbase, R, key16, &bin_bytes);
+
+    HIP_TRY(hipMemsetAsync(img.ranges, 0, tiles * sizeof(uint2), stream), "ranges memset");
+    if (R > 0) {
+        {
+            StageScope sc(ST_DUPLICATE, stream);
+            HIP_TRY(launch_duplicate(P, geom, radii, gx, gy, bin, key16, stream), "duplicate");
+        }
+        if (int rc = check_debug(debug, stream, "duplicate")) return rc;
+        {
+            StageScope sc(ST_TILE_SORT, stream);
+            HIP_TRY(tile_sort(bin, R, bit, key16, stream), "tile_sort");
+        }
+        if (int rc = check_debug(debug, stream, "tile_sort")) return rc;
+        {
+            StageScope sc(ST_FINALIZE, stream);
+            HIP_TRY(launch_finalize(R, bin, img.ranges, key16, stream), "finalize");
+        }
+        if (int rc = check_debug(debug, stream, "finalize")) return rc;
+    }
+    {
+        StageScope sc(ST_RENDER_FWD, stream);
+        RenderFwdArgs ra{};
+        ra.W = width; ra.H = height; ra.gx = gx; ra.gy = gy; ra.ranges = img.ranges; ra.sorted_gid = bin.sorted_gid;
+        ra.rec0 = geom.rec0; ra.rec1 = geom.rec1; ra.rec2 = geom.rec2; ra.bg = background;
+        ra.out_color = out_color; ra.out_invdepth = out_invdepth; ra.img = img;
+        HIP_TRY(launch_render_fwd(ra, stream), "render_fwd");
+    }
+    if (int rc = check_debug(debug, stream, "render_fwd")) return rc;
+    if (num_rendered) *num_rendered = (int)R;
+    return GSR_OK;
+}
+
+int gsr_rasterize_backward(int P, int D, int M, int R, const float* background, int width, int height,
+                           const float* means3D, const float* shs, const float* colors_precomp,
+                           const float* opacities, const float* scales, float scale_modifier, const float* rotations,
+                           const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix,
+                           const float* campos, float tan_fovx, float tan_fovy, const int* radii, void* geom_buffer,
+                           void* binning_buffer, void* image_buffer, const float* dL_dpix, const float* dL_dinvdepths,
+                           float* dL_dmean2D, float* dL_dconic, float* dL_dopacity, float* dL_dcolor,
+                           float* dL_dinvdepth, float* dL_dmean3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscale,
+                           float* dL_drot, int antialiasing, int debug, gsr_alloc_fn scratch_alloc,
+                           void* scratch_ctx, void* stream_) {
+    using namespace gsr;
+    g_err[0] = 0;
+    hipStream_t stream = (hipStream_t)stream_;
+    if (P < 0 || R < 0 || width <= 0 || height <= 0)
+        return fail(GSR_ERR_ARGUMENT, "rasterize_backward: invalid sizes P=%d R=%d W=%d H=%d", P, R, width, height);
+    if (P == 0) return GSR_OK;
+    if (!geom_buffer || !image_buffer || (R > 0 && !binning_buffer))
+        return fail(GSR_ERR_ARGUMENT, "rasterize_backward: missing forward buffers");
+    if (!means3D || !opacities || !radii || !dL_dpix || !dL_dmean2D || !dL_dopacity || !dL_dcolor || !dL_dmean3D ||
+        !dL_dcov3D || !viewmatrix || !projmatrix || !background)
+        return fail(GSR_ERR_ARGUMENT, "rasterize_backward: missing required pointer");
+    if (shs && (!dL_dsh || !campos)) return fail(GSR_ERR_ARGUMENT, "rasterize_backward: SH gradient needs dL_dsh");
+    if (scales && (!rotations || !dL_dscale || !dL_drot))
+        return fail(GSR_ERR_ARGUMENT, "rasterize_backward: scale/rotation gradients need outputs");
+    if ((dL_dinvdepths == nullptr) != (dL_dinvdepth == nullptr))
+        return fail(GSR_ERR_ARGUMENT, "rasterize_backward: dL_dinvdepths and dL_dinvdepth go together");
+
+    const float focal_y = height / (2.0f * tan_fovy);
+    const float focal_x = width / (2.0f * tan_fovx);
+    const uint32_t gx = (width + kTile - 1) / kTile, gy = (height + kTile - 1) / kTile;
+    const uint32_t tiles = gx * gy;
+    const bool key16 = tiles <= 65536u;
+    size_t tmp = 0;
+    GeomState geom = carve_geom((char*)geom_buffer, P, &tmp);
+    ImageState img = carve_image((char*)image_buffer, width, height, tiles, &tmp);
+    BinningState bin = carve_binning((char*)binning_buffer, (size_t)R, key16, &tmp);
+    size_t rec_bytes = 0;
+    carve_recs(nullptr, (size_t)R, &rec_bytes);
+    char* rbase = (char*)call_alloc(scratch_alloc, scratch_ctx, rec_bytes);
+    if (!rbase) return fail(GSR_ERR_ALLOC, "rasterize_backward: scratch allocation failed");
+    GradRecs recs = carve_recs(rbase, (size_t)R, &rec_bytes);
+
+    if (R > 0) {
+        StageScope sc(ST_RENDER_BWD, stream);
+        RenderBwdArgs ra{};
+        ra.W = width; ra.H = height; ra.gx = gx; ra.gy = gy; ra.ranges = img.ranges; ra.sorted_gid = bin.sorted_gid;
+        ra.e_sorted = bin.e_sorted; ra.rec0 = geom.rec0; ra.rec1 = geom.rec1; ra.rec2 = geom.rec2;
+        ra.bg = background; ra.dL_dpix = dL_dpix; ra.dL_dinvdepth = dL_dinvdepths; ra.img = img; ra.recs = recs;
+        HIP_TRY(launch_render_bwd(ra, stream), "render_bwd");
+    }
+    if (int rc = check_debug(debug, stream, "render_bwd")) return rc;
+    {
+        StageScope sc(ST_GAUSS_BWD, stream);
+        GaussBwdArgs ga{};
+        ga.P = P; ga.D = D; ga.M = M; ga.W = width; ga.H = height;
+        ga.means3D = means3D; ga.shs = colors_precomp ? nullptr : shs; ga.opacities = opacities; ga.scales = scales;
+        ga.rotations = rotations; ga.cov3D_precomp = cov3D_precomp; ga.scale_modifier = scale_modifier;
+        ga.viewmatrix = viewmatrix; ga.projmatrix = projmatrix; ga.campos = campos;
+        ga.tan_fovx = tan_fovx; ga.tan_fovy = tan_fovy; ga.focal_x = focal_x; ga.focal_y = focal_y;
+        ga.antialiasing = antialiasing; ga.radii = radii; ga.geom = geom; ga.recs = recs;
+        ga.have_invdepth = dL_dinvdepths != nullptr;
+        ga.dL_dmean2D = dL_dmean2D; ga.dL_dconic = dL_dconic; ga.dL_dopacity = dL_dopacity; ga.dL_dcolor = dL_dcolor;
+        ga.dL_dinvdepth = dL_dinvdepth; ga.dL_dmean3D = dL_dmean3D; ga.dL_dcov3D = dL_dcov3D;
+        ga.dL_dsh = M > 0 ? dL_dsh : nullptr; ga.dL_dscale = dL_dscale; ga.dL_drot = dL_drot;
+        HIP_TRY(launch_gauss_bwd(ga, stream), "gauss_bwd");
+    }
+    if (int rc = check_debug(debug, stream, "gauss_bwd")) return rc;
+    return GSR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,165 @@
+// gsr_common.h -- shared definitions for the gfx950 Gaussian tile rasterizer.
+//
+// Everything here is written for CDNA4 (wave64, 160 KiB LDS per CU).  The
+// algorithm it implements is the reference's tile rasterizer
+// (submodules/diff-gaussian-rasterization/cuda_rasterizer, "CR" below); the
+// data layout and the kernel decomposition are this project's own.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+namespace gsr {
+
+constexpr int kTile = 16;                 // tile edge in pixels (CR/config.h:16-17)
+constexpr int kTilePix = kTile * kTile;   // 256 pixels = 256 threads = 4 waves
+constexpr int kWave = 64;
+constexpr int kChannels = 3;              // CR/config.h:15
+constexpr size_t kAlign = 256;            // sub-array alignment inside the scratch buffers
+
+// Spherical-harmonics constants (CR/auxiliary.h:23-40).
+constexpr float SH_C0 = 0.28209479177387814f;
+constexpr float SH_C1 = 0.4886025119029199f;
+constexpr float SH_C2_0 = 1.0925484305920792f, SH_C2_1 = -1.0925484305920792f, SH_C2_2 = 0.31539156525252005f,
+                SH_C2_3 = -1.0925484305920792f, SH_C2_4 = 0.5462742152960396f;
+constexpr float SH_C3_0 = -0.5900435899266435f, SH_C3_1 = 2.890611442640554f, SH_C3_2 = -0.4570457994644658f,
+                SH_C3_3 = 0.3731763325901154f, SH_C3_4 = -0.4570457994644658f, SH_C3_5 = 1.445305721320277f,
+                SH_C3_6 = -0.5900435899266435f;
+
+// ---------------------------------------------------------------------------
+// Per-Gaussian splat record written by preprocess, read (gathered) by both
+// render passes: three 16-byte rows so a gather is three dwordx4 loads.
+//   r0 = (x_pix, y_pix, conic.a, conic.b)
+//   r1 = (conic.c, opacity_eff, 1/depth, bbox_x packed)
+//   r2 = (r, g, b, bbox_y packed)
+// bbox_* are the conservative pixel bounds of the alpha >= 1/255 footprint
+// (int16 lo | int16 hi << 16), used to skip whole waves (DESIGN.md "footprint
+// culling").  lo > hi means "never contributes".
+// ---------------------------------------------------------------------------
+struct SplatRec {
+    float4 r0, r1, r2;
+};
+
+__host__ __device__ inline size_t align_up(size_t x, size_t a = kAlign) { return (x + a - 1) / a * a; }
+
+// Bump allocator over a caller-provided chunk (the three opaque uint8 tensors of
+// the reference, CR/rasterizer_impl.h:26-90; contents are private to us).
+struct Carver {
+    char* base;
+    size_t off;
+    template <typename T>
+    T* take(size_t count) {
+        off = align_up(off);
+        T* p = reinterpret_cast<T*>(base ? base + off : nullptr);
+        off += count * sizeof(T);
+        return p;
+    }
+};
+
+// Geometry state: per Gaussian (P).
+struct GeomState {
+    float4* rec0;
+    float4* rec1;
+    float4* rec2;
+    uint32_t* depth_key;        // float bits of view-space z, 0xffffffff if culled
+    uint32_t* depth_key_sorted; // sort output (unused after sorting)
+    uint32_t* gid_by_rank;      // Gaussians in (depth, index) order
+    uint32_t* rank_of;          // inverse permutation
+    uint32_t* tiles_touched;    // per Gaussian (CR/forward.cu:350)
+    uint32_t* tiles_ranked;     // tiles_touched in rank order
+    unsigned long long* offsets;// inclusive scan of tiles_ranked (64-bit: overflow-checked)
+    uint8_t* clamped;           // SH clamp mask, 3 bits (CR/forward.cu:74-76)
+    uint32_t* status;           // device status word (prefiltered violation, ...)
+    void* sort_temp;
+    size_t sort_temp_bytes;
+    void* scan_temp;
+    size_t scan_temp_bytes;
+};
+
+// Image state: per pixel (N) and per tile.
+struct ImageState {
+    float* final_T;       // [N]
+    uint32_t* n_contrib;  // [N]
+    float* accum;         // [4][N]: colour r,g,b and inverse depth, without background
+    uint2* ranges;        // [tiles]
+};
+
+// Binning state: per instance (R).  Key type is 16-bit while tiles <= 65536.
+struct BinningState {
+    void* keys;             // unsorted tile ids (u16 or u32), emission order
+    void* keys_sorted;      // sorted tile ids
+    uint32_t* emit_gid;     // Gaussian of each emitted instance
+    uint32_t* e_sorted;     // emission index of each sorted instance
+    uint32_t* sorted_gid;   // Gaussian of each sorted instance
+    void* sort_temp;
+    size_t sort_temp_bytes;
+};
+
+// Per-instance gradient records (backward scratch), SoA so stores are aligned.
+struct GradRecs {
+    float4* a;  // (dcolor.r, dcolor.g, dcolor.b, dinvdepth)
+    float4* b;  // (dmean2D.x, dmean2D.y, dopacity_eff, dconic.b)
+    float2* c;  // (dconic.a, dconic.c)
+};
+
+// ---------------------------------------------------------------------------
+// Device math helpers (CR/auxiliary.h:43-117)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float3 xform_point_4x3(const float3& p, const float* m) {
+    return make_float3(m[0] * p.x + m[4] * p.y + m[8] * p.z + m[12], m[1] * p.x + m[5] * p.y + m[9] * p.z + m[13],
+                       m[2] * p.x + m[6] * p.y + m[10] * p.z + m[14]);
+}
+__device__ __forceinline__ float4 xform_point_4x4(const float3& p, const float* m) {
+    return make_float4(m[0] * p.x + m[4] * p.y + m[8] * p.z + m[12], m[1] * p.x + m[5] * p.y + m[9] * p.z + m[13],
+                       m[2] * p.x + m[6] * p.y + m[10] * p.z + m[14], m[3] * p.x + m[7] * p.y + m[11] * p.z + m[15]);
+}
+// ndc2Pix: the reference's literal 1.0 makes this a double expression (CR/auxiliary.h:45).
+__device__ __forceinline__ float ndc2pix(float v, int S) { return (float)((((double)v + 1.0) * S - 1.0) * 0.5); }
+
+// getRect (CR/auxiliary.h:49-59).  float->int conversion on gfx950 saturates like CUDA's.
+__device__ __forceinline__ void get_rect(float px, float py, int max_radius, uint32_t gx, uint32_t gy, uint2& rmin,
+                                         uint2& rmax) {
+    const float r = (float)max_radius;
+    int v;
+    v = max(0, (int)((px - r) / (float)kTile));
+    rmin.x = min(gx, (uint32_t)v);
+    v = max(0, (int)((py - r) / (float)kTile));
+    rmin.y = min(gy, (uint32_t)v);
+    v = max(0, (int)((((px + r) + (float)kTile) - 1.0f) / (float)kTile));
+    rmax.x = min(gx, (uint32_t)v);
+    v = max(0, (int)((((py + r) + (float)kTile) - 1.0f) / (float)kTile));
+    rmax.y = min(gy, (uint32_t)v);
+}
+
+__device__ __forceinline__ uint32_t pack_i16x2(int lo, int hi) {
+    lo = max(-32768, min(32767, lo));
+    hi = max(-32768, min(32767, hi));
+    return ((uint32_t)(uint16_t)(int16_t)lo) | ((uint32_t)(uint16_t)(int16_t)hi << 16);
+}
+__device__ __forceinline__ int unpack_lo(uint32_t v) { return (int)(int16_t)(uint16_t)(v & 0xffffu); }
+__device__ __forceinline__ int unpack_hi(uint32_t v) { return (int)(int16_t)(uint16_t)(v >> 16); }
+
+// Wave64 helpers.
+__device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
+
+template <int CTRL, int ROW_MASK, bool BOUND_ZERO>
+__device__ __forceinline__ float dpp_f32(float v) {
+    return __builtin_bit_cast(float,
+                              __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROW_MASK, 0xf, BOUND_ZERO));
+}
+
+// Full wave64 sum, valid in lane 63: Hillis-Steele prefix inside each 16-lane row
+// (row_shr 1,2,4,8 with zero fill), then row_bcast:15 / row_bcast:31 carry the row
+// totals upward.  Six VALU ops, no LDS traffic.
+__device__ __forceinline__ float wave_sum_to_lane63(float v) {
+    v += dpp_f32<0x111, 0xf, true>(v);
+    v += dpp_f32<0x112, 0xf, true>(v);
+    v += dpp_f32<0x114, 0xf, true>(v);
+    v += dpp_f32<0x118, 0xf, true>(v);
+    v += dpp_f32<0x142, 0xa, false>(v);
+    v += dpp_f32<0x143, 0xc, false>(v);
+    return v;
+}
+
+}  // namespace gsr

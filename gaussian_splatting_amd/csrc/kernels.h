@@ -1,0 +1,107 @@
+// kernels.h -- launch arguments and entry points shared by the .hip translation units.
+#pragma once
+
+#include "gsr_common.h"
+
+namespace gsr {
+
+struct PreprocessArgs {
+    int P, D, M, W, H;
+    const float* means3D;
+    const float* scales;
+    float scale_modifier;
+    const float* rotations;
+    const float* opacities;
+    const float* shs;
+    const float* cov3D_precomp;
+    const float* colors_precomp;
+    const float* viewmatrix;
+    const float* projmatrix;
+    const float* campos;
+    float tan_fovx, tan_fovy, focal_x, focal_y;
+    uint32_t gx, gy;
+    int prefiltered, antialiasing, footprint_cull;
+    int* radii;
+    GeomState geom;
+};
+
+struct RenderFwdArgs {
+    int W, H;
+    uint32_t gx, gy;
+    const uint2* ranges;
+    const uint32_t* sorted_gid;
+    const float4* rec0;
+    const float4* rec1;
+    const float4* rec2;
+    const float* bg;
+    float* out_color;
+    float* out_invdepth;
+    ImageState img;
+};
+
+struct RenderBwdArgs {
+    int W, H;
+    uint32_t gx, gy;
+    const uint2* ranges;
+    const uint32_t* sorted_gid;
+    const uint32_t* e_sorted;
+    const float4* rec0;
+    const float4* rec1;
+    const float4* rec2;
+    const float* bg;
+    const float* dL_dpix;       // [3,H,W]
+    const float* dL_dinvdepth;  // [H,W] or null
+    ImageState img;
+    GradRecs recs;
+};
+
+struct GaussBwdArgs {
+    int P, D, M, W, H;
+    const float* means3D;
+    const float* shs;
+    const float* opacities;
+    const float* scales;
+    const float* rotations;
+    const float* cov3D_precomp;
+    float scale_modifier;
+    const float* viewmatrix;
+    const float* projmatrix;
+    const float* campos;
+    float tan_fovx, tan_fovy, focal_x, focal_y;
+    int antialiasing;
+    const int* radii;
+    GeomState geom;
+    GradRecs recs;
+    int have_invdepth;
+    float* dL_dmean2D;    // [P,3]
+    float* dL_dconic;     // [P,4] or null
+    float* dL_dopacity;   // [P]
+    float* dL_dcolor;     // [P,3]
+    float* dL_dinvdepth;  // [P] or null
+    float* dL_dmean3D;    // [P,3]
+    float* dL_dcov3D;     // [P,6]
+    float* dL_dsh;        // [P,M,3] or null (M == 0)
+    float* dL_dscale;     // [P,3] or null
+    float* dL_drot;       // [P,4] or null
+};
+
+// preprocess.hip
+hipError_t launch_preprocess(const PreprocessArgs& a, hipStream_t stream);
+hipError_t launch_mark_visible(int P, const float* means3D, const float* view, bool* present, hipStream_t stream);
+// binning.hip
+size_t depth_sort_temp_bytes(int P);
+hipError_t depth_sort(GeomState& g, int P, hipStream_t stream);
+size_t scan_temp_bytes(int P);
+hipError_t rank_and_scan(GeomState& g, int P, hipStream_t stream);
+hipError_t launch_duplicate(int P, const GeomState& g, const int* radii, uint32_t gx, uint32_t gy,
+                            const BinningState& b, bool key16, hipStream_t stream);
+size_t tile_sort_temp_bytes(size_t R, bool key16);
+hipError_t tile_sort(BinningState& b, size_t R, unsigned end_bit, bool key16, hipStream_t stream);
+hipError_t launch_finalize(size_t R, const BinningState& b, uint2* ranges, bool key16, hipStream_t stream);
+// render.hip
+hipError_t launch_render_fwd(const RenderFwdArgs& a, hipStream_t stream);
+hipError_t launch_render_bwd(const RenderBwdArgs& a, hipStream_t stream);
+// backward.hip
+hipError_t launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t stream);
+
+}  // namespace gsr

@@ -1,0 +1,70 @@
+"""View-sharded data parallelism over GPUs.
+
+The reference trains on one GPU, one view per iteration (train.py:131-143).  Views
+are independent, so N ranks each render their own view with a replicated copy of
+the Gaussians, and exchange exactly one thing: the parameter gradients.  The six
+parameter groups of ``GaussianModel`` (``_xyz``, ``_features_dc``, ``_features_rest``,
+``_opacity``, ``_scaling``, ``_rotation``; scene/gaussian_model.py:235-242) are laid
+out back to back in one flat fp32 arena -- 59 floats per Gaussian at SH degree 3 --
+that the backward writes into directly, followed by ONE all-reduce over RCCL
+(backend "nccl" on ROCm).  Every rank then applies the same optimizer step, so the
+replicas stay identical without a broadcast.
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional
+
+import torch
+import torch.distributed as dist
+
+# block order inside the arena; shapes are per-Gaussian
+_BLOCKS = (("dL_dmeans3D", (3,)), ("dL_dsh", None), ("dL_dopacity", (1,)), ("dL_dscales", (3,)),
+           ("dL_drotations", (4,)))
+
+
+class GradArena:
+    """Flat gradient buffer with per-parameter views, reduced by a single collective."""
+
+    def __init__(self, P: int, M: int, device, dtype=torch.float32):
+        self.P, self.M = P, M
+        per = {"dL_dmeans3D": 3, "dL_dsh": 3 * M, "dL_dopacity": 1, "dL_dscales": 3, "dL_drotations": 4}
+        self.floats_per_gaussian = sum(per.values())
+        self.flat = torch.empty(P * self.floats_per_gaussian, device=device, dtype=dtype)
+        self._views: Dict[str, torch.Tensor] = {}
+        off = 0
+        for name, shape in _BLOCKS:
+            n = P * per[name]
+            shp = (P, M, 3) if name == "dL_dsh" else (P,) + shape
+            self._views[name] = self.flat[off:off + n].view(shp)
+            off += n
+
+    def views(self) -> Dict[str, torch.Tensor]:
+        """Output tensors for ``_C.rasterize_gaussians_backward(..., out=...)``."""
+        return self._views
+
+    def all_reduce(self, op=None, group: Optional[dist.ProcessGroup] = None, average: bool = False) -> None:
+        """Sum (or average) the arena over all ranks in one collective."""
+        if not dist.is_initialized() or dist.get_world_size(group) == 1:
+            return
+        dist.all_reduce(self.flat, op=op or dist.ReduceOp.SUM, group=group)
+        if average:
+            self.flat.div_(dist.get_world_size(group))
+
+    def split_features(self):
+        """(f_dc, f_rest) gradient views, matching GaussianModel._features_dc / _features_rest."""
+        sh = self._views["dL_dsh"]
+        return sh[:, :1, :], sh[:, 1:, :]
+
+
+def reduce_densification_stats(grad_norm_sum: torch.Tensor, denom: torch.Tensor, max_radii2D: torch.Tensor,
+                               group: Optional[dist.ProcessGroup] = None) -> None:
+    """Make densification statistics global (train.py:212-215, gaussian_model.py:643-654):
+    SUM of the screen-space gradient norms and their counts, MAX of the 2-D radii."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return
+    stats = torch.cat([grad_norm_sum.reshape(-1), denom.reshape(-1)])
+    dist.all_reduce(stats, op=dist.ReduceOp.SUM, group=group)
+    n = grad_norm_sum.numel()
+    grad_norm_sum.copy_(stats[:n].view_as(grad_norm_sum))
+    denom.copy_(stats[n:].view_as(denom))
+    dist.all_reduce(max_radii2D, op=dist.ReduceOp.MAX, group=group)

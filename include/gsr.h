@@ -1,0 +1,115 @@
+/*
+ * gsr.h -- C ABI of the MI355X (gfx950) differentiable Gaussian tile rasterizer.
+ *
+ * This is the drop-in boundary for the reference's native rasterizer
+ * (mango1118/gaussian_splatting, submodules/diff-gaussian-rasterization).  Each
+ * entry point replaces one C++ interface of the reference:
+ *
+ *   gsr_rasterize_forward   <- CudaRasterizer::Rasterizer::forward
+ *                              (cuda_rasterizer/rasterizer.h:31-58,
+ *                               cuda_rasterizer/rasterizer_impl.cu:227-370)
+ *   gsr_rasterize_backward  <- CudaRasterizer::Rasterizer::backward
+ *                              (cuda_rasterizer/rasterizer.h:60-91,
+ *                               cuda_rasterizer/rasterizer_impl.cu:374-479)
+ *   gsr_mark_visible        <- CudaRasterizer::Rasterizer::markVisible
+ *                              (cuda_rasterizer/rasterizer.h:23-29,
+ *                               cuda_rasterizer/rasterizer_impl.cu:169-181)
+ *
+ * and, one layer up, the three pybind functions of ext.cpp:15-19
+ * (rasterize_gaussians / rasterize_gaussians_backward / mark_visible), whose
+ * tensor handling lives in the Python host layer (gaussian_splatting_amd/_C.py).
+ *
+ * Conventions (same as the reference):
+ *  - every float array is a device pointer to contiguous fp32 data; an absent
+ *    optional input is NULL (the reference's data_ptr() == nullptr test);
+ *  - viewmatrix / projmatrix are 16 floats read column-major
+ *    (cuda_rasterizer/auxiliary.h:75-95);
+ *  - the three scratch buffers are obtained through allocation callbacks exactly
+ *    like the reference's std::function<char*(size_t)> resize functors
+ *    (rasterize_points.cu:29-43); their contents are private to this library and
+ *    must be passed back unchanged to gsr_rasterize_backward;
+ *  - all work is enqueued on `stream` (a hipStream_t; NULL = the default stream).
+ *    gsr_rasterize_forward synchronises that stream once, to learn the number of
+ *    tile instances (cuda_rasterizer/rasterizer_impl.cu:313).
+ *
+ * Every function returns 0 on success or a nonzero GSR_ERR_* code; the message
+ * of the last failure on the calling thread is available from gsr_last_error().
+ */
+#ifndef GSR_H_INCLUDED
+#define GSR_H_INCLUDED
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GSR_OK 0
+#define GSR_ERR_ARGUMENT 1      /* invalid argument (shape, size, null pointer) */
+#define GSR_ERR_HIP 2           /* a HIP runtime / kernel launch error */
+#define GSR_ERR_ALLOC 3         /* an allocation callback returned NULL */
+#define GSR_ERR_OVERFLOW 4      /* more than INT_MAX tile instances */
+#define GSR_ERR_PREFILTERED 5   /* prefiltered=1 but a point failed the frustum test */
+
+/* Scratch allocation callback: return a device pointer to at least `nbytes`
+ * bytes that stays valid until the matching backward call has returned.
+ * Replaces std::function<char*(size_t)> (rasterize_points.cu:29-43). */
+typedef void* (*gsr_alloc_fn)(void* ctx, size_t nbytes);
+
+/* Forward pass (CudaRasterizer::Rasterizer::forward).
+ * P Gaussians, active SH degree D, M SH coefficients per Gaussian (0 if shs is NULL).
+ * out_color [3,H,W], out_invdepth [1,H,W] and radii [P] are written for every
+ * element.  *num_rendered receives the number of (tile, Gaussian) instances. */
+int gsr_rasterize_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_alloc, void* binning_ctx,
+                          gsr_alloc_fn image_alloc, void* image_ctx, int P, int D, int M, const float* background,
+                          int width, int height, const float* means3D, const float* shs, const float* colors_precomp,
+                          const float* opacities, const float* scales, float scale_modifier, const float* rotations,
+                          const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix,
+                          const float* cam_pos, float tan_fovx, float tan_fovy, int prefiltered, float* out_color,
+                          float* out_invdepth, int antialiasing, int* radii, int debug, void* stream,
+                          int* num_rendered);
+
+/* Backward pass (CudaRasterizer::Rasterizer::backward).
+ * R = num_rendered from the forward; geom/binning/image buffers are the ones the
+ * forward's callbacks returned.  dL_dinvdepths ([1,H,W]) may be NULL, in which
+ * case dL_dinvdepth must be NULL too.  dL_dconic ([P,4]) may be NULL.  Every
+ * element of every non-NULL output is written (no pre-zeroing needed).
+ * `scratch_alloc` provides 40 bytes per tile instance for the per-instance
+ * gradient records. */
+int gsr_rasterize_backward(int P, int D, int M, int R, const float* background, int width, int height,
+                           const float* means3D, const float* shs, const float* colors_precomp,
+                           const float* opacities, const float* scales, float scale_modifier, const float* rotations,
+                           const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix,
+                           const float* campos, float tan_fovx, float tan_fovy, const int* radii, void* geom_buffer,
+                           void* binning_buffer, void* image_buffer, const float* dL_dpix, const float* dL_dinvdepths,
+                           float* dL_dmean2D, float* dL_dconic, float* dL_dopacity, float* dL_dcolor,
+                           float* dL_dinvdepth, float* dL_dmean3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscale,
+                           float* dL_drot, int antialiasing, int debug, gsr_alloc_fn scratch_alloc,
+                           void* scratch_ctx, void* stream);
+
+/* Frustum test, view-space z > 0.2 (CudaRasterizer::Rasterizer::markVisible).
+ * `present` is P bytes (bool). */
+int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
+                     unsigned char* present, void* stream);
+
+/* Message of the last error on this thread ("" if none). */
+const char* gsr_last_error(void);
+
+/* Library version string, e.g. "gsr 0.1.0 gfx950". */
+const char* gsr_version(void);
+
+/* Per-stage device timing with hipEvents recorded on the launch stream.
+ * enable=1 turns it on (it adds one event pair per stage).  collect() waits for
+ * the recorded events and adds their elapsed times to running per-stage totals;
+ * it returns the number of stages and fills up to max_stages totals (ms) and
+ * call counts.  Stage names come from gsr_profile_stage_name(). */
+int gsr_profile_enable(int enable);
+int gsr_profile_collect(double* total_ms, long long* calls, int max_stages);
+void gsr_profile_reset(void);
+const char* gsr_profile_stage_name(int stage);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GSR_H_INCLUDED */

@@ -1,0 +1,39 @@
+#!/bin/bash
+# One GPU-box session: parity tests, bench, rocprofv3 kernel trace.  Stops at the
+# first crash / timeout (exit codes other than 0 = pass and 1 = test failures).
+# Usage: scripts/gpu_session.sh TAG [tests] [bench] [prof] [pmc] [full]
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+ROOT=$(pwd)
+TAG=$1; shift
+OUT=$ROOT/gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+echo "host: $(hostname) cpus=$(nproc)" > "$OUT/host.txt"
+ok() { local rc=$1; [ "$rc" -eq 0 ] || [ "$rc" -eq 1 ]; }
+for stage in "$@"; do
+  case $stage in
+    tests)
+      timeout -k 10 900 python -m pytest tests -m gpu -q -x -k "not fullsize" > "$OUT/pytest.log" 2>&1; rc=$?
+      echo "tests rc=$rc"; tail -5 "$OUT/pytest.log"; ok $rc || exit $rc ;;
+    full)
+      timeout -k 10 900 python -m pytest tests -m gpu -q -k "fullsize" > "$OUT/pytest_full.log" 2>&1; rc=$?
+      echo "full rc=$rc"; tail -5 "$OUT/pytest_full.log"; ok $rc || exit $rc ;;
+    bench)
+      timeout -k 10 600 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"; rc=$?
+      echo "bench rc=$rc"; cat "$OUT/bench.json"; tail -3 "$OUT/bench.err"; [ $rc -eq 0 ] || exit $rc ;;
+    benchquick)
+      timeout -k 10 600 python bench.py --no-cpu-baseline > "$OUT/bench.json" 2> "$OUT/bench.err"; rc=$?
+      echo "bench rc=$rc"; cat "$OUT/bench.json"; tail -3 "$OUT/bench.err"; [ $rc -eq 0 ] || exit $rc ;;
+    prof)
+      (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
+        python3 "$ROOT/bench.py" --steps 10 --warmup 2 --no-cpu-baseline > "$OUT/prof.log" 2>&1); rc=$?
+      echo "prof rc=$rc"; tail -3 "$OUT/prof.log"; [ $rc -eq 0 ] || exit $rc ;;
+    pmc)
+      for ctr in "FETCH_SIZE" "WRITE_SIZE"; do
+        (cd /tmp && timeout -k 10 600 rocprofv3 --pmc $ctr --output-format csv -d "$OUT/pmc_$ctr" -o run -- \
+          python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/pmc_$ctr.log" 2>&1); rc=$?
+        echo "pmc $ctr rc=$rc"; tail -2 "$OUT/pmc_$ctr.log"; [ $rc -eq 0 ] || exit $rc
+      done ;;
+  esac
+done
