@@ -53,6 +53,7 @@ def algorithmic_bytes(stage: str, P: int, I: int, W: int, H: int, K: int) -> flo
         # gather 44 B per instance; read 24 B per pixel; write the per-Gaussian accumulators (10 floats)
         "render_bwd": 44 * I + 24 * N + 40 * P,
         # read accumulators 40 + preprocess inputs 48 + 12K; write grads 56 + 12K
+        "gauss_reduce": 40 * I + 40 * P,
         "gauss_bwd": (40 + 48 + 12 * K + 56 + 12 * K) * P,
     }
     return float(table.get(stage, 0))

@@ -45,11 +45,12 @@ enum Stage {
     ST_FINALIZE,
     ST_RENDER_FWD,
     ST_RENDER_BWD,
+    ST_GAUSS_REDUCE,
     ST_GAUSS_BWD,
     ST_COUNT
 };
 const char* kStageNames[ST_COUNT] = {"preprocess", "depth_sort", "scan",       "duplicate", "tile_sort",
-                                     "finalize",   "render_fwd", "render_bwd", "gauss_bwd"};
+                                     "finalize",   "render_fwd", "render_bwd", "gauss_reduce", "gauss_bwd"};
 
 struct Profiler {
     bool on = false;
@@ -156,22 +157,23 @@ gsr::BinningState carve_binning(char* base, size_t R, bool key16, size_t* total)
     b.keys_sorted = c.take<char>(R * ks);
     b.emit_gid = c.take<uint32_t>(R);
     b.e_sorted = c.take<uint32_t>(R);
-    b.sorted_gid = c.take<uint32_t>(R);
     b.sort_temp_bytes = R ? tile_sort_temp_bytes(R, key16) : 0;
     b.sort_temp = c.take<char>(b.sort_temp_bytes);
     *total = align_up(c.off);
     return b;
 }
 
-gsr::GradRecs carve_recs(char* base, size_t R, size_t* total) {
+// Backward scratch: R per-instance records followed by P per-rank sums.
+void carve_recs(char* base, size_t R, size_t P, gsr::GradRecs* recs, gsr::GradRecs* sums, size_t* total) {
     using namespace gsr;
     Carver c{base, 0};
-    GradRecs r{};
-    r.a = c.take<float4>(R);
-    r.b = c.take<float4>(R);
-    r.c = c.take<float2>(R);
+    recs->a = c.take<float4>(R);
+    recs->b = c.take<float4>(R);
+    recs->c = c.take<float2>(R);
+    sums->a = c.take<float4>(P);
+    sums->b = c.take<float4>(P);
+    sums->c = c.take<float2>(P);
     *total = align_up(c.off);
-    return r;
 }
 
 void* call_alloc(gsr_alloc_fn fn, void* ctx, size_t bytes) {
@@ -355,7 +357,7 @@ int gsr_rasterize_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn 
     {
         StageScope sc(ST_RENDER_FWD, stream);
         RenderFwdArgs ra{};
-        ra.W = width; ra.H = height; ra.gx = gx; ra.gy = gy; ra.ranges = img.ranges; ra.sorted_gid = bin.sorted_gid;
+        ra.W = width; ra.H = height; ra.gx = gx; ra.gy = gy; ra.ranges = img.ranges; ra.emit_gid = bin.emit_gid; ra.e_sorted = bin.e_sorted;
         ra.rec0 = geom.rec0; ra.rec1 = geom.rec1; ra.rec2 = geom.rec2; ra.bg = background;
         ra.out_color = out_color; ra.out_invdepth = out_invdepth; ra.img = img;
         HIP_TRY(launch_render_fwd(ra, stream), "render_fwd");
@@ -402,20 +404,26 @@ int gsr_rasterize_backward(int P, int D, int M, int R, const float* background, 
     ImageState img = carve_image((char*)image_buffer, width, height, tiles, &tmp);
     BinningState bin = carve_binning((char*)binning_buffer, (size_t)R, key16, &tmp);
     size_t rec_bytes = 0;
-    carve_recs(nullptr, (size_t)R, &rec_bytes);
+    GradRecs recs{}, sums{};
+    carve_recs(nullptr, (size_t)R, (size_t)P, &recs, &sums, &rec_bytes);
     char* rbase = (char*)call_alloc(scratch_alloc, scratch_ctx, rec_bytes);
     if (!rbase) return fail(GSR_ERR_ALLOC, "rasterize_backward: scratch allocation failed");
-    GradRecs recs = carve_recs(rbase, (size_t)R, &rec_bytes);
+    carve_recs(rbase, (size_t)R, (size_t)P, &recs, &sums, &rec_bytes);
 
     if (R > 0) {
         StageScope sc(ST_RENDER_BWD, stream);
         RenderBwdArgs ra{};
-        ra.W = width; ra.H = height; ra.gx = gx; ra.gy = gy; ra.ranges = img.ranges; ra.sorted_gid = bin.sorted_gid;
+        ra.W = width; ra.H = height; ra.gx = gx; ra.gy = gy; ra.ranges = img.ranges; ra.emit_gid = bin.emit_gid;
         ra.e_sorted = bin.e_sorted; ra.rec0 = geom.rec0; ra.rec1 = geom.rec1; ra.rec2 = geom.rec2;
         ra.bg = background; ra.dL_dpix = dL_dpix; ra.dL_dinvdepth = dL_dinvdepths; ra.img = img; ra.recs = recs;
         HIP_TRY(launch_render_bwd(ra, stream), "render_bwd");
     }
     if (int rc = check_debug(debug, stream, "render_bwd")) return rc;
+    {
+        StageScope sc(ST_GAUSS_REDUCE, stream);
+        HIP_TRY(launch_gauss_reduce(P, geom.offsets, recs, sums, stream), "gauss_reduce");
+    }
+    if (int rc = check_debug(debug, stream, "gauss_reduce")) return rc;
     {
         StageScope sc(ST_GAUSS_BWD, stream);
         GaussBwdArgs ga{};
@@ -424,7 +432,7 @@ int gsr_rasterize_backward(int P, int D, int M, int R, const float* background, 
         ga.rotations = rotations; ga.cov3D_precomp = cov3D_precomp; ga.scale_modifier = scale_modifier;
         ga.viewmatrix = viewmatrix; ga.projmatrix = projmatrix; ga.campos = campos;
         ga.tan_fovx = tan_fovx; ga.tan_fovy = tan_fovy; ga.focal_x = focal_x; ga.focal_y = focal_y;
-        ga.antialiasing = antialiasing; ga.radii = radii; ga.geom = geom; ga.recs = recs;
+        ga.antialiasing = antialiasing; ga.radii = radii; ga.geom = geom; ga.sums = sums;
         ga.have_invdepth = dL_dinvdepths != nullptr;
         ga.dL_dmean2D = dL_dmean2D; ga.dL_dconic = dL_dconic; ga.dL_dopacity = dL_dopacity; ga.dL_dcolor = dL_dcolor;
         ga.dL_dinvdepth = dL_dinvdepth; ga.dL_dmean3D = dL_dmean3D; ga.dL_dcov3D = dL_dcov3D;

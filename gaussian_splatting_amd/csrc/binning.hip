@@ -18,17 +18,22 @@
 
 namespace gsr {
 
+// Always take the onesweep radix path: rocPRIM's default switches to block sort +
+// merge sort up to 2^20 items, which costs 20+ launches at P = 1M.
+using SortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                              rocprim::default_config, 0>;
+
 // ---- 1. depth pre-sort ------------------------------------------------------
 size_t depth_sort_temp_bytes(int P) {
     size_t bytes = 0;
-    (void)rocprim::radix_sort_pairs(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+    (void)rocprim::radix_sort_pairs<SortConfig>(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
                                     rocprim::counting_iterator<uint32_t>(0), (uint32_t*)nullptr, (size_t)P, 0, 32);
     return bytes;
 }
 
 hipError_t depth_sort(GeomState& g, int P, hipStream_t stream) {
     size_t bytes = g.sort_temp_bytes;
-    return rocprim::radix_sort_pairs(g.sort_temp, bytes, g.depth_key, g.depth_key_sorted,
+    return rocprim::radix_sort_pairs<SortConfig>(g.sort_temp, bytes, g.depth_key, g.depth_key_sorted,
                                      rocprim::counting_iterator<uint32_t>(0), g.gid_by_rank, (size_t)P, 0, 32, stream);
 }
 
@@ -143,10 +148,10 @@ hipError_t launch_duplicate(int P, const GeomState& g, const int* radii, uint32_
 size_t tile_sort_temp_bytes(size_t R, bool key16) {
     size_t bytes = 0;
     if (key16)
-        (void)rocprim::radix_sort_pairs(nullptr, bytes, (const uint16_t*)nullptr, (uint16_t*)nullptr,
+        (void)rocprim::radix_sort_pairs<SortConfig>(nullptr, bytes, (const uint16_t*)nullptr, (uint16_t*)nullptr,
                                   rocprim::counting_iterator<uint32_t>(0), (uint32_t*)nullptr, R, 0, 16);
     else
-        (void)rocprim::radix_sort_pairs(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+        (void)rocprim::radix_sort_pairs<SortConfig>(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
                                         rocprim::counting_iterator<uint32_t>(0), (uint32_t*)nullptr, R, 0, 32);
     return bytes;
 }
@@ -154,20 +159,17 @@ size_t tile_sort_temp_bytes(size_t R, bool key16) {
 hipError_t tile_sort(BinningState& b, size_t R, unsigned end_bit, bool key16, hipStream_t stream) {
     size_t bytes = b.sort_temp_bytes;
     if (key16)
-        return rocprim::radix_sort_pairs(b.sort_temp, bytes, (const uint16_t*)b.keys, (uint16_t*)b.keys_sorted,
+        return rocprim::radix_sort_pairs<SortConfig>(b.sort_temp, bytes, (const uint16_t*)b.keys, (uint16_t*)b.keys_sorted,
                                          rocprim::counting_iterator<uint32_t>(0), b.e_sorted, R, 0, end_bit, stream);
-    return rocprim::radix_sort_pairs(b.sort_temp, bytes, (const uint32_t*)b.keys, (uint32_t*)b.keys_sorted,
+    return rocprim::radix_sort_pairs<SortConfig>(b.sort_temp, bytes, (const uint32_t*)b.keys, (uint32_t*)b.keys_sorted,
                                      rocprim::counting_iterator<uint32_t>(0), b.e_sorted, R, 0, end_bit, stream);
 }
 
-// ---- 5. sorted Gaussian ids + per-tile [start, end) (identifyTileRanges, CR/rasterizer_impl.cu:132-164)
+// ---- 5. per-tile [start, end) (identifyTileRanges, CR/rasterizer_impl.cu:132-164)
 template <typename KeyT>
-__global__ void finalize_kernel(uint32_t R, const KeyT* __restrict__ keys_sorted, const uint32_t* __restrict__ e_sorted,
-                                const uint32_t* __restrict__ emit_gid, uint32_t* __restrict__ sorted_gid,
-                                uint2* __restrict__ ranges) {
+__global__ void finalize_kernel(uint32_t R, const KeyT* __restrict__ keys_sorted, uint2* __restrict__ ranges) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= R) return;
-    sorted_gid[i] = emit_gid[e_sorted[i]];
     const uint32_t cur = keys_sorted[i];
     if (i == 0) {
         ranges[cur].x = 0;
@@ -185,10 +187,10 @@ hipError_t launch_finalize(size_t R, const BinningState& b, uint2* ranges, bool 
     const dim3 grid((unsigned)((R + 255) / 256)), block(256);
     if (key16)
         hipLaunchKernelGGL(finalize_kernel<uint16_t>, grid, block, 0, stream, (uint32_t)R,
-                           (const uint16_t*)b.keys_sorted, b.e_sorted, b.emit_gid, b.sorted_gid, ranges);
+                           (const uint16_t*)b.keys_sorted, ranges);
     else
         hipLaunchKernelGGL(finalize_kernel<uint32_t>, grid, block, 0, stream, (uint32_t)R,
-                           (const uint32_t*)b.keys_sorted, b.e_sorted, b.emit_gid, b.sorted_gid, ranges);
+                           (const uint32_t*)b.keys_sorted, ranges);
     return hipGetLastError();
 }
 

@@ -90,8 +90,7 @@ struct BinningState {
     void* keys;             // unsorted tile ids (u16 or u32), emission order
     void* keys_sorted;      // sorted tile ids
     uint32_t* emit_gid;     // Gaussian of each emitted instance
-    uint32_t* e_sorted;     // emission index of each sorted instance
-    uint32_t* sorted_gid;   // Gaussian of each sorted instance
+    uint32_t* e_sorted;     // emission index of each sorted instance (Gaussian = emit_gid[e])
     void* sort_temp;
     size_t sort_temp_bytes;
 };

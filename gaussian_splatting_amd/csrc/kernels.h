@@ -29,7 +29,8 @@ struct RenderFwdArgs {
     int W, H;
     uint32_t gx, gy;
     const uint2* ranges;
-    const uint32_t* sorted_gid;
+    const uint32_t* e_sorted;
+    const uint32_t* emit_gid;
     const float4* rec0;
     const float4* rec1;
     const float4* rec2;
@@ -43,8 +44,8 @@ struct RenderBwdArgs {
     int W, H;
     uint32_t gx, gy;
     const uint2* ranges;
-    const uint32_t* sorted_gid;
     const uint32_t* e_sorted;
+    const uint32_t* emit_gid;
     const float4* rec0;
     const float4* rec1;
     const float4* rec2;
@@ -71,7 +72,7 @@ struct GaussBwdArgs {
     int antialiasing;
     const int* radii;
     GeomState geom;
-    GradRecs recs;
+    GradRecs sums;  // per depth rank: summed render gradients
     int have_invdepth;
     float* dL_dmean2D;    // [P,3]
     float* dL_dconic;     // [P,4] or null
@@ -102,6 +103,8 @@ hipError_t launch_finalize(size_t R, const BinningState& b, uint2* ranges, bool 
 hipError_t launch_render_fwd(const RenderFwdArgs& a, hipStream_t stream);
 hipError_t launch_render_bwd(const RenderBwdArgs& a, hipStream_t stream);
 // backward.hip
+hipError_t launch_gauss_reduce(int P, const unsigned long long* offsets, const GradRecs& recs, const GradRecs& sums,
+                               hipStream_t stream);
 hipError_t launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t stream);
 
 }  // namespace gsr

@@ -78,7 +78,7 @@ __global__ void __launch_bounds__(64) render_fwd_kernel(RenderFwdArgs a) {
     for (int b0 = 0; b0 < n && alive; b0 += kBatch) {
         uint32_t qm = 0;
         if (b0 + lane < n) {
-            const uint32_t g = a.sorted_gid[range.x + b0 + lane];
+            const uint32_t g = a.emit_gid[a.e_sorted[range.x + b0 + lane]];
             const float4 v0 = a.rec0[g], v1 = a.rec1[g], v2 = a.rec2[g];
             qm = quad_bits(v1, v2, tile_x0, tile_y0);
             s_r0[lane] = v0;
@@ -205,7 +205,7 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a) {
         }
         uint32_t qm = 0;
         if (has) {
-            const uint32_t g = a.sorted_gid[range.x + b0 + lane];
+            const uint32_t g = a.emit_gid[e];
             const float4 v0 = a.rec0[g], v1 = a.rec1[g], v2 = a.rec2[g];
             qm = quad_bits(v1, v2, tile_x0, tile_y0);
             s_r0[lane] = v0;
