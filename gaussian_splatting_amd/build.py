@@ -33,41 +33,55 @@ def _newest_input_mtime() -> float:
     return max(os.path.getmtime(f) for f in files)
 
 
-def _compile(src: str) -> str:
-    obj = os.path.join(OBJ, src.replace(".hip", ".o"))
-    cmd = [HIPCC, *CXXFLAGS, "-c", os.path.join(CSRC, src), "-o", obj]
+# Per-file flags.  The SLP vectorizer packs adjacent fp32 ops into v_pk_*_f32 plus
+# v_mov shuffles; on gfx950 packed fp32 is not faster than two plain ops
+# (MI355X_MICROARCH.md, "price of one filler"), so the VALU-bound kernels opt out.
+FILE_FLAGS = {"render.hip": ["-fno-slp-vectorize"], "preprocess.hip": ["-fno-slp-vectorize"]}
+
+
+def _compile(src: str, objdir: str = OBJ, extra=()) -> str:
+    obj = os.path.join(objdir, src.replace(".hip", ".o"))
+    cmd = [HIPCC, *CXXFLAGS, *FILE_FLAGS.get(src, []), *extra, "-c", os.path.join(CSRC, src), "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
     return obj
 
 
-def build(force: bool = False, jobs: int = 5, verbose: bool = True) -> str:
-    """Compile every HIP source for gfx950 and link libgsr.so; returns the library path."""
-    if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= _newest_input_mtime():
-        return LIB
-    os.makedirs(OBJ, exist_ok=True)
+def build(force: bool = False, jobs: int = 5, verbose: bool = True, variant: str = "", extra=()) -> str:
+    """Compile every HIP source for gfx950 and link libgsr.so; returns the library path.
+
+    ``variant``/``extra`` build a side library ``libgsr_<variant>.so`` with extra compiler
+    flags (for A/B measurements; select it at run time with GSR_LIBRARY)."""
+    lib = LIB if not variant else os.path.join(LIB_DIR, f"libgsr_{variant}.so")
+    objdir = OBJ if not variant else os.path.join(OBJ, variant)
+    if not force and os.path.exists(lib) and os.path.getmtime(lib) >= _newest_input_mtime():
+        return lib
+    os.makedirs(objdir, exist_ok=True)
     os.makedirs(LIB_DIR, exist_ok=True)
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-        objs = list(ex.map(_compile, SOURCES))
-    tmp = LIB + ".tmp"
+        objs = list(ex.map(lambda f: _compile(f, objdir, extra), SOURCES))
+    LIB_OUT = lib
+    tmp = LIB_OUT + ".tmp"
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
-    os.replace(tmp, LIB)
+    os.replace(tmp, LIB_OUT)
     if verbose:
-        print(f"[gsr] built {LIB}")
-    return LIB
+        print(f"[gsr] built {LIB_OUT}")
+    return LIB_OUT
 
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--jobs", type=int, default=5)
+    ap.add_argument("--variant", default="")
+    ap.add_argument("--cflags", default="")
     args = ap.parse_args()
     try:
-        build(force=args.force, jobs=args.jobs)
+        build(force=args.force, jobs=args.jobs, variant=args.variant, extra=tuple(args.cflags.split()))
     except RuntimeError as e:
         print(e, file=sys.stderr)
         sys.exit(1)

@@ -161,4 +161,13 @@ __device__ __forceinline__ float wave_sum_to_lane63(float v) {
     return v;
 }
 
+// Sum over each 16-lane row, valid in lanes 15, 31, 47 and 63 (four DPP ops).
+__device__ __forceinline__ float row_sum_to_lane15(float v) {
+    v += dpp_f32<0x111, 0xf, true>(v);
+    v += dpp_f32<0x112, 0xf, true>(v);
+    v += dpp_f32<0x114, 0xf, true>(v);
+    v += dpp_f32<0x118, 0xf, true>(v);
+    return v;
+}
+
 }  // namespace gsr

@@ -34,6 +34,10 @@ namespace gsr {
 
 constexpr int kBatch = 64;  // list entries staged per round (one per lane)
 
+#ifndef GSR_ROWRED
+#define GSR_ROWRED 0
+#endif
+
 // Quadrant mask of one splat's footprint box inside the tile at (tile_x0, tile_y0).
 __device__ __forceinline__ uint32_t quad_bits(float4 v1, float4 v2, int tile_x0, int tile_y0) {
     const uint32_t bx = __float_as_uint(v1.w), by = __float_as_uint(v2.w);
@@ -96,28 +100,25 @@ __global__ void __launch_bounds__(64) render_fwd_kernel(RenderFwdArgs a) {
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 if (!(m & (1u << q))) continue;  // uniform: footprint misses this quadrant
-                if (!done[q]) {
-                    const float dx = v0.x - (pxf0 + (float)((q & 1) * 8));
-                    const float dy = v0.y - (pyf0 + (float)((q >> 1) * 8));
-                    const float power = -0.5f * (v0.z * dx * dx + v1.x * dy * dy) - v0.w * dx * dy;
-                    if (power <= 0.0f) {
-                        const float alpha = fminf(0.99f, v1.y * __expf(power));
-                        if (alpha >= 1.0f / 255.0f) {
-                            const float test_T = T[q] * (1.f - alpha);
-                            if (test_T < 0.0001f) {
-                                done[q] = true;
-                            } else {
-                                const float w = alpha * T[q];
-                                C0[q] += v2.x * w;
-                                C1[q] += v2.y * w;
-                                C2[q] += v2.z * w;
-                                D[q] += v1.z * w;
-                                T[q] = test_T;
-                                last[q] = pos1;
-                            }
-                        }
-                    }
-                }
+                // The reference's three tests become predicates (power is clamped to <= 0 before
+                // exp so skipped lanes stay finite); the update runs only if some lane passes.
+                const float dx = v0.x - (pxf0 + (float)((q & 1) * 8));
+                const float dy = v0.y - (pyf0 + (float)((q >> 1) * 8));
+                const float power = -0.5f * (v0.z * dx * dx + v1.x * dy * dy) - v0.w * dx * dy;
+                const float alpha = fminf(0.99f, v1.y * __expf(fminf(power, 0.f)));
+                const bool hit = !done[q] && power <= 0.0f && alpha >= 1.0f / 255.0f;
+                if (!__any(hit)) continue;  // uniform
+                const float test_T = T[q] * (1.f - alpha);
+                const bool term = hit && test_T < 0.0001f;  // CR/forward.cu:477-482: ends the pixel, not added
+                const bool add = hit && !term;
+                done[q] = done[q] || term;
+                const float w = add ? alpha * T[q] : 0.f;
+                C0[q] += v2.x * w;
+                C1[q] += v2.y * w;
+                C2[q] += v2.z * w;
+                D[q] += v1.z * w;
+                T[q] = add ? test_T : T[q];
+                last[q] = add ? pos1 : last[q];
                 if (__all(done[q])) alive &= ~(1u << q);
             }
         }
@@ -158,7 +159,13 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a) {
     const int lx = lane & 7, ly = lane >> 3;
 
     __shared__ float4 s_r0[kBatch], s_r1[kBatch], s_r2[kBatch];
+#if GSR_ROWRED
+    // per entry: four 16-lane row partials of the 10 sums (12 floats each), padded stride
+    constexpr int kPart = 52;
+    __shared__ __attribute__((aligned(16))) float s_part[kBatch * kPart];
+#else
     __shared__ float4 s_acc[kBatch][3];  // per entry: 10 reduced sums (+2 pad)
+#endif
 
     const size_t N = (size_t)a.W * a.H;
     float T[4], gB[4], g0[4], g1[4], g2[4], gi[4], bgt[4];
@@ -228,38 +235,54 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a) {
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 if (!(m & (1u << q))) continue;  // uniform
-                if (pos < nc[q]) {
-                    const float dx = v0.x - (pxf0 + (float)((q & 1) * 8));
-                    const float dy = v0.y - (pyf0 + (float)((q >> 1) * 8));
-                    const float power = -0.5f * (v0.z * dx * dx + v1.x * dy * dy) - v0.w * dx * dy;
-                    if (power <= 0.0f) {
-                        const float G = __expf(power);
-                        const float alpha = fminf(0.99f, v1.y * G);
-                        if (alpha >= 1.0f / 255.0f) {
-                            contrib = true;
-                            const float w = alpha * T[q];
-                            const float s = g0[q] * v2.x + g1[q] * v2.y + g2[q] * v2.z + gi[q] * v1.z;
-                            gB[q] -= w * s;  // now dL/dpix . (colour strictly behind this entry)
-                            const float one_m_a = 1.f - alpha;
-                            const float dLda = T[q] * s - (gB[q] + bgt[q]) * __builtin_amdgcn_rcpf(one_m_a);
-                            const float u = dLda * G;
-                            r0 += w * g0[q];
-                            r1 += w * g1[q];
-                            r2 += w * g2[q];
-                            r3 += w * gi[q];
-                            const float udx = u * dx, udy = u * dy;
-                            r4 += udx;
-                            r5 += udy;
-                            r6 += udx * dx;
-                            r7 += udx * dy;
-                            r8 += udy * dy;
-                            r9 += u;
-                            T[q] *= one_m_a;
-                        }
-                    }
-                }
+                // Same tests as the forward, as predicates; the gradient work runs only if some
+                // lane of the slot passes them.
+                const float dx = v0.x - (pxf0 + (float)((q & 1) * 8));
+                const float dy = v0.y - (pyf0 + (float)((q >> 1) * 8));
+                const float power = -0.5f * (v0.z * dx * dx + v1.x * dy * dy) - v0.w * dx * dy;
+                const float G = __expf(fminf(power, 0.f));
+                const float alpha = fminf(0.99f, v1.y * G);
+                const bool hit = pos < nc[q] && power <= 0.0f && alpha >= 1.0f / 255.0f;
+                if (!__any(hit)) continue;  // uniform
+                contrib = true;
+                const float w = hit ? alpha * T[q] : 0.f;
+                const float sdot = g0[q] * v2.x + g1[q] * v2.y + g2[q] * v2.z + gi[q] * v1.z;
+                gB[q] -= w * sdot;  // now dL/dpix . (colour strictly behind this entry)
+                const float one_m_a = 1.f - alpha;
+                const float dLda = T[q] * sdot - (gB[q] + bgt[q]) * __builtin_amdgcn_rcpf(one_m_a);
+                const float u = hit ? dLda * G : 0.f;
+                r0 += w * g0[q];
+                r1 += w * g1[q];
+                r2 += w * g2[q];
+                r3 += w * gi[q];
+                const float udx = u * dx, udy = u * dy;
+                r4 += udx;
+                r5 += udy;
+                r6 += udx * dx;
+                r7 += udx * dy;
+                r8 += udy * dy;
+                r9 += u;
+                T[q] = hit ? T[q] * one_m_a : T[q];
             }
-            if (__any(contrib)) {  // uniform
+            if (contrib) {  // uniform
+#if GSR_ROWRED
+                r0 = row_sum_to_lane15(r0);
+                r1 = row_sum_to_lane15(r1);
+                r2 = row_sum_to_lane15(r2);
+                r3 = row_sum_to_lane15(r3);
+                r4 = row_sum_to_lane15(r4);
+                r5 = row_sum_to_lane15(r5);
+                r6 = row_sum_to_lane15(r6);
+                r7 = row_sum_to_lane15(r7);
+                r8 = row_sum_to_lane15(r8);
+                r9 = row_sum_to_lane15(r9);
+                if ((lane & 15) == 15) {
+                    float4* p = reinterpret_cast<float4*>(&s_part[j * kPart + (lane >> 4) * 12]);
+                    p[0] = make_float4(r0, r1, r2, r3);
+                    p[1] = make_float4(r4, r5, r6, r7);
+                    p[2] = make_float4(r8, r9, 0.f, 0.f);
+                }
+#else
                 r0 = wave_sum_to_lane63(r0);
                 r1 = wave_sum_to_lane63(r1);
                 r2 = wave_sum_to_lane63(r2);
@@ -275,6 +298,7 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a) {
                     s_acc[j][1] = make_float4(r4, r5, r6, r7);
                     s_acc[j][2] = make_float4(r8, r9, 0.f, 0.f);
                 }
+#endif
                 written |= 1ull << j;
             }
         }
@@ -283,7 +307,19 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a) {
             float4 ra = make_float4(0.f, 0.f, 0.f, 0.f), rb = ra;
             float2 rc = make_float2(0.f, 0.f);
             if ((written >> lane) & 1ull) {
+#if GSR_ROWRED
+                const float4* p = reinterpret_cast<const float4*>(&s_part[lane * kPart]);
+                float4 A = p[0], B = p[1], Cc = p[2];
+#pragma unroll
+                for (int rr = 1; rr < 4; rr++) {  // fixed order: deterministic
+                    const float4 a4 = p[3 * rr], b4 = p[3 * rr + 1], c4 = p[3 * rr + 2];
+                    A.x += a4.x; A.y += a4.y; A.z += a4.z; A.w += a4.w;
+                    B.x += b4.x; B.y += b4.y; B.z += b4.z; B.w += b4.w;
+                    Cc.x += c4.x; Cc.y += c4.y;
+                }
+#else
                 const float4 A = s_acc[lane][0], B = s_acc[lane][1], Cc = s_acc[lane][2];
+#endif
                 const float4 v0 = s_r0[lane], v1 = s_r1[lane];
                 const float o = v1.y, ca = v0.z, cb = v0.w, cc = v1.x;
                 // dL/dmean2D in NDC units (x 0.5 W, 0.5 H, CR/backward.cu:509-510,600-601);

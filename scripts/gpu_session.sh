@@ -25,6 +25,14 @@ for stage in "$@"; do
     benchquick)
       timeout -k 10 600 python bench.py --no-cpu-baseline > "$OUT/bench.json" 2> "$OUT/bench.err"; rc=$?
       echo "bench rc=$rc"; cat "$OUT/bench.json"; tail -3 "$OUT/bench.err"; [ $rc -eq 0 ] || exit $rc ;;
+    variants)
+      for lib in gaussian_splatting_amd/lib/libgsr_*.so; do
+        v=$(basename $lib .so)
+        GSR_LIBRARY=$ROOT/$lib timeout -k 10 600 python -m pytest tests/test_gpu_parity.py -m gpu -q -x > "$OUT/pytest_$v.log" 2>&1; rc=$?
+        echo "variant $v tests rc=$rc: $(tail -1 $OUT/pytest_$v.log)"; ok $rc || exit $rc
+        GSR_LIBRARY=$ROOT/$lib timeout -k 10 300 python bench.py --no-cpu-baseline --steps 30 > "$OUT/bench_$v.json" 2> "$OUT/bench_$v.err"; rc=$?
+        echo "variant $v rc=$rc"; python -c "import json,sys; d=json.load(open('$OUT/bench_$v.json')); print(' ', d['ms_per_step'], d['stage_ms'])"; [ $rc -eq 0 ] || exit $rc
+      done ;;
     prof)
       (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
         python3 "$ROOT/bench.py" --steps 10 --warmup 2 --no-cpu-baseline > "$OUT/prof.log" 2>&1); rc=$?
