@@ -170,4 +170,18 @@ __device__ __forceinline__ float row_sum_to_lane15(float v) {
     return v;
 }
 
+// Reduce-scatter halving steps built on gfx950's lane-swap instructions.
+// half_fold(x, y): lanes 0-31 get x[l] + x[l+32], lanes 32-63 get y[l-32] + y[l]
+// (v_permlane32_swap exchanges the upper half of x with the lower half of y).
+__device__ __forceinline__ float half_fold(float x, float y) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(y), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+// row_fold(x, y): on 16-lane rows, row 0 gets x0 + x1, row 1 y0 + y1, row 2 x2 + x3,
+// row 3 y2 + y3 (v_permlane16_swap exchanges odd rows of x with even rows of y).
+__device__ __forceinline__ float row_fold(float x, float y) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(y), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 }  // namespace gsr

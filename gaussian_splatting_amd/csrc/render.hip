@@ -34,10 +34,6 @@ namespace gsr {
 
 constexpr int kBatch = 64;  // list entries staged per round (one per lane)
 
-#ifndef GSR_ROWRED
-#define GSR_ROWRED 0
-#endif
-
 // Quadrant mask of one splat's footprint box inside the tile at (tile_x0, tile_y0).
 __device__ __forceinline__ uint32_t quad_bits(float4 v1, float4 v2, int tile_x0, int tile_y0) {
     const uint32_t bx = __float_as_uint(v1.w), by = __float_as_uint(v2.w);
@@ -53,29 +49,52 @@ __device__ __forceinline__ uint32_t quad_bits(float4 v1, float4 v2, int tile_x0,
 
 __device__ __forceinline__ uint32_t uniform_u32(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// Staged form of a splat's conic: the exponent is evaluated as
+//   power * log2(e) = dx * (A dx + B dy) + C dy^2,  A = -a/2 log2e, B = -b log2e, C = -c/2 log2e
+// so the per-pixel cost is five VALU ops and exp2 takes it directly.  The
+// coefficients are computed once per list entry while staging (one lane each).
+constexpr float kLog2e = 1.4426950408889634f;
+
+__device__ __forceinline__ float4 stage_conic(float4 v0, float4 v1, uint32_t qm) {
+    return make_float4(-0.5f * kLog2e * v0.z, -kLog2e * v0.w, -0.5f * kLog2e * v1.x, __uint_as_float(qm));
+}
+
+// The reference's two skip tests (power > 0, alpha < 1/255; CR/forward.cu:466-472) folded into
+// one value: the exponent is forced to -inf when positive so alpha becomes 0, and alpha below
+// 1/255 is zeroed.  Returns alpha for a contributing pixel, 0 otherwise; G = exp(power).
+__device__ __forceinline__ float splat_alpha(float p2, float opacity, float& G) {
+    G = __builtin_amdgcn_exp2f(p2 > 0.f ? -INFINITY : p2);  // raw v_exp_f32: tiny results are zeroed below
+    const float alpha = fminf(0.99f, opacity * G);
+    return alpha >= 1.0f / 255.0f ? alpha : 0.f;
+}
+
 // ---------------------------------------------------------------------------
+// Per-pixel state is arithmetic, not boolean: Tl is the live transmittance and
+// drops to 0 when the pixel terminates (CR/forward.cu:477-482); Tf then holds the
+// transmittance at termination.  A finished pixel therefore blends with weight 0
+// without any mask bookkeeping, and the only wave-level decisions are "does any
+// lane of this slot blend this splat" and "is any pixel of this slot still live".
 __global__ void __launch_bounds__(64) render_fwd_kernel(RenderFwdArgs a) {
     const uint32_t tile = blockIdx.x;
     const int tile_x0 = (int)(tile % a.gx) * kTile, tile_y0 = (int)(tile / a.gx) * kTile;
     const int lane = threadIdx.x;
     const int lx = lane & 7, ly = lane >> 3;
 
-    __shared__ float4 s_r0[kBatch], s_r1[kBatch], s_r2[kBatch];
+    __shared__ float4 s_xy[kBatch], s_cq[kBatch], s_col[kBatch];  // (x, y, o, 1/z), (A, B, C, quads), rgb
 
-    float T[4], C0[4], C1[4], C2[4], D[4];
+    float Tl[4], Tf[4], C0[4], C1[4], C2[4], D[4], pxq[4], pyq[4];
     uint32_t last[4];
-    bool done[4];
     uint32_t alive = 0;  // wave-uniform: slots with at least one pixel still blending
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         const int px = tile_x0 + (q & 1) * 8 + lx, py = tile_y0 + (q >> 1) * 8 + ly;
-        done[q] = !(px < a.W && py < a.H);
-        T[q] = 1.f;
-        C0[q] = C1[q] = C2[q] = D[q] = 0.f;
+        Tl[q] = (px < a.W && py < a.H) ? 1.f : 0.f;
+        Tf[q] = C0[q] = C1[q] = C2[q] = D[q] = 0.f;
         last[q] = 0;
-        if (__any(!done[q])) alive |= 1u << q;
+        pxq[q] = (float)px;
+        pyq[q] = (float)py;
+        if (__any(Tl[q] > 0.f)) alive |= 1u << q;
     }
-    const float pxf0 = (float)(tile_x0 + lx), pyf0 = (float)(tile_y0 + ly);
 
     const uint2 range = a.ranges[tile];
     const int n = (int)(range.y - range.x);
@@ -85,41 +104,39 @@ __global__ void __launch_bounds__(64) render_fwd_kernel(RenderFwdArgs a) {
             const uint32_t g = a.emit_gid[a.e_sorted[range.x + b0 + lane]];
             const float4 v0 = a.rec0[g], v1 = a.rec1[g], v2 = a.rec2[g];
             qm = quad_bits(v1, v2, tile_x0, tile_y0);
-            s_r0[lane] = v0;
-            s_r1[lane] = make_float4(v1.x, v1.y, v1.z, __uint_as_float(qm));
-            s_r2[lane] = v2;
+            s_xy[lane] = make_float4(v0.x, v0.y, v1.y, v1.z);
+            s_cq[lane] = stage_conic(v0, v1, qm);
+            s_col[lane] = v2;
         }
         __syncthreads();
         unsigned long long todo = __ballot(qm != 0);
         while (todo && alive) {
             const int j = __builtin_ctzll(todo);
             todo &= todo - 1;
-            const float4 v0 = s_r0[j], v1 = s_r1[j], v2 = s_r2[j];
-            const uint32_t m = uniform_u32(__float_as_uint(v1.w)) & alive;
+            const float4 xy = s_xy[j], cq = s_cq[j], col = s_col[j];
+            const uint32_t m = uniform_u32(__float_as_uint(cq.w)) & alive;
             const uint32_t pos1 = (uint32_t)(b0 + j + 1);
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 if (!(m & (1u << q))) continue;  // uniform: footprint misses this quadrant
-                // The reference's three tests become predicates (power is clamped to <= 0 before
-                // exp so skipped lanes stay finite); the update runs only if some lane passes.
-                const float dx = v0.x - (pxf0 + (float)((q & 1) * 8));
-                const float dy = v0.y - (pyf0 + (float)((q >> 1) * 8));
-                const float power = -0.5f * (v0.z * dx * dx + v1.x * dy * dy) - v0.w * dx * dy;
-                const float alpha = fminf(0.99f, v1.y * __expf(fminf(power, 0.f)));
-                const bool hit = !done[q] && power <= 0.0f && alpha >= 1.0f / 255.0f;
-                if (!__any(hit)) continue;  // uniform
-                const float test_T = T[q] * (1.f - alpha);
-                const bool term = hit && test_T < 0.0001f;  // CR/forward.cu:477-482: ends the pixel, not added
-                const bool add = hit && !term;
-                done[q] = done[q] || term;
-                const float w = add ? alpha * T[q] : 0.f;
-                C0[q] += v2.x * w;
-                C1[q] += v2.y * w;
-                C2[q] += v2.z * w;
-                D[q] += v1.z * w;
-                T[q] = add ? test_T : T[q];
-                last[q] = add ? pos1 : last[q];
-                if (__all(done[q])) alive &= ~(1u << q);
+                const float dx = xy.x - pxq[q], dy = xy.y - pyq[q];
+                const float p2 = dx * (cq.x * dx + cq.y * dy) + cq.z * dy * dy;
+                float G;
+                const float alpha = splat_alpha(p2, xy.z, G);
+                const float w0 = alpha * Tl[q];  // > 0 iff this pixel blends the splat
+                if (!__any(w0 > 0.f)) continue;  // uniform
+                const float test_T = Tl[q] * (1.f - alpha);
+                const bool term = test_T < 0.0001f;  // live pixel: ends it, splat not added
+                const float w = term ? 0.f : w0;
+                // first termination wins (later ones see Tl = 0); both are >= 0, so an integer max
+                Tf[q] = __uint_as_float(max(__float_as_uint(Tf[q]), term ? __float_as_uint(Tl[q]) : 0u));
+                Tl[q] = term ? 0.f : test_T;
+                C0[q] += col.x * w;
+                C1[q] += col.y * w;
+                C2[q] += col.z * w;
+                D[q] += xy.w * w;
+                last[q] = w > 0.f ? pos1 : last[q];
+                if (!__any(Tl[q] > 0.f)) alive &= ~(1u << q);
             }
         }
         __syncthreads();
@@ -130,15 +147,16 @@ __global__ void __launch_bounds__(64) render_fwd_kernel(RenderFwdArgs a) {
         const int px = tile_x0 + (q & 1) * 8 + lx, py = tile_y0 + (q >> 1) * 8 + ly;
         if (px < a.W && py < a.H) {
             const size_t pix = (size_t)py * a.W + px;
-            a.img.final_T[pix] = T[q];
+            const float T = Tl[q] > 0.f ? Tl[q] : Tf[q];
+            a.img.final_T[pix] = T;
             a.img.n_contrib[pix] = last[q];
             a.img.accum[pix] = C0[q];
             a.img.accum[N + pix] = C1[q];
             a.img.accum[2 * N + pix] = C2[q];
             a.img.accum[3 * N + pix] = D[q];
-            a.out_color[pix] = C0[q] + T[q] * a.bg[0];
-            a.out_color[N + pix] = C1[q] + T[q] * a.bg[1];
-            a.out_color[2 * N + pix] = C2[q] + T[q] * a.bg[2];
+            a.out_color[pix] = C0[q] + T * a.bg[0];
+            a.out_color[N + pix] = C1[q] + T * a.bg[1];
+            a.out_color[2 * N + pix] = C2[q] + T * a.bg[2];
             a.out_invdepth[pix] = D[q];
         }
     }
@@ -158,25 +176,21 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a) {
     const int lane = threadIdx.x;
     const int lx = lane & 7, ly = lane >> 3;
 
-    __shared__ float4 s_r0[kBatch], s_r1[kBatch], s_r2[kBatch];
-#if GSR_ROWRED
-    // per entry: four 16-lane row partials of the 10 sums (12 floats each), padded stride
-    constexpr int kPart = 52;
-    __shared__ __attribute__((aligned(16))) float s_part[kBatch * kPart];
-#else
-    __shared__ float4 s_acc[kBatch][3];  // per entry: 10 reduced sums (+2 pad)
-#endif
+    __shared__ float4 s_xy[kBatch], s_cq[kBatch], s_col[kBatch];  // as in the forward
+    __shared__ float4 s_acc[kBatch][3];                           // per entry: the 10 reduced sums (+2 pad)
 
     const size_t N = (size_t)a.W * a.H;
-    float T[4], gB[4], g0[4], g1[4], g2[4], gi[4], bgt[4];
+    float T[4], gB[4], g0[4], g1[4], g2[4], gi[4], pxq[4], pyq[4];
     int nc[4];
     uint32_t wmax = 0;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         const int px = tile_x0 + (q & 1) * 8 + lx, py = tile_y0 + (q >> 1) * 8 + ly;
+        pxq[q] = (float)px;
+        pyq[q] = (float)py;
         T[q] = 1.f;
         nc[q] = 0;
-        gB[q] = g0[q] = g1[q] = g2[q] = gi[q] = bgt[q] = 0.f;
+        gB[q] = g0[q] = g1[q] = g2[q] = gi[q] = 0.f;
         if (px < a.W && py < a.H) {
             const size_t pix = (size_t)py * a.W + px;
             nc[q] = (int)a.img.n_contrib[pix];
@@ -184,18 +198,19 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a) {
             g1[q] = a.dL_dpix[N + pix];
             g2[q] = a.dL_dpix[2 * N + pix];
             if (a.dL_dinvdepth) gi[q] = a.dL_dinvdepth[pix];
-            // dL/dpix . (everything the forward accumulated) -- shrinks to "behind" as we walk
+            // dL/dpix . (everything the forward accumulated + the background term of dL/dalpha,
+            // CR/backward.cu:587-590); shrinks to "behind this entry" as the walk proceeds
             gB[q] = g0[q] * a.img.accum[pix] + g1[q] * a.img.accum[N + pix] + g2[q] * a.img.accum[2 * N + pix] +
-                    gi[q] * a.img.accum[3 * N + pix];
-            // background term of dL/dalpha (CR/backward.cu:587-590)
-            bgt[q] = a.img.final_T[pix] * (a.bg[0] * g0[q] + a.bg[1] * g1[q] + a.bg[2] * g2[q]);
+                    gi[q] * a.img.accum[3 * N + pix] +
+                    a.img.final_T[pix] * (a.bg[0] * g0[q] + a.bg[1] * g1[q] + a.bg[2] * g2[q]);
         }
         wmax = max(wmax, (uint32_t)nc[q]);
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) wmax = max(wmax, (uint32_t)__shfl_xor((int)wmax, off));
     const int limit = (int)uniform_u32(wmax);  // entries at positions >= limit reach no pixel of this tile
-    const float pxf0 = (float)(tile_x0 + lx), pyf0 = (float)(tile_y0 + ly);
+    // where this lane's row of the reduce-scatter lands in s_acc (see below)
+    const int row = lane >> 4, slot_k = ((row & 1) << 1) | (row >> 1);
 
     const uint2 range = a.ranges[tile];
     const int n = (int)(range.y - range.x);
@@ -211,13 +226,18 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a) {
             continue;
         }
         uint32_t qm = 0;
+        float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f);
+        float o = 0.f, cc = 0.f;
         if (has) {
             const uint32_t g = a.emit_gid[e];
-            const float4 v0 = a.rec0[g], v1 = a.rec1[g], v2 = a.rec2[g];
+            v0 = a.rec0[g];
+            const float4 v1 = a.rec1[g], v2 = a.rec2[g];
             qm = quad_bits(v1, v2, tile_x0, tile_y0);
-            s_r0[lane] = v0;
-            s_r1[lane] = make_float4(v1.x, v1.y, v1.z, __uint_as_float(qm));
-            s_r2[lane] = v2;
+            o = v1.y;
+            cc = v1.x;
+            s_xy[lane] = make_float4(v0.x, v0.y, v1.y, v1.z);
+            s_cq[lane] = stage_conic(v0, v1, qm);
+            s_col[lane] = v2;
         }
         __syncthreads();
         unsigned long long todo = __ballot(qm != 0);
@@ -228,29 +248,26 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a) {
             const int j = __builtin_ctzll(todo);
             todo &= todo - 1;
             const int pos = b0 + j;
-            const float4 v0 = s_r0[j], v1 = s_r1[j], v2 = s_r2[j];
-            const uint32_t m = uniform_u32(__float_as_uint(v1.w));
+            const float4 xy = s_xy[j], cq = s_cq[j], col = s_col[j];
+            const uint32_t m = uniform_u32(__float_as_uint(cq.w));
             float r0 = 0.f, r1 = 0.f, r2 = 0.f, r3 = 0.f, r4 = 0.f, r5 = 0.f, r6 = 0.f, r7 = 0.f, r8 = 0.f, r9 = 0.f;
             bool contrib = false;
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 if (!(m & (1u << q))) continue;  // uniform
-                // Same tests as the forward, as predicates; the gradient work runs only if some
-                // lane of the slot passes them.
-                const float dx = v0.x - (pxf0 + (float)((q & 1) * 8));
-                const float dy = v0.y - (pyf0 + (float)((q >> 1) * 8));
-                const float power = -0.5f * (v0.z * dx * dx + v1.x * dy * dy) - v0.w * dx * dy;
-                const float G = __expf(fminf(power, 0.f));
-                const float alpha = fminf(0.99f, v1.y * G);
-                const bool hit = pos < nc[q] && power <= 0.0f && alpha >= 1.0f / 255.0f;
-                if (!__any(hit)) continue;  // uniform
+                const float dx = xy.x - pxq[q], dy = xy.y - pyq[q];
+                const float p2 = dx * (cq.x * dx + cq.y * dy) + cq.z * dy * dy;
+                float G;
+                float alpha = splat_alpha(p2, xy.z, G);
+                alpha = pos < nc[q] ? alpha : 0.f;  // the forward stopped this pixel before `pos`
+                if (!__any(alpha > 0.f)) continue;  // uniform
                 contrib = true;
-                const float w = hit ? alpha * T[q] : 0.f;
-                const float sdot = g0[q] * v2.x + g1[q] * v2.y + g2[q] * v2.z + gi[q] * v1.z;
-                gB[q] -= w * sdot;  // now dL/dpix . (colour strictly behind this entry)
+                const float w = alpha * T[q];
+                const float sdot = g0[q] * col.x + g1[q] * col.y + g2[q] * col.z + gi[q] * xy.w;
+                gB[q] -= w * sdot;  // now dL/dpix . (colour strictly behind this entry) + background term
                 const float one_m_a = 1.f - alpha;
-                const float dLda = T[q] * sdot - (gB[q] + bgt[q]) * __builtin_amdgcn_rcpf(one_m_a);
-                const float u = hit ? dLda * G : 0.f;
+                const float dLda = T[q] * sdot - gB[q] * __builtin_amdgcn_rcpf(one_m_a);
+                const float u = alpha > 0.f ? dLda * G : 0.f;
                 r0 += w * g0[q];
                 r1 += w * g1[q];
                 r2 += w * g2[q];
@@ -262,43 +279,23 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a) {
                 r7 += udx * dy;
                 r8 += udy * dy;
                 r9 += u;
-                T[q] = hit ? T[q] * one_m_a : T[q];
+                T[q] *= one_m_a;  // alpha = 0 leaves T unchanged
             }
             if (contrib) {  // uniform
-#if GSR_ROWRED
-                r0 = row_sum_to_lane15(r0);
-                r1 = row_sum_to_lane15(r1);
-                r2 = row_sum_to_lane15(r2);
-                r3 = row_sum_to_lane15(r3);
-                r4 = row_sum_to_lane15(r4);
-                r5 = row_sum_to_lane15(r5);
-                r6 = row_sum_to_lane15(r6);
-                r7 = row_sum_to_lane15(r7);
-                r8 = row_sum_to_lane15(r8);
-                r9 = row_sum_to_lane15(r9);
+                // Reduce-scatter over the wave: two lane-swap halvings take the ten sums from
+                // 64 lanes to 16 (packing four sums per register), then one 16-lane row sum.
+                const float h0 = half_fold(r0, r1), h1 = half_fold(r2, r3), h2 = half_fold(r4, r5),
+                            h3 = half_fold(r6, r7), h4 = half_fold(r8, r9);
+                // rows of w0: r0 r2 r1 r3; w1: r4 r6 r5 r7; w2: r8 r8 r9 r9
+                const float w0 = row_sum_to_lane15(row_fold(h0, h1));
+                const float w1 = row_sum_to_lane15(row_fold(h2, h3));
+                const float w2 = row_sum_to_lane15(row_fold(h4, h4));
                 if ((lane & 15) == 15) {
-                    float4* p = reinterpret_cast<float4*>(&s_part[j * kPart + (lane >> 4) * 12]);
-                    p[0] = make_float4(r0, r1, r2, r3);
-                    p[1] = make_float4(r4, r5, r6, r7);
-                    p[2] = make_float4(r8, r9, 0.f, 0.f);
+                    float* acc = reinterpret_cast<float*>(&s_acc[j][0]);
+                    acc[slot_k] = w0;
+                    acc[4 + slot_k] = w1;
+                    if (slot_k < 2) acc[8 + slot_k] = w2;
                 }
-#else
-                r0 = wave_sum_to_lane63(r0);
-                r1 = wave_sum_to_lane63(r1);
-                r2 = wave_sum_to_lane63(r2);
-                r3 = wave_sum_to_lane63(r3);
-                r4 = wave_sum_to_lane63(r4);
-                r5 = wave_sum_to_lane63(r5);
-                r6 = wave_sum_to_lane63(r6);
-                r7 = wave_sum_to_lane63(r7);
-                r8 = wave_sum_to_lane63(r8);
-                r9 = wave_sum_to_lane63(r9);
-                if (lane == 63) {
-                    s_acc[j][0] = make_float4(r0, r1, r2, r3);
-                    s_acc[j][1] = make_float4(r4, r5, r6, r7);
-                    s_acc[j][2] = make_float4(r8, r9, 0.f, 0.f);
-                }
-#endif
                 written |= 1ull << j;
             }
         }
@@ -307,21 +304,8 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a) {
             float4 ra = make_float4(0.f, 0.f, 0.f, 0.f), rb = ra;
             float2 rc = make_float2(0.f, 0.f);
             if ((written >> lane) & 1ull) {
-#if GSR_ROWRED
-                const float4* p = reinterpret_cast<const float4*>(&s_part[lane * kPart]);
-                float4 A = p[0], B = p[1], Cc = p[2];
-#pragma unroll
-                for (int rr = 1; rr < 4; rr++) {  // fixed order: deterministic
-                    const float4 a4 = p[3 * rr], b4 = p[3 * rr + 1], c4 = p[3 * rr + 2];
-                    A.x += a4.x; A.y += a4.y; A.z += a4.z; A.w += a4.w;
-                    B.x += b4.x; B.y += b4.y; B.z += b4.z; B.w += b4.w;
-                    Cc.x += c4.x; Cc.y += c4.y;
-                }
-#else
                 const float4 A = s_acc[lane][0], B = s_acc[lane][1], Cc = s_acc[lane][2];
-#endif
-                const float4 v0 = s_r0[lane], v1 = s_r1[lane];
-                const float o = v1.y, ca = v0.z, cb = v0.w, cc = v1.x;
+                const float ca = v0.z, cb = v0.w;
                 // dL/dmean2D in NDC units (x 0.5 W, 0.5 H, CR/backward.cu:509-510,600-601);
                 // dL/dconic with the reference's -0.5 factors (CR/backward.cu:604-606)
                 ra = A;

@@ -1,0 +1,13 @@
+#!/bin/bash
+# PMC counter passes (each pass its own rocprofv3 run, --pmc only; no tracing domains).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+ROOT=$(pwd); TAG=$1; OUT=$ROOT/gpurun_out/$TAG; mkdir -p "$OUT"; export TMPDIR=/tmp
+i=0
+while read -r ctrs; do
+  [ -z "$ctrs" ] && continue
+  i=$((i+1))
+  (cd /tmp && timeout -k 10 300 rocprofv3 --pmc $ctrs --output-format csv -d "$OUT/pmc$i" -o run -- \
+     python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/pmc$i.log" 2>&1); rc=$?
+  echo "pass $i ($ctrs) rc=$rc"; [ $rc -eq 0 ] || exit $rc
+done < "$2"
