@@ -10,8 +10,9 @@
 //  * ONE wave64 per 16x16 tile.  Lane l owns pixel (l & 7, l >> 3) of each of the
 //    four 8x8 quadrants ("slots" 0..3), so a lane carries four pixels' state;
 //  * list entries are staged 64 at a time (one per lane) into LDS as 48-byte
-//    splat records; while loading, each entry's conservative alpha >= 1/255
-//    footprint box is tested against the four quadrants (4-bit mask);
+//    splat records; while loading, each entry's alpha >= 1/255 footprint (its
+//    box, then the ellipse itself) is tested against the four quadrants (4-bit
+//    mask, conservative);
 //  * the wave walks only entries whose mask is non-zero (scalar bit scan of a
 //    ballot) and, per entry, runs only the slots whose bit is set -- uniform
 //    branches, no vector work for culled quadrants;
@@ -23,8 +24,10 @@
 // enters dL/dalpha only through the dot product with dL/dpixel, so each pixel
 // keeps one running scalar gB = dL/dpix . (colour behind) + dL/dinvdepth .
 // (inverse depth behind), initialised from the forward's accumulated colour.
-// Per-Gaussian sums over the tile's pixels are first summed over the lane's four
-// slots in registers, then over the wave with DPP reductions -- once per
+// A slot is retired once the walk passes the last contributor of all its pixels
+// (n_contrib from the forward).  Per-Gaussian sums over the tile's pixels are
+// first summed over the lane's four slots in registers, then over the wave with a
+// lane-swap reduce-scatter and DPP row sums -- once per
 // (tile, Gaussian) instance -- and written with plain stores.  There are no
 // float atomics anywhere, so the result is bitwise reproducible (the reference
 // issues 10 global float atomics per pixel-Gaussian pair, CR/backward.cu:569-609).
@@ -43,6 +46,47 @@ __device__ __forceinline__ uint32_t quad_bits(float4 v1, float4 v2, int tile_x0,
     for (int k = 0; k < 4; k++) {
         const int qx0 = tile_x0 + (k & 1) * 8, qy0 = tile_y0 + (k >> 1) * 8;
         if (x0 <= qx0 + 7 && x1 >= qx0 && y0 <= qy0 + 7 && y1 >= qy0) q |= 1u << k;
+    }
+    return q;
+}
+
+// Conic quadratic form Q(d) = a dx^2 + 2 b dx dy + c dy^2 (power = -Q/2), minimised over the
+// pixel-centre rectangle [x0,x1] x [y0,y1] of offsets d = p - mean.  For a positive-definite
+// conic the minimum is 0 if the mean is inside, otherwise on an edge, where Q is a 1-D
+// parabola minimised at the clamped vertex.
+__device__ __forceinline__ float rect_min_form(float a, float b, float c, float ra, float rc, float x0, float x1,
+                                               float y0, float y1) {
+    if (x0 <= 0.f && x1 >= 0.f && y0 <= 0.f && y1 >= 0.f) return 0.f;
+    float best = INFINITY;
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        const float dx = k ? x1 : x0;
+        const float dy = fminf(y1, fmaxf(y0, -b * dx * rc));
+        best = fminf(best, a * dx * dx + (2.f * b * dx + c * dy) * dy);
+        const float ey = k ? y1 : y0;
+        const float ex = fminf(x1, fmaxf(x0, -b * ey * ra));
+        best = fminf(best, c * ey * ey + (2.f * b * ey + a * ex) * ex);
+    }
+    return best;
+}
+
+// Quadrant mask refined by the footprint ellipse itself: a quadrant the box overlaps is
+// dropped when no pixel centre of it lies inside the alpha >= 1/255 ellipse
+// Q <= 2 ln(255 o), with the same relative/absolute margin the box uses (preprocess.hip), so
+// the test stays conservative under fp32 rounding of the per-pixel evaluation.  Degenerate
+// conics keep the box result.  Runs while staging, one list entry per lane.
+__device__ __forceinline__ uint32_t quad_bits_exact(float4 v0, float4 v1, float4 v2, int tile_x0, int tile_y0) {
+    uint32_t q = quad_bits(v1, v2, tile_x0, tile_y0);
+    const float a = v0.z, b = v0.w, c = v1.x, o = v1.y;
+    if (q == 0 || !(a > 0.f && c > 0.f && a * c - b * b > 0.f) || !(o > 0.f)) return q;
+    const float tau = fmaxf(0.f, __logf(255.f * o)) * 1.001f + 0.01f;
+    const float lim = 2.f * tau;
+    const float ra = 1.f / a, rc = 1.f / c;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        if (!(q & (1u << k))) continue;
+        const float x0 = (float)(tile_x0 + (k & 1) * 8) - v0.x, y0 = (float)(tile_y0 + (k >> 1) * 8) - v0.y;
+        if (rect_min_form(a, b, c, ra, rc, x0, x0 + 7.f, y0, y0 + 7.f) > lim) q &= ~(1u << k);
     }
     return q;
 }
@@ -103,7 +147,7 @@ __global__ void __launch_bounds__(64) render_fwd_kernel(RenderFwdArgs a) {
         if (b0 + lane < n) {
             const uint32_t g = a.emit_gid[a.e_sorted[range.x + b0 + lane]];
             const float4 v0 = a.rec0[g], v1 = a.rec1[g], v2 = a.rec2[g];
-            qm = quad_bits(v1, v2, tile_x0, tile_y0);
+            qm = quad_bits_exact(v0, v1, v2, tile_x0, tile_y0);
             s_xy[lane] = make_float4(v0.x, v0.y, v1.y, v1.z);
             s_cq[lane] = stage_conic(v0, v1, qm);
             s_col[lane] = v2;
@@ -182,7 +226,6 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a) {
     const size_t N = (size_t)a.W * a.H;
     float T[4], gB[4], g0[4], g1[4], g2[4], gi[4], pxq[4], pyq[4];
     int nc[4];
-    uint32_t wmax = 0;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         const int px = tile_x0 + (q & 1) * 8 + lx, py = tile_y0 + (q >> 1) * 8 + ly;
@@ -204,11 +247,26 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a) {
                     gi[q] * a.img.accum[3 * N + pix] +
                     a.img.final_T[pix] * (a.bg[0] * g0[q] + a.bg[1] * g1[q] + a.bg[2] * g2[q]);
         }
-        wmax = max(wmax, (uint32_t)nc[q]);
     }
+    // Per-slot limits: entries at positions >= slim[q] reach no pixel of slot q (the forward
+    // stopped all of them earlier), so the slot is skipped from there on.
+    int slim[4];
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) wmax = max(wmax, (uint32_t)__shfl_xor((int)wmax, off));
-    const int limit = (int)uniform_u32(wmax);  // entries at positions >= limit reach no pixel of this tile
+    for (int q = 0; q < 4; q++) {
+        int v = nc[q];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off));
+        slim[q] = (int)uniform_u32((uint32_t)v);
+    }
+    const int limit = max(max(slim[0], slim[1]), max(slim[2], slim[3]));
+    uint32_t live = 0;  // slots still reachable at the current position (uniform)
+    int next_lim = limit;  // smallest slot limit among live slots
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+        if (slim[q] > 0) {
+            live |= 1u << q;
+            next_lim = min(next_lim, slim[q]);
+        }
     // where this lane's row of the reduce-scatter lands in s_acc (see below)
     const int row = lane >> 4, slot_k = ((row & 1) << 1) | (row >> 1);
 
@@ -232,7 +290,7 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a) {
             const uint32_t g = a.emit_gid[e];
             v0 = a.rec0[g];
             const float4 v1 = a.rec1[g], v2 = a.rec2[g];
-            qm = quad_bits(v1, v2, tile_x0, tile_y0);
+            qm = quad_bits_exact(v0, v1, v2, tile_x0, tile_y0);
             o = v1.y;
             cc = v1.x;
             s_xy[lane] = make_float4(v0.x, v0.y, v1.y, v1.z);
@@ -249,7 +307,16 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a) {
             todo &= todo - 1;
             const int pos = b0 + j;
             const float4 xy = s_xy[j], cq = s_cq[j], col = s_col[j];
-            const uint32_t m = uniform_u32(__float_as_uint(cq.w));
+            if (pos >= next_lim) {  // uniform: retire the slots whose last contributor has passed
+                next_lim = limit;
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    if (pos >= slim[q]) live &= ~(1u << q);
+                    else next_lim = min(next_lim, slim[q]);
+                }
+            }
+            const uint32_t m = uniform_u32(__float_as_uint(cq.w)) & live;
+            if (m == 0) continue;
             float r0 = 0.f, r1 = 0.f, r2 = 0.f, r3 = 0.f, r4 = 0.f, r5 = 0.f, r6 = 0.f, r7 = 0.f, r8 = 0.f, r9 = 0.f;
             bool contrib = false;
 #pragma unroll
