@@ -3,6 +3,7 @@ GPU call with the same arguments, and comparison utilities."""
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 from typing import Optional
 
@@ -152,3 +153,30 @@ SMALL_CASES = [
     Case("yawed_view", P=300, W=64, H=48, yaw=15.0),
     Case("dense_opaque", P=2000, W=64, H=64, opacity_std=3.0, scale_range=(0.05, 0.3)),
 ]
+
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+RASTER_FIXTURES = sorted(f[len("raster_"):-len(".npz")] for f in os.listdir(GOLDEN)
+                         if f.startswith("raster_") and f.endswith(".npz"))
+
+
+def load_raster(name):
+    """A rasterizer golden vector (tests/golden/make_golden.py): (inp, expected, (grad_color, grad_invdepth))."""
+    z = np.load(os.path.join(GOLDEN, f"raster_{name}.npz"))
+    inp = dict(bg=None, means3D=None, opacities=None, shs=None, sh_degree=0, scales=None, rotations=None,
+               colors_precomp=None, cov3D_precomp=None)
+    for k in z.files:
+        if k.startswith("in_"):
+            v = z[k]
+            inp[k[3:]] = torch.from_numpy(v.copy()) if v.ndim > 0 else v.item()
+    for k in ("H", "W", "sh_degree"):
+        inp[k] = int(inp[k])
+    for k in ("tanfovx", "tanfovy", "scale_modifier"):
+        inp[k] = float(inp[k])
+    inp["antialiasing"] = bool(inp["antialiasing"])
+    exp = {k[4:]: z[k] for k in z.files if k.startswith("out_")}
+    exp["num_rendered"] = int(exp["num_rendered"])
+    grads = None
+    if "grad_color" in z.files:
+        grads = (torch.from_numpy(z["grad_color"].copy()), torch.from_numpy(z["grad_invdepth"].copy()))
+    return inp, exp, grads
