@@ -115,9 +115,7 @@ gsr::GeomState carve_geom(char* base, int P, size_t* total) {
     using namespace gsr;
     Carver c{base, 0};
     GeomState g{};
-    g.rec0 = c.take<float4>(P);
-    g.rec1 = c.take<float4>(P);
-    g.rec2 = c.take<float4>(P);
+    g.rec = c.take<float4>((size_t)kRecRows * P);
     g.depth_key = c.take<uint32_t>(P);
     g.depth_key_sorted = c.take<uint32_t>(P);
     g.gid_by_rank = c.take<uint32_t>(P);
@@ -156,17 +154,19 @@ gsr::BinningState carve_binning(char* base, size_t R, bool key16, size_t* total)
     b.keys = c.take<char>(R * ks);
     b.keys_sorted = c.take<char>(R * ks);
     b.emit_gid = c.take<uint32_t>(R);
-    b.e_sorted = c.take<uint32_t>(R);
+    b.gid_sorted = c.take<uint32_t>(R);
     b.sort_temp_bytes = R ? tile_sort_temp_bytes(R, key16) : 0;
     b.sort_temp = c.take<char>(b.sort_temp_bytes);
     *total = align_up(c.off);
     return b;
 }
 
-// Backward scratch: R per-instance records followed by P per-rank sums.
-void carve_recs(char* base, size_t R, size_t P, gsr::GradRecs* recs, gsr::GradRecs* sums, size_t* total) {
+// Backward scratch: R per-instance records, P per-rank sums, the per-tile rank limits.
+void carve_recs(char* base, size_t R, size_t P, size_t tiles, gsr::GradRecs* recs, gsr::GradRecs* sums,
+                uint32_t** rank_lim, size_t* total) {
     using namespace gsr;
     Carver c{base, 0};
+    *rank_lim = c.take<uint32_t>(tiles);
     recs->a = c.take<float4>(R);
     recs->b = c.take<float4>(R);
     recs->c = c.take<float2>(R);
@@ -357,8 +357,8 @@ int gsr_rasterize_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn 
     {
         StageScope sc(ST_RENDER_FWD, stream);
         RenderFwdArgs ra{};
-        ra.W = width; ra.H = height; ra.gx = gx; ra.gy = gy; ra.ranges = img.ranges; ra.emit_gid = bin.emit_gid; ra.e_sorted = bin.e_sorted;
-        ra.rec0 = geom.rec0; ra.rec1 = geom.rec1; ra.rec2 = geom.rec2; ra.bg = background;
+        ra.W = width; ra.H = height; ra.gx = gx; ra.gy = gy; ra.ranges = img.ranges; ra.gid_sorted = bin.gid_sorted;
+        ra.rec = geom.rec; ra.bg = background;
         ra.out_color = out_color; ra.out_invdepth = out_invdepth; ra.img = img;
         HIP_TRY(launch_render_fwd(ra, stream), "render_fwd");
     }
@@ -405,23 +405,25 @@ int gsr_rasterize_backward(int P, int D, int M, int R, const float* background, 
     BinningState bin = carve_binning((char*)binning_buffer, (size_t)R, key16, &tmp);
     size_t rec_bytes = 0;
     GradRecs recs{}, sums{};
-    carve_recs(nullptr, (size_t)R, (size_t)P, &recs, &sums, &rec_bytes);
+    uint32_t* rank_lim = nullptr;
+    carve_recs(nullptr, (size_t)R, (size_t)P, tiles, &recs, &sums, &rank_lim, &rec_bytes);
     char* rbase = (char*)call_alloc(scratch_alloc, scratch_ctx, rec_bytes);
     if (!rbase) return fail(GSR_ERR_ALLOC, "rasterize_backward: scratch allocation failed");
-    carve_recs(rbase, (size_t)R, (size_t)P, &recs, &sums, &rec_bytes);
+    carve_recs(rbase, (size_t)R, (size_t)P, tiles, &recs, &sums, &rank_lim, &rec_bytes);
 
     if (R > 0) {
         StageScope sc(ST_RENDER_BWD, stream);
         RenderBwdArgs ra{};
-        ra.W = width; ra.H = height; ra.gx = gx; ra.gy = gy; ra.ranges = img.ranges; ra.emit_gid = bin.emit_gid;
-        ra.e_sorted = bin.e_sorted; ra.rec0 = geom.rec0; ra.rec1 = geom.rec1; ra.rec2 = geom.rec2;
+        ra.W = width; ra.H = height; ra.gx = gx; ra.gy = gy; ra.ranges = img.ranges; ra.gid_sorted = bin.gid_sorted;
+        ra.rec = geom.rec;
         ra.bg = background; ra.dL_dpix = dL_dpix; ra.dL_dinvdepth = dL_dinvdepths; ra.img = img; ra.recs = recs;
+        ra.rank_of = geom.rank_of; ra.rank_lim = rank_lim;
         HIP_TRY(launch_render_bwd(ra, stream), "render_bwd");
     }
     if (int rc = check_debug(debug, stream, "render_bwd")) return rc;
     {
         StageScope sc(ST_GAUSS_REDUCE, stream);
-        HIP_TRY(launch_gauss_reduce(P, geom.offsets, recs, sums, stream), "gauss_reduce");
+        HIP_TRY(launch_gauss_reduce(P, geom.offsets, bin.keys, key16, rank_lim, recs, sums, stream), "gauss_reduce");
     }
     if (int rc = check_debug(debug, stream, "gauss_reduce")) return rc;
     {

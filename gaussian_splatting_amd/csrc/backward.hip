@@ -26,11 +26,17 @@ namespace gsr {
 // One wave per 64 consecutive ranks.  Their records form one contiguous range
 // [E0, E1); it is streamed through LDS 64 records at a time with fully coalesced
 // loads, and every lane sums the rows of its own segment from LDS in order, so
-// the result does not depend on scheduling.
+// the result does not depend on scheduling.  The render backward writes records
+// only for entries before each tile's last contributor; an instance (rank r,
+// tile t) has one iff r < rank_lim[t], and the others are read as zeros without
+// touching memory (render.hip, "Entries at positions >= limit").
 constexpr int kRecStride = 12;  // floats per staged record row (10 used), 48 B
 
+template <typename KeyT>
 __global__ void __launch_bounds__(64) gauss_reduce_kernel(int P, const unsigned long long* __restrict__ offsets,
-                                                          GradRecs recs, GradRecs sums) {
+                                                          const KeyT* __restrict__ keys,
+                                                          const uint32_t* __restrict__ rank_lim, GradRecs recs,
+                                                          GradRecs sums) {
     __shared__ __attribute__((aligned(16))) float s_rec[64 * kRecStride];
     const int lane = threadIdx.x;
     const int r0 = blockIdx.x * 64;
@@ -44,9 +50,18 @@ __global__ void __launch_bounds__(64) gauss_reduce_kernel(int P, const unsigned 
     float2 sc = make_float2(0.f, 0.f);
     for (unsigned long long base = E0; base < E1; base += 64) {
         const unsigned long long e = base + lane;
+        // owner of slot e: the largest lane whose segment starts at or before it
+        const unsigned long long my0c = my0;
+        int owner = 0;
+#pragma unroll
+        for (int step = 32; step > 0; step >>= 1) {
+            const int cand = owner + step;
+            const unsigned long long v = __shfl(my0c, cand & 63);
+            if (cand < 64 && v <= e) owner = cand;
+        }
         float4 x = make_float4(0.f, 0.f, 0.f, 0.f), y = x;
         float2 z = make_float2(0.f, 0.f);
-        if (e < E1) {
+        if (e < E1 && (uint32_t)(r0 + owner) < rank_lim[keys[e]]) {
             x = recs.a[e];
             y = recs.b[e];
             z = recs.c[e];
@@ -74,10 +89,15 @@ __global__ void __launch_bounds__(64) gauss_reduce_kernel(int P, const unsigned 
     }
 }
 
-hipError_t launch_gauss_reduce(int P, const unsigned long long* offsets, const GradRecs& recs, const GradRecs& sums,
-                               hipStream_t stream) {
+hipError_t launch_gauss_reduce(int P, const unsigned long long* offsets, const void* keys, bool key16,
+                               const uint32_t* rank_lim, const GradRecs& recs, const GradRecs& sums, hipStream_t stream) {
     if (P == 0) return hipSuccess;
-    hipLaunchKernelGGL(gauss_reduce_kernel, dim3((P + 63) / 64), dim3(64), 0, stream, P, offsets, recs, sums);
+    if (key16)
+        hipLaunchKernelGGL(gauss_reduce_kernel<uint16_t>, dim3((P + 63) / 64), dim3(64), 0, stream, P, offsets,
+                           (const uint16_t*)keys, rank_lim, recs, sums);
+    else
+        hipLaunchKernelGGL(gauss_reduce_kernel<uint32_t>, dim3((P + 63) / 64), dim3(64), 0, stream, P, offsets,
+                           (const uint32_t*)keys, rank_lim, recs, sums);
     return hipGetLastError();
 }
 

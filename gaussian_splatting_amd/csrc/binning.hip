@@ -75,7 +75,7 @@ hipError_t rank_and_scan(GeomState& g, int P, hipStream_t stream) {
 template <typename KeyT>
 __global__ void __launch_bounds__(256) duplicate_kernel(int P, const uint32_t* __restrict__ gid_by_rank,
                                                         const unsigned long long* __restrict__ offsets,
-                                                        const int* __restrict__ radii, const float4* __restrict__ rec0,
+                                                        const int* __restrict__ radii, float4* __restrict__ rec,
                                                         uint32_t gx, uint32_t gy, KeyT* __restrict__ keys,
                                                         uint32_t* __restrict__ emit_gid) {
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
@@ -90,12 +90,15 @@ __global__ void __launch_bounds__(256) duplicate_kernel(int P, const uint32_t* _
         incl = offsets[r];
         const int rad = radii[gid];
         if (rad > 0) {
-            const float4 v = rec0[gid];
+            const float4 v = rec[(size_t)kRecRows * gid];
             get_rect(v.x, v.y, rad, gx, gy, rmin, rmax);
             count = (rmax.y - rmin.y) * (rmax.x - rmin.x);
         }
     }
     const unsigned long long excl = incl - count;
+    // first emission index of this Gaussian -> record row 3 (the render backward addresses
+    // its per-instance gradient records with it)
+    if (count) reinterpret_cast<uint32_t*>(rec + (size_t)kRecRows * gid + 3)[3] = (uint32_t)excl;
     // The wave's ranks are consecutive: its emissions are [E0, E1) with both ends
     // read from the scan (wave-uniform addresses -> scalar loads).
     const int r0 = r - lane;
@@ -137,10 +140,10 @@ hipError_t launch_duplicate(int P, const GeomState& g, const int* radii, uint32_
     const dim3 grid((P + 255) / 256), block(256);
     if (key16)
         hipLaunchKernelGGL(duplicate_kernel<uint16_t>, grid, block, 0, stream, P, g.gid_by_rank, g.offsets, radii,
-                           g.rec0, gx, gy, (uint16_t*)b.keys, b.emit_gid);
+                           g.rec, gx, gy, (uint16_t*)b.keys, b.emit_gid);
     else
         hipLaunchKernelGGL(duplicate_kernel<uint32_t>, grid, block, 0, stream, P, g.gid_by_rank, g.offsets, radii,
-                           g.rec0, gx, gy, (uint32_t*)b.keys, b.emit_gid);
+                           g.rec, gx, gy, (uint32_t*)b.keys, b.emit_gid);
     return hipGetLastError();
 }
 
@@ -149,10 +152,10 @@ size_t tile_sort_temp_bytes(size_t R, bool key16) {
     size_t bytes = 0;
     if (key16)
         (void)rocprim::radix_sort_pairs<SortConfig>(nullptr, bytes, (const uint16_t*)nullptr, (uint16_t*)nullptr,
-                                  rocprim::counting_iterator<uint32_t>(0), (uint32_t*)nullptr, R, 0, 16);
+                                                    (const uint32_t*)nullptr, (uint32_t*)nullptr, R, 0, 16);
     else
         (void)rocprim::radix_sort_pairs<SortConfig>(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                                        rocprim::counting_iterator<uint32_t>(0), (uint32_t*)nullptr, R, 0, 32);
+                                                    (const uint32_t*)nullptr, (uint32_t*)nullptr, R, 0, 32);
     return bytes;
 }
 
@@ -160,9 +163,9 @@ hipError_t tile_sort(BinningState& b, size_t R, unsigned end_bit, bool key16, hi
     size_t bytes = b.sort_temp_bytes;
     if (key16)
         return rocprim::radix_sort_pairs<SortConfig>(b.sort_temp, bytes, (const uint16_t*)b.keys, (uint16_t*)b.keys_sorted,
-                                         rocprim::counting_iterator<uint32_t>(0), b.e_sorted, R, 0, end_bit, stream);
+                                                     (const uint32_t*)b.emit_gid, b.gid_sorted, R, 0, end_bit, stream);
     return rocprim::radix_sort_pairs<SortConfig>(b.sort_temp, bytes, (const uint32_t*)b.keys, (uint32_t*)b.keys_sorted,
-                                     rocprim::counting_iterator<uint32_t>(0), b.e_sorted, R, 0, end_bit, stream);
+                                                 (const uint32_t*)b.emit_gid, b.gid_sorted, R, 0, end_bit, stream);
 }
 
 // ---- 5. per-tile [start, end) (identifyTileRanges, CR/rasterizer_impl.cu:132-164)

@@ -28,18 +28,21 @@ constexpr float SH_C3_0 = -0.5900435899266435f, SH_C3_1 = 2.890611442640554f, SH
                 SH_C3_6 = -0.5900435899266435f;
 
 // ---------------------------------------------------------------------------
-// Per-Gaussian splat record written by preprocess, read (gathered) by both
-// render passes: three 16-byte rows so a gather is three dwordx4 loads.
-//   r0 = (x_pix, y_pix, conic.a, conic.b)
-//   r1 = (conic.c, opacity_eff, 1/depth, bbox_x packed)
-//   r2 = (r, g, b, bbox_y packed)
+// Per-Gaussian splat record written by preprocess, gathered by both render
+// passes: one 64-byte, 64-byte-aligned block, so a gather touches one cache line.
+//   row 0 = (x_pix, y_pix, conic.a, conic.b)
+//   row 1 = (conic.c, opacity_eff, 1/depth, bbox_x packed)
+//   row 2 = (r, g, b, bbox_y packed)
+//   row 3 = (rect_min.x, rect_min.y, rect width, e0) as u32 bits
 // bbox_* are the conservative pixel bounds of the alpha >= 1/255 footprint
 // (int16 lo | int16 hi << 16), used to skip whole waves (DESIGN.md "footprint
-// culling").  lo > hi means "never contributes".
+// culling"); lo > hi means "never contributes".  Row 3 is the tile rectangle of
+// getRect and the Gaussian's first emission index (written by the duplicate
+// pass): the instance of this Gaussian in tile (tx, ty) has emission index
+// e0 + (ty - min.y) * width + (tx - min.x), the row-major order of
+// duplicateWithKeys (CR/rasterizer_impl.cu:108-124).
 // ---------------------------------------------------------------------------
-struct SplatRec {
-    float4 r0, r1, r2;
-};
+constexpr int kRecRows = 4;
 
 __host__ __device__ inline size_t align_up(size_t x, size_t a = kAlign) { return (x + a - 1) / a * a; }
 
@@ -59,9 +62,7 @@ struct Carver {
 
 // Geometry state: per Gaussian (P).
 struct GeomState {
-    float4* rec0;
-    float4* rec1;
-    float4* rec2;
+    float4* rec;                // [P][kRecRows] splat records
     uint32_t* depth_key;        // float bits of view-space z, 0xffffffff if culled
     uint32_t* depth_key_sorted; // sort output (unused after sorting)
     uint32_t* gid_by_rank;      // Gaussians in (depth, index) order
@@ -90,7 +91,7 @@ struct BinningState {
     void* keys;             // unsorted tile ids (u16 or u32), emission order
     void* keys_sorted;      // sorted tile ids
     uint32_t* emit_gid;     // Gaussian of each emitted instance
-    uint32_t* e_sorted;     // emission index of each sorted instance (Gaussian = emit_gid[e])
+    uint32_t* gid_sorted;   // Gaussian of each sorted instance (the tile lists)
     void* sort_temp;
     size_t sort_temp_bytes;
 };

@@ -29,11 +29,8 @@ struct RenderFwdArgs {
     int W, H;
     uint32_t gx, gy;
     const uint2* ranges;
-    const uint32_t* e_sorted;
-    const uint32_t* emit_gid;
-    const float4* rec0;
-    const float4* rec1;
-    const float4* rec2;
+    const uint32_t* gid_sorted;
+    const float4* rec;
     const float* bg;
     float* out_color;
     float* out_invdepth;
@@ -44,16 +41,15 @@ struct RenderBwdArgs {
     int W, H;
     uint32_t gx, gy;
     const uint2* ranges;
-    const uint32_t* e_sorted;
-    const uint32_t* emit_gid;
-    const float4* rec0;
-    const float4* rec1;
-    const float4* rec2;
+    const uint32_t* gid_sorted;
+    const float4* rec;
     const float* bg;
     const float* dL_dpix;       // [3,H,W]
     const float* dL_dinvdepth;  // [H,W] or null
     ImageState img;
     GradRecs recs;
+    const uint32_t* rank_of;    // depth rank of each Gaussian
+    uint32_t* rank_lim;         // [tiles] out: 1 + rank of the last entry that has a record (0: none)
 };
 
 struct GaussBwdArgs {
@@ -103,8 +99,8 @@ hipError_t launch_finalize(size_t R, const BinningState& b, uint2* ranges, bool 
 hipError_t launch_render_fwd(const RenderFwdArgs& a, hipStream_t stream);
 hipError_t launch_render_bwd(const RenderBwdArgs& a, hipStream_t stream);
 // backward.hip
-hipError_t launch_gauss_reduce(int P, const unsigned long long* offsets, const GradRecs& recs, const GradRecs& sums,
-                               hipStream_t stream);
+hipError_t launch_gauss_reduce(int P, const unsigned long long* offsets, const void* keys, bool key16,
+                               const uint32_t* rank_lim, const GradRecs& recs, const GradRecs& sums, hipStream_t stream);
 hipError_t launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t stream);
 
 }  // namespace gsr

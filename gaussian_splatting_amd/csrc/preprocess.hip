@@ -202,9 +202,11 @@ __global__ void __launch_bounds__(256) preprocess_kernel(PreprocessArgs a) {
 
     a.geom.depth_key[idx] = __float_as_uint(p_view.z);
     a.radii[idx] = irad;
-    a.geom.rec0[idx] = make_float4(px, py, ca, cb);
-    a.geom.rec1[idx] = make_float4(cc, o_eff, 1.0f / p_view.z, __uint_as_float(bbx));
-    a.geom.rec2[idx] = make_float4(rgb.x, rgb.y, rgb.z, __uint_as_float(bby));
+    float4* rec = a.geom.rec + (size_t)kRecRows * idx;
+    rec[0] = make_float4(px, py, ca, cb);
+    rec[1] = make_float4(cc, o_eff, 1.0f / p_view.z, __uint_as_float(bbx));
+    rec[2] = make_float4(rgb.x, rgb.y, rgb.z, __uint_as_float(bby));
+    rec[3] = make_float4(__uint_as_float(rmin.x), __uint_as_float(rmin.y), __uint_as_float(rmax.x - rmin.x), 0.f);
     a.geom.tiles_touched[idx] = touched;
 }
 

@@ -37,6 +37,14 @@ namespace gsr {
 
 constexpr int kBatch = 64;  // list entries staged per round (one per lane)
 
+// Occupancy target of the backward (waves per SIMD).  One wave per tile means 8160
+// waves at 1080p for 1024 SIMDs; the register budget decides how many run at once.
+#ifdef GSR_BWD_WAVES
+#define GSR_BWD_OCCUPANCY __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVES, GSR_BWD_WAVES)))
+#else
+#define GSR_BWD_OCCUPANCY
+#endif
+
 // Quadrant mask of one splat's footprint box inside the tile at (tile_x0, tile_y0).
 __device__ __forceinline__ uint32_t quad_bits(float4 v1, float4 v2, int tile_x0, int tile_y0) {
     const uint32_t bx = __float_as_uint(v1.w), by = __float_as_uint(v2.w);
@@ -123,10 +131,11 @@ __global__ void __launch_bounds__(64) render_fwd_kernel(RenderFwdArgs a) {
     const int tile_x0 = (int)(tile % a.gx) * kTile, tile_y0 = (int)(tile / a.gx) * kTile;
     const int lane = threadIdx.x;
     const int lx = lane & 7, ly = lane >> 3;
+    const float pxf0 = (float)(tile_x0 + lx), pyf0 = (float)(tile_y0 + ly);  // this lane's pixel in quadrant 0
 
     __shared__ float4 s_xy[kBatch], s_cq[kBatch], s_col[kBatch];  // (x, y, o, 1/z), (A, B, C, quads), rgb
 
-    float Tl[4], Tf[4], C0[4], C1[4], C2[4], D[4], pxq[4], pyq[4];
+    float Tl[4], Tf[4], C0[4], C1[4], C2[4], D[4];
     uint32_t last[4];
     uint32_t alive = 0;  // wave-uniform: slots with at least one pixel still blending
 #pragma unroll
@@ -135,8 +144,6 @@ __global__ void __launch_bounds__(64) render_fwd_kernel(RenderFwdArgs a) {
         Tl[q] = (px < a.W && py < a.H) ? 1.f : 0.f;
         Tf[q] = C0[q] = C1[q] = C2[q] = D[q] = 0.f;
         last[q] = 0;
-        pxq[q] = (float)px;
-        pyq[q] = (float)py;
         if (__any(Tl[q] > 0.f)) alive |= 1u << q;
     }
 
@@ -145,12 +152,12 @@ __global__ void __launch_bounds__(64) render_fwd_kernel(RenderFwdArgs a) {
     for (int b0 = 0; b0 < n && alive; b0 += kBatch) {
         uint32_t qm = 0;
         if (b0 + lane < n) {
-            const uint32_t g = a.emit_gid[a.e_sorted[range.x + b0 + lane]];
-            const float4 v0 = a.rec0[g], v1 = a.rec1[g], v2 = a.rec2[g];
-            qm = quad_bits_exact(v0, v1, v2, tile_x0, tile_y0);
+            const float4* rec = a.rec + (size_t)kRecRows * a.gid_sorted[range.x + b0 + lane];
+            const float4 v0 = rec[0], v1 = rec[1], v2 = rec[2];
             s_xy[lane] = make_float4(v0.x, v0.y, v1.y, v1.z);
-            s_cq[lane] = stage_conic(v0, v1, qm);
             s_col[lane] = v2;
+            qm = quad_bits_exact(v0, v1, v2, tile_x0, tile_y0);
+            s_cq[lane] = stage_conic(v0, v1, qm);
         }
         __syncthreads();
         unsigned long long todo = __ballot(qm != 0);
@@ -163,7 +170,7 @@ __global__ void __launch_bounds__(64) render_fwd_kernel(RenderFwdArgs a) {
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 if (!(m & (1u << q))) continue;  // uniform: footprint misses this quadrant
-                const float dx = xy.x - pxq[q], dy = xy.y - pyq[q];
+                const float dx = xy.x - (pxf0 + (float)((q & 1) * 8)), dy = xy.y - (pyf0 + (float)((q >> 1) * 8));
                 const float p2 = dx * (cq.x * dx + cq.y * dy) + cq.z * dy * dy;
                 float G;
                 const float alpha = splat_alpha(p2, xy.z, G);
@@ -214,23 +221,23 @@ hipError_t launch_render_fwd(const RenderFwdArgs& a, hipStream_t stream) {
 }
 
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a) {
+__global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(RenderBwdArgs a) {
     const uint32_t tile = blockIdx.x;
     const int tile_x0 = (int)(tile % a.gx) * kTile, tile_y0 = (int)(tile / a.gx) * kTile;
     const int lane = threadIdx.x;
     const int lx = lane & 7, ly = lane >> 3;
+    const float pxf0 = (float)(tile_x0 + lx), pyf0 = (float)(tile_y0 + ly);  // this lane's pixel in quadrant 0
 
     __shared__ float4 s_xy[kBatch], s_cq[kBatch], s_col[kBatch];  // as in the forward
+    __shared__ float4 s_abc[kBatch];                              // raw conic (a, b, c) for the flush
     __shared__ float4 s_acc[kBatch][3];                           // per entry: the 10 reduced sums (+2 pad)
 
     const size_t N = (size_t)a.W * a.H;
-    float T[4], gB[4], g0[4], g1[4], g2[4], gi[4], pxq[4], pyq[4];
+    float T[4], gB[4], g0[4], g1[4], g2[4], gi[4];
     int nc[4];
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         const int px = tile_x0 + (q & 1) * 8 + lx, py = tile_y0 + (q >> 1) * 8 + ly;
-        pxq[q] = (float)px;
-        pyq[q] = (float)py;
         T[q] = 1.f;
         nc[q] = 0;
         gB[q] = g0[q] = g1[q] = g2[q] = gi[q] = 0.f;
@@ -272,35 +279,29 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a) {
 
     const uint2 range = a.ranges[tile];
     const int n = (int)(range.y - range.x);
-    for (int b0 = 0; b0 < n; b0 += kBatch) {
-        const bool has = b0 + lane < n;
-        const uint32_t e = has ? a.e_sorted[range.x + b0 + lane] : 0u;
-        if (b0 >= limit) {  // uniform: zero records for entries no pixel reaches
-            if (has) {
-                a.recs.a[e] = make_float4(0.f, 0.f, 0.f, 0.f);
-                a.recs.b[e] = make_float4(0.f, 0.f, 0.f, 0.f);
-                a.recs.c[e] = make_float2(0.f, 0.f);
-            }
-            continue;
-        }
-        uint32_t qm = 0;
-        float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f);
-        float o = 0.f, cc = 0.f;
+    // Entries at positions >= limit get no gradient record at all: the per-Gaussian
+    // reduction recognises them by depth rank (tile lists are in rank order), using
+    // rank_lim[tile] = 1 + rank of the entry at position limit - 1 (0: none).
+    if (lane == 0)
+        a.rank_lim[tile] = limit > 0 ? a.rank_of[a.gid_sorted[range.x + limit - 1]] + 1u : 0u;
+    const uint32_t ttx = tile % a.gx, tty = tile / a.gx;
+    for (int b0 = 0; b0 < limit; b0 += kBatch) {
+        const bool has = b0 + lane < limit;
+        uint32_t qm = 0, e = 0;
         if (has) {
-            const uint32_t g = a.emit_gid[e];
-            v0 = a.rec0[g];
-            const float4 v1 = a.rec1[g], v2 = a.rec2[g];
-            qm = quad_bits_exact(v0, v1, v2, tile_x0, tile_y0);
-            o = v1.y;
-            cc = v1.x;
+            const float4* rec = a.rec + (size_t)kRecRows * a.gid_sorted[range.x + b0 + lane];
+            const float4 v0 = rec[0], v1 = rec[1], v2 = rec[2], v3 = rec[3];
+            // this instance's emission index (row 3: tile rectangle and first emission)
+            e = __float_as_uint(v3.w) + (tty - __float_as_uint(v3.y)) * __float_as_uint(v3.z) +
+                (ttx - __float_as_uint(v3.x));
             s_xy[lane] = make_float4(v0.x, v0.y, v1.y, v1.z);
-            s_cq[lane] = stage_conic(v0, v1, qm);
             s_col[lane] = v2;
+            s_abc[lane] = make_float4(v0.z, v0.w, v1.x, 0.f);  // raw conic, for the flush
+            qm = quad_bits_exact(v0, v1, v2, tile_x0, tile_y0);
+            s_cq[lane] = stage_conic(v0, v1, qm);
         }
         __syncthreads();
         unsigned long long todo = __ballot(qm != 0);
-        const int span = limit - b0;  // only positions < limit matter
-        if (span < 64) todo &= (1ull << span) - 1ull;
         unsigned long long written = 0;
         while (todo) {
             const int j = __builtin_ctzll(todo);
@@ -322,7 +323,7 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a) {
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 if (!(m & (1u << q))) continue;  // uniform
-                const float dx = xy.x - pxq[q], dy = xy.y - pyq[q];
+                const float dx = xy.x - (pxf0 + (float)((q & 1) * 8)), dy = xy.y - (pyf0 + (float)((q >> 1) * 8));
                 const float p2 = dx * (cq.x * dx + cq.y * dy) + cq.z * dy * dy;
                 float G;
                 float alpha = splat_alpha(p2, xy.z, G);
@@ -372,7 +373,8 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a) {
             float2 rc = make_float2(0.f, 0.f);
             if ((written >> lane) & 1ull) {
                 const float4 A = s_acc[lane][0], B = s_acc[lane][1], Cc = s_acc[lane][2];
-                const float ca = v0.z, cb = v0.w;
+                const float4 abc = s_abc[lane];
+                const float ca = abc.x, cb = abc.y, cc = abc.z, o = s_xy[lane].z;
                 // dL/dmean2D in NDC units (x 0.5 W, 0.5 H, CR/backward.cu:509-510,600-601);
                 // dL/dconic with the reference's -0.5 factors (CR/backward.cu:604-606)
                 ra = A;
