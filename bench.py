@@ -34,6 +34,9 @@ from gaussian_splatting_amd import synthetic as syn  # noqa: E402
 from gaussian_splatting_amd.distributed import GradArena  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+# HBM bytes per launch measured with rocprofv3 PMC passes (scripts/pmc_session.sh -> tools/pmc_summary.py);
+# reported as roofline.traffic for the dominant kernel when the profile has it.
+PMC_PROFILE = os.path.join(ROOT, "profiles", "pmc_latest.json")
 
 
 def algorithmic_bytes(stage: str, P: int, I: int, W: int, H: int, K: int) -> float:
@@ -64,21 +67,26 @@ def step_algorithmic_bytes(P, I, W, H, K):
     return (304 + 36 * K) * P + 132 * I + 48 * W * H
 
 
-def cpu_baseline(cfg_name: str, P: int, W: int, H: int, threads: int):
-    """Oracle (C restatement of the reference) forward + backward on the host, full frame, 1 rep."""
+def cpu_baseline(cfg_name: str, P: int, W: int, H: int, threads: int, min_seconds: float = 10.0):
+    """Oracle (C restatement of the reference, oracle/) forward + backward on the host, on the same
+    frame as the GPU, repeated until at least ``min_seconds`` of CPU work (a bounded sample)."""
     from oracle import oracle
 
     scene, cam = syn.config_scene(cfg_name, seed=0, P=P)
     gc, gd = syn.upstream_grads(H, W)
-    t0 = time.perf_counter()
-    r = oracle.forward(scene.means3D, scene.opacities, cam.viewmatrix, cam.projmatrix, cam.campos, cam.tanfovx,
-                       cam.tanfovy, H, W, shs=scene.shs, sh_degree=scene.sh_degree, scales=scene.scales,
-                       rotations=scene.rotations, nthreads=threads)
-    r.handle.backward(gc, gd, nthreads=threads)
-    dt = time.perf_counter() - t0
-    return {"value": P / dt, "unit": "Gaussian-splats/s", "cores": threads, "kind": "port",
-            "sample": f"full {cfg_name} frame ({P} Gaussians, {W}x{H}), forward+backward, 1 rep, "
-                      f"{dt:.2f} s on {threads} OpenMP threads (oracle/gsr_oracle.c, float32)"}
+    reps, total = 0, 0.0
+    while total < min_seconds and reps < 50:
+        t0 = time.perf_counter()
+        r = oracle.forward(scene.means3D, scene.opacities, cam.viewmatrix, cam.projmatrix, cam.campos, cam.tanfovx,
+                           cam.tanfovy, H, W, shs=scene.shs, sh_degree=scene.sh_degree, scales=scene.scales,
+                           rotations=scene.rotations, nthreads=threads)
+        r.handle.backward(gc, gd, nthreads=threads)
+        total += time.perf_counter() - t0
+        reps += 1
+        del r
+    return {"value": reps * P / total, "unit": "Gaussian-splats/s", "cores": threads, "kind": "port",
+            "sample": f"{reps} full {cfg_name} frames ({P} Gaussians, {W}x{H}), forward+backward, "
+                      f"{total:.1f} s on {threads} OpenMP threads (oracle/gsr_oracle.c, float32)"}
 
 
 def main():
@@ -152,6 +160,13 @@ def main():
         dom = max(per_stage, key=per_stage.get)
         dom_ms = per_stage[dom]
         alg = algorithmic_bytes(dom, P, nr, W, H, K)
+        traffic, traffic_src = None, None
+        if args.config == "1m_1080p_sh3" and os.path.exists(PMC_PROFILE):
+            prof = json.load(open(PMC_PROFILE))
+            kk = prof.get("kernels", {}).get(dom)
+            if kk:
+                traffic = kk["hbm_read_bytes"] + kk["hbm_write_bytes"]
+                traffic_src = prof.get("source")
         achieved = alg / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
         line = {
             "metric": "Gaussian-splats/sec fwd+bwd @1080p, 1M Gaussians",
@@ -170,7 +185,7 @@ def main():
                        "num_rendered": nr, "views": "one per GPU, yaw 5 deg x rank",
                        "parallelism": f"view-sharded x{world}" + (" + RCCL all-reduce" if world > 1 else "")},
             "roofline": {"kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "algorithmic_bytes_per_launch": alg, "mean_launch_ms": dom_ms},
             "stage_ms": {k: round(v, 4) for k, v in per_stage.items()},
             "step_algorithmic_GBs": step_algorithmic_bytes(P, nr, W, H, K) / (ms_per_step * 1e-3) / 1e9,

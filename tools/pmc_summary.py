@@ -42,8 +42,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
     ap.add_argument("--out")
+    ap.add_argument("--json", help="also write {kernel: {hbm_read_bytes, hbm_write_bytes, ...}} here")
     a = ap.parse_args()
     vals, meta = load(a.dir)
+    table = {}
     lines = ["| kernel | VGPR | LDS B | grid | VALU | SALU | LDS ops | VMEM rd | WAVE_CYC | ACTIVE_ANY | WAIT_INST | WAIT_ANY"
              " | LDS bank cf | HBM rd MB | HBM wr MB |", "|" + "---|" * 15]
     order = sorted(vals, key=lambda k: -sum(vals[k].get("SQ_WAVE_CYCLES", [0])) / max(1, len(vals[k].get("SQ_WAVE_CYCLES", [1]))))
@@ -57,12 +59,20 @@ def main():
         vg, lds, grid, wg = meta[k]
         rd = 2 * m("FETCH_SIZE") * 1024 / 1e6
         wr = m("WRITE_SIZE") * 1024 / 1e6
+        table[k] = {"hbm_read_bytes": rd * 1e6, "hbm_write_bytes": wr * 1e6, "valu_insts": m("SQ_INSTS_VALU"),
+                    "salu_insts": m("SQ_INSTS_SALU"), "wave_cycles": m("SQ_WAVE_CYCLES")}
         lines.append(f"| {k} | {vg} | {lds} | {grid} | {m('SQ_INSTS_VALU'):.3g} | {m('SQ_INSTS_SALU'):.3g} | "
                      f"{m('SQ_INSTS_LDS'):.3g} | {m('SQ_INSTS_VMEM_RD'):.3g} | {m('SQ_WAVE_CYCLES'):.3g} | "
                      f"{m('SQ_ACTIVE_INST_ANY'):.3g} | {m('SQ_WAIT_INST_ANY'):.3g} | {m('SQ_WAIT_ANY'):.3g} | "
                      f"{m('SQ_LDS_BANK_CONFLICT'):.3g} | {rd:.1f} | {wr:.1f} |")
     text = "\n".join(lines)
     print(text)
+    if a.json:
+        import json
+
+        with open(a.json, "w") as f:
+            json.dump({"source": a.dir, "correction": "read = 2 x FETCH_SIZE KiB (gfx950), write = WRITE_SIZE KiB",
+                       "kernels": table}, f, indent=1)
     if a.out:
         with open(a.out, "w") as f:
             f.write(f"# PMC summary ({a.dir}): mean per dispatch\n\n"
