@@ -13,6 +13,7 @@ Error behaviour follows the reference: a malformed ``means3D`` raises
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -20,6 +21,28 @@ import torch
 from . import _lib
 
 __all__ = ["rasterize_gaussians", "rasterize_gaussians_backward", "mark_visible"]
+
+
+# Sync-free forward (gsr_rasterize_forward_ex): the binning buffer is sized from a capacity
+# hint -- a slowly decaying maximum of recent num_rendered for the same (device, P, W, H),
+# plus a margin -- so the forward never waits for the host mid-way.  A hint that turns
+# out too small only costs a redo of the binning stage inside the library.
+# GSR_SYNC_FORWARD=1 restores the reference's synchronising forward.
+_capacity: dict = {}
+_CAP_MARGIN = 1.05
+_CAP_DECAY = 0.98
+_INT_MAX = 2**31 - 1
+
+
+def _capacity_hint(key) -> int:
+    if os.environ.get("GSR_SYNC_FORWARD", "0") == "1":
+        return 0
+    last = _capacity.get(key, 0)
+    return min(_INT_MAX, int(last * _CAP_MARGIN) + 1024) if last > 0 else 0
+
+
+def _note_rendered(key, nr: int) -> None:
+    _capacity[key] = max(int(nr), int(_capacity.get(key, 0) * _CAP_DECAY))
 
 
 def _stream_handle(device: torch.device) -> ctypes.c_void_p:
@@ -105,8 +128,10 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     ins = _Inputs(device)
     rg, rb, ri = _Resizer(geom), _Resizer(binning), _Resizer(img)
     nr = ctypes.c_int(0)
+    cap = ctypes.c_int(0)
+    key = (device.index, P, W, H)
     with torch.cuda.device(device):
-        rc = lib.gsr_rasterize_forward(
+        rc = lib.gsr_rasterize_forward_ex(
             rg.cb, None, rb.cb, None, ri.cb, None, P, int(degree), M,
             ins.req(background, "bg", small=True), W, H,
             ins.req(means3D, "means3D"), ins.opt(sh, "sh", align16=True), ins.opt(colors, "colors_precomp"),
@@ -116,8 +141,11 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
             ins.opt(campos if campos is not None and campos.device.type == "cuda" else
                     (campos.to(device) if campos is not None else None), "campos"),
             float(tan_fovx), float(tan_fovy), int(bool(prefiltered)), out_color.data_ptr(), out_invdepth.data_ptr(),
-            int(bool(antialiasing)), radii.data_ptr(), int(bool(debug)), _stream_handle(device), ctypes.byref(nr))
+            int(bool(antialiasing)), radii.data_ptr(), int(bool(debug)), _stream_handle(device), ctypes.byref(nr),
+            _capacity_hint(key), ctypes.byref(cap))
     _lib.check(rc, "rasterize_gaussians")
+    _note_rendered(key, nr.value)
+    binning._gsr_capacity = int(cap.value)  # the layout the backward must use (kept across save_for_backward)
     return int(nr.value), out_color, radii, geom, binning, img, out_invdepth
 
 
@@ -169,7 +197,7 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, opacities, 
     scratch = torch.empty(0, dtype=torch.uint8, device=device)
     rs = _Resizer(scratch)
     with torch.cuda.device(device):
-        rc = lib.gsr_rasterize_backward(
+        rc = lib.gsr_rasterize_backward_ex(
             P, int(degree), M, int(R), ins.req(background, "bg", small=True), W, H,
             ins.req(means3D, "means3D"), ins.opt(sh, "sh"), ins.opt(colors, "colors_precomp"),
             ins.req(opacities, "opacities"), ins.opt(scales, "scales"), float(scale_modifier),
@@ -184,7 +212,8 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, opacities, 
             dL_dmeans2D.data_ptr(), None, dL_dopacity.data_ptr(), dL_dcolors.data_ptr(),
             dL_dinvdepths.data_ptr() if has_inv else None, dL_dmeans3D.data_ptr(), dL_dcov3D.data_ptr(),
             dL_dsh.data_ptr() if M > 0 else None, dL_dscales.data_ptr(), dL_drotations.data_ptr(),
-            int(bool(antialiasing)), int(bool(debug)), rs.cb, None, _stream_handle(device))
+            int(bool(antialiasing)), int(bool(debug)), rs.cb, None, _stream_handle(device),
+            int(getattr(binningBuffer, "_gsr_capacity", 0)), int(binningBuffer.numel()))
     _lib.check(rc, "rasterize_gaussians_backward")
     return result
 

@@ -29,6 +29,12 @@ SIGNATURES = {
     "gsr_rasterize_backward": (_i, [_i, _i, _i, _i, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp,
                                     _vp, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                     _vp, _vp, _vp, _i, _i, ALLOC_FN, _vp, _vp]),
+    "gsr_rasterize_forward_ex": (_i, [ALLOC_FN, _vp, ALLOC_FN, _vp, ALLOC_FN, _vp, _i, _i, _i, _vp, _i, _i, _vp, _vp,
+                                      _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp, _f, _f, _i, _vp, _vp, _i, _vp, _i,
+                                      _vp, ctypes.POINTER(_i), _i, ctypes.POINTER(_i)]),
+    "gsr_rasterize_backward_ex": (_i, [_i, _i, _i, _i, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp,
+                                       _vp, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                       _vp, _vp, _vp, _i, _i, ALLOC_FN, _vp, _vp, _i, ctypes.c_size_t]),
     "gsr_mark_visible": (_i, [_i, _vp, _vp, _vp, _vp, _vp]),
     "gsr_last_error": (ctypes.c_char_p, []),
     "gsr_version": (ctypes.c_char_p, []),
@@ -84,8 +90,29 @@ def version() -> str:
 
 
 # ---- stage profiler ---------------------------------------------------------------
-def profile_enable(on: bool = True) -> None:
-    load().gsr_profile_enable(1 if on else 0)
+def stage_names() -> list:
+    lib = load()
+    out, i = [], 0
+    while True:
+        n = lib.gsr_profile_stage_name(i).decode()
+        if not n:
+            return out
+        out.append(n)
+        i += 1
+
+
+def profile_enable(on: bool = True, stages=None) -> None:
+    """Time all stages (stages=None) or only the named ones; on=False turns timing off."""
+    if not on:
+        mask = 0
+    elif stages is None:
+        mask = -1
+    else:
+        names = stage_names()
+        mask = 0
+        for s in stages:
+            mask |= 1 << names.index(s)
+    load().gsr_profile_enable(mask)
 
 
 def profile_reset() -> None:

@@ -53,7 +53,7 @@ const char* kStageNames[ST_COUNT] = {"preprocess", "depth_sort", "scan",       "
                                      "finalize",   "render_fwd", "render_bwd", "gauss_reduce", "gauss_bwd"};
 
 struct Profiler {
-    bool on = false;
+    unsigned mask = 0;  // bit s: record stage s
     std::mutex mu;
     struct Pending {
         int stage;
@@ -81,7 +81,7 @@ struct StageScope {
     hipStream_t stream;
     hipEvent_t a = nullptr;
     StageScope(int s, hipStream_t st) : stage(s), stream(st) {
-        if (g_prof.on) {
+        if ((g_prof.mask >> s) & 1u) {
             std::lock_guard<std::mutex> lk(g_prof.mu);
             a = g_prof.get();
             (void)hipEventRecord(a, stream);
@@ -189,9 +189,9 @@ const char* gsr_last_error(void) { return g_err; }
 
 const char* gsr_version(void) { return "gsr 0.1.0 gfx950"; }
 
-int gsr_profile_enable(int enable) {
+int gsr_profile_enable(int stage_mask) {
     std::lock_guard<std::mutex> lk(g_prof.mu);
-    g_prof.on = enable != 0;
+    g_prof.mask = (unsigned)stage_mask;
     return GSR_OK;
 }
 
@@ -244,18 +244,20 @@ int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const
     return GSR_OK;
 }
 
-int gsr_rasterize_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_alloc, void* binning_ctx,
-                          gsr_alloc_fn image_alloc, void* image_ctx, int P, int D, int M, const float* background,
-                          int width, int height, const float* means3D, const float* shs, const float* colors_precomp,
-                          const float* opacities, const float* scales, float scale_modifier, const float* rotations,
-                          const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix,
-                          const float* cam_pos, float tan_fovx, float tan_fovy, int prefiltered, float* out_color,
-                          float* out_invdepth, int antialiasing, int* radii, int debug, void* stream_,
-                          int* num_rendered) {
+namespace {
+int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_alloc, void* binning_ctx,
+                 gsr_alloc_fn image_alloc, void* image_ctx, int P, int D, int M, const float* background, int width,
+                 int height, const float* means3D, const float* shs, const float* colors_precomp,
+                 const float* opacities, const float* scales, float scale_modifier, const float* rotations,
+                 const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix, const float* cam_pos,
+                 float tan_fovx, float tan_fovy, int prefiltered, float* out_color, float* out_invdepth,
+                 int antialiasing, int* radii, int debug, void* stream_, int* num_rendered, int capacity_hint,
+                 int* binning_capacity) {
     using namespace gsr;
     g_err[0] = 0;
     hipStream_t stream = (hipStream_t)stream_;
     if (num_rendered) *num_rendered = 0;
+    if (binning_capacity) *binning_capacity = 0;
     if (P < 0 || width <= 0 || height <= 0)
         return fail(GSR_ERR_ARGUMENT, "rasterize_forward: invalid sizes P=%d W=%d H=%d", P, width, height);
     if (P == 0) return GSR_OK;  // RI/rasterize_points.cu:108: nothing is launched
@@ -274,7 +276,7 @@ int gsr_rasterize_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn 
     const float focal_x = width / (2.0f * tan_fovx);
     const uint32_t gx = (width + kTile - 1) / kTile, gy = (height + kTile - 1) / kTile;
     const uint32_t tiles = gx * gy;
-    const bool key16 = tiles <= 65536u;
+    const bool key16 = tiles < 65536u;  // the capacity-mode sentinel (= tiles) must fit the key
     const unsigned bit = bit_length(tiles);
 
     size_t geom_bytes = 0, img_bytes = 0;
@@ -321,62 +323,116 @@ int gsr_rasterize_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn 
     }
     if (int rc = check_debug(debug, stream, "scan")) return rc;
 
-    // The one host synchronisation of the forward (CR/rasterizer_impl.cu:313).
+    // Binning + render for a binning buffer of capacity C.  In exact mode C = R is read
+    // back first -- the reference's one host synchronisation (CR/rasterizer_impl.cu:313).
+    // In capacity mode (capacity_hint > 0) nothing waits for the host: the slots past the
+    // device-side instance count are padded with a sentinel tile, and R is read once at
+    // the end; if it exceeds C the binning is redone exactly.
+    auto read_total = [&](unsigned long long* total) -> int {
+        HIP_TRY(hipMemcpyAsync(total, geom.offsets + (P - 1), sizeof(*total), hipMemcpyDeviceToHost, stream),
+                "num_rendered copy");
+        HIP_TRY(hipStreamSynchronize(stream), "num_rendered sync");
+        if (*total > (unsigned long long)INT_MAX)
+            return fail(GSR_ERR_OVERFLOW, "rasterize_forward: %llu tile instances exceed INT_MAX", *total);
+        return GSR_OK;
+    };
+    auto bin_and_render = [&](size_t C, bool padded) -> int {
+        size_t bin_bytes = 0;
+        carve_binning(nullptr, C, key16, &bin_bytes);
+        char* bbase = (char*)call_alloc(binning_alloc, binning_ctx, bin_bytes);
+        if (!bbase) return fail(GSR_ERR_ALLOC, "rasterize_forward: binning buffer allocation failed");
+        BinningState bin = carve_binning(bbase, C, key16, &bin_bytes);
+        HIP_TRY(hipMemsetAsync(img.ranges, 0, tiles * sizeof(uint2), stream), "ranges memset");
+        if (C > 0) {
+            {
+                StageScope sc(ST_DUPLICATE, stream);
+                if (padded) HIP_TRY(launch_pad_keys(geom.offsets + (P - 1), C, bin, key16, tiles, stream), "pad");
+                HIP_TRY(launch_duplicate(P, geom, radii, gx, gy, bin, key16, C, stream), "duplicate");
+            }
+            if (int rc = check_debug(debug, stream, "duplicate")) return rc;
+            {
+                StageScope sc(ST_TILE_SORT, stream);
+                HIP_TRY(tile_sort(bin, C, bit, key16, stream), "tile_sort");
+            }
+            if (int rc = check_debug(debug, stream, "tile_sort")) return rc;
+            {
+                StageScope sc(ST_FINALIZE, stream);
+                HIP_TRY(launch_finalize(C, tiles, bin, img.ranges, key16, stream), "finalize");
+            }
+            if (int rc = check_debug(debug, stream, "finalize")) return rc;
+        }
+        {
+            StageScope sc(ST_RENDER_FWD, stream);
+            RenderFwdArgs ra{};
+            ra.W = width; ra.H = height; ra.gx = gx; ra.gy = gy; ra.ranges = img.ranges;
+            ra.gid_sorted = bin.gid_sorted; ra.rec = geom.rec; ra.bg = background;
+            ra.out_color = out_color; ra.out_invdepth = out_invdepth; ra.img = img;
+            HIP_TRY(launch_render_fwd(ra, stream), "render_fwd");
+        }
+        return check_debug(debug, stream, "render_fwd");
+    };
+
     unsigned long long total = 0;
-    HIP_TRY(hipMemcpyAsync(&total, geom.offsets + (P - 1), sizeof(total), hipMemcpyDeviceToHost, stream),
-            "num_rendered copy");
-    HIP_TRY(hipStreamSynchronize(stream), "num_rendered sync");
-    if (total > (unsigned long long)INT_MAX)
-        return fail(GSR_ERR_OVERFLOW, "rasterize_forward: %llu tile instances exceed INT_MAX", total);
-    const size_t R = (size_t)total;
-
-    size_t bin_bytes = 0;
-    carve_binning(nullptr, R, key16, &bin_bytes);
-    char* bbase = (char*)call_alloc(binning_alloc, binning_ctx, bin_bytes);
-    if (!bbase) return fail(GSR_ERR_ALLOC, "rasterize_forward: binning buffer allocation failed");
-    BinningState bin = carve_binning(bbase, R, key16, &bin_bytes);
-
-    HIP_TRY(hipMemsetAsync(img.ranges, 0, tiles * sizeof(uint2), stream), "ranges memset");
-    if (R > 0) {
-        {
-            StageScope sc(ST_DUPLICATE, stream);
-            HIP_TRY(launch_duplicate(P, geom, radii, gx, gy, bin, key16, stream), "duplicate");
+    size_t C = 0;
+    if (capacity_hint <= 0) {
+        if (int rc = read_total(&total)) return rc;
+        C = (size_t)total;
+        if (int rc = bin_and_render(C, false)) return rc;
+    } else {
+        C = (size_t)capacity_hint;
+        if (int rc = bin_and_render(C, true)) return rc;
+        if (int rc = read_total(&total)) return rc;
+        if (total > C) {  // the hint was too small: redo exactly (the buffer is re-requested larger)
+            C = (size_t)total;
+            if (int rc = bin_and_render(C, false)) return rc;
         }
-        if (int rc = check_debug(debug, stream, "duplicate")) return rc;
-        {
-            StageScope sc(ST_TILE_SORT, stream);
-            HIP_TRY(tile_sort(bin, R, bit, key16, stream), "tile_sort");
-        }
-        if (int rc = check_debug(debug, stream, "tile_sort")) return rc;
-        {
-            StageScope sc(ST_FINALIZE, stream);
-            HIP_TRY(launch_finalize(R, bin, img.ranges, key16, stream), "finalize");
-        }
-        if (int rc = check_debug(debug, stream, "finalize")) return rc;
     }
-    {
-        StageScope sc(ST_RENDER_FWD, stream);
-        RenderFwdArgs ra{};
-        ra.W = width; ra.H = height; ra.gx = gx; ra.gy = gy; ra.ranges = img.ranges; ra.gid_sorted = bin.gid_sorted;
-        ra.rec = geom.rec; ra.bg = background;
-        ra.out_color = out_color; ra.out_invdepth = out_invdepth; ra.img = img;
-        HIP_TRY(launch_render_fwd(ra, stream), "render_fwd");
-    }
-    if (int rc = check_debug(debug, stream, "render_fwd")) return rc;
-    if (num_rendered) *num_rendered = (int)R;
+    if (num_rendered) *num_rendered = (int)total;
+    if (binning_capacity) *binning_capacity = (int)C;
     return GSR_OK;
 }
+}  // namespace
 
-int gsr_rasterize_backward(int P, int D, int M, int R, const float* background, int width, int height,
-                           const float* means3D, const float* shs, const float* colors_precomp,
-                           const float* opacities, const float* scales, float scale_modifier, const float* rotations,
-                           const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix,
-                           const float* campos, float tan_fovx, float tan_fovy, const int* radii, void* geom_buffer,
-                           void* binning_buffer, void* image_buffer, const float* dL_dpix, const float* dL_dinvdepths,
-                           float* dL_dmean2D, float* dL_dconic, float* dL_dopacity, float* dL_dcolor,
-                           float* dL_dinvdepth, float* dL_dmean3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscale,
-                           float* dL_drot, int antialiasing, int debug, gsr_alloc_fn scratch_alloc,
-                           void* scratch_ctx, void* stream_) {
+int gsr_rasterize_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_alloc, void* binning_ctx,
+                          gsr_alloc_fn image_alloc, void* image_ctx, int P, int D, int M, const float* background,
+                          int width, int height, const float* means3D, const float* shs, const float* colors_precomp,
+                          const float* opacities, const float* scales, float scale_modifier, const float* rotations,
+                          const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix,
+                          const float* cam_pos, float tan_fovx, float tan_fovy, int prefiltered, float* out_color,
+                          float* out_invdepth, int antialiasing, int* radii, int debug, void* stream,
+                          int* num_rendered) {
+    return forward_impl(geom_alloc, geom_ctx, binning_alloc, binning_ctx, image_alloc, image_ctx, P, D, M, background,
+                        width, height, means3D, shs, colors_precomp, opacities, scales, scale_modifier, rotations,
+                        cov3D_precomp, viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, prefiltered, out_color,
+                        out_invdepth, antialiasing, radii, debug, stream, num_rendered, 0, nullptr);
+}
+
+int gsr_rasterize_forward_ex(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_alloc, void* binning_ctx,
+                             gsr_alloc_fn image_alloc, void* image_ctx, int P, int D, int M, const float* background,
+                             int width, int height, const float* means3D, const float* shs,
+                             const float* colors_precomp, const float* opacities, const float* scales,
+                             float scale_modifier, const float* rotations, const float* cov3D_precomp,
+                             const float* viewmatrix, const float* projmatrix, const float* cam_pos, float tan_fovx,
+                             float tan_fovy, int prefiltered, float* out_color, float* out_invdepth, int antialiasing,
+                             int* radii, int debug, void* stream, int* num_rendered, int capacity_hint,
+                             int* binning_capacity) {
+    return forward_impl(geom_alloc, geom_ctx, binning_alloc, binning_ctx, image_alloc, image_ctx, P, D, M, background,
+                        width, height, means3D, shs, colors_precomp, opacities, scales, scale_modifier, rotations,
+                        cov3D_precomp, viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, prefiltered, out_color,
+                        out_invdepth, antialiasing, radii, debug, stream, num_rendered, capacity_hint,
+                        binning_capacity);
+}
+
+namespace {
+int backward_impl(int P, int D, int M, int R, const float* background, int width, int height, const float* means3D,
+                  const float* shs, const float* colors_precomp, const float* opacities, const float* scales,
+                  float scale_modifier, const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
+                  const float* projmatrix, const float* campos, float tan_fovx, float tan_fovy, const int* radii,
+                  void* geom_buffer, void* binning_buffer, void* image_buffer, const float* dL_dpix,
+                  const float* dL_dinvdepths, float* dL_dmean2D, float* dL_dconic, float* dL_dopacity,
+                  float* dL_dcolor, float* dL_dinvdepth, float* dL_dmean3D, float* dL_dcov3D, float* dL_dsh,
+                  float* dL_dscale, float* dL_drot, int antialiasing, int debug, gsr_alloc_fn scratch_alloc,
+                  void* scratch_ctx, void* stream_, int binning_capacity, size_t binning_bytes) {
     using namespace gsr;
     g_err[0] = 0;
     hipStream_t stream = (hipStream_t)stream_;
@@ -398,11 +454,20 @@ int gsr_rasterize_backward(int P, int D, int M, int R, const float* background, 
     const float focal_x = width / (2.0f * tan_fovx);
     const uint32_t gx = (width + kTile - 1) / kTile, gy = (height + kTile - 1) / kTile;
     const uint32_t tiles = gx * gy;
-    const bool key16 = tiles <= 65536u;
+    const bool key16 = tiles < 65536u;
+    // the binning buffer is laid out for the capacity the forward used (>= R)
+    const size_t C = binning_capacity > 0 ? (size_t)binning_capacity : (size_t)R;
+    if (C < (size_t)R) return fail(GSR_ERR_ARGUMENT, "rasterize_backward: binning capacity %zu < R=%d", C, R);
     size_t tmp = 0;
+    if (binning_bytes) {
+        carve_binning(nullptr, C, key16, &tmp);
+        if (tmp != binning_bytes)
+            return fail(GSR_ERR_ARGUMENT, "rasterize_backward: binning buffer of %zu bytes does not match capacity %zu",
+                        binning_bytes, C);
+    }
     GeomState geom = carve_geom((char*)geom_buffer, P, &tmp);
     ImageState img = carve_image((char*)image_buffer, width, height, tiles, &tmp);
-    BinningState bin = carve_binning((char*)binning_buffer, (size_t)R, key16, &tmp);
+    BinningState bin = carve_binning((char*)binning_buffer, C, key16, &tmp);
     size_t rec_bytes = 0;
     GradRecs recs{}, sums{};
     uint32_t* rank_lim = nullptr;
@@ -443,6 +508,43 @@ int gsr_rasterize_backward(int P, int D, int M, int R, const float* background, 
     }
     if (int rc = check_debug(debug, stream, "gauss_bwd")) return rc;
     return GSR_OK;
+}
+}  // namespace
+
+int gsr_rasterize_backward(int P, int D, int M, int R, const float* background, int width, int height,
+                           const float* means3D, const float* shs, const float* colors_precomp,
+                           const float* opacities, const float* scales, float scale_modifier, const float* rotations,
+                           const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix,
+                           const float* campos, float tan_fovx, float tan_fovy, const int* radii, void* geom_buffer,
+                           void* binning_buffer, void* image_buffer, const float* dL_dpix, const float* dL_dinvdepths,
+                           float* dL_dmean2D, float* dL_dconic, float* dL_dopacity, float* dL_dcolor,
+                           float* dL_dinvdepth, float* dL_dmean3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscale,
+                           float* dL_drot, int antialiasing, int debug, gsr_alloc_fn scratch_alloc,
+                           void* scratch_ctx, void* stream) {
+    return backward_impl(P, D, M, R, background, width, height, means3D, shs, colors_precomp, opacities, scales,
+                         scale_modifier, rotations, cov3D_precomp, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy,
+                         radii, geom_buffer, binning_buffer, image_buffer, dL_dpix, dL_dinvdepths, dL_dmean2D,
+                         dL_dconic, dL_dopacity, dL_dcolor, dL_dinvdepth, dL_dmean3D, dL_dcov3D, dL_dsh, dL_dscale,
+                         dL_drot, antialiasing, debug, scratch_alloc, scratch_ctx, stream, 0, 0);
+}
+
+int gsr_rasterize_backward_ex(int P, int D, int M, int R, const float* background, int width, int height,
+                              const float* means3D, const float* shs, const float* colors_precomp,
+                              const float* opacities, const float* scales, float scale_modifier,
+                              const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
+                              const float* projmatrix, const float* campos, float tan_fovx, float tan_fovy,
+                              const int* radii, void* geom_buffer, void* binning_buffer, void* image_buffer,
+                              const float* dL_dpix, const float* dL_dinvdepths, float* dL_dmean2D, float* dL_dconic,
+                              float* dL_dopacity, float* dL_dcolor, float* dL_dinvdepth, float* dL_dmean3D,
+                              float* dL_dcov3D, float* dL_dsh, float* dL_dscale, float* dL_drot, int antialiasing,
+                              int debug, gsr_alloc_fn scratch_alloc, void* scratch_ctx, void* stream,
+                              int binning_capacity, size_t binning_bytes) {
+    return backward_impl(P, D, M, R, background, width, height, means3D, shs, colors_precomp, opacities, scales,
+                         scale_modifier, rotations, cov3D_precomp, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy,
+                         radii, geom_buffer, binning_buffer, image_buffer, dL_dpix, dL_dinvdepths, dL_dmean2D,
+                         dL_dconic, dL_dopacity, dL_dcolor, dL_dinvdepth, dL_dmean3D, dL_dcov3D, dL_dsh, dL_dscale,
+                         dL_drot, antialiasing, debug, scratch_alloc, scratch_ctx, stream, binning_capacity,
+                         binning_bytes);
 }
 
 }  // extern "C"

@@ -77,7 +77,7 @@ __global__ void __launch_bounds__(256) duplicate_kernel(int P, const uint32_t* _
                                                         const unsigned long long* __restrict__ offsets,
                                                         const int* __restrict__ radii, float4* __restrict__ rec,
                                                         uint32_t gx, uint32_t gy, KeyT* __restrict__ keys,
-                                                        uint32_t* __restrict__ emit_gid) {
+                                                        uint32_t* __restrict__ emit_gid, unsigned long long cap) {
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
     const int lane = threadIdx.x & 63;
     if (r - lane >= P) return;  // whole wave past the end (wave-uniform)
@@ -124,7 +124,7 @@ __global__ void __launch_bounds__(256) duplicate_kernel(int P, const uint32_t* _
         const uint32_t o_x0 = __shfl(rmin.x, lo);
         const uint32_t o_y0 = __shfl(rmin.y, lo);
         const uint32_t o_gid = __shfl(gid, lo);
-        if (k < total) {
+        if (k < total && E0 + k < cap) {  // cap: instances the binning buffer holds
             const uint32_t local = k - o_start;
             const uint32_t ty = local / o_w;
             const uint32_t tx = local - ty * o_w;
@@ -136,14 +136,38 @@ __global__ void __launch_bounds__(256) duplicate_kernel(int P, const uint32_t* _
 }
 
 hipError_t launch_duplicate(int P, const GeomState& g, const int* radii, uint32_t gx, uint32_t gy,
-                            const BinningState& b, bool key16, hipStream_t stream) {
+                            const BinningState& b, bool key16, size_t cap, hipStream_t stream) {
     const dim3 grid((P + 255) / 256), block(256);
     if (key16)
         hipLaunchKernelGGL(duplicate_kernel<uint16_t>, grid, block, 0, stream, P, g.gid_by_rank, g.offsets, radii,
-                           g.rec, gx, gy, (uint16_t*)b.keys, b.emit_gid);
+                           g.rec, gx, gy, (uint16_t*)b.keys, b.emit_gid, (unsigned long long)cap);
     else
         hipLaunchKernelGGL(duplicate_kernel<uint32_t>, grid, block, 0, stream, P, g.gid_by_rank, g.offsets, radii,
-                           g.rec, gx, gy, (uint32_t*)b.keys, b.emit_gid);
+                           g.rec, gx, gy, (uint32_t*)b.keys, b.emit_gid, (unsigned long long)cap);
+    return hipGetLastError();
+}
+
+// ---- 3b. capacity mode: the slots past the device-side instance count get the
+// sentinel tile id `tiles` (it fits in bit_length(tiles) bits and sorts last), so
+// the sort can run on a host-known capacity without a host round trip.
+template <typename KeyT>
+__global__ void pad_keys_kernel(const unsigned long long* __restrict__ total, unsigned long long cap,
+                                KeyT* __restrict__ keys, KeyT sentinel) {
+    const unsigned long long R = *total;
+    for (unsigned long long i = R + blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x; i < cap;
+         i += (unsigned long long)gridDim.x * blockDim.x)
+        keys[i] = sentinel;
+}
+
+hipError_t launch_pad_keys(const unsigned long long* total, size_t cap, const BinningState& b, bool key16,
+                           uint32_t sentinel, hipStream_t stream) {
+    const dim3 grid(512), block(256);
+    if (key16)
+        hipLaunchKernelGGL(pad_keys_kernel<uint16_t>, grid, block, 0, stream, total, (unsigned long long)cap,
+                           (uint16_t*)b.keys, (uint16_t)sentinel);
+    else
+        hipLaunchKernelGGL(pad_keys_kernel<uint32_t>, grid, block, 0, stream, total, (unsigned long long)cap,
+                           (uint32_t*)b.keys, sentinel);
     return hipGetLastError();
 }
 
@@ -169,11 +193,17 @@ hipError_t tile_sort(BinningState& b, size_t R, unsigned end_bit, bool key16, hi
 }
 
 // ---- 5. per-tile [start, end) (identifyTileRanges, CR/rasterizer_impl.cu:132-164)
+// Keys >= tiles are capacity-mode padding (sorted last) and own no range.
 template <typename KeyT>
-__global__ void finalize_kernel(uint32_t R, const KeyT* __restrict__ keys_sorted, uint2* __restrict__ ranges) {
+__global__ void finalize_kernel(uint32_t R, uint32_t tiles, const KeyT* __restrict__ keys_sorted,
+                                uint2* __restrict__ ranges) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= R) return;
     const uint32_t cur = keys_sorted[i];
+    if (cur >= tiles) {
+        if (i > 0 && keys_sorted[i - 1] < tiles) ranges[keys_sorted[i - 1]].y = i;
+        return;
+    }
     if (i == 0) {
         ranges[cur].x = 0;
     } else {
@@ -186,13 +216,14 @@ __global__ void finalize_kernel(uint32_t R, const KeyT* __restrict__ keys_sorted
     if (i == R - 1) ranges[cur].y = R;
 }
 
-hipError_t launch_finalize(size_t R, const BinningState& b, uint2* ranges, bool key16, hipStream_t stream) {
+hipError_t launch_finalize(size_t R, uint32_t tiles, const BinningState& b, uint2* ranges, bool key16,
+                           hipStream_t stream) {
     const dim3 grid((unsigned)((R + 255) / 256)), block(256);
     if (key16)
-        hipLaunchKernelGGL(finalize_kernel<uint16_t>, grid, block, 0, stream, (uint32_t)R,
+        hipLaunchKernelGGL(finalize_kernel<uint16_t>, grid, block, 0, stream, (uint32_t)R, tiles,
                            (const uint16_t*)b.keys_sorted, ranges);
     else
-        hipLaunchKernelGGL(finalize_kernel<uint32_t>, grid, block, 0, stream, (uint32_t)R,
+        hipLaunchKernelGGL(finalize_kernel<uint32_t>, grid, block, 0, stream, (uint32_t)R, tiles,
                            (const uint32_t*)b.keys_sorted, ranges);
     return hipGetLastError();
 }

@@ -91,10 +91,13 @@ hipError_t depth_sort(GeomState& g, int P, hipStream_t stream);
 size_t scan_temp_bytes(int P);
 hipError_t rank_and_scan(GeomState& g, int P, hipStream_t stream);
 hipError_t launch_duplicate(int P, const GeomState& g, const int* radii, uint32_t gx, uint32_t gy,
-                            const BinningState& b, bool key16, hipStream_t stream);
+                            const BinningState& b, bool key16, size_t cap, hipStream_t stream);
+hipError_t launch_pad_keys(const unsigned long long* total, size_t cap, const BinningState& b, bool key16,
+                           uint32_t sentinel, hipStream_t stream);
 size_t tile_sort_temp_bytes(size_t R, bool key16);
 hipError_t tile_sort(BinningState& b, size_t R, unsigned end_bit, bool key16, hipStream_t stream);
-hipError_t launch_finalize(size_t R, const BinningState& b, uint2* ranges, bool key16, hipStream_t stream);
+hipError_t launch_finalize(size_t R, uint32_t tiles, const BinningState& b, uint2* ranges, bool key16,
+                           hipStream_t stream);
 // render.hip
 hipError_t launch_render_fwd(const RenderFwdArgs& a, hipStream_t stream);
 hipError_t launch_render_bwd(const RenderBwdArgs& a, hipStream_t stream);

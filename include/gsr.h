@@ -69,6 +69,25 @@ int gsr_rasterize_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn 
                           float* out_invdepth, int antialiasing, int* radii, int debug, void* stream,
                           int* num_rendered);
 
+/* Same as gsr_rasterize_forward, without the mid-forward host synchronisation.
+ * The binning buffer is requested for capacity_hint instances before the count is
+ * known (typically the previous call's num_rendered plus a margin), the tile sort
+ * runs on that capacity with the unused slots padded, and the stream is
+ * synchronised once at the end to read num_rendered.  If num_rendered exceeds the
+ * hint, the binning stage is redone exactly (the binning callback is called again
+ * with a larger size).  capacity_hint <= 0 behaves like gsr_rasterize_forward.
+ * *binning_capacity receives the capacity the binning buffer was laid out for;
+ * pass it to gsr_rasterize_backward_ex. */
+int gsr_rasterize_forward_ex(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_alloc, void* binning_ctx,
+                             gsr_alloc_fn image_alloc, void* image_ctx, int P, int D, int M, const float* background,
+                             int width, int height, const float* means3D, const float* shs,
+                             const float* colors_precomp, const float* opacities, const float* scales,
+                             float scale_modifier, const float* rotations, const float* cov3D_precomp,
+                             const float* viewmatrix, const float* projmatrix, const float* cam_pos, float tan_fovx,
+                             float tan_fovy, int prefiltered, float* out_color, float* out_invdepth, int antialiasing,
+                             int* radii, int debug, void* stream, int* num_rendered, int capacity_hint,
+                             int* binning_capacity);
+
 /* Backward pass (CudaRasterizer::Rasterizer::backward).
  * R = num_rendered from the forward; geom/binning/image buffers are the ones the
  * forward's callbacks returned.  dL_dinvdepths ([1,H,W]) may be NULL, in which
@@ -87,6 +106,21 @@ int gsr_rasterize_backward(int P, int D, int M, int R, const float* background, 
                            float* dL_drot, int antialiasing, int debug, gsr_alloc_fn scratch_alloc,
                            void* scratch_ctx, void* stream);
 
+/* Backward for a forward made by gsr_rasterize_forward_ex: binning_capacity is the
+ * value it returned (0 = R); binning_bytes, if nonzero, is the binning buffer's size
+ * and is checked against the layout (a mismatch is GSR_ERR_ARGUMENT). */
+int gsr_rasterize_backward_ex(int P, int D, int M, int R, const float* background, int width, int height,
+                              const float* means3D, const float* shs, const float* colors_precomp,
+                              const float* opacities, const float* scales, float scale_modifier,
+                              const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
+                              const float* projmatrix, const float* campos, float tan_fovx, float tan_fovy,
+                              const int* radii, void* geom_buffer, void* binning_buffer, void* image_buffer,
+                              const float* dL_dpix, const float* dL_dinvdepths, float* dL_dmean2D, float* dL_dconic,
+                              float* dL_dopacity, float* dL_dcolor, float* dL_dinvdepth, float* dL_dmean3D,
+                              float* dL_dcov3D, float* dL_dsh, float* dL_dscale, float* dL_drot, int antialiasing,
+                              int debug, gsr_alloc_fn scratch_alloc, void* scratch_ctx, void* stream,
+                              int binning_capacity, size_t binning_bytes);
+
 /* Frustum test, view-space z > 0.2 (CudaRasterizer::Rasterizer::markVisible).
  * `present` is P bytes (bool). */
 int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
@@ -99,11 +133,14 @@ const char* gsr_last_error(void);
 const char* gsr_version(void);
 
 /* Per-stage device timing with hipEvents recorded on the launch stream.
- * enable=1 turns it on (it adds one event pair per stage).  collect() waits for
- * the recorded events and adds their elapsed times to running per-stage totals;
- * it returns the number of stages and fills up to max_stages totals (ms) and
- * call counts.  Stage names come from gsr_profile_stage_name(). */
-int gsr_profile_enable(int enable);
+ * stage_mask selects the stages to time (bit s = stage s, -1 = all, 0 = off);
+ * each timed stage adds one event pair to the stream (~10 us of idle GPU per
+ * event on gfx950, so time only what you need inside a measured region).
+ * collect() waits for the recorded events and adds their elapsed times to
+ * running per-stage totals; it returns the number of stages and fills up to
+ * max_stages totals (ms) and call counts.  Stage names come from
+ * gsr_profile_stage_name(). */
+int gsr_profile_enable(int stage_mask);
 int gsr_profile_collect(double* total_ms, long long* calls, int max_stages);
 void gsr_profile_reset(void);
 const char* gsr_profile_stage_name(int stage);

@@ -209,3 +209,31 @@ def test_matches_golden_fixture(name):
     torch.cuda.synchronize()
     for k, got in zip(C.GRAD_NAMES, out):
         assert C.rel_err(_to_np(got), exp[k]) <= RTOL_BWD, (name, k, C.rel_err(_to_np(got), exp[k]))
+
+
+def _run_pair(inp, gc, gd):
+    fwd = C.run_gpu_forward(inp)
+    out = C.run_gpu_backward(inp, fwd, gc, gd)
+    torch.cuda.synchronize()
+    return [fwd[0]] + [_to_np(fwd[i]) for i in (1, 2, 6)] + [_to_np(o) for o in out]
+
+
+@pytest.mark.parametrize("hint", ["previous", "too_small", "too_large"])
+def test_capacity_forward_matches_sync_forward(hint, monkeypatch):
+    """gsr_rasterize_forward_ex (no mid-forward host sync, binning sized from a capacity hint) gives bitwise
+    the same results as the reference-style synchronising forward, whether the hint fits, is too small (the
+    binning stage is redone) or is far too large (heavy sentinel padding in the sort)."""
+    from gaussian_splatting_amd import _C as CM
+
+    case = C.SMALL_CASES[-1]
+    inp = C.build(case)
+    gc, gd = C.unit_grads(case.H, case.W)
+    monkeypatch.setenv("GSR_SYNC_FORWARD", "1")
+    ref = _run_pair(inp, gc, gd)
+    monkeypatch.setenv("GSR_SYNC_FORWARD", "0")
+    key = (torch.cuda.current_device(), case.P, case.W, case.H)
+    CM._capacity[key] = {"previous": ref[0], "too_small": 10, "too_large": 40 * ref[0]}[hint]
+    got = _run_pair(inp, gc, gd)
+    assert got[0] == ref[0]
+    for a, b in zip(got[1:], ref[1:]):
+        np.testing.assert_array_equal(a, b)
