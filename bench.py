@@ -46,11 +46,11 @@ def algorithmic_bytes(stage: str, P: int, I: int, W: int, H: int, K: int) -> flo
         # reads means 12, scale 12, rot 16, opacity 4, SH 12K; writes radii 4, means2D 8, depth 4, conic+opacity 16,
         # rgb 12, tiles_touched 4
         "preprocess": (44 + 12 * K + 48) * P,
-        "depth_sort": 4 * 8 * P,  # 4 key bytes + 4 value bytes, read + write, one pass
-        "scan": 8 * P,
-        "duplicate": 20 * P + 12 * I,
-        "tile_sort": 24 * I,
-        "finalize": 8 * I,
+        # binning.hip: K1+K2 read rect 8 + tiles_touched 4 per Gaussian; K3 reads rect, tiles_touched, depth 16 and
+        # writes record starts 4 per Gaussian plus an 8 B key per instance; K4 reads the keys, writes 4 B ids
+        "bin_count": 12 * P,
+        "bin_scatter": 20 * P + 8 * I,
+        "tile_sort": 12 * I,
         # gather 44 B per instance (xy 8, conic+opacity 16, rgb 12, depth 4, index 4); write 24 B per pixel
         "render_fwd": 44 * I + 24 * N,
         # gather 44 B per instance; read 24 B per pixel; write the per-Gaussian accumulators (10 floats)

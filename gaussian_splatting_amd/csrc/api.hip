@@ -38,19 +38,17 @@ int fail(int code, const char* fmt, ...) {
 // ---- stage profiler -----------------------------------------------------------
 enum Stage {
     ST_PREPROCESS = 0,
-    ST_DEPTH_SORT,
-    ST_SCAN,
-    ST_DUPLICATE,
-    ST_TILE_SORT,
-    ST_FINALIZE,
+    ST_BIN_COUNT,    // K1 + K2 of binning.hip
+    ST_BIN_SCATTER,  // K3
+    ST_TILE_SORT,    // K4
     ST_RENDER_FWD,
     ST_RENDER_BWD,
     ST_GAUSS_REDUCE,
     ST_GAUSS_BWD,
     ST_COUNT
 };
-const char* kStageNames[ST_COUNT] = {"preprocess", "depth_sort", "scan",       "duplicate", "tile_sort",
-                                     "finalize",   "render_fwd", "render_bwd", "gauss_reduce", "gauss_bwd"};
+const char* kStageNames[ST_COUNT] = {"preprocess", "bin_count",  "bin_scatter",  "tile_sort",
+                                     "render_fwd", "render_bwd", "gauss_reduce", "gauss_bwd"};
 
 struct Profiler {
     unsigned mask = 0;  // bit s: record stage s
@@ -105,30 +103,24 @@ int check_debug(int debug, hipStream_t stream, const char* stage) {
     return GSR_OK;
 }
 
-unsigned bit_length(uint32_t n) {  // getHigherMsb (CR/rasterizer_impl.cu:36-51)
-    unsigned b = 0;
-    while (b < 32 && (n >> b)) b++;
-    return b;
-}
 
-gsr::GeomState carve_geom(char* base, int P, size_t* total) {
+gsr::GeomState carve_geom(char* base, int P, uint32_t tiles, size_t* total) {
     using namespace gsr;
     Carver c{base, 0};
     GeomState g{};
     g.rec = c.take<float4>((size_t)kRecRows * P);
     g.depth_key = c.take<uint32_t>(P);
-    g.depth_key_sorted = c.take<uint32_t>(P);
-    g.gid_by_rank = c.take<uint32_t>(P);
-    g.rank_of = c.take<uint32_t>(P);
     g.tiles_touched = c.take<uint32_t>(P);
-    g.tiles_ranked = c.take<uint32_t>(P);
-    g.offsets = c.take<unsigned long long>(P);
+    g.rect = c.take<uint2>(P);
+    g.rec_start = c.take<uint32_t>(P);
     g.clamped = c.take<uint8_t>(P);
     g.status = c.take<uint32_t>(4);
-    g.sort_temp_bytes = depth_sort_temp_bytes(P);
-    g.sort_temp = c.take<char>(g.sort_temp_bytes);
-    g.scan_temp_bytes = scan_temp_bytes(P);
-    g.scan_temp = c.take<char>(g.scan_temp_bytes);
+    g.tile_cnt = c.take<uint32_t>(tiles);
+    g.tile_cursor = c.take<uint32_t>(tiles);
+    const size_t chunks = bin_chunk_count(P);
+    g.chunk_total = c.take<unsigned long long>(chunks);
+    g.chunk_base = c.take<unsigned long long>(chunks);
+    g.total = c.take<unsigned long long>(1);
     *total = align_up(c.off);
     return g;
 }
@@ -146,27 +138,22 @@ gsr::ImageState carve_image(char* base, int W, int H, uint32_t tiles, size_t* to
     return im;
 }
 
-gsr::BinningState carve_binning(char* base, size_t R, bool key16, size_t* total) {
+gsr::BinningState carve_binning(char* base, size_t C, size_t* total) {
     using namespace gsr;
     Carver c{base, 0};
     BinningState b{};
-    const size_t ks = key16 ? 2 : 4;
-    b.keys = c.take<char>(R * ks);
-    b.keys_sorted = c.take<char>(R * ks);
-    b.emit_gid = c.take<uint32_t>(R);
-    b.gid_sorted = c.take<uint32_t>(R);
-    b.sort_temp_bytes = R ? tile_sort_temp_bytes(R, key16) : 0;
-    b.sort_temp = c.take<char>(b.sort_temp_bytes);
+    b.keys = c.take<unsigned long long>(C);
+    b.gid_sorted = c.take<uint32_t>(C);
     *total = align_up(c.off);
     return b;
 }
 
-// Backward scratch: R per-instance records, P per-rank sums, the per-tile rank limits.
+// Backward scratch: per-tile limit keys, R per-instance records, P per-Gaussian sums.
 void carve_recs(char* base, size_t R, size_t P, size_t tiles, gsr::GradRecs* recs, gsr::GradRecs* sums,
-                uint32_t** rank_lim, size_t* total) {
+                unsigned long long** lim_key, size_t* total) {
     using namespace gsr;
     Carver c{base, 0};
-    *rank_lim = c.take<uint32_t>(tiles);
+    *lim_key = c.take<unsigned long long>(tiles);
     recs->a = c.take<float4>(R);
     recs->b = c.take<float4>(R);
     recs->c = c.take<float2>(R);
@@ -276,14 +263,15 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
     const float focal_x = width / (2.0f * tan_fovx);
     const uint32_t gx = (width + kTile - 1) / kTile, gy = (height + kTile - 1) / kTile;
     const uint32_t tiles = gx * gy;
-    const bool key16 = tiles < 65536u;  // the capacity-mode sentinel (= tiles) must fit the key
-    const unsigned bit = bit_length(tiles);
+    if (gx > 65535u || gy > 65535u)
+        return fail(GSR_ERR_ARGUMENT, "rasterize_forward: image of %dx%d has more than 65535 tile columns/rows",
+                    width, height);
 
     size_t geom_bytes = 0, img_bytes = 0;
-    carve_geom(nullptr, P, &geom_bytes);
+    carve_geom(nullptr, P, tiles, &geom_bytes);
     char* gbase = (char*)call_alloc(geom_alloc, geom_ctx, geom_bytes);
     if (!gbase) return fail(GSR_ERR_ALLOC, "rasterize_forward: geometry buffer allocation failed");
-    GeomState geom = carve_geom(gbase, P, &geom_bytes);
+    GeomState geom = carve_geom(gbase, P, tiles, &geom_bytes);
     carve_image(nullptr, width, height, tiles, &img_bytes);
     char* ibase = (char*)call_alloc(image_alloc, image_ctx, img_bytes);
     if (!ibase) return fail(GSR_ERR_ALLOC, "rasterize_forward: image buffer allocation failed");
@@ -312,54 +300,45 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
             return fail(GSR_ERR_PREFILTERED,
                         "Point is filtered although prefiltered is set. This shouldn't happen! (CR/auxiliary.h:184)");
     }
+    // exact mode: counts first (ranges unclamped), then the host reads R
+    const size_t kNoCap = ~(size_t)0;
     {
-        StageScope sc(ST_DEPTH_SORT, stream);
-        HIP_TRY(depth_sort(geom, P, stream), "depth_sort");
+        StageScope sc(ST_BIN_COUNT, stream);
+        HIP_TRY(launch_bin_count(P, geom, gx, gy, img.ranges, capacity_hint > 0 ? (size_t)capacity_hint : kNoCap,
+                                 stream),
+                "bin_count");
     }
-    if (int rc = check_debug(debug, stream, "depth_sort")) return rc;
-    {
-        StageScope sc(ST_SCAN, stream);
-        HIP_TRY(rank_and_scan(geom, P, stream), "scan");
-    }
-    if (int rc = check_debug(debug, stream, "scan")) return rc;
+    if (int rc = check_debug(debug, stream, "bin_count")) return rc;
 
-    // Binning + render for a binning buffer of capacity C.  In exact mode C = R is read
-    // back first -- the reference's one host synchronisation (CR/rasterizer_impl.cu:313).
-    // In capacity mode (capacity_hint > 0) nothing waits for the host: the slots past the
-    // device-side instance count are padded with a sentinel tile, and R is read once at
-    // the end; if it exceeds C the binning is redone exactly.
+    // Scatter + tile sort + render into a binning buffer of capacity C.  In exact mode
+    // C = R is read back first -- the reference's one host synchronisation
+    // (CR/rasterizer_impl.cu:313).  In capacity mode (capacity_hint > 0) nothing waits
+    // for the host: R is read once at the end, and if it exceeds C the lists are
+    // rebuilt into a buffer of exactly R.
     auto read_total = [&](unsigned long long* total) -> int {
-        HIP_TRY(hipMemcpyAsync(total, geom.offsets + (P - 1), sizeof(*total), hipMemcpyDeviceToHost, stream),
-                "num_rendered copy");
+        HIP_TRY(hipMemcpyAsync(total, geom.total, sizeof(*total), hipMemcpyDeviceToHost, stream), "num_rendered copy");
         HIP_TRY(hipStreamSynchronize(stream), "num_rendered sync");
         if (*total > (unsigned long long)INT_MAX)
             return fail(GSR_ERR_OVERFLOW, "rasterize_forward: %llu tile instances exceed INT_MAX", *total);
         return GSR_OK;
     };
-    auto bin_and_render = [&](size_t C, bool padded) -> int {
+    auto bin_and_render = [&](size_t C) -> int {
         size_t bin_bytes = 0;
-        carve_binning(nullptr, C, key16, &bin_bytes);
+        carve_binning(nullptr, C, &bin_bytes);
         char* bbase = (char*)call_alloc(binning_alloc, binning_ctx, bin_bytes);
         if (!bbase) return fail(GSR_ERR_ALLOC, "rasterize_forward: binning buffer allocation failed");
-        BinningState bin = carve_binning(bbase, C, key16, &bin_bytes);
-        HIP_TRY(hipMemsetAsync(img.ranges, 0, tiles * sizeof(uint2), stream), "ranges memset");
+        BinningState bin = carve_binning(bbase, C, &bin_bytes);
         if (C > 0) {
             {
-                StageScope sc(ST_DUPLICATE, stream);
-                if (padded) HIP_TRY(launch_pad_keys(geom.offsets + (P - 1), C, bin, key16, tiles, stream), "pad");
-                HIP_TRY(launch_duplicate(P, geom, radii, gx, gy, bin, key16, C, stream), "duplicate");
+                StageScope sc(ST_BIN_SCATTER, stream);
+                HIP_TRY(launch_bin_scatter(P, geom, gx, gy, bin, C, stream), "bin_scatter");
             }
-            if (int rc = check_debug(debug, stream, "duplicate")) return rc;
+            if (int rc = check_debug(debug, stream, "bin_scatter")) return rc;
             {
                 StageScope sc(ST_TILE_SORT, stream);
-                HIP_TRY(tile_sort(bin, C, bit, key16, stream), "tile_sort");
+                HIP_TRY(launch_tile_sort(tiles, img.ranges, bin, C, stream), "tile_sort");
             }
             if (int rc = check_debug(debug, stream, "tile_sort")) return rc;
-            {
-                StageScope sc(ST_FINALIZE, stream);
-                HIP_TRY(launch_finalize(C, tiles, bin, img.ranges, key16, stream), "finalize");
-            }
-            if (int rc = check_debug(debug, stream, "finalize")) return rc;
         }
         {
             StageScope sc(ST_RENDER_FWD, stream);
@@ -377,14 +356,15 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
     if (capacity_hint <= 0) {
         if (int rc = read_total(&total)) return rc;
         C = (size_t)total;
-        if (int rc = bin_and_render(C, false)) return rc;
+        if (int rc = bin_and_render(C)) return rc;
     } else {
         C = (size_t)capacity_hint;
-        if (int rc = bin_and_render(C, true)) return rc;
+        if (int rc = bin_and_render(C)) return rc;
         if (int rc = read_total(&total)) return rc;
-        if (total > C) {  // the hint was too small: redo exactly (the buffer is re-requested larger)
+        if (total > C) {  // the hint was too small: recount (resets the cursors) and rebuild exactly
             C = (size_t)total;
-            if (int rc = bin_and_render(C, false)) return rc;
+            HIP_TRY(launch_bin_count(P, geom, gx, gy, img.ranges, C, stream), "bin_count");
+            if (int rc = bin_and_render(C)) return rc;
         }
     }
     if (num_rendered) *num_rendered = (int)total;
@@ -454,27 +434,26 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
     const float focal_x = width / (2.0f * tan_fovx);
     const uint32_t gx = (width + kTile - 1) / kTile, gy = (height + kTile - 1) / kTile;
     const uint32_t tiles = gx * gy;
-    const bool key16 = tiles < 65536u;
     // the binning buffer is laid out for the capacity the forward used (>= R)
     const size_t C = binning_capacity > 0 ? (size_t)binning_capacity : (size_t)R;
     if (C < (size_t)R) return fail(GSR_ERR_ARGUMENT, "rasterize_backward: binning capacity %zu < R=%d", C, R);
     size_t tmp = 0;
-    if (binning_bytes) {
-        carve_binning(nullptr, C, key16, &tmp);
+    if (binning_bytes && C > 0) {  // (an empty forward still got a 1-byte buffer)
+        carve_binning(nullptr, C, &tmp);
         if (tmp != binning_bytes)
             return fail(GSR_ERR_ARGUMENT, "rasterize_backward: binning buffer of %zu bytes does not match capacity %zu",
                         binning_bytes, C);
     }
-    GeomState geom = carve_geom((char*)geom_buffer, P, &tmp);
+    GeomState geom = carve_geom((char*)geom_buffer, P, tiles, &tmp);
     ImageState img = carve_image((char*)image_buffer, width, height, tiles, &tmp);
-    BinningState bin = carve_binning((char*)binning_buffer, C, key16, &tmp);
+    BinningState bin = carve_binning((char*)binning_buffer, C, &tmp);
     size_t rec_bytes = 0;
     GradRecs recs{}, sums{};
-    uint32_t* rank_lim = nullptr;
-    carve_recs(nullptr, (size_t)R, (size_t)P, tiles, &recs, &sums, &rank_lim, &rec_bytes);
+    unsigned long long* lim_key = nullptr;
+    carve_recs(nullptr, (size_t)R, (size_t)P, tiles, &recs, &sums, &lim_key, &rec_bytes);
     char* rbase = (char*)call_alloc(scratch_alloc, scratch_ctx, rec_bytes);
     if (!rbase) return fail(GSR_ERR_ALLOC, "rasterize_backward: scratch allocation failed");
-    carve_recs(rbase, (size_t)R, (size_t)P, tiles, &recs, &sums, &rank_lim, &rec_bytes);
+    carve_recs(rbase, (size_t)R, (size_t)P, tiles, &recs, &sums, &lim_key, &rec_bytes);
 
     if (R > 0) {
         StageScope sc(ST_RENDER_BWD, stream);
@@ -482,13 +461,13 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
         ra.W = width; ra.H = height; ra.gx = gx; ra.gy = gy; ra.ranges = img.ranges; ra.gid_sorted = bin.gid_sorted;
         ra.rec = geom.rec;
         ra.bg = background; ra.dL_dpix = dL_dpix; ra.dL_dinvdepth = dL_dinvdepths; ra.img = img; ra.recs = recs;
-        ra.rank_of = geom.rank_of; ra.rank_lim = rank_lim;
+        ra.depth_key = geom.depth_key; ra.lim_key = lim_key;
         HIP_TRY(launch_render_bwd(ra, stream), "render_bwd");
     }
     if (int rc = check_debug(debug, stream, "render_bwd")) return rc;
     {
         StageScope sc(ST_GAUSS_REDUCE, stream);
-        HIP_TRY(launch_gauss_reduce(P, geom.offsets, bin.keys, key16, rank_lim, recs, sums, stream), "gauss_reduce");
+        HIP_TRY(launch_gauss_reduce(P, geom, gx, lim_key, recs, sums, stream), "gauss_reduce");
     }
     if (int rc = check_debug(debug, stream, "gauss_reduce")) return rc;
     {

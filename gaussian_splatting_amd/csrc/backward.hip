@@ -1,9 +1,9 @@
 // backward.hip -- per-Gaussian backward.
 //
-//   gauss_reduce_kernel (one thread per depth rank): sums each Gaussian's
-//     per-(tile) gradient records.  They are contiguous in emission (= rank)
-//     order, so consecutive lanes read consecutive memory and the sum is
-//     deterministic -- no atomics.
+//   gauss_reduce_kernel (one lane per Gaussian): sums each Gaussian's
+//     per-(tile) gradient records.  They are contiguous per Gaussian and the
+//     Gaussians' ranges follow each other, so consecutive lanes read
+//     consecutive memory and the sum is deterministic -- no atomics.
 //   gauss_bwd_kernel (one wave per 64 Gaussians):
 //     - computeCov2DCUDA (CR/backward.cu:153-290) including the tail that the
 //       vendored file truncates (dL/dcov3D and dL/dmean3D through the EWA
@@ -22,82 +22,97 @@
 
 namespace gsr {
 
-// ---- 1. segmented sums of the per-instance records, in rank order -------------
-// One wave per 64 consecutive ranks.  Their records form one contiguous range
-// [E0, E1); it is streamed through LDS 64 records at a time with fully coalesced
-// loads, and every lane sums the rows of its own segment from LDS in order, so
-// the result does not depend on scheduling.  The render backward writes records
-// only for entries before each tile's last contributor; an instance (rank r,
-// tile t) has one iff r < rank_lim[t], and the others are read as zeros without
-// touching memory (render.hip, "Entries at positions >= limit").
+// ---- 1. segmented sums of the per-instance records ------------------------------
+// One wave per 64 consecutive Gaussians.  Their records form one contiguous range
+// [E0, E1) (record index = rec_start[g] + k, k = the tile's row-major index in g's
+// rectangle); it is streamed through LDS 64 records at a time with fully coalesced
+// loads, and every lane sums the rows of its own segment from LDS in order, so the
+// result does not depend on scheduling.  The render backward writes records only
+// for entries before each tile's last contributor; instance (g, tile t) has one iff
+// key(g) = depth bits << 32 | g <= lim_key[t] (tile lists are sorted by key), and
+// the others are read as zeros without touching memory (render.hip, "Entries at
+// positions >= limit").
 constexpr int kRecStride = 12;  // floats per staged record row (10 used), 48 B
 
-template <typename KeyT>
-__global__ void __launch_bounds__(64) gauss_reduce_kernel(int P, const unsigned long long* __restrict__ offsets,
-                                                          const KeyT* __restrict__ keys,
-                                                          const uint32_t* __restrict__ rank_lim, GradRecs recs,
-                                                          GradRecs sums) {
+__global__ void __launch_bounds__(64) gauss_reduce_kernel(int P, const uint32_t* __restrict__ rec_start,
+                                                          const uint32_t* __restrict__ tiles_touched,
+                                                          const uint2* __restrict__ rect,
+                                                          const uint32_t* __restrict__ depth_key, uint32_t gx,
+                                                          const unsigned long long* __restrict__ lim_key,
+                                                          GradRecs recs, GradRecs sums) {
     __shared__ __attribute__((aligned(16))) float s_rec[64 * kRecStride];
     const int lane = threadIdx.x;
-    const int r0 = blockIdx.x * 64;
-    const int r = r0 + lane;
-    const int r_last = min(r0 + 63, P - 1);
-    const unsigned long long E0 = r0 == 0 ? 0ull : offsets[r0 - 1];
-    const unsigned long long E1 = offsets[r_last];
-    const unsigned long long my1 = r < P ? offsets[r] : E1;
-    const unsigned long long my0 = r == 0 ? 0ull : (r < P ? offsets[r - 1] : E1);
+    const int g0 = blockIdx.x * 64;
+    const int g = g0 + lane;
+    const bool valid = g < P;
+    const int g_last = min(g0 + 63, P - 1);
+    const uint32_t E0 = rec_start[g0];
+    const uint32_t E1 = rec_start[g_last] + tiles_touched[g_last];
+    const uint32_t n = valid ? tiles_touched[g] : 0u;
+    const uint32_t my0 = valid ? rec_start[g] : E1;
+    const uint32_t my1 = my0 + n;
+    uint32_t x0 = 0, y0 = 0, w = 1;
+    unsigned long long key = ~0ull;
+    if (n) {
+        const uint2 rr = rect[g];
+        x0 = rr.x & 0xffffu;
+        y0 = rr.x >> 16;
+        w = (rr.y & 0xffffu) - x0;
+        key = ((unsigned long long)depth_key[g] << 32) | (uint32_t)g;
+    }
     float4 sa = make_float4(0.f, 0.f, 0.f, 0.f), sb = sa;
     float2 sc = make_float2(0.f, 0.f);
-    for (unsigned long long base = E0; base < E1; base += 64) {
-        const unsigned long long e = base + lane;
+    for (uint32_t base = E0; base < E1; base += 64) {
+        const uint32_t e = base + lane;
         // owner of slot e: the largest lane whose segment starts at or before it
-        const unsigned long long my0c = my0;
         int owner = 0;
 #pragma unroll
         for (int step = 32; step > 0; step >>= 1) {
             const int cand = owner + step;
-            const unsigned long long v = __shfl(my0c, cand & 63);
+            const uint32_t v = __shfl(my0, cand & 63);
             if (cand < 64 && v <= e) owner = cand;
         }
+        const uint32_t o0 = __shfl(my0, owner), ow = __shfl(w, owner), ox = __shfl(x0, owner),
+                       oy = __shfl(y0, owner);
+        const unsigned long long okey = __shfl(key, owner);
         float4 x = make_float4(0.f, 0.f, 0.f, 0.f), y = x;
         float2 z = make_float2(0.f, 0.f);
-        if (e < E1 && (uint32_t)(r0 + owner) < rank_lim[keys[e]]) {
-            x = recs.a[e];
-            y = recs.b[e];
-            z = recs.c[e];
+        if (e < E1) {
+            const uint32_t k = e - o0, ty = k / ow, tile = (oy + ty) * gx + ox + (k - ty * ow);
+            if (okey <= lim_key[tile]) {
+                x = recs.a[e];
+                y = recs.b[e];
+                z = recs.c[e];
+            }
         }
         float4* row = reinterpret_cast<float4*>(&s_rec[lane * kRecStride]);
         row[0] = x;
         row[1] = y;
         row[2] = make_float4(z.x, z.y, 0.f, 0.f);
         __syncthreads();
-        const unsigned long long lo = my0 > base ? my0 : base;
-        const unsigned long long hi = my1 < base + 64 ? my1 : base + 64;
-        for (unsigned long long k = lo; k < hi; k++) {
+        const uint32_t lo = my0 > base ? my0 : base;
+        const uint32_t hi = my1 < base + 64 ? my1 : base + 64;
+        for (uint32_t k = lo; k < hi; k++) {
             const float4* rr = reinterpret_cast<const float4*>(&s_rec[(int)(k - base) * kRecStride]);
-            const float4 p = rr[0], q = rr[1], w = rr[2];
+            const float4 p = rr[0], q = rr[1], ww = rr[2];
             sa.x += p.x; sa.y += p.y; sa.z += p.z; sa.w += p.w;
             sb.x += q.x; sb.y += q.y; sb.z += q.z; sb.w += q.w;
-            sc.x += w.x; sc.y += w.y;
+            sc.x += ww.x; sc.y += ww.y;
         }
         __syncthreads();
     }
-    if (r < P) {
-        sums.a[r] = sa;
-        sums.b[r] = sb;
-        sums.c[r] = sc;
+    if (valid) {
+        sums.a[g] = sa;
+        sums.b[g] = sb;
+        sums.c[g] = sc;
     }
 }
 
-hipError_t launch_gauss_reduce(int P, const unsigned long long* offsets, const void* keys, bool key16,
-                               const uint32_t* rank_lim, const GradRecs& recs, const GradRecs& sums, hipStream_t stream) {
+hipError_t launch_gauss_reduce(int P, const GeomState& g, uint32_t gx, const unsigned long long* lim_key,
+                               const GradRecs& recs, const GradRecs& sums, hipStream_t stream) {
     if (P == 0) return hipSuccess;
-    if (key16)
-        hipLaunchKernelGGL(gauss_reduce_kernel<uint16_t>, dim3((P + 63) / 64), dim3(64), 0, stream, P, offsets,
-                           (const uint16_t*)keys, rank_lim, recs, sums);
-    else
-        hipLaunchKernelGGL(gauss_reduce_kernel<uint32_t>, dim3((P + 63) / 64), dim3(64), 0, stream, P, offsets,
-                           (const uint32_t*)keys, rank_lim, recs, sums);
+    hipLaunchKernelGGL(gauss_reduce_kernel, dim3((P + 63) / 64), dim3(64), 0, stream, P, g.rec_start, g.tiles_touched,
+                       g.rect, g.depth_key, gx, lim_key, recs, sums);
     return hipGetLastError();
 }
 
@@ -228,7 +243,7 @@ __global__ void __launch_bounds__(64) gauss_bwd_kernel(GaussBwdArgs a) {
     }
     if (visible) {
         // ---- summed render gradients of this Gaussian
-        const uint32_t r = a.geom.rank_of[idx];
+        const uint32_t r = (uint32_t)idx;  // sums are per Gaussian
         const float4 sa = a.sums.a[r], sb = a.sums.b[r];
         const float2 sc = a.sums.c[r];
         const float3 dcol = make_float3(sa.x, sa.y, sa.z);

@@ -1,230 +1,355 @@
-// binning.hip -- depth pre-sort, tile-touch scan, wave-cooperative instance
-// emission, 16-bit tile radix sort and tile ranges.
+// binning.hip -- per-tile Gaussian lists in (depth, index) order, without a
+// global sort.
 //
-// The reference sorts one 64-bit key (tile << 32 | depth bits) per instance
-// with a stable radix sort over 32+log2(tiles) bits (CR/rasterizer_impl.cu:78-126,
-// 332-340).  Here the same total order -- (tile, depth, Gaussian index) -- is
-// produced in two cheaper sorts:
-//   1. a stable 32-bit sort of the P Gaussians by depth bits (ties keep index order),
-//   2. instances are emitted in that depth order and stably sorted by tile id only
-//      (16 bits while tiles <= 65536: two radix passes instead of six).
-// Stability of (2) keeps each tile's list in (depth, index) order, which is
-// exactly the reference's order.
-#include <cstring>
-
+// The reference emits one (tile << 32 | depth) key per (tile, Gaussian) instance
+// and radix-sorts all of them over 32 + log2(tiles) bits (duplicateWithKeys and
+// the CUB sort, CR/rasterizer_impl.cu:78-126, 332-340), which yields each tile's
+// list in (depth, index) order.  Here the same lists are built in four passes:
+//
+//   K1 tile_count    every workgroup owns a contiguous chunk of Gaussians and
+//                    counts its tile hits in an LDS histogram (two 16-bit
+//                    counters per word), flushed with one atomic add per tile;
+//                    it also sums the chunk's tiles_touched;
+//   K2 tile_scan     one workgroup: exclusive scans of the tile counts (-> the
+//                    per-tile ranges, identifyTileRanges' output) and of the
+//                    chunk totals (-> each chunk's first record index);
+//   K3 tile_scatter  every chunk reserves a block per tile with ONE returning
+//                    atomic and scatters 64-bit keys (depth bits << 32 | index)
+//                    into it; it also writes each Gaussian's first record index;
+//   K4 tile_sort     per tile, an in-LDS sorting network on the keys (one
+//                    workgroup per tile, sized by the list length), writing the
+//                    Gaussian ids -- the tile lists the render passes walk.
+//
+// The order inside a tile is fully determined by the (depth bits, index) keys,
+// which is exactly the reference's order (its sort is stable on index-ordered
+// input), so the result is deterministic although K3's scatter order is not.
+// No global sort, no memsets of lookback state, no host round trip: the
+// instance count never leaves the device until the forward ends.
 #include "kernels.h"
-
-#include <rocprim/rocprim.hpp>
 
 namespace gsr {
 
-// Always take the onesweep radix path: rocPRIM's default switches to block sort +
-// merge sort up to 2^20 items, which costs 20+ launches at P = 1M.
-using SortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
-                                              rocprim::default_config, 0>;
+constexpr int kBinThreads = 1024;
+constexpr uint32_t kLdsTilesMax = 36864;  // K3 keeps one u32 per tile in LDS (144 KiB)
 
-// ---- 1. depth pre-sort ------------------------------------------------------
-size_t depth_sort_temp_bytes(int P) {
-    size_t bytes = 0;
-    (void)rocprim::radix_sort_pairs<SortConfig>(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                                    rocprim::counting_iterator<uint32_t>(0), (uint32_t*)nullptr, (size_t)P, 0, 32);
-    return bytes;
+__device__ __forceinline__ void unpack_rect(uint2 r, uint32_t& x0, uint32_t& y0, uint32_t& x1, uint32_t& y1) {
+    x0 = r.x & 0xffffu;
+    y0 = r.x >> 16;
+    x1 = r.y & 0xffffu;
+    y1 = r.y >> 16;
 }
 
-hipError_t depth_sort(GeomState& g, int P, hipStream_t stream) {
-    size_t bytes = g.sort_temp_bytes;
-    return rocprim::radix_sort_pairs<SortConfig>(g.sort_temp, bytes, g.depth_key, g.depth_key_sorted,
-                                     rocprim::counting_iterator<uint32_t>(0), g.gid_by_rank, (size_t)P, 0, 32, stream);
+// Sum over the workgroup (a multiple of 64 threads); result valid in every thread.
+template <typename T>
+__device__ T block_sum(T v, T* s_tmp) {
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) s_tmp[w] = v;
+    __syncthreads();
+    T t = 0;
+    for (int i = 0; i < nw; i++) t += s_tmp[i];
+    return t;
 }
 
-// ---- 2. ranked tile counts + inverse permutation, then a 64-bit inclusive scan
-__global__ void rank_prep_kernel(int P, const uint32_t* __restrict__ gid_by_rank,
-                                 const uint32_t* __restrict__ tiles_touched, uint32_t* __restrict__ tiles_ranked,
-                                 uint32_t* __restrict__ rank_of) {
-    const int r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= P) return;
-    const uint32_t gid = gid_by_rank[r];
-    tiles_ranked[r] = tiles_touched[gid];
-    rank_of[gid] = (uint32_t)r;
+// Exclusive scan over the workgroup of one value per thread (thread order).
+template <typename T>
+__device__ T block_exclusive_scan(T v, T* s_tmp, T* total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    T incl = v;
+    for (int off = 1; off < 64; off <<= 1) {
+        const T u = __shfl_up(incl, off);
+        if (lane >= off) incl += u;
+    }
+    __syncthreads();
+    if (lane == 63) s_tmp[w] = incl;
+    __syncthreads();
+    T base = 0, all = 0;
+    for (int i = 0; i < nw; i++) {
+        if (i < w) base += s_tmp[i];
+        all += s_tmp[i];
+    }
+    if (total) *total = all;
+    return base + incl - v;
 }
 
-size_t scan_temp_bytes(int P) {
-    size_t bytes = 0;
-    (void)rocprim::inclusive_scan(nullptr, bytes, (const uint32_t*)nullptr, (unsigned long long*)nullptr, (size_t)P,
-                            rocprim::plus<unsigned long long>());
-    return bytes;
+// ---- K1 ---------------------------------------------------------------------
+template <bool LDS>
+__global__ void __launch_bounds__(kBinThreads) tile_count_kernel(int P, int chunk, const uint2* __restrict__ rect,
+                                                                 const uint32_t* __restrict__ tiles_touched,
+                                                                 uint32_t tiles, uint32_t gx, uint32_t* __restrict__ cnt,
+                                                                 unsigned long long* __restrict__ chunk_total) {
+    extern __shared__ uint32_t s_hist[];  // (tiles + 1) / 2 words: 16-bit counters (a chunk has < 65536 Gaussians)
+    __shared__ unsigned long long s_tmp[kBinThreads / 64];
+    const int g0 = blockIdx.x * chunk, g1 = min(P, g0 + chunk);
+    const uint32_t words = (tiles + 1) / 2;
+    if (LDS) {
+        for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) s_hist[i] = 0;
+        __syncthreads();
+    }
+    unsigned long long mine = 0;
+    for (int g = g0 + threadIdx.x; g < g1; g += blockDim.x) {
+        const uint32_t n = tiles_touched[g];
+        if (n == 0) continue;
+        mine += n;
+        uint32_t x0, y0, x1, y1;
+        unpack_rect(rect[g], x0, y0, x1, y1);
+        for (uint32_t y = y0; y < y1; y++)
+            for (uint32_t x = x0; x < x1; x++) {
+                const uint32_t t = y * gx + x;
+                if (LDS)
+                    atomicAdd(&s_hist[t >> 1], 1u << ((t & 1u) * 16));
+                else
+                    atomicAdd(&cnt[t], 1u);
+            }
+    }
+    const unsigned long long total = block_sum(mine, s_tmp);
+    if (threadIdx.x == 0) chunk_total[blockIdx.x] = total;
+    if (LDS) {
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) {
+            const uint32_t w = s_hist[i];
+            if (w & 0xffffu) atomicAdd(&cnt[2 * i], w & 0xffffu);
+            if ((w >> 16) && 2 * i + 1 < tiles) atomicAdd(&cnt[2 * i + 1], w >> 16);
+        }
+    }
 }
 
-hipError_t rank_and_scan(GeomState& g, int P, hipStream_t stream) {
-    hipLaunchKernelGGL(rank_prep_kernel, dim3((P + 255) / 256), dim3(256), 0, stream, P, g.gid_by_rank, g.tiles_touched,
-                       g.tiles_ranked, g.rank_of);
-    hipError_t e = hipGetLastError();
+// ---- K2 ---------------------------------------------------------------------
+// One workgroup.  Thread t scans a contiguous run of tiles (then of chunks).
+__global__ void __launch_bounds__(kBinThreads) tile_scan_kernel(uint32_t tiles, const uint32_t* __restrict__ cnt,
+                                                                uint2* __restrict__ ranges, uint32_t* __restrict__ cursor,
+                                                                int nchunks,
+                                                                const unsigned long long* __restrict__ chunk_total,
+                                                                unsigned long long* __restrict__ chunk_base,
+                                                                unsigned long long* __restrict__ total,
+                                                                unsigned long long cap) {
+    __shared__ unsigned long long s_tmp[kBinThreads / 64];
+    const uint32_t T = blockDim.x;
+    {
+        const uint32_t per = (tiles + T - 1) / T, b = threadIdx.x * per, e = min(tiles, b + per);
+        unsigned long long run = 0;
+        for (uint32_t t = b; t < e; t++) run += cnt[t];
+        unsigned long long all = 0;
+        unsigned long long at = block_exclusive_scan(run, s_tmp, &all);
+        for (uint32_t t = b; t < e; t++) {
+            const uint32_t c = cnt[t];
+            // clamped to the binning capacity: with a too-small capacity hint the lists are
+            // truncated (and rebuilt after the forward reads the count), never overrun
+            const unsigned long long lo = at < cap ? at : cap, hi = at + c < cap ? at + c : cap;
+            ranges[t] = make_uint2((uint32_t)lo, (uint32_t)hi);
+            cursor[t] = (uint32_t)at;
+            at += c;
+        }
+        if (threadIdx.x == 0) total[0] = all;
+    }
+    {
+        const uint32_t n = (uint32_t)nchunks, per = (n + T - 1) / T, b = threadIdx.x * per, e = min(n, b + per);
+        unsigned long long run = 0;
+        for (uint32_t c = b; c < e; c++) run += chunk_total[c];
+        unsigned long long at = block_exclusive_scan(run, s_tmp, (unsigned long long*)nullptr);
+        for (uint32_t c = b; c < e; c++) {
+            chunk_base[c] = at;
+            at += chunk_total[c];
+        }
+    }
+}
+
+// ---- K3 ---------------------------------------------------------------------
+// Thread i of a chunk owns Gaussians [g0 + i*per, g0 + (i+1)*per): contiguous runs,
+// so the record offsets are an in-order block scan.
+template <bool LDS>
+__global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
+    int P, int chunk, const uint2* __restrict__ rect, const uint32_t* __restrict__ tiles_touched,
+    const uint32_t* __restrict__ depth_key, uint32_t tiles, uint32_t gx, uint32_t* __restrict__ cursor,
+    const unsigned long long* __restrict__ chunk_base, unsigned long long* __restrict__ keys, unsigned long long cap,
+    uint32_t* __restrict__ rec_start, float4* __restrict__ rec) {
+    extern __shared__ uint32_t s_cur[];  // tiles words
+    __shared__ unsigned long long s_tmp[kBinThreads / 64];
+    const int g0 = blockIdx.x * chunk, g1 = min(P, g0 + chunk);
+    const int per = (chunk + (int)blockDim.x - 1) / (int)blockDim.x;
+    const int b = g0 + (int)threadIdx.x * per, e = min(g1, b + per);
+
+    // first record index of every Gaussian: chunk base + in-order scan of tiles_touched
+    unsigned long long run = 0;
+    for (int g = b; g < e; g++) run += tiles_touched[g];
+    unsigned long long at = chunk_base[blockIdx.x] + block_exclusive_scan(run, s_tmp, (unsigned long long*)nullptr);
+    for (int g = b; g < e; g++) {
+        const uint32_t n = tiles_touched[g];
+        rec_start[g] = (uint32_t)at;
+        if (n) reinterpret_cast<uint32_t*>(rec + (size_t)kRecRows * g + 3)[3] = (uint32_t)at;
+        at += n;
+    }
+
+    if (LDS) {
+        for (uint32_t i = threadIdx.x; i < tiles; i += blockDim.x) s_cur[i] = 0;
+        __syncthreads();
+        for (int g = b; g < e; g++) {
+            if (tiles_touched[g] == 0) continue;
+            uint32_t x0, y0, x1, y1;
+            unpack_rect(rect[g], x0, y0, x1, y1);
+            for (uint32_t y = y0; y < y1; y++)
+                for (uint32_t x = x0; x < x1; x++) atomicAdd(&s_cur[y * gx + x], 1u);
+        }
+        __syncthreads();
+        // one reservation per (chunk, tile)
+        for (uint32_t i = threadIdx.x; i < tiles; i += blockDim.x) {
+            const uint32_t c = s_cur[i];
+            if (c) s_cur[i] = atomicAdd(&cursor[i], c);
+        }
+        __syncthreads();
+    }
+    for (int g = b; g < e; g++) {
+        if (tiles_touched[g] == 0) continue;
+        const unsigned long long key = ((unsigned long long)depth_key[g] << 32) | (uint32_t)g;
+        uint32_t x0, y0, x1, y1;
+        unpack_rect(rect[g], x0, y0, x1, y1);
+        for (uint32_t y = y0; y < y1; y++)
+            for (uint32_t x = x0; x < x1; x++) {
+                const uint32_t t = y * gx + x;
+                const uint32_t pos = LDS ? atomicAdd(&s_cur[t], 1u) : atomicAdd(&cursor[t], 1u);
+                if (pos < cap) keys[pos] = key;  // cap: capacity of the binning buffer (redone if exceeded)
+            }
+    }
+}
+
+// ---- K4 ---------------------------------------------------------------------
+// Sorting network with ascending comparators only ("flip" bitonic form): for
+// k = 2, 4, .., N2 the first step pairs i with i ^ (k - 1), the others with
+// i ^ j.  Every comparator puts the minimum at the lower index, so elements past
+// n behave as +infinity and are never touched: any n sorts in place.
+template <typename Load, typename Store>
+__device__ __forceinline__ void sort_network(uint32_t n, Load ld, Store st) {
+    uint32_t N2 = 1;
+    while (N2 < n) N2 <<= 1;
+    for (uint32_t k = 2; k <= N2; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t p = threadIdx.x; p < N2 / 2; p += blockDim.x) {
+                // p-th pair of this step: lo has bit j clear
+                const uint32_t lo = ((p & ~(j - 1)) << 1) | (p & (j - 1));
+                const uint32_t hi = (j == (k >> 1)) ? (lo ^ (k - 1)) : (lo | j);
+                if (hi < n) {
+                    const unsigned long long a = ld(lo), b = ld(hi);
+                    if (b < a) {
+                        st(lo, b);
+                        st(hi, a);
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t tile_len(uint2 r, unsigned long long cap) {
+    const unsigned long long hi = r.y < cap ? r.y : cap;
+    return hi > r.x ? (uint32_t)(hi - r.x) : 0u;
+}
+
+template <int T, int CAP>
+__global__ void __launch_bounds__(T) tile_sort_lds_kernel(const uint2* __restrict__ ranges,
+                                                         const unsigned long long* __restrict__ keys,
+                                                         unsigned long long cap, uint32_t* __restrict__ gid_sorted,
+                                                         uint32_t min_exclusive) {
+    __shared__ unsigned long long s[CAP];
+    const uint2 r = ranges[blockIdx.x];
+    const uint32_t n = tile_len(r, cap);
+    if (n <= min_exclusive || n > (uint32_t)CAP) return;  // another kernel's size class
+    for (uint32_t i = threadIdx.x; i < n; i += T) s[i] = keys[r.x + i];
+    __syncthreads();
+    sort_network(
+        n, [&](uint32_t i) { return s[i]; }, [&](uint32_t i, unsigned long long v) { s[i] = v; });
+    for (uint32_t i = threadIdx.x; i < n; i += T) gid_sorted[r.x + i] = (uint32_t)s[i];
+}
+
+// Lists longer than the LDS classes: the same network directly on the global keys
+// (one workgroup per tile; correct for any length, slow -- real scenes rarely need it).
+__global__ void __launch_bounds__(kBinThreads) tile_sort_global_kernel(const uint2* __restrict__ ranges,
+                                                                       unsigned long long* __restrict__ keys,
+                                                                       unsigned long long cap,
+                                                                       uint32_t* __restrict__ gid_sorted,
+                                                                       uint32_t min_exclusive) {
+    const uint2 r = ranges[blockIdx.x];
+    const uint32_t n = tile_len(r, cap);
+    if (n <= min_exclusive) return;
+    unsigned long long* k = keys + r.x;
+    sort_network(
+        n, [&](uint32_t i) { return k[i]; }, [&](uint32_t i, unsigned long long v) { k[i] = v; });
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) gid_sorted[r.x + i] = (uint32_t)k[i];
+}
+
+// ---- launchers ----------------------------------------------------------------
+int bin_chunks(int P, int* chunk) {
+    // ~256 chunks (enough workgroups for the chip), each < 65536 Gaussians (16-bit LDS counters)
+    int n = (P + 1023) / 1024;
+    if (n > 256) n = 256;
+    if (n < 1) n = 1;
+    int c = (P + n - 1) / n;
+    if (c > 65535) {
+        c = 65535;
+        n = (P + c - 1) / c;
+    }
+    *chunk = c;
+    return n;
+}
+
+size_t bin_chunk_count(int P) {
+    int chunk = 0;
+    return (size_t)bin_chunks(P, &chunk);
+}
+
+// K1 + K2: tile counts, ranges, cursors, record bases and the instance count (g.total).
+hipError_t launch_bin_count(int P, const GeomState& g, uint32_t gx, uint32_t gy, uint2* ranges, size_t cap,
+                            hipStream_t stream) {
+    const uint32_t tiles = gx * gy;
+    int chunk = 0;
+    const int nchunks = bin_chunks(P, &chunk);
+    const bool lds = tiles <= kLdsTilesMax;
+    const dim3 grid(nchunks), block(kBinThreads);
+    hipError_t e = hipMemsetAsync(g.tile_cnt, 0, tiles * sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
-    size_t bytes = g.scan_temp_bytes;
-    return rocprim::inclusive_scan(g.scan_temp, bytes, g.tiles_ranked, g.offsets, (size_t)P,
-                                   rocprim::plus<unsigned long long>(), stream);
-}
-
-// ---- 3. instance emission ----------------------------------------------------
-// One thread per depth rank.  A wave's 64 Gaussians own one contiguous range of
-// the emission order; the wave walks it 64 slots at a time, so every store is a
-// full coalesced wave store no matter how unevenly the tile counts are spread
-// (the reference's thread-per-Gaussian loop writes 1..hundreds of entries per
-// thread, CR/rasterizer_impl.cu:108-124).  Each slot finds its owning lane by a
-// 6-step binary search over the lanes' exclusive starts (ds_bpermute).
-template <typename KeyT>
-__global__ void __launch_bounds__(256) duplicate_kernel(int P, const uint32_t* __restrict__ gid_by_rank,
-                                                        const unsigned long long* __restrict__ offsets,
-                                                        const int* __restrict__ radii, float4* __restrict__ rec,
-                                                        uint32_t gx, uint32_t gy, KeyT* __restrict__ keys,
-                                                        uint32_t* __restrict__ emit_gid, unsigned long long cap) {
-    const int r = blockIdx.x * blockDim.x + threadIdx.x;
-    const int lane = threadIdx.x & 63;
-    if (r - lane >= P) return;  // whole wave past the end (wave-uniform)
-    const bool valid = r < P;
-    uint32_t gid = 0, count = 0;
-    uint2 rmin = make_uint2(0, 0), rmax = make_uint2(0, 0);
-    unsigned long long incl = 0;
-    if (valid) {
-        gid = gid_by_rank[r];
-        incl = offsets[r];
-        const int rad = radii[gid];
-        if (rad > 0) {
-            const float4 v = rec[(size_t)kRecRows * gid];
-            get_rect(v.x, v.y, rad, gx, gy, rmin, rmax);
-            count = (rmax.y - rmin.y) * (rmax.x - rmin.x);
-        }
-    }
-    const unsigned long long excl = incl - count;
-    // first emission index of this Gaussian -> record row 3 (the render backward addresses
-    // its per-instance gradient records with it)
-    if (count) reinterpret_cast<uint32_t*>(rec + (size_t)kRecRows * gid + 3)[3] = (uint32_t)excl;
-    // The wave's ranks are consecutive: its emissions are [E0, E1) with both ends
-    // read from the scan (wave-uniform addresses -> scalar loads).
-    const int r0 = r - lane;
-    const int r_last = min(r0 + 63, P - 1);
-    const unsigned long long E0 = r0 == 0 ? 0ull : offsets[r0 - 1];
-    const unsigned long long E1 = offsets[r_last];
-    const uint32_t total = (uint32_t)(E1 - E0);
-    const uint32_t my_start = valid ? (uint32_t)(excl - E0) : total;  // invalid lanes start at the end
-    const uint32_t w = rmax.x - rmin.x;
-
-    for (uint32_t base = 0; base < total; base += 64) {
-        const uint32_t k = base + lane;
-        // largest lane whose start <= k (starts are non-decreasing across lanes)
-        int lo = 0;
-#pragma unroll
-        for (int step = 32; step > 0; step >>= 1) {
-            const int cand = lo + step;
-            const uint32_t v = __shfl(my_start, cand & 63);
-            if (cand < 64 && v <= k) lo = cand;
-        }
-        const uint32_t o_start = __shfl(my_start, lo);
-        const uint32_t o_w = __shfl(w, lo);
-        const uint32_t o_x0 = __shfl(rmin.x, lo);
-        const uint32_t o_y0 = __shfl(rmin.y, lo);
-        const uint32_t o_gid = __shfl(gid, lo);
-        if (k < total && E0 + k < cap) {  // cap: instances the binning buffer holds
-            const uint32_t local = k - o_start;
-            const uint32_t ty = local / o_w;
-            const uint32_t tx = local - ty * o_w;
-            const uint32_t tile = (o_y0 + ty) * gx + (o_x0 + tx);
-            keys[E0 + k] = (KeyT)tile;
-            emit_gid[E0 + k] = o_gid;
-        }
-    }
-}
-
-hipError_t launch_duplicate(int P, const GeomState& g, const int* radii, uint32_t gx, uint32_t gy,
-                            const BinningState& b, bool key16, size_t cap, hipStream_t stream) {
-    const dim3 grid((P + 255) / 256), block(256);
-    if (key16)
-        hipLaunchKernelGGL(duplicate_kernel<uint16_t>, grid, block, 0, stream, P, g.gid_by_rank, g.offsets, radii,
-                           g.rec, gx, gy, (uint16_t*)b.keys, b.emit_gid, (unsigned long long)cap);
+    const size_t hist_bytes = lds ? ((tiles + 1) / 2) * sizeof(uint32_t) : 0;
+    if (lds)
+        hipLaunchKernelGGL(tile_count_kernel<true>, grid, block, hist_bytes, stream, P, chunk, g.rect, g.tiles_touched,
+                           tiles, gx, g.tile_cnt, g.chunk_total);
     else
-        hipLaunchKernelGGL(duplicate_kernel<uint32_t>, grid, block, 0, stream, P, g.gid_by_rank, g.offsets, radii,
-                           g.rec, gx, gy, (uint32_t*)b.keys, b.emit_gid, (unsigned long long)cap);
+        hipLaunchKernelGGL(tile_count_kernel<false>, grid, block, 0, stream, P, chunk, g.rect, g.tiles_touched, tiles,
+                           gx, g.tile_cnt, g.chunk_total);
+    hipLaunchKernelGGL(tile_scan_kernel, dim3(1), block, 0, stream, tiles, g.tile_cnt, ranges, g.tile_cursor, nchunks,
+                       g.chunk_total, g.chunk_base, g.total, (unsigned long long)cap);
     return hipGetLastError();
 }
 
-// ---- 3b. capacity mode: the slots past the device-side instance count get the
-// sentinel tile id `tiles` (it fits in bit_length(tiles) bits and sorts last), so
-// the sort can run on a host-known capacity without a host round trip.
-template <typename KeyT>
-__global__ void pad_keys_kernel(const unsigned long long* __restrict__ total, unsigned long long cap,
-                                KeyT* __restrict__ keys, KeyT sentinel) {
-    const unsigned long long R = *total;
-    for (unsigned long long i = R + blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x; i < cap;
-         i += (unsigned long long)gridDim.x * blockDim.x)
-        keys[i] = sentinel;
-}
-
-hipError_t launch_pad_keys(const unsigned long long* total, size_t cap, const BinningState& b, bool key16,
-                           uint32_t sentinel, hipStream_t stream) {
-    const dim3 grid(512), block(256);
-    if (key16)
-        hipLaunchKernelGGL(pad_keys_kernel<uint16_t>, grid, block, 0, stream, total, (unsigned long long)cap,
-                           (uint16_t*)b.keys, (uint16_t)sentinel);
+// K3: scatter the keys into a binning buffer of capacity `cap` (after launch_bin_count).
+hipError_t launch_bin_scatter(int P, const GeomState& g, uint32_t gx, uint32_t gy, const BinningState& b, size_t cap,
+                              hipStream_t stream) {
+    const uint32_t tiles = gx * gy;
+    int chunk = 0;
+    const int nchunks = bin_chunks(P, &chunk);
+    const bool lds = tiles <= kLdsTilesMax;
+    const dim3 grid(nchunks), block(kBinThreads);
+    const size_t cur_bytes = lds ? tiles * sizeof(uint32_t) : 0;
+    if (lds)
+        hipLaunchKernelGGL(tile_scatter_kernel<true>, grid, block, cur_bytes, stream, P, chunk, g.rect,
+                           g.tiles_touched, g.depth_key, tiles, gx, g.tile_cursor, g.chunk_base, b.keys,
+                           (unsigned long long)cap, g.rec_start, g.rec);
     else
-        hipLaunchKernelGGL(pad_keys_kernel<uint32_t>, grid, block, 0, stream, total, (unsigned long long)cap,
-                           (uint32_t*)b.keys, sentinel);
+        hipLaunchKernelGGL(tile_scatter_kernel<false>, grid, block, 0, stream, P, chunk, g.rect, g.tiles_touched,
+                           g.depth_key, tiles, gx, g.tile_cursor, g.chunk_base, b.keys, (unsigned long long)cap,
+                           g.rec_start, g.rec);
     return hipGetLastError();
 }
 
-// ---- 4. stable tile sort over bits [0, bit_length(tiles)) ---------------------
-size_t tile_sort_temp_bytes(size_t R, bool key16) {
-    size_t bytes = 0;
-    if (key16)
-        (void)rocprim::radix_sort_pairs<SortConfig>(nullptr, bytes, (const uint16_t*)nullptr, (uint16_t*)nullptr,
-                                                    (const uint32_t*)nullptr, (uint32_t*)nullptr, R, 0, 16);
-    else
-        (void)rocprim::radix_sort_pairs<SortConfig>(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                                                    (const uint32_t*)nullptr, (uint32_t*)nullptr, R, 0, 32);
-    return bytes;
-}
-
-hipError_t tile_sort(BinningState& b, size_t R, unsigned end_bit, bool key16, hipStream_t stream) {
-    size_t bytes = b.sort_temp_bytes;
-    if (key16)
-        return rocprim::radix_sort_pairs<SortConfig>(b.sort_temp, bytes, (const uint16_t*)b.keys, (uint16_t*)b.keys_sorted,
-                                                     (const uint32_t*)b.emit_gid, b.gid_sorted, R, 0, end_bit, stream);
-    return rocprim::radix_sort_pairs<SortConfig>(b.sort_temp, bytes, (const uint32_t*)b.keys, (uint32_t*)b.keys_sorted,
-                                                 (const uint32_t*)b.emit_gid, b.gid_sorted, R, 0, end_bit, stream);
-}
-
-// ---- 5. per-tile [start, end) (identifyTileRanges, CR/rasterizer_impl.cu:132-164)
-// Keys >= tiles are capacity-mode padding (sorted last) and own no range.
-template <typename KeyT>
-__global__ void finalize_kernel(uint32_t R, uint32_t tiles, const KeyT* __restrict__ keys_sorted,
-                                uint2* __restrict__ ranges) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= R) return;
-    const uint32_t cur = keys_sorted[i];
-    if (cur >= tiles) {
-        if (i > 0 && keys_sorted[i - 1] < tiles) ranges[keys_sorted[i - 1]].y = i;
-        return;
-    }
-    if (i == 0) {
-        ranges[cur].x = 0;
-    } else {
-        const uint32_t prev = keys_sorted[i - 1];
-        if (cur != prev) {
-            ranges[prev].y = i;
-            ranges[cur].x = i;
-        }
-    }
-    if (i == R - 1) ranges[cur].y = R;
-}
-
-hipError_t launch_finalize(size_t R, uint32_t tiles, const BinningState& b, uint2* ranges, bool key16,
-                           hipStream_t stream) {
-    const dim3 grid((unsigned)((R + 255) / 256)), block(256);
-    if (key16)
-        hipLaunchKernelGGL(finalize_kernel<uint16_t>, grid, block, 0, stream, (uint32_t)R, tiles,
-                           (const uint16_t*)b.keys_sorted, ranges);
-    else
-        hipLaunchKernelGGL(finalize_kernel<uint32_t>, grid, block, 0, stream, (uint32_t)R, tiles,
-                           (const uint32_t*)b.keys_sorted, ranges);
+hipError_t launch_tile_sort(uint32_t tiles, const uint2* ranges, const BinningState& b, size_t cap,
+                            hipStream_t stream) {
+    if (tiles == 0 || cap == 0) return hipSuccess;
+    const unsigned long long c = cap;
+    hipLaunchKernelGGL((tile_sort_lds_kernel<256, 2048>), dim3(tiles), dim3(256), 0, stream, ranges, b.keys, c,
+                       b.gid_sorted, 0u);
+    hipLaunchKernelGGL((tile_sort_lds_kernel<512, 8192>), dim3(tiles), dim3(512), 0, stream, ranges, b.keys, c,
+                       b.gid_sorted, 2048u);
+    hipLaunchKernelGGL(tile_sort_global_kernel, dim3(tiles), dim3(kBinThreads), 0, stream, ranges, b.keys, c,
+                       b.gid_sorted, 8192u);
     return hipGetLastError();
 }
 

@@ -64,18 +64,17 @@ struct Carver {
 struct GeomState {
     float4* rec;                // [P][kRecRows] splat records
     uint32_t* depth_key;        // float bits of view-space z, 0xffffffff if culled
-    uint32_t* depth_key_sorted; // sort output (unused after sorting)
-    uint32_t* gid_by_rank;      // Gaussians in (depth, index) order
-    uint32_t* rank_of;          // inverse permutation
     uint32_t* tiles_touched;    // per Gaussian (CR/forward.cu:350)
-    uint32_t* tiles_ranked;     // tiles_touched in rank order
-    unsigned long long* offsets;// inclusive scan of tiles_ranked (64-bit: overflow-checked)
+    uint2* rect;                // getRect, packed: (min.x | min.y << 16, max.x | max.y << 16)
+    uint32_t* rec_start;        // first gradient-record index (exclusive scan of tiles_touched)
     uint8_t* clamped;           // SH clamp mask, 3 bits (CR/forward.cu:74-76)
     uint32_t* status;           // device status word (prefiltered violation, ...)
-    void* sort_temp;
-    size_t sort_temp_bytes;
-    void* scan_temp;
-    size_t scan_temp_bytes;
+    // binning scratch (binning.hip)
+    uint32_t* tile_cnt;         // [tiles] instances per tile
+    uint32_t* tile_cursor;      // [tiles] scatter cursors
+    unsigned long long* chunk_total;  // [chunks] tiles_touched per Gaussian chunk
+    unsigned long long* chunk_base;   // [chunks] its exclusive scan
+    unsigned long long* total;        // [1] number of instances (num_rendered)
 };
 
 // Image state: per pixel (N) and per tile.
@@ -86,14 +85,10 @@ struct ImageState {
     uint2* ranges;        // [tiles]
 };
 
-// Binning state: per instance (R).  Key type is 16-bit while tiles <= 65536.
+// Binning state: per instance (R, or the capacity the buffer was requested for).
 struct BinningState {
-    void* keys;             // unsorted tile ids (u16 or u32), emission order
-    void* keys_sorted;      // sorted tile ids
-    uint32_t* emit_gid;     // Gaussian of each emitted instance
-    uint32_t* gid_sorted;   // Gaussian of each sorted instance (the tile lists)
-    void* sort_temp;
-    size_t sort_temp_bytes;
+    unsigned long long* keys;  // per instance, grouped by tile: depth bits << 32 | Gaussian index
+    uint32_t* gid_sorted;      // Gaussian of each instance in (tile, depth, index) order: the tile lists
 };
 
 // Per-instance gradient records (backward scratch), SoA so stores are aligned.

@@ -48,8 +48,8 @@ struct RenderBwdArgs {
     const float* dL_dinvdepth;  // [H,W] or null
     ImageState img;
     GradRecs recs;
-    const uint32_t* rank_of;    // depth rank of each Gaussian
-    uint32_t* rank_lim;         // [tiles] out: 1 + rank of the last entry that has a record (0: none)
+    const uint32_t* depth_key;          // per Gaussian
+    unsigned long long* lim_key;        // [tiles] out: key of the last entry that has a record (0: none)
 };
 
 struct GaussBwdArgs {
@@ -86,24 +86,19 @@ struct GaussBwdArgs {
 hipError_t launch_preprocess(const PreprocessArgs& a, hipStream_t stream);
 hipError_t launch_mark_visible(int P, const float* means3D, const float* view, bool* present, hipStream_t stream);
 // binning.hip
-size_t depth_sort_temp_bytes(int P);
-hipError_t depth_sort(GeomState& g, int P, hipStream_t stream);
-size_t scan_temp_bytes(int P);
-hipError_t rank_and_scan(GeomState& g, int P, hipStream_t stream);
-hipError_t launch_duplicate(int P, const GeomState& g, const int* radii, uint32_t gx, uint32_t gy,
-                            const BinningState& b, bool key16, size_t cap, hipStream_t stream);
-hipError_t launch_pad_keys(const unsigned long long* total, size_t cap, const BinningState& b, bool key16,
-                           uint32_t sentinel, hipStream_t stream);
-size_t tile_sort_temp_bytes(size_t R, bool key16);
-hipError_t tile_sort(BinningState& b, size_t R, unsigned end_bit, bool key16, hipStream_t stream);
-hipError_t launch_finalize(size_t R, uint32_t tiles, const BinningState& b, uint2* ranges, bool key16,
-                           hipStream_t stream);
+size_t bin_chunk_count(int P);
+hipError_t launch_bin_count(int P, const GeomState& g, uint32_t gx, uint32_t gy, uint2* ranges, size_t cap,
+                            hipStream_t stream);
+hipError_t launch_bin_scatter(int P, const GeomState& g, uint32_t gx, uint32_t gy, const BinningState& b, size_t cap,
+                              hipStream_t stream);
+hipError_t launch_tile_sort(uint32_t tiles, const uint2* ranges, const BinningState& b, size_t cap,
+                            hipStream_t stream);
 // render.hip
 hipError_t launch_render_fwd(const RenderFwdArgs& a, hipStream_t stream);
 hipError_t launch_render_bwd(const RenderBwdArgs& a, hipStream_t stream);
 // backward.hip
-hipError_t launch_gauss_reduce(int P, const unsigned long long* offsets, const void* keys, bool key16,
-                               const uint32_t* rank_lim, const GradRecs& recs, const GradRecs& sums, hipStream_t stream);
+hipError_t launch_gauss_reduce(int P, const GeomState& g, uint32_t gx, const unsigned long long* lim_key,
+                               const GradRecs& recs, const GradRecs& sums, hipStream_t stream);
 hipError_t launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t stream);
 
 }  // namespace gsr

@@ -208,6 +208,7 @@ __global__ void __launch_bounds__(256) preprocess_kernel(PreprocessArgs a) {
     rec[2] = make_float4(rgb.x, rgb.y, rgb.z, __uint_as_float(bby));
     rec[3] = make_float4(__uint_as_float(rmin.x), __uint_as_float(rmin.y), __uint_as_float(rmax.x - rmin.x), 0.f);
     a.geom.tiles_touched[idx] = touched;
+    a.geom.rect[idx] = make_uint2(rmin.x | (rmin.y << 16), rmax.x | (rmax.y << 16));
 }
 
 hipError_t launch_preprocess(const PreprocessArgs& a, hipStream_t stream) {

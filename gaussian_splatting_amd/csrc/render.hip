@@ -279,11 +279,18 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
 
     const uint2 range = a.ranges[tile];
     const int n = (int)(range.y - range.x);
-    // Entries at positions >= limit get no gradient record at all: the per-Gaussian
-    // reduction recognises them by depth rank (tile lists are in rank order), using
-    // rank_lim[tile] = 1 + rank of the entry at position limit - 1 (0: none).
-    if (lane == 0)
-        a.rank_lim[tile] = limit > 0 ? a.rank_of[a.gid_sorted[range.x + limit - 1]] + 1u : 0u;
+    // Entries at positions >= limit get no gradient record at all.  The per-Gaussian
+    // reduction recognises them by key (tile lists are sorted by depth bits << 32 |
+    // index): lim_key[tile] = key of the entry at position limit - 1, 0 if none (a
+    // visible Gaussian's depth bits are never 0).
+    if (lane == 0) {
+        unsigned long long lk = 0;
+        if (limit > 0) {
+            const uint32_t gl = a.gid_sorted[range.x + limit - 1];
+            lk = ((unsigned long long)a.depth_key[gl] << 32) | gl;
+        }
+        a.lim_key[tile] = lk;
+    }
     const uint32_t ttx = tile % a.gx, tty = tile / a.gx;
     for (int b0 = 0; b0 < limit; b0 += kBatch) {
         const bool has = b0 + lane < limit;

@@ -82,17 +82,21 @@ int main() {
     CK(hipMemcpy(d_tk, tk.data(), R * 2, hipMemcpyHostToDevice));
 
     time_sort<DEF>("depth default(onesweep)", d_dk, d_dko, d_v, P, 32);
-    time_sort<OS<256, 8, 8>>("depth os<256,8,rb8>", d_dk, d_dko, d_v, P, 32);
-    time_sort<OS<256, 12, 8>>("depth os<256,12,rb8>", d_dk, d_dko, d_v, P, 32);
+    time_sort<OS<256, 16, 11>>("depth os<256,16,rb11>", d_dk, d_dko, d_v, P, 32);
+    time_sort<OS<512, 8, 11>>("depth os<512,8,rb11>", d_dk, d_dko, d_v, P, 32);
+    time_sort<OS<256, 8, 11>>("depth os<256,8,rb11>", d_dk, d_dko, d_v, P, 32);
+    time_sort<OS<256, 4, 11>>("depth os<256,4,rb11>", d_dk, d_dko, d_v, P, 32);
+    time_sort<OS<1024, 4, 8>>("depth os<1024,4,rb8>", d_dk, d_dko, d_v, P, 32);
     time_sort<OS<256, 4, 8>>("depth os<256,4,rb8>", d_dk, d_dko, d_v, P, 32);
+    time_sort<OS<128, 4, 8>>("depth os<128,4,rb8>", d_dk, d_dko, d_v, P, 32);
 
     time_sort<DEF>("tile default(onesweep)", d_tk, d_tko, d_v, R, 13);
     time_sort<OS<256, 12, 7>>("tile os<256,12,rb7>", d_tk, d_tko, d_v, R, 13);
-    time_sort<OS<512, 12, 7>>("tile os<512,12,rb7>", d_tk, d_tko, d_v, R, 13);
-    time_sort<OS<256, 16, 7>>("tile os<256,16,rb7>", d_tk, d_tko, d_v, R, 13);
     time_sort<OS<512, 16, 7>>("tile os<512,16,rb7>", d_tk, d_tko, d_v, R, 13);
-    time_sort<OS<512, 8, 7>>("tile os<512,8,rb7>", d_tk, d_tko, d_v, R, 13);
-    time_sort<OS<256, 16, 8>>("tile os<256,16,rb8>", d_tk, d_tko, d_v, R, 13);
+    time_sort<OS<256, 16, 13>>("tile os<256,16,rb13>", d_tk, d_tko, d_v, R, 13);
+    time_sort<OS<512, 16, 13>>("tile os<512,16,rb13>", d_tk, d_tko, d_v, R, 13);
+    time_sort<OS<1024, 8, 13>>("tile os<1024,8,rb13>", d_tk, d_tko, d_v, R, 13);
+    time_sort<OS<512, 8, 11>>("tile os<512,8,rb11>", d_tk, d_tko, d_v, R, 13);
     // memcpy reference: bytes moved by one pass (read+write key+value)
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
