@@ -45,6 +45,22 @@ def _note_rendered(key, nr: int) -> None:
     _capacity[key] = max(int(nr), int(_capacity.get(key, 0) * _CAP_DECAY))
 
 
+# GSR_POISON=1 (the GPU test suite sets it): every scratch buffer the library requests is
+# filled with 0xff bytes and every output the kernels are meant to overwrite completely is
+# filled with NaN before the call, so a read of memory no kernel wrote, or an output element
+# no kernel wrote, shows up in the parity tests instead of depending on what the caching
+# allocator happened to hand out.
+def _poison() -> bool:
+    return os.environ.get("GSR_POISON", "0") == "1"
+
+
+def _empty(shape, **kw) -> torch.Tensor:
+    t = torch.empty(shape, **kw)
+    if _poison():
+        t.fill_(float("nan") if t.dtype.is_floating_point else -1)
+    return t
+
+
 def _stream_handle(device: torch.device) -> ctypes.c_void_p:
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
@@ -93,6 +109,8 @@ class _Resizer:
     def _resize(self, _ctx, nbytes):
         try:
             self.tensor.resize_(int(nbytes))
+            if _poison():
+                self.tensor.fill_(255)
             return self.tensor.data_ptr()
         except Exception:  # e.g. out of memory: the library reports GSR_ERR_ALLOC
             return None
@@ -114,7 +132,7 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     P = means3D.size(0)
     H, W = int(image_height), int(image_width)
     f32 = dict(dtype=torch.float32, device=device)
-    alloc = torch.empty if P > 0 else torch.zeros  # every pixel / Gaussian is written when P > 0
+    alloc = _empty if P > 0 else torch.zeros  # every pixel / Gaussian is written when P > 0
     out_color = alloc((3, H, W), **f32)
     out_invdepth = alloc((1, H, W), **f32)
     radii = alloc((P,), dtype=torch.int32, device=device)
@@ -168,7 +186,7 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, opacities, 
     H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))
     M = sh.size(1) if (sh is not None and sh.numel() != 0 and sh.size(0) != 0) else 0
     f32 = dict(dtype=torch.float32, device=device)
-    alloc = torch.empty if P > 0 else torch.zeros
+    alloc = _empty if P > 0 else torch.zeros
     out = dict(out or {})
 
     def buf(name, shape):

@@ -62,7 +62,7 @@ def build(force: bool = False, jobs: int = 5, verbose: bool = True, variant: str
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         objs = list(ex.map(lambda f: _compile(f, objdir, extra), SOURCES))
     LIB_OUT = lib
-    tmp = LIB_OUT + ".tmp"
+    tmp = os.path.join(os.path.dirname(LIB_OUT), "tmp_" + os.path.basename(LIB_OUT))
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:

@@ -104,7 +104,7 @@ int check_debug(int debug, hipStream_t stream, const char* stage) {
 }
 
 
-gsr::GeomState carve_geom(char* base, int P, uint32_t tiles, size_t* total) {
+gsr::GeomState carve_geom(char* base, int P, uint32_t gx, uint32_t gy, size_t* total) {
     using namespace gsr;
     Carver c{base, 0};
     GeomState g{};
@@ -115,9 +115,19 @@ gsr::GeomState carve_geom(char* base, int P, uint32_t tiles, size_t* total) {
     g.rec_start = c.take<uint32_t>(P);
     g.clamped = c.take<uint8_t>(P);
     g.status = c.take<uint32_t>(4);
-    g.tile_cnt = c.take<uint32_t>(tiles);
-    g.tile_cursor = c.take<uint32_t>(tiles);
+    const uint32_t tiles = gx * gy;
+    const size_t cells = bin_cell_count(gx, gy);
+    g.tile_cnt = c.take<uint32_t>(tiles + cells);
+    g.cell_cnt = g.tile_cnt + tiles;
+    g.tile_base = c.take<uint32_t>(tiles);
     const size_t chunks = bin_chunk_count(P);
+    g.cell_off = c.take<uint32_t>(chunks * cells);
+    g.order = c.take<uint32_t>(P);
+    g.n_visible = c.take<uint32_t>(1);
+
+    g.chunk_off = c.take<uint32_t>(chunks * tiles);
+    g.cls_list = c.take<uint32_t>(3 * (size_t)tiles);
+    g.cls_count = c.take<uint32_t>(3);
     g.chunk_total = c.take<unsigned long long>(chunks);
     g.chunk_base = c.take<unsigned long long>(chunks);
     g.total = c.take<unsigned long long>(1);
@@ -268,10 +278,10 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
                     width, height);
 
     size_t geom_bytes = 0, img_bytes = 0;
-    carve_geom(nullptr, P, tiles, &geom_bytes);
+    carve_geom(nullptr, P, gx, gy, &geom_bytes);
     char* gbase = (char*)call_alloc(geom_alloc, geom_ctx, geom_bytes);
     if (!gbase) return fail(GSR_ERR_ALLOC, "rasterize_forward: geometry buffer allocation failed");
-    GeomState geom = carve_geom(gbase, P, tiles, &geom_bytes);
+    GeomState geom = carve_geom(gbase, P, gx, gy, &geom_bytes);
     carve_image(nullptr, width, height, tiles, &img_bytes);
     char* ibase = (char*)call_alloc(image_alloc, image_ctx, img_bytes);
     if (!ibase) return fail(GSR_ERR_ALLOC, "rasterize_forward: image buffer allocation failed");
@@ -328,15 +338,18 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
         char* bbase = (char*)call_alloc(binning_alloc, binning_ctx, bin_bytes);
         if (!bbase) return fail(GSR_ERR_ALLOC, "rasterize_forward: binning buffer allocation failed");
         BinningState bin = carve_binning(bbase, C, &bin_bytes);
+        {
+            // always launched: besides the keys (none when C == 0) it writes every Gaussian's
+            // first record index, which the backward's reduction reads even when nothing
+            // was rendered
+            StageScope sc(ST_BIN_SCATTER, stream);
+            HIP_TRY(launch_bin_scatter(P, geom, gx, gy, bin, C, stream), "bin_scatter");
+        }
+        if (int rc = check_debug(debug, stream, "bin_scatter")) return rc;
         if (C > 0) {
             {
-                StageScope sc(ST_BIN_SCATTER, stream);
-                HIP_TRY(launch_bin_scatter(P, geom, gx, gy, bin, C, stream), "bin_scatter");
-            }
-            if (int rc = check_debug(debug, stream, "bin_scatter")) return rc;
-            {
                 StageScope sc(ST_TILE_SORT, stream);
-                HIP_TRY(launch_tile_sort(tiles, img.ranges, bin, C, stream), "tile_sort");
+                HIP_TRY(launch_tile_sort(tiles, img.ranges, geom, bin, C, stream), "tile_sort");
             }
             if (int rc = check_debug(debug, stream, "tile_sort")) return rc;
         }
@@ -444,7 +457,7 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
             return fail(GSR_ERR_ARGUMENT, "rasterize_backward: binning buffer of %zu bytes does not match capacity %zu",
                         binning_bytes, C);
     }
-    GeomState geom = carve_geom((char*)geom_buffer, P, tiles, &tmp);
+    GeomState geom = carve_geom((char*)geom_buffer, P, gx, gy, &tmp);
     ImageState img = carve_image((char*)image_buffer, width, height, tiles, &tmp);
     BinningState bin = carve_binning((char*)binning_buffer, C, &tmp);
     size_t rec_bytes = 0;

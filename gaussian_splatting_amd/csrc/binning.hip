@@ -8,17 +8,29 @@
 //
 //   K1 tile_count    every workgroup owns a contiguous chunk of Gaussians and
 //                    counts its tile hits in an LDS histogram (two 16-bit
-//                    counters per word), flushed with one atomic add per tile;
-//                    it also sums the chunk's tiles_touched;
+//                    counters per word); the flush is one RETURNING atomic add
+//                    per (chunk, tile), whose result -- the chunk's offset inside
+//                    the tile's block -- is kept in chunk_off[chunk][tile];
 //   K2 tile_scan     one workgroup: exclusive scans of the tile counts (-> the
 //                    per-tile ranges, identifyTileRanges' output) and of the
-//                    chunk totals (-> each chunk's first record index);
-//   K3 tile_scatter  every chunk reserves a block per tile with ONE returning
-//                    atomic and scatters 64-bit keys (depth bits << 32 | index)
-//                    into it; it also writes each Gaussian's first record index;
-//   K4 tile_sort     per tile, an in-LDS sorting network on the keys (one
-//                    workgroup per tile, sized by the list length), writing the
-//                    Gaussian ids -- the tile lists the render passes walk.
+//                    chunk totals (-> each chunk's first record index); it also
+//                    lists the tiles too long for one wave's sort (three classes);
+//   K3 tile_scatter  every chunk loads its cursors (tile start + chunk offset)
+//                    into LDS and scatters 64-bit keys (depth bits << 32 |
+//                    index) with LDS atomics; it also writes each Gaussian's
+//                    first record index;
+//   K4 tile_sort     per tile, a bitonic network held in registers (exchanges
+//                    inside a lane, across lanes by swizzle/permute, across
+//                    waves through LDS), writing the Gaussian ids -- the tile
+//                    lists the render passes walk.  One wave per tile up to 1024
+//                    keys; longer lists go to persistent kernels walking K2's
+//                    class lists.
+//
+// K1 and K3 enumerate (Gaussian, tile) instances flattened over the wave: the 64
+// Gaussians of a wave are scanned by tile count and every lane takes one
+// instance per step, so a Gaussian covering 100 tiles costs its wave two steps,
+// not 100 serial iterations of one lane (the reference's per-thread tile loop,
+// CR/rasterizer_impl.cu:108-124).
 //
 // The order inside a tile is fully determined by the (depth bits, index) keys,
 // which is exactly the reference's order (its sort is stable on index-ordered
@@ -30,7 +42,17 @@
 namespace gsr {
 
 constexpr int kBinThreads = 1024;
+constexpr int kBinWaves = kBinThreads / 64;
 constexpr uint32_t kLdsTilesMax = 36864;  // K3 keeps one u32 per tile in LDS (144 KiB)
+constexpr uint32_t kSortWaveMax = 1024;   // longest list tile_sort_kernel sorts (one wave, 16 keys per lane)
+constexpr uint32_t kSortMidMax = 2048;    // class 1: (1024, 2048], 128 threads x 16 keys
+constexpr uint32_t kBigRegMax = 8192;     // class 2: (2048, 8192], 512 threads x 16 keys; class 3: longer
+
+typedef unsigned long long u64;
+
+GSR_STAMP_BUFFER(g_st_count);
+GSR_STAMP_BUFFER(g_st_scatter);
+GSR_STAMP_BUFFER(g_st_sort);
 
 __device__ __forceinline__ void unpack_rect(uint2 r, uint32_t& x0, uint32_t& y0, uint32_t& x1, uint32_t& y1) {
     x0 = r.x & 0xffffu;
@@ -73,209 +95,464 @@ __device__ T block_exclusive_scan(T v, T* s_tmp, T* total) {
     return base + incl - v;
 }
 
+// Calls f(valid, owner, tile) once per step on every lane of the wave; over all
+// steps, the valid calls are exactly the (Gaussian, tile) instances of the wave's
+// 64 Gaussians (lane l: n tiles in rectangle r), each once; `owner` is the lane of
+// the instance's Gaussian.  f may shuffle from `owner` (all lanes are active).
+template <class F>
+__device__ __forceinline__ void for_each_instance(uint32_t n, uint2 r, uint32_t gx, F&& f) {
+    const int lane = threadIdx.x & 63;
+    uint32_t incl = n;
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t u = __shfl_up(incl, off);
+        if (lane >= off) incl += u;
+    }
+    const uint32_t excl = incl - n;
+    const uint32_t total = __shfl(incl, 63);
+    const uint32_t w = (r.y & 0xffffu) - (r.x & 0xffffu);
+    for (uint32_t base = 0; base < total; base += 64) {
+        const uint32_t s = base + lane;
+        // owner: the largest lane whose exclusive offset is <= s (its count covers s)
+        int owner = 0;
+#pragma unroll
+        for (int step = 32; step > 0; step >>= 1) {
+            const int cand = owner + step;
+            if (__shfl(excl, cand) <= s) owner = cand;
+        }
+        const uint32_t k = s - __shfl(excl, owner);
+        const uint32_t ow = __shfl(w, owner), org = __shfl(r.x, owner);
+        const bool valid = s < total;
+        uint32_t tile = 0;
+        if (valid) {
+            const uint32_t ty = k / ow, tx = k - ty * ow;
+            tile = ((org >> 16) + ty) * gx + (org & 0xffffu) + tx;
+        }
+        f(valid, owner, tile);
+    }
+}
+
+// ---- K0: spatial order ------------------------------------------------------
+// The visible Gaussians are counting-sorted by screen cell (kCell x kCell tiles,
+// cell of the footprint rectangle's centre) into order[0, V).  K1 and K3 walk
+// Gaussians in this order, so a chunk covers a compact screen region: it touches
+// few tiles, with long runs per tile, and K3's key stores land in long contiguous
+// runs instead of a few bytes per (chunk, tile) across the whole image.
+constexpr uint32_t kCell = 4;
+
+__device__ __forceinline__ uint32_t cell_of(uint2 r, uint32_t cgx) {
+    const uint32_t cx = ((r.x & 0xffffu) + (r.y & 0xffffu)) >> 1, cy = ((r.x >> 16) + (r.y >> 16)) >> 1;
+    return (cy / kCell) * cgx + cx / kCell;
+}
+
+// K0a: per-chunk cell histogram in LDS; one returning atomic per (chunk, cell) gives the
+// chunk's offset inside the cell's block (kept in cell_off[chunk][cell]).  Also the
+// chunk's instance total (index order), for the record starts.
+__global__ void __launch_bounds__(kBinThreads) cell_count_kernel(int P, int chunk, const uint2* __restrict__ rect,
+                                                                 const uint32_t* __restrict__ tiles_touched,
+                                                                 uint32_t cells, uint32_t cgx,
+                                                                 uint32_t* __restrict__ cell_cnt,
+                                                                 uint32_t* __restrict__ cell_off,
+                                                                 u64* __restrict__ chunk_total) {
+    extern __shared__ uint32_t s_c[];  // cells words
+    __shared__ u64 s_tmp[kBinWaves];
+    const int g0 = blockIdx.x * chunk, g1 = min(P, g0 + chunk);
+    for (uint32_t i = threadIdx.x; i < cells; i += blockDim.x) s_c[i] = 0;
+    __syncthreads();
+    u64 mine = 0;
+    for (int g = g0 + (int)threadIdx.x; g < g1; g += kBinThreads) {
+        const uint32_t n = tiles_touched[g];
+        mine += n;
+        if (n) atomicAdd(&s_c[cell_of(rect[g], cgx)], 1u);
+    }
+    const u64 total = block_sum(mine, s_tmp);  // ends with a barrier: the histogram is complete
+    if (threadIdx.x == 0) chunk_total[blockIdx.x] = total;
+    uint32_t* off = cell_off + (size_t)blockIdx.x * cells;
+    for (uint32_t i = threadIdx.x; i < cells; i += blockDim.x) {
+        const uint32_t c = s_c[i];
+        if (c) off[i] = atomicAdd(&cell_cnt[i], c);
+    }
+}
+
+// K0c: every chunk scans the cell counts (redundantly, cells are few), then scatters its
+// visible Gaussians' indices into their cells' blocks.  Block 0 publishes V.
+__global__ void __launch_bounds__(kBinThreads) cell_scatter_kernel(int P, int chunk, const uint2* __restrict__ rect,
+                                                                   const uint32_t* __restrict__ tiles_touched,
+                                                                   uint32_t cells, uint32_t cgx,
+                                                                   const uint32_t* __restrict__ cell_cnt,
+                                                                   const uint32_t* __restrict__ cell_off,
+                                                                   uint32_t* __restrict__ order,
+                                                                   uint32_t* __restrict__ n_visible) {
+    extern __shared__ uint32_t s_c[];  // cells words
+    __shared__ uint32_t s_tmp[kBinWaves];
+    const int g0 = blockIdx.x * chunk, g1 = min(P, g0 + chunk);
+    const uint32_t* off = cell_off + (size_t)blockIdx.x * cells;
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < cells; base += kBinThreads) {
+        const uint32_t i = base + threadIdx.x;
+        const uint32_t c = i < cells ? cell_cnt[i] : 0u;
+        uint32_t all = 0;
+        const uint32_t at = carry + block_exclusive_scan(c, s_tmp, &all);
+        if (i < cells) s_c[i] = at + (c ? off[i] : 0u);  // off[] is written only where this chunk has entries
+        carry += all;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) n_visible[0] = carry;
+    __syncthreads();
+    for (int g = g0 + (int)threadIdx.x; g < g1; g += kBinThreads)
+        if (tiles_touched[g]) order[atomicAdd(&s_c[cell_of(rect[g], cgx)], 1u)] = (uint32_t)g;
+}
+
 // ---- K1 ---------------------------------------------------------------------
 template <bool LDS>
 __global__ void __launch_bounds__(kBinThreads) tile_count_kernel(int P, int chunk, const uint2* __restrict__ rect,
                                                                  const uint32_t* __restrict__ tiles_touched,
+                                                                 const uint32_t* __restrict__ order,
+                                                                 const uint32_t* __restrict__ n_visible,
                                                                  uint32_t tiles, uint32_t gx, uint32_t* __restrict__ cnt,
-                                                                 unsigned long long* __restrict__ chunk_total) {
+                                                                 uint32_t* __restrict__ chunk_off) {
     extern __shared__ uint32_t s_hist[];  // (tiles + 1) / 2 words: 16-bit counters (a chunk has < 65536 Gaussians)
-    __shared__ unsigned long long s_tmp[kBinThreads / 64];
-    const int g0 = blockIdx.x * chunk, g1 = min(P, g0 + chunk);
+    const int V = (int)n_visible[0];
+    const int g0 = blockIdx.x * chunk, g1 = min(V, g0 + chunk);  // positions in order[]
     const uint32_t words = (tiles + 1) / 2;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    GSR_STAMP(g_st_count, blockIdx.x, 0);
     if (LDS) {
         for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) s_hist[i] = 0;
         __syncthreads();
     }
-    unsigned long long mine = 0;
-    for (int g = g0 + threadIdx.x; g < g1; g += blockDim.x) {
-        const uint32_t n = tiles_touched[g];
-        if (n == 0) continue;
-        mine += n;
-        uint32_t x0, y0, x1, y1;
-        unpack_rect(rect[g], x0, y0, x1, y1);
-        for (uint32_t y = y0; y < y1; y++)
-            for (uint32_t x = x0; x < x1; x++) {
-                const uint32_t t = y * gx + x;
-                if (LDS)
-                    atomicAdd(&s_hist[t >> 1], 1u << ((t & 1u) * 16));
-                else
-                    atomicAdd(&cnt[t], 1u);
-            }
+    GSR_STAMP(g_st_count, blockIdx.x, 1);
+    for (int pb = g0 + wave * 64; pb < g1; pb += kBinThreads) {
+        const int p = pb + lane;
+        const uint32_t g = p < g1 ? order[p] : 0u;
+        const uint32_t n = p < g1 ? tiles_touched[g] : 0u;
+        const uint2 r = n ? rect[g] : make_uint2(0u, 0u);
+        for_each_instance(n, r, gx, [&](bool valid, int, uint32_t t) {
+            if (!valid) return;
+            if (LDS)
+                atomicAdd(&s_hist[t >> 1], 1u << ((t & 1u) * 16));
+            else
+                atomicAdd(&cnt[t], 1u);
+        });
     }
-    const unsigned long long total = block_sum(mine, s_tmp);
-    if (threadIdx.x == 0) chunk_total[blockIdx.x] = total;
     if (LDS) {
         __syncthreads();
+        GSR_STAMP(g_st_count, blockIdx.x, 2);
+        uint32_t* off = chunk_off + (size_t)blockIdx.x * tiles;
         for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) {
             const uint32_t w = s_hist[i];
-            if (w & 0xffffu) atomicAdd(&cnt[2 * i], w & 0xffffu);
-            if ((w >> 16) && 2 * i + 1 < tiles) atomicAdd(&cnt[2 * i + 1], w >> 16);
+            if (w & 0xffffu) off[2 * i] = atomicAdd(&cnt[2 * i], w & 0xffffu);
+            if ((w >> 16) && 2 * i + 1 < tiles) off[2 * i + 1] = atomicAdd(&cnt[2 * i + 1], w >> 16);
         }
+        __syncthreads();
+        GSR_STAMP(g_st_count, blockIdx.x, 3);
     }
 }
 
 // ---- K2 ---------------------------------------------------------------------
-// One workgroup.  Thread t scans a contiguous run of tiles (then of chunks).
+// One workgroup.  Rounds of blockDim * 8 tiles: each thread loads 8 consecutive
+// counts (independent loads), then one block scan per round.
+constexpr int kScanV = 8;
+
 __global__ void __launch_bounds__(kBinThreads) tile_scan_kernel(uint32_t tiles, const uint32_t* __restrict__ cnt,
-                                                                uint2* __restrict__ ranges, uint32_t* __restrict__ cursor,
-                                                                int nchunks,
-                                                                const unsigned long long* __restrict__ chunk_total,
-                                                                unsigned long long* __restrict__ chunk_base,
-                                                                unsigned long long* __restrict__ total,
-                                                                unsigned long long cap) {
-    __shared__ unsigned long long s_tmp[kBinThreads / 64];
+                                                                uint2* __restrict__ ranges,
+                                                                uint32_t* __restrict__ tile_base, int nchunks,
+                                                                const u64* __restrict__ chunk_total,
+                                                                u64* __restrict__ chunk_base, u64* __restrict__ total,
+                                                                u64 cap, uint32_t* __restrict__ cls_list,
+                                                                uint32_t* __restrict__ cls_count) {
+    __shared__ u64 s_tmp[kBinWaves];
+    __shared__ uint32_t s_cls[3];
+    if (threadIdx.x < 3) s_cls[threadIdx.x] = 0;  // published by the scan's barriers
     const uint32_t T = blockDim.x;
-    {
-        const uint32_t per = (tiles + T - 1) / T, b = threadIdx.x * per, e = min(tiles, b + per);
-        unsigned long long run = 0;
-        for (uint32_t t = b; t < e; t++) run += cnt[t];
-        unsigned long long all = 0;
-        unsigned long long at = block_exclusive_scan(run, s_tmp, &all);
-        for (uint32_t t = b; t < e; t++) {
-            const uint32_t c = cnt[t];
-            // clamped to the binning capacity: with a too-small capacity hint the lists are
-            // truncated (and rebuilt after the forward reads the count), never overrun
-            const unsigned long long lo = at < cap ? at : cap, hi = at + c < cap ? at + c : cap;
-            ranges[t] = make_uint2((uint32_t)lo, (uint32_t)hi);
-            cursor[t] = (uint32_t)at;
-            at += c;
+    u64 carry = 0;
+    for (uint32_t base = 0; base < tiles; base += T * kScanV) {
+        const uint32_t b = base + threadIdx.x * kScanV;
+        uint32_t v[kScanV];
+        u64 run = 0;
+#pragma unroll
+        for (int i = 0; i < kScanV; i++) {
+            v[i] = b + i < tiles ? cnt[b + i] : 0u;
+            run += v[i];
         }
-        if (threadIdx.x == 0) total[0] = all;
-    }
-    {
-        const uint32_t n = (uint32_t)nchunks, per = (n + T - 1) / T, b = threadIdx.x * per, e = min(n, b + per);
-        unsigned long long run = 0;
-        for (uint32_t c = b; c < e; c++) run += chunk_total[c];
-        unsigned long long at = block_exclusive_scan(run, s_tmp, (unsigned long long*)nullptr);
-        for (uint32_t c = b; c < e; c++) {
-            chunk_base[c] = at;
-            at += chunk_total[c];
+        u64 all = 0;
+        u64 at = carry + block_exclusive_scan(run, s_tmp, &all);
+#pragma unroll
+        for (int i = 0; i < kScanV; i++) {
+            if (b + i < tiles) {
+                // clamped to the binning capacity: with a too-small capacity hint the lists are
+                // truncated (and rebuilt after the forward reads the count), never overrun
+                const u64 lo = at < cap ? at : cap, hi = at + v[i] < cap ? at + v[i] : cap;
+                ranges[b + i] = make_uint2((uint32_t)lo, (uint32_t)hi);
+                tile_base[b + i] = (uint32_t)at;
+                if (v[i] > kSortWaveMax) {  // long list: class 1, 2 or 3 (K4)
+                    const int c = v[i] <= kSortMidMax ? 0 : v[i] <= kBigRegMax ? 1 : 2;
+                    cls_list[(size_t)c * tiles + atomicAdd(&s_cls[c], 1u)] = b + i;
+                }
+            }
+            at += v[i];
         }
+        carry += all;
     }
+    if (threadIdx.x == 0) total[0] = carry;
+    carry = 0;
+    for (uint32_t base = 0; base < (uint32_t)nchunks; base += T) {
+        const uint32_t c = base + threadIdx.x;
+        const u64 v = c < (uint32_t)nchunks ? chunk_total[c] : 0ull;
+        u64 all = 0;
+        const u64 at = carry + block_exclusive_scan(v, s_tmp, &all);
+        if (c < (uint32_t)nchunks) chunk_base[c] = at;
+        carry += all;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) cls_count[threadIdx.x] = s_cls[threadIdx.x];
 }
 
 // ---- K3 ---------------------------------------------------------------------
-// Thread i of a chunk owns Gaussians [g0 + i*per, g0 + (i+1)*per): contiguous runs,
-// so the record offsets are an in-order block scan.
 template <bool LDS>
 __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
     int P, int chunk, const uint2* __restrict__ rect, const uint32_t* __restrict__ tiles_touched,
-    const uint32_t* __restrict__ depth_key, uint32_t tiles, uint32_t gx, uint32_t* __restrict__ cursor,
-    const unsigned long long* __restrict__ chunk_base, unsigned long long* __restrict__ keys, unsigned long long cap,
+    const uint32_t* __restrict__ depth_key, const uint32_t* __restrict__ order, const uint32_t* __restrict__ n_visible,
+    uint32_t tiles, uint32_t gx, uint32_t* __restrict__ tile_base,
+    const uint32_t* __restrict__ chunk_off, const u64* __restrict__ chunk_base, u64* __restrict__ keys, u64 cap,
     uint32_t* __restrict__ rec_start, float4* __restrict__ rec) {
     extern __shared__ uint32_t s_cur[];  // tiles words
-    __shared__ unsigned long long s_tmp[kBinThreads / 64];
+    __shared__ u64 s_tmp[kBinWaves];
     const int g0 = blockIdx.x * chunk, g1 = min(P, g0 + chunk);
-    const int per = (chunk + (int)blockDim.x - 1) / (int)blockDim.x;
-    const int b = g0 + (int)threadIdx.x * per, e = min(g1, b + per);
-
-    // first record index of every Gaussian: chunk base + in-order scan of tiles_touched
-    unsigned long long run = 0;
-    for (int g = b; g < e; g++) run += tiles_touched[g];
-    unsigned long long at = chunk_base[blockIdx.x] + block_exclusive_scan(run, s_tmp, (unsigned long long*)nullptr);
-    for (int g = b; g < e; g++) {
-        const uint32_t n = tiles_touched[g];
-        rec_start[g] = (uint32_t)at;
-        if (n) reinterpret_cast<uint32_t*>(rec + (size_t)kRecRows * g + 3)[3] = (uint32_t)at;
-        at += n;
-    }
-
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    GSR_STAMP(g_st_scatter, blockIdx.x, 0);
     if (LDS) {
-        for (uint32_t i = threadIdx.x; i < tiles; i += blockDim.x) s_cur[i] = 0;
-        __syncthreads();
-        for (int g = b; g < e; g++) {
-            if (tiles_touched[g] == 0) continue;
-            uint32_t x0, y0, x1, y1;
-            unpack_rect(rect[g], x0, y0, x1, y1);
-            for (uint32_t y = y0; y < y1; y++)
-                for (uint32_t x = x0; x < x1; x++) atomicAdd(&s_cur[y * gx + x], 1u);
-        }
-        __syncthreads();
-        // one reservation per (chunk, tile)
-        for (uint32_t i = threadIdx.x; i < tiles; i += blockDim.x) {
-            const uint32_t c = s_cur[i];
-            if (c) s_cur[i] = atomicAdd(&cursor[i], c);
-        }
-        __syncthreads();
+        // this chunk's cursors: tile start + the chunk's offset inside the tile (K1); entries of
+        // tiles the chunk does not touch are garbage and never used
+        const uint32_t* off = chunk_off + (size_t)blockIdx.x * tiles;
+        for (uint32_t i = threadIdx.x; i < tiles; i += blockDim.x) s_cur[i] = tile_base[i] + off[i];
     }
-    for (int g = b; g < e; g++) {
-        if (tiles_touched[g] == 0) continue;
-        const unsigned long long key = ((unsigned long long)depth_key[g] << 32) | (uint32_t)g;
-        uint32_t x0, y0, x1, y1;
-        unpack_rect(rect[g], x0, y0, x1, y1);
-        for (uint32_t y = y0; y < y1; y++)
-            for (uint32_t x = x0; x < x1; x++) {
-                const uint32_t t = y * gx + x;
-                const uint32_t pos = LDS ? atomicAdd(&s_cur[t], 1u) : atomicAdd(&cursor[t], 1u);
-                if (pos < cap) keys[pos] = key;  // cap: capacity of the binning buffer (redone if exceeded)
-            }
+    // first record index of every Gaussian: chunk base + in-order scan of tiles_touched
+    u64 carry = chunk_base[blockIdx.x];
+    for (int gb = g0; gb < g1; gb += kBinThreads) {
+        const int g = gb + (int)threadIdx.x;
+        const uint32_t n = g < g1 ? tiles_touched[g] : 0u;
+        u64 all = 0;
+        const u64 at = carry + block_exclusive_scan((u64)n, s_tmp, &all);
+        if (g < g1) {
+            rec_start[g] = (uint32_t)at;
+            if (n) reinterpret_cast<uint32_t*>(rec + (size_t)kRecRows * g + 3)[3] = (uint32_t)at;
+        }
+        carry += all;
     }
+    if (LDS) __syncthreads();
+    GSR_STAMP(g_st_scatter, blockIdx.x, 1);
+    // the keys: chunk positions [q0, q1) of the spatial order (K0), as K1 counted them
+    const int V = (int)n_visible[0];
+    const int q0 = blockIdx.x * chunk, q1 = min(V, q0 + chunk);
+    for (int pb = q0 + wave * 64; pb < q1; pb += kBinThreads) {
+        const int p = pb + lane;
+        const uint32_t g = p < q1 ? order[p] : 0u;
+        const uint32_t n = p < q1 ? tiles_touched[g] : 0u;
+        const uint2 r = n ? rect[g] : make_uint2(0u, 0u);
+        const uint32_t dk = n ? depth_key[g] : 0u;
+        for_each_instance(n, r, gx, [&](bool valid, int owner, uint32_t t) {
+            const uint32_t kh = __shfl(dk, owner), kg = __shfl(g, owner);
+            if (!valid) return;
+            const uint32_t pos = LDS ? atomicAdd(&s_cur[t], 1u) : atomicAdd(&tile_base[t], 1u);
+            if (pos < cap) keys[pos] = ((u64)kh << 32) | kg;  // cap: redone if exceeded
+        });
+    }
+#ifdef GSR_STAMPS
+    __syncthreads();
+#endif
+    GSR_STAMP(g_st_scatter, blockIdx.x, 2);
 }
 
 // ---- K4 ---------------------------------------------------------------------
-// Sorting network with ascending comparators only ("flip" bitonic form): for
-// k = 2, 4, .., N2 the first step pairs i with i ^ (k - 1), the others with
-// i ^ j.  Every comparator puts the minimum at the lower index, so elements past
-// n behave as +infinity and are never touched: any n sorts in place.
-template <typename Load, typename Store>
-__device__ __forceinline__ void sort_network(uint32_t n, Load ld, Store st) {
-    uint32_t N2 = 1;
-    while (N2 < n) N2 <<= 1;
+// Bitonic sorting network over N2 = T * E keys, element i = thread * E + r held in
+// register a[r] (keys past the list are +infinity = ~0).  Exchange distance j:
+//   j < E        inside the thread (registers),
+//   E <= j < 64E across lanes, lane distance j / E: DPP (1, 2, 4, 8) or the gfx950
+//                lane-swap instructions (16, 32) -- VALU only, no LDS traffic,
+//   j >= 64E     across waves, through LDS (T > 64 only).
+// Every compare-exchange is one 64-bit compare whose result is flipped by the
+// direction mask, then selects.
+template <int S>
+__device__ __forceinline__ uint32_t lane_xor(uint32_t v) {
+    const int x = (int)v;
+    if constexpr (S == 1) {
+        return (uint32_t)__builtin_amdgcn_mov_dpp(x, 0xB1, 0xf, 0xf, true);  // quad_perm [1,0,3,2]
+    } else if constexpr (S == 2) {
+        return (uint32_t)__builtin_amdgcn_mov_dpp(x, 0x4E, 0xf, 0xf, true);  // quad_perm [2,3,0,1]
+    } else if constexpr (S == 4) {
+        const int up = __builtin_amdgcn_mov_dpp(x, 0x104, 0xf, 0xf, true);  // row_shl:4, lane + 4
+        const int dn = __builtin_amdgcn_mov_dpp(x, 0x114, 0xf, 0xf, true);  // row_shr:4, lane - 4
+        return (uint32_t)((threadIdx.x & 4) ? dn : up);
+    } else if constexpr (S == 8) {
+        return (uint32_t)__builtin_amdgcn_mov_dpp(x, 0x128, 0xf, 0xf, true);  // row_ror:8
+    } else if constexpr (S == 16) {
+        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);  // rows (0,1), (2,3) swapped
+        return (threadIdx.x & 16) ? r[0] : r[1];
+    } else {
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);  // halves swapped
+        return (threadIdx.x & 32) ? r[0] : r[1];
+    }
+}
+
+template <int S>
+__device__ __forceinline__ u64 lane_xor_u64(u64 v) {
+    return ((u64)lane_xor<S>((uint32_t)(v >> 32)) << 32) | lane_xor<S>((uint32_t)v);
+}
+
+template <int E, int S>
+__device__ __forceinline__ void xlane_step(u64 (&a)[E], bool keep_min) {
+#pragma unroll
+    for (int r = 0; r < E; r++) {
+        const u64 b = lane_xor_u64<S>(a[r]);
+        a[r] = ((b < a[r]) == keep_min) ? b : a[r];
+    }
+}
+
+template <int T, int E>
+__device__ __forceinline__ void bitonic_regs(u64 (&a)[E], u64* s_x) {
+    constexpr uint32_t N2 = (uint32_t)T * E;
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+#pragma unroll
     for (uint32_t k = 2; k <= N2; k <<= 1) {
+#pragma unroll
         for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            for (uint32_t p = threadIdx.x; p < N2 / 2; p += blockDim.x) {
-                // p-th pair of this step: lo has bit j clear
-                const uint32_t lo = ((p & ~(j - 1)) << 1) | (p & (j - 1));
-                const uint32_t hi = (j == (k >> 1)) ? (lo ^ (k - 1)) : (lo | j);
-                if (hi < n) {
-                    const unsigned long long a = ld(lo), b = ld(hi);
-                    if (b < a) {
-                        st(lo, b);
-                        st(hi, a);
-                    }
+            if (j < (uint32_t)E) {
+#pragma unroll
+                for (int r = 0; r < E; r++) {
+                    if (r & j) continue;
+                    const int p = r | (int)j;
+                    const bool desc = ((tid * E + r) & k) != 0;
+                    const u64 lo = a[r], hi = a[p];
+                    const bool sw = (hi < lo) != desc;
+                    a[r] = sw ? hi : lo;
+                    a[p] = sw ? lo : hi;
                 }
+            } else if (j < 64u * E) {
+                const uint32_t s = j / E;
+                const bool keep_min = ((lane & s) == 0) == (((tid * E) & k) == 0);
+                switch (s) {  // compile-time after unrolling
+                    case 1: xlane_step<E, 1>(a, keep_min); break;
+                    case 2: xlane_step<E, 2>(a, keep_min); break;
+                    case 4: xlane_step<E, 4>(a, keep_min); break;
+                    case 8: xlane_step<E, 8>(a, keep_min); break;
+                    case 16: xlane_step<E, 16>(a, keep_min); break;
+                    default: xlane_step<E, 32>(a, keep_min); break;
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < E; r++) s_x[tid * E + r] = a[r];
+                __syncthreads();
+                const uint32_t i0 = tid * E;  // j >= 64E: partner of i0 + r is (i0 ^ j) + r
+                const bool keep_min = ((i0 & j) == 0) == ((i0 & k) == 0);
+#pragma unroll
+                for (int r = 0; r < E; r++) {
+                    const u64 b = s_x[(i0 ^ j) + r];
+                    a[r] = ((b < a[r]) == keep_min) ? b : a[r];
+                }
+                __syncthreads();
             }
-            __syncthreads();
         }
     }
 }
 
-__device__ __forceinline__ uint32_t tile_len(uint2 r, unsigned long long cap) {
-    const unsigned long long hi = r.y < cap ? r.y : cap;
+// Sort keys[lo, lo + n) (n <= T * E, T = the workgroup size) and write the Gaussian
+// ids (low key halves).
+template <int T, int E>
+__device__ __forceinline__ void sort_list(const u64* __restrict__ keys, uint32_t lo, uint32_t n,
+                                          uint32_t* __restrict__ gid_sorted, u64* s_x) {
+    u64 a[E];
+    const uint32_t i0 = threadIdx.x * E;
+#pragma unroll
+    for (int r = 0; r < E; r++) a[r] = i0 + r < n ? keys[lo + i0 + r] : ~0ull;
+    bitonic_regs<T, E>(a, s_x);
+#pragma unroll
+    for (int r = 0; r < E; r++)
+        if (i0 + r < n) gid_sorted[lo + i0 + r] = (uint32_t)a[r];
+}
+
+__device__ __forceinline__ uint32_t tile_len(uint2 r, u64 cap) {
+    const u64 hi = r.y < cap ? r.y : cap;
     return hi > r.x ? (uint32_t)(hi - r.x) : 0u;
 }
 
-template <int T, int CAP>
-__global__ void __launch_bounds__(T) tile_sort_lds_kernel(const uint2* __restrict__ ranges,
-                                                         const unsigned long long* __restrict__ keys,
-                                                         unsigned long long cap, uint32_t* __restrict__ gid_sorted,
-                                                         uint32_t min_exclusive) {
-    __shared__ unsigned long long s[CAP];
+// One wave per tile, lists up to kSortWaveMax (64 x 16 keys in registers, no LDS, no
+// barrier).  Longer lists were put on K2's class lists and go to the kernels below.
+__global__ void __launch_bounds__(64) tile_sort_kernel(const uint2* __restrict__ ranges,
+                                                       const u64* __restrict__ keys, u64 cap,
+                                                       uint32_t* __restrict__ gid_sorted) {
     const uint2 r = ranges[blockIdx.x];
     const uint32_t n = tile_len(r, cap);
-    if (n <= min_exclusive || n > (uint32_t)CAP) return;  // another kernel's size class
-    for (uint32_t i = threadIdx.x; i < n; i += T) s[i] = keys[r.x + i];
-    __syncthreads();
-    sort_network(
-        n, [&](uint32_t i) { return s[i]; }, [&](uint32_t i, unsigned long long v) { s[i] = v; });
-    for (uint32_t i = threadIdx.x; i < n; i += T) gid_sorted[r.x + i] = (uint32_t)s[i];
+    GSR_STAMP(g_st_sort, blockIdx.x, 0);
+    GSR_STAMP_VAL(g_st_sort, blockIdx.x, 2, n);
+    if (n <= 1) {
+        if (n == 1 && threadIdx.x == 0) gid_sorted[r.x] = (uint32_t)keys[r.x];
+        return;
+    }
+    if (n <= 64)
+        sort_list<64, 1>(keys, r.x, n, gid_sorted, nullptr);
+    else if (n <= 128)
+        sort_list<64, 2>(keys, r.x, n, gid_sorted, nullptr);
+    else if (n <= 256)
+        sort_list<64, 4>(keys, r.x, n, gid_sorted, nullptr);
+    else if (n <= 512)
+        sort_list<64, 8>(keys, r.x, n, gid_sorted, nullptr);
+    else if (n <= kSortWaveMax)
+        sort_list<64, 16>(keys, r.x, n, gid_sorted, nullptr);
+    GSR_STAMP(g_st_sort, blockIdx.x, 1);
 }
 
-// Lists longer than the LDS classes: the same network directly on the global keys
-// (one workgroup per tile; correct for any length, slow -- real scenes rarely need it).
+// Persistent: T-thread workgroups walk one class list of long tiles (K2) and sort
+// each list of (lo_excl, T * 16] keys in registers.
+template <int T>
+__global__ void __launch_bounds__(T) tile_sort_class_kernel(const uint2* __restrict__ ranges,
+                                                            const u64* __restrict__ keys, u64 cap,
+                                                            uint32_t* __restrict__ gid_sorted,
+                                                            const uint32_t* __restrict__ list,
+                                                            const uint32_t* __restrict__ count) {
+    __shared__ u64 s_x[T * 16];
+    const uint32_t nb = count[0];
+    for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
+        const uint2 r = ranges[list[b]];
+        const uint32_t n = tile_len(r, cap);  // may be shorter than its class when truncated by cap
+        sort_list<T, 16>(keys, r.x, n, gid_sorted, s_x);
+        __syncthreads();  // s_x is reused by the next tile
+    }
+}
+
+// Lists beyond kBigRegMax: the network on the global keys, one workgroup per list
+// (any length; slow -- real scenes rarely produce such tiles).  "Flip" form: every
+// comparator is ascending; for block size k the first step pairs i with i ^ (k - 1),
+// the others with i ^ j, so keys past n behave as +infinity and are never touched.
 __global__ void __launch_bounds__(kBinThreads) tile_sort_global_kernel(const uint2* __restrict__ ranges,
-                                                                       unsigned long long* __restrict__ keys,
-                                                                       unsigned long long cap,
+                                                                       u64* __restrict__ keys, u64 cap,
                                                                        uint32_t* __restrict__ gid_sorted,
-                                                                       uint32_t min_exclusive) {
-    const uint2 r = ranges[blockIdx.x];
-    const uint32_t n = tile_len(r, cap);
-    if (n <= min_exclusive) return;
-    unsigned long long* k = keys + r.x;
-    sort_network(
-        n, [&](uint32_t i) { return k[i]; }, [&](uint32_t i, unsigned long long v) { k[i] = v; });
-    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) gid_sorted[r.x + i] = (uint32_t)k[i];
+                                                                       const uint32_t* __restrict__ list,
+                                                                       const uint32_t* __restrict__ count) {
+    const uint32_t nb = count[0];
+    for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
+        const uint2 r = ranges[list[b]];
+        const uint32_t n = tile_len(r, cap);
+        u64* k = keys + r.x;
+        uint32_t N2 = 1;
+        while (N2 < n) N2 <<= 1;
+        for (uint32_t kk = 2; kk <= N2; kk <<= 1) {
+            for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
+                for (uint32_t p = threadIdx.x; p < N2 / 2; p += blockDim.x) {
+                    const uint32_t lo = ((p & ~(j - 1)) << 1) | (p & (j - 1));  // p-th index with bit j clear
+                    const uint32_t hi = (j == (kk >> 1)) ? (lo ^ (kk - 1)) : (lo | j);
+                    if (hi < n) {
+                        const u64 x = k[lo], y = k[hi];
+                        if (y < x) {
+                            k[lo] = y;
+                            k[hi] = x;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) gid_sorted[r.x + i] = (uint32_t)k[i];
+        __syncthreads();
+    }
 }
 
 // ---- launchers ----------------------------------------------------------------
@@ -298,25 +575,44 @@ size_t bin_chunk_count(int P) {
     return (size_t)bin_chunks(P, &chunk);
 }
 
-// K1 + K2: tile counts, ranges, cursors, record bases and the instance count (g.total).
+uint32_t bin_cells(uint32_t gx, uint32_t gy, uint32_t* cgx) {
+    *cgx = (gx + kCell - 1) / kCell;
+    return *cgx * ((gy + kCell - 1) / kCell);
+}
+
+size_t bin_cell_count(uint32_t gx, uint32_t gy) {
+    uint32_t cgx = 0;
+    return bin_cells(gx, gy, &cgx);
+}
+
+// K0 + K1 + K2: spatial order, tile counts, ranges, tile starts, chunk offsets, record
+// bases, the long-list class lists and the instance count (g.total).
 hipError_t launch_bin_count(int P, const GeomState& g, uint32_t gx, uint32_t gy, uint2* ranges, size_t cap,
                             hipStream_t stream) {
     const uint32_t tiles = gx * gy;
     int chunk = 0;
     const int nchunks = bin_chunks(P, &chunk);
+    uint32_t cgx = 0;
+    const uint32_t cells = bin_cells(gx, gy, &cgx);
     const bool lds = tiles <= kLdsTilesMax;
     const dim3 grid(nchunks), block(kBinThreads);
-    hipError_t e = hipMemsetAsync(g.tile_cnt, 0, tiles * sizeof(uint32_t), stream);
+    if (cells > kLdsTilesMax) return hipErrorInvalidValue;  // > 589k tiles: far beyond any image size
+    hipError_t e = hipMemsetAsync(g.tile_cnt, 0, (tiles + cells) * sizeof(uint32_t), stream);  // + cell_cnt
     if (e != hipSuccess) return e;
+    const size_t cell_bytes = cells * sizeof(uint32_t);
+    hipLaunchKernelGGL(cell_count_kernel, grid, block, cell_bytes, stream, P, chunk, g.rect, g.tiles_touched, cells,
+                       cgx, g.cell_cnt, g.cell_off, g.chunk_total);
+    hipLaunchKernelGGL(cell_scatter_kernel, grid, block, cell_bytes, stream, P, chunk, g.rect, g.tiles_touched,
+                       cells, cgx, g.cell_cnt, g.cell_off, g.order, g.n_visible);
     const size_t hist_bytes = lds ? ((tiles + 1) / 2) * sizeof(uint32_t) : 0;
     if (lds)
         hipLaunchKernelGGL(tile_count_kernel<true>, grid, block, hist_bytes, stream, P, chunk, g.rect, g.tiles_touched,
-                           tiles, gx, g.tile_cnt, g.chunk_total);
+                           g.order, g.n_visible, tiles, gx, g.tile_cnt, g.chunk_off);
     else
-        hipLaunchKernelGGL(tile_count_kernel<false>, grid, block, 0, stream, P, chunk, g.rect, g.tiles_touched, tiles,
-                           gx, g.tile_cnt, g.chunk_total);
-    hipLaunchKernelGGL(tile_scan_kernel, dim3(1), block, 0, stream, tiles, g.tile_cnt, ranges, g.tile_cursor, nchunks,
-                       g.chunk_total, g.chunk_base, g.total, (unsigned long long)cap);
+        hipLaunchKernelGGL(tile_count_kernel<false>, grid, block, 0, stream, P, chunk, g.rect, g.tiles_touched,
+                           g.order, g.n_visible, tiles, gx, g.tile_cnt, g.chunk_off);
+    hipLaunchKernelGGL(tile_scan_kernel, dim3(1), block, 0, stream, tiles, g.tile_cnt, ranges, g.tile_base, nchunks,
+                       g.chunk_total, g.chunk_base, g.total, (u64)cap, g.cls_list, g.cls_count);
     return hipGetLastError();
 }
 
@@ -331,26 +627,39 @@ hipError_t launch_bin_scatter(int P, const GeomState& g, uint32_t gx, uint32_t g
     const size_t cur_bytes = lds ? tiles * sizeof(uint32_t) : 0;
     if (lds)
         hipLaunchKernelGGL(tile_scatter_kernel<true>, grid, block, cur_bytes, stream, P, chunk, g.rect,
-                           g.tiles_touched, g.depth_key, tiles, gx, g.tile_cursor, g.chunk_base, b.keys,
-                           (unsigned long long)cap, g.rec_start, g.rec);
+                           g.tiles_touched, g.depth_key, g.order, g.n_visible, tiles, gx, g.tile_base, g.chunk_off,
+                           g.chunk_base, b.keys, (u64)cap, g.rec_start, g.rec);
     else
         hipLaunchKernelGGL(tile_scatter_kernel<false>, grid, block, 0, stream, P, chunk, g.rect, g.tiles_touched,
-                           g.depth_key, tiles, gx, g.tile_cursor, g.chunk_base, b.keys, (unsigned long long)cap,
-                           g.rec_start, g.rec);
+                           g.depth_key, g.order, g.n_visible, tiles, gx, g.tile_base, g.chunk_off, g.chunk_base,
+                           b.keys, (u64)cap, g.rec_start, g.rec);
     return hipGetLastError();
 }
 
-hipError_t launch_tile_sort(uint32_t tiles, const uint2* ranges, const BinningState& b, size_t cap,
-                            hipStream_t stream) {
+hipError_t launch_tile_sort(uint32_t tiles, const uint2* ranges, const GeomState& g, const BinningState& b,
+                            size_t cap, hipStream_t stream) {
     if (tiles == 0 || cap == 0) return hipSuccess;
-    const unsigned long long c = cap;
-    hipLaunchKernelGGL((tile_sort_lds_kernel<256, 2048>), dim3(tiles), dim3(256), 0, stream, ranges, b.keys, c,
-                       b.gid_sorted, 0u);
-    hipLaunchKernelGGL((tile_sort_lds_kernel<512, 8192>), dim3(tiles), dim3(512), 0, stream, ranges, b.keys, c,
-                       b.gid_sorted, 2048u);
-    hipLaunchKernelGGL(tile_sort_global_kernel, dim3(tiles), dim3(kBinThreads), 0, stream, ranges, b.keys, c,
-                       b.gid_sorted, 8192u);
+    const u64 c = cap;
+    hipLaunchKernelGGL(tile_sort_kernel, dim3(tiles), dim3(64), 0, stream, ranges, b.keys, c, b.gid_sorted);
+    // persistent class kernels: grids sized to fill the chip when their lists are long
+    const auto grid = [&](uint32_t want) { return dim3(tiles < want ? tiles : want); };
+    hipLaunchKernelGGL(tile_sort_class_kernel<128>, grid(2048), dim3(128), 0, stream, ranges, b.keys, c,
+                       b.gid_sorted, g.cls_list, g.cls_count);
+    hipLaunchKernelGGL(tile_sort_class_kernel<512>, grid(512), dim3(512), 0, stream, ranges, b.keys, c,
+                       b.gid_sorted, g.cls_list + tiles, g.cls_count + 1);
+    hipLaunchKernelGGL(tile_sort_global_kernel, grid(256), dim3(kBinThreads), 0, stream, ranges, b.keys, c,
+                       b.gid_sorted, g.cls_list + 2 * (size_t)tiles, g.cls_count + 2);
     return hipGetLastError();
 }
 
 }  // namespace gsr
+
+#ifdef GSR_STAMPS
+extern "C" int gsr_diag_stamps_binning(int which, unsigned long long* out, size_t n) {
+    using namespace gsr;
+    if (n > kStampCap) n = kStampCap;
+    const void* sym = which == 0 ? (const void*)&g_st_count : which == 1 ? (const void*)&g_st_scatter
+                                                                          : (const void*)&g_st_sort;
+    return (int)hipMemcpyFromSymbol(out, sym, n * sizeof(unsigned long long), 0, hipMemcpyDeviceToHost);
+}
+#endif

@@ -70,8 +70,15 @@ struct GeomState {
     uint8_t* clamped;           // SH clamp mask, 3 bits (CR/forward.cu:74-76)
     uint32_t* status;           // device status word (prefiltered violation, ...)
     // binning scratch (binning.hip)
-    uint32_t* tile_cnt;         // [tiles] instances per tile
-    uint32_t* tile_cursor;      // [tiles] scatter cursors
+    uint32_t* tile_cnt;         // [tiles] instances per tile; cell_cnt follows it (one memset)
+    uint32_t* cell_cnt;         // [cells] visible Gaussians per screen cell (spatial order, binning.hip K0)
+    uint32_t* cell_off;         // [chunks][cells] each chunk's offset inside each cell's block
+    uint32_t* order;            // [P] visible Gaussians grouped by screen cell
+    uint32_t* n_visible;        // [1] entries of order
+    uint32_t* tile_base;        // [tiles] first instance of each tile (scatter cursors without LDS)
+    uint32_t* chunk_off;        // [chunks][tiles] each chunk's offset inside each tile's block
+    uint32_t* cls_list;         // [3][tiles] tiles whose lists are too long for one wave's sort, by class
+    uint32_t* cls_count;        // [3] entries of each class list
     unsigned long long* chunk_total;  // [chunks] tiles_touched per Gaussian chunk
     unsigned long long* chunk_base;   // [chunks] its exclusive scan
     unsigned long long* total;        // [1] number of instances (num_rendered)
@@ -134,6 +141,49 @@ __device__ __forceinline__ uint32_t pack_i16x2(int lo, int hi) {
 }
 __device__ __forceinline__ int unpack_lo(uint32_t v) { return (int)(int16_t)(uint16_t)(v & 0xffffu); }
 __device__ __forceinline__ int unpack_hi(uint32_t v) { return (int)(int16_t)(uint16_t)(v >> 16); }
+
+// ---------------------------------------------------------------------------
+// Diagnostic timestamps (variant builds only: -DGSR_STAMPS).  Thread 0 of a
+// workgroup writes s_memtime (shader clock) into a per-translation-unit device
+// buffer, slot = workgroup * kStampSlots + phase; tools/stamps.py reads them back
+// through gsr_diag_stamps().  Compiled out of the product library.
+// ---------------------------------------------------------------------------
+constexpr int kStampSlots = 8;
+constexpr size_t kStampCap = (size_t)1 << 20;
+#ifdef GSR_STAMPS
+#define GSR_STAMP_BUFFER(name) static __device__ unsigned long long name[kStampCap]
+#define GSR_STAMP(buf, wg, phase)                                                                       \
+    do {                                                                                                \
+        if (threadIdx.x == 0 && (size_t)(wg) * kStampSlots + (phase) < kStampCap)                      \
+            buf[(size_t)(wg) * kStampSlots + (phase)] = __builtin_amdgcn_s_memtime();                   \
+    } while (0)
+// s_memrealtime (constant 100 MHz, one time base for the whole device; s_memtime is a
+// per-CU shader-clock counter, fine for durations, not comparable across CUs)
+#define GSR_STAMP_RT(buf, wg, slot)                                                                     \
+    do {                                                                                                \
+        if (threadIdx.x == 0 && (size_t)(wg) * kStampSlots + (slot) < kStampCap)                       \
+            buf[(size_t)(wg) * kStampSlots + (slot)] = __builtin_amdgcn_s_memrealtime();                \
+    } while (0)
+// slot 7: hardware placement, XCC id << 32 | HW_ID (simd [5:4], cu [11:8], sh [12], se [15:13])
+#define GSR_STAMP_HWID(buf, wg)                                                                         \
+    do {                                                                                                \
+        if (threadIdx.x == 0 && (size_t)(wg) * kStampSlots + 7 < kStampCap)                            \
+            buf[(size_t)(wg) * kStampSlots + 7] =                                                       \
+                ((unsigned long long)__builtin_amdgcn_s_getreg((15 << 11) | 20) << 32) |                \
+                (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);                                     \
+    } while (0)
+#define GSR_STAMP_VAL(buf, wg, phase, v)                                                                \
+    do {                                                                                                \
+        if (threadIdx.x == 0 && (size_t)(wg) * kStampSlots + (phase) < kStampCap)                      \
+            buf[(size_t)(wg) * kStampSlots + (phase)] = (unsigned long long)(v);                        \
+    } while (0)
+#else
+#define GSR_STAMP_BUFFER(name) static_assert(true, "")
+#define GSR_STAMP_HWID(buf, wg) do { } while (0)
+#define GSR_STAMP_RT(buf, wg, slot) do { } while (0)
+#define GSR_STAMP(buf, wg, phase) do { } while (0)
+#define GSR_STAMP_VAL(buf, wg, phase, v) do { } while (0)
+#endif
 
 // Wave64 helpers.
 __device__ __forceinline__ int lane_id() { return (int)__lane_id(); }

@@ -87,12 +87,13 @@ hipError_t launch_preprocess(const PreprocessArgs& a, hipStream_t stream);
 hipError_t launch_mark_visible(int P, const float* means3D, const float* view, bool* present, hipStream_t stream);
 // binning.hip
 size_t bin_chunk_count(int P);
+size_t bin_cell_count(uint32_t gx, uint32_t gy);
 hipError_t launch_bin_count(int P, const GeomState& g, uint32_t gx, uint32_t gy, uint2* ranges, size_t cap,
                             hipStream_t stream);
 hipError_t launch_bin_scatter(int P, const GeomState& g, uint32_t gx, uint32_t gy, const BinningState& b, size_t cap,
                               hipStream_t stream);
-hipError_t launch_tile_sort(uint32_t tiles, const uint2* ranges, const BinningState& b, size_t cap,
-                            hipStream_t stream);
+hipError_t launch_tile_sort(uint32_t tiles, const uint2* ranges, const GeomState& g, const BinningState& b,
+                            size_t cap, hipStream_t stream);
 // render.hip
 hipError_t launch_render_fwd(const RenderFwdArgs& a, hipStream_t stream);
 hipError_t launch_render_bwd(const RenderBwdArgs& a, hipStream_t stream);

@@ -37,6 +37,9 @@ namespace gsr {
 
 constexpr int kBatch = 64;  // list entries staged per round (one per lane)
 
+GSR_STAMP_BUFFER(g_st_rfwd);
+GSR_STAMP_BUFFER(g_st_rbwd);
+
 // Occupancy target of the backward (waves per SIMD).  One wave per tile means 8160
 // waves at 1080p for 1024 SIMDs; the register budget decides how many run at once.
 #ifdef GSR_BWD_WAVES
@@ -99,6 +102,19 @@ __device__ __forceinline__ uint32_t quad_bits_exact(float4 v0, float4 v1, float4
     return q;
 }
 
+// One quadrant's bit of quad_bits_exact: does the alpha >= 1/255 footprint (box, then
+// ellipse) reach a pixel centre of the 8x8 quadrant at (qx0, qy0)?
+__device__ __forceinline__ bool quad_hit(float4 v0, float4 v1, float4 v2, int qx0, int qy0) {
+    const uint32_t bx = __float_as_uint(v1.w), by = __float_as_uint(v2.w);
+    if (!(unpack_lo(bx) <= qx0 + 7 && unpack_hi(bx) >= qx0 && unpack_lo(by) <= qy0 + 7 && unpack_hi(by) >= qy0))
+        return false;
+    const float a = v0.z, b = v0.w, c = v1.x, o = v1.y;
+    if (!(a > 0.f && c > 0.f && a * c - b * b > 0.f) || !(o > 0.f)) return true;
+    const float tau = fmaxf(0.f, __logf(255.f * o)) * 1.001f + 0.01f;
+    const float x0 = (float)qx0 - v0.x, y0 = (float)qy0 - v0.y;
+    return rect_min_form(a, b, c, 1.f / a, 1.f / c, x0, x0 + 7.f, y0, y0 + 7.f) <= 2.f * tau;
+}
+
 __device__ __forceinline__ uint32_t uniform_u32(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // Staged form of a splat's conic: the exponent is evaluated as
@@ -126,12 +142,16 @@ __device__ __forceinline__ float splat_alpha(float p2, float opacity, float& G) 
 // transmittance at termination.  A finished pixel therefore blends with weight 0
 // without any mask bookkeeping, and the only wave-level decisions are "does any
 // lane of this slot blend this splat" and "is any pixel of this slot still live".
-__global__ void __launch_bounds__(64) render_fwd_kernel(RenderFwdArgs a) {
+__global__ void __launch_bounds__(64) render_fwd_tile_kernel(RenderFwdArgs a) {
+  {
     const uint32_t tile = blockIdx.x;
     const int tile_x0 = (int)(tile % a.gx) * kTile, tile_y0 = (int)(tile / a.gx) * kTile;
     const int lane = threadIdx.x;
     const int lx = lane & 7, ly = lane >> 3;
     const float pxf0 = (float)(tile_x0 + lx), pyf0 = (float)(tile_y0 + ly);  // this lane's pixel in quadrant 0
+    GSR_STAMP(g_st_rfwd, tile, 0);  // (stamp slots are per tile here, per unit in the quad kernel)
+    GSR_STAMP_HWID(g_st_rfwd, tile);
+    GSR_STAMP_RT(g_st_rfwd, tile, 4);
 
     __shared__ float4 s_xy[kBatch], s_cq[kBatch], s_col[kBatch];  // (x, y, o, 1/z), (A, B, C, quads), rgb
 
@@ -191,7 +211,13 @@ __global__ void __launch_bounds__(64) render_fwd_kernel(RenderFwdArgs a) {
             }
         }
         __syncthreads();
+#ifdef GSR_STAMPS
+        if (threadIdx.x == 0) g_st_rfwd[(size_t)tile * kStampSlots + 3] = (unsigned long long)(b0 + kBatch);
+#endif
     }
+    GSR_STAMP(g_st_rfwd, tile, 1);
+    GSR_STAMP_RT(g_st_rfwd, tile, 5);
+    GSR_STAMP_VAL(g_st_rfwd, tile, 2, n);
     const size_t N = (size_t)a.W * a.H;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
@@ -211,17 +237,128 @@ __global__ void __launch_bounds__(64) render_fwd_kernel(RenderFwdArgs a) {
             a.out_invdepth[pix] = D[q];
         }
     }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Quadrant units.  One wave per (tile, 8x8 quadrant), one pixel per lane: four
+// independent waves per tile.  With one wave per tile (render_fwd_tile_kernel) a
+// SIMD holds ~8 tiles for the whole launch and the kernel ends with the SIMD whose
+// tiles happened to be slowest, running its last waves alone at a fraction of its
+// issue rate (measured: slowest wave ~2x the mean).  Four times as many, four times
+// shorter units let the workgroup dispatcher keep every SIMD full until the end.
+// Every unit stages its tile's list itself (the records of one tile are read by its
+// four units, close in time on the same XCD, so the repeats hit that XCD's L2) and
+// keeps only the entries whose alpha >= 1/255 footprint reaches its quadrant.
+__device__ __forceinline__ uint32_t unit_of_block(uint32_t b, uint32_t units) {
+    // blocks are dealt round-robin over the 8 XCDs: make XCD x run units [x U/8, (x+1) U/8)
+    // in order, so a tile's four units share an L2 and each L2 sees one band of the image
+    if (units % 8u) return b;
+    return (b % 8u) * (units / 8u) + b / 8u;
+}
+
+__global__ void __launch_bounds__(64) render_fwd_quad_kernel(RenderFwdArgs a) {
+    const uint32_t units = a.gx * a.gy * 4u;
+    const uint32_t u = unit_of_block(blockIdx.x, units);
+    const uint32_t tile = u >> 2, q = u & 3u;
+    const int lane = threadIdx.x;
+    const int qx0 = (int)(tile % a.gx) * kTile + (int)(q & 1u) * 8, qy0 = (int)(tile / a.gx) * kTile + (int)(q >> 1) * 8;
+    const int px = qx0 + (lane & 7), py = qy0 + (lane >> 3);
+    const float pxf = (float)px, pyf = (float)py;
+    GSR_STAMP(g_st_rfwd, u, 0);
+    GSR_STAMP_HWID(g_st_rfwd, u);
+    GSR_STAMP_RT(g_st_rfwd, u, 4);
+
+    __shared__ float4 s_xy[kBatch], s_cq[kBatch], s_col[kBatch];  // (x, y, o, 1/z), (A, B, C, -), rgb
+
+    float Tl = (px < a.W && py < a.H) ? 1.f : 0.f, Tf = 0.f, C0 = 0.f, C1 = 0.f, C2 = 0.f, D = 0.f;
+    uint32_t last = 0;
+    bool alive = __any(Tl > 0.f);
+
+    const uint2 range = a.ranges[tile];
+    const int n = (int)(range.y - range.x);
+    for (int b0 = 0; b0 < n && alive; b0 += kBatch) {
+        bool hit = false;
+        if (b0 + lane < n) {
+            const float4* rec = a.rec + (size_t)kRecRows * a.gid_sorted[range.x + b0 + lane];
+            const float4 v0 = rec[0], v1 = rec[1], v2 = rec[2];
+            s_xy[lane] = make_float4(v0.x, v0.y, v1.y, v1.z);
+            s_col[lane] = v2;
+            s_cq[lane] = stage_conic(v0, v1, 0u);
+            hit = quad_hit(v0, v1, v2, qx0, qy0);
+        }
+        __syncthreads();
+        unsigned long long todo = __ballot(hit);
+        while (todo) {
+            const int j = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const float4 xy = s_xy[j], cq = s_cq[j], col = s_col[j];
+            const float dx = xy.x - pxf, dy = xy.y - pyf;
+            const float p2 = dx * (cq.x * dx + cq.y * dy) + cq.z * dy * dy;
+            float G;
+            const float alpha = splat_alpha(p2, xy.z, G);
+            const float w0 = alpha * Tl;  // > 0 iff this pixel blends the splat
+            if (!__any(w0 > 0.f)) continue;  // uniform
+            const float test_T = Tl * (1.f - alpha);
+            const bool term = test_T < 0.0001f;  // live pixel: ends it, splat not added
+            const float w = term ? 0.f : w0;
+            // first termination wins (a finished pixel has Tl = 0); both are >= 0, so an integer max
+            Tf = __uint_as_float(max(__float_as_uint(Tf), term ? __float_as_uint(Tl) : 0u));
+            Tl = term ? 0.f : test_T;
+            C0 += col.x * w;
+            C1 += col.y * w;
+            C2 += col.z * w;
+            D += xy.w * w;
+            last = w > 0.f ? (uint32_t)(b0 + j + 1) : last;
+            if (!__any(Tl > 0.f)) {  // uniform: every pixel of the quadrant has terminated
+                alive = false;
+                break;
+            }
+        }
+        __syncthreads();
+    }
+    GSR_STAMP(g_st_rfwd, u, 1);
+    GSR_STAMP_RT(g_st_rfwd, u, 5);
+    GSR_STAMP_VAL(g_st_rfwd, u, 2, n);
+    if (px < a.W && py < a.H) {
+        const size_t N = (size_t)a.W * a.H;
+        const size_t pix = (size_t)py * a.W + px;
+        const float T = Tl > 0.f ? Tl : Tf;
+        a.img.final_T[pix] = T;
+        a.img.n_contrib[pix] = last;
+        a.img.accum[pix] = C0;
+        a.img.accum[N + pix] = C1;
+        a.img.accum[2 * N + pix] = C2;
+        a.img.accum[3 * N + pix] = D;
+        a.out_color[pix] = C0 + T * a.bg[0];
+        a.out_color[N + pix] = C1 + T * a.bg[1];
+        a.out_color[2 * N + pix] = C2 + T * a.bg[2];
+        a.out_invdepth[pix] = D;
+    }
+}
+
+static int render_variant() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("GSR_RENDER_FWD");
+        v = (e && e[0] == 't') ? 0 : 1;  // "tile": one wave per tile; default: quadrant units
+    }
+    return v;
 }
 
 hipError_t launch_render_fwd(const RenderFwdArgs& a, hipStream_t stream) {
     const uint32_t tiles = a.gx * a.gy;
     if (tiles == 0) return hipSuccess;
-    hipLaunchKernelGGL(render_fwd_kernel, dim3(tiles), dim3(kWave), 0, stream, a);
+    if (render_variant() == 0)
+        hipLaunchKernelGGL(render_fwd_tile_kernel, dim3(tiles), dim3(kWave), 0, stream, a);
+    else
+        hipLaunchKernelGGL(render_fwd_quad_kernel, dim3(tiles * 4), dim3(kWave), 0, stream, a);
     return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(RenderBwdArgs a) {
+  {
     const uint32_t tile = blockIdx.x;
     const int tile_x0 = (int)(tile % a.gx) * kTile, tile_y0 = (int)(tile / a.gx) * kTile;
     const int lane = threadIdx.x;
@@ -231,6 +368,9 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
     __shared__ float4 s_xy[kBatch], s_cq[kBatch], s_col[kBatch];  // as in the forward
     __shared__ float4 s_abc[kBatch];                              // raw conic (a, b, c) for the flush
     __shared__ float4 s_acc[kBatch][3];                           // per entry: the 10 reduced sums (+2 pad)
+    GSR_STAMP(g_st_rbwd, tile, 0);
+    GSR_STAMP_HWID(g_st_rbwd, tile);
+    GSR_STAMP_RT(g_st_rbwd, tile, 4);
 
     const size_t N = (size_t)a.W * a.H;
     float T[4], gB[4], g0[4], g1[4], g2[4], gi[4];
@@ -395,6 +535,11 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
         }
         __syncthreads();
     }
+    GSR_STAMP(g_st_rbwd, tile, 1);
+    GSR_STAMP_RT(g_st_rbwd, tile, 5);
+    GSR_STAMP_VAL(g_st_rbwd, tile, 2, n);
+    GSR_STAMP_VAL(g_st_rbwd, tile, 3, limit);
+  }
 }
 
 hipError_t launch_render_bwd(const RenderBwdArgs& a, hipStream_t stream) {
@@ -405,3 +550,12 @@ hipError_t launch_render_bwd(const RenderBwdArgs& a, hipStream_t stream) {
 }
 
 }  // namespace gsr
+
+#ifdef GSR_STAMPS
+extern "C" int gsr_diag_stamps_render(int which, unsigned long long* out, size_t n) {
+    using namespace gsr;
+    if (n > kStampCap) n = kStampCap;
+    const void* sym = which == 0 ? (const void*)&g_st_rfwd : (const void*)&g_st_rbwd;
+    return (int)hipMemcpyFromSymbol(out, sym, n * sizeof(unsigned long long), 0, hipMemcpyDeviceToHost);
+}
+#endif

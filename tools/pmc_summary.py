@@ -15,9 +15,10 @@ import glob
 import os
 
 SHORT = [("render_bwd", "render_bwd"), ("render_fwd", "render_fwd"), ("gauss_bwd", "gauss_bwd"),
-         ("gauss_reduce", "gauss_reduce"), ("preprocess", "preprocess"), ("duplicate", "duplicate"),
-         ("rank_prep", "rank_prep"), ("finalize", "finalize"), ("onesweep", "rocprim onesweep"),
-         ("histogram", "rocprim histogram"), ("scan", "rocprim scan")]
+         ("gauss_reduce", "gauss_reduce"), ("preprocess", "preprocess"), ("tile_count", "tile_count"),
+         ("tile_scan", "tile_scan"), ("tile_scatter", "tile_scatter"), ("tile_sort_class_kernel<128>", "tile_sort_c1"),
+         ("tile_sort_class_kernel<512>", "tile_sort_c2"), ("tile_sort_global", "tile_sort_c3"),
+         ("tile_sort_kernel", "tile_sort")]
 
 
 def short(name: str) -> str:
