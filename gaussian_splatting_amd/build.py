@@ -21,7 +21,7 @@ OBJ = os.path.join(PKG, "build")
 LIB_DIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIB_DIR, "libgsr.so")
 SOURCES = ["api.hip", "preprocess.hip", "binning.hip", "render.hip", "backward.hip"]
-HEADERS = ["gsr_common.h", "kernels.h"]
+HEADERS = ["gsr_common.h", "kernels.h", "footprint.h"]
 ARCH = os.environ.get("GSR_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-result",

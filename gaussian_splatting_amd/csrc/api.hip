@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <climits>
+#include <cstdlib>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -126,8 +127,8 @@ gsr::GeomState carve_geom(char* base, int P, uint32_t gx, uint32_t gy, size_t* t
     g.n_visible = c.take<uint32_t>(1);
 
     g.chunk_off = c.take<uint32_t>(chunks * tiles);
-    g.cls_list = c.take<uint32_t>(3 * (size_t)tiles);
-    g.cls_count = c.take<uint32_t>(3);
+    g.cls_list = c.take<uint32_t>(4 * (size_t)tiles);
+    g.cls_count = c.take<uint32_t>(4);
     g.chunk_total = c.take<unsigned long long>(chunks);
     g.chunk_base = c.take<unsigned long long>(chunks);
     g.total = c.take<unsigned long long>(1);
@@ -144,6 +145,8 @@ gsr::ImageState carve_image(char* base, int W, int H, uint32_t tiles, size_t* to
     im.n_contrib = c.take<uint32_t>(N);
     im.accum = c.take<float>(4 * N);
     im.ranges = c.take<uint2>(tiles);
+    im.cost = c.take<uint32_t>(tiles);
+    im.order = c.take<uint32_t>(tiles);
     *total = align_up(c.off);
     return im;
 }
@@ -257,6 +260,9 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
     if (binning_capacity) *binning_capacity = 0;
     if (P < 0 || width <= 0 || height <= 0)
         return fail(GSR_ERR_ARGUMENT, "rasterize_forward: invalid sizes P=%d W=%d H=%d", P, width, height);
+    if (P >= kMaxGaussians)
+        return fail(GSR_ERR_ARGUMENT, "rasterize_forward: P=%d exceeds the tile-list entry limit %d", P,
+                    kMaxGaussians - 1);
     if (P == 0) return GSR_OK;  // RI/rasterize_points.cu:108: nothing is launched
     if (!means3D || !opacities || !viewmatrix || !projmatrix || !background || !out_color || !out_invdepth || !radii)
         return fail(GSR_ERR_ARGUMENT, "rasterize_forward: missing required input");
@@ -475,6 +481,7 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
         ra.rec = geom.rec;
         ra.bg = background; ra.dL_dpix = dL_dpix; ra.dL_dinvdepth = dL_dinvdepths; ra.img = img; ra.recs = recs;
         ra.depth_key = geom.depth_key; ra.lim_key = lim_key;
+        HIP_TRY(launch_tile_order(tiles, img.cost, img.order, stream), "tile_order");
         HIP_TRY(launch_render_bwd(ra, stream), "render_bwd");
     }
     if (int rc = check_debug(debug, stream, "render_bwd")) return rc;

@@ -34,15 +34,15 @@ namespace gsr {
 // positions >= limit").
 constexpr int kRecStride = 12;  // floats per staged record row (10 used), 48 B
 
-__global__ void __launch_bounds__(64) gauss_reduce_kernel(int P, const uint32_t* __restrict__ rec_start,
-                                                          const uint32_t* __restrict__ tiles_touched,
-                                                          const uint2* __restrict__ rect,
-                                                          const uint32_t* __restrict__ depth_key, uint32_t gx,
-                                                          const unsigned long long* __restrict__ lim_key,
-                                                          GradRecs recs, GradRecs sums) {
-    __shared__ __attribute__((aligned(16))) float s_rec[64 * kRecStride];
+// Sums of the records of the wave's 64 consecutive Gaussians [g0, g0 + 64), one
+// Gaussian per lane (zeros for lanes past P).  s_rec: 64 * kRecStride floats of LDS.
+__device__ __forceinline__ void reduce_records(int P, int g0, const uint32_t* __restrict__ rec_start,
+                                               const uint32_t* __restrict__ tiles_touched,
+                                               const uint2* __restrict__ rect,
+                                               const uint32_t* __restrict__ depth_key, uint32_t gx,
+                                               const unsigned long long* __restrict__ lim_key, const GradRecs& recs,
+                                               float* s_rec, float4& sa, float4& sb, float2& sc) {
     const int lane = threadIdx.x;
-    const int g0 = blockIdx.x * 64;
     const int g = g0 + lane;
     const bool valid = g < P;
     const int g_last = min(g0 + 63, P - 1);
@@ -60,8 +60,9 @@ __global__ void __launch_bounds__(64) gauss_reduce_kernel(int P, const uint32_t*
         w = (rr.y & 0xffffu) - x0;
         key = ((unsigned long long)depth_key[g] << 32) | (uint32_t)g;
     }
-    float4 sa = make_float4(0.f, 0.f, 0.f, 0.f), sb = sa;
-    float2 sc = make_float2(0.f, 0.f);
+    sa = make_float4(0.f, 0.f, 0.f, 0.f);
+    sb = sa;
+    sc = make_float2(0.f, 0.f);
     for (uint32_t base = E0; base < E1; base += 64) {
         const uint32_t e = base + lane;
         // owner of slot e: the largest lane whose segment starts at or before it
@@ -101,7 +102,21 @@ __global__ void __launch_bounds__(64) gauss_reduce_kernel(int P, const uint32_t*
         }
         __syncthreads();
     }
-    if (valid) {
+}
+
+__global__ void __launch_bounds__(64) gauss_reduce_kernel(int P, const uint32_t* __restrict__ rec_start,
+                                                          const uint32_t* __restrict__ tiles_touched,
+                                                          const uint2* __restrict__ rect,
+                                                          const uint32_t* __restrict__ depth_key, uint32_t gx,
+                                                          const unsigned long long* __restrict__ lim_key,
+                                                          GradRecs recs, GradRecs sums) {
+    __shared__ __attribute__((aligned(16))) float s_rec[64 * kRecStride];
+    const int g = blockIdx.x * 64 + (int)threadIdx.x;
+    float4 sa, sb;
+    float2 sc;
+    reduce_records(P, blockIdx.x * 64, rec_start, tiles_touched, rect, depth_key, gx, lim_key, recs, s_rec, sa, sb,
+                   sc);
+    if (g < P) {
         sums.a[g] = sa;
         sums.b[g] = sb;
         sums.c[g] = sc;
@@ -196,6 +211,8 @@ constexpr int kShRow = 48;     // floats per SH row staged through LDS (M = 16)
 constexpr int kShStride = 52;  // padded LDS row stride: conflict-free ds_read/write_b128
 
 // ---- 3. fused per-Gaussian backward ---------------------------------------------
+// (Folding the record sums into this kernel was measured slower: the sums' dependent loads
+// then run at this kernel's LDS-limited occupancy.)
 template <bool SH_LDS>
 __global__ void __launch_bounds__(64) gauss_bwd_kernel(GaussBwdArgs a) {
     __shared__ __attribute__((aligned(16))) float s_sh[SH_LDS ? 64 * kShStride : 4];

@@ -14,11 +14,12 @@
 //   K2 tile_scan     one workgroup: exclusive scans of the tile counts (-> the
 //                    per-tile ranges, identifyTileRanges' output) and of the
 //                    chunk totals (-> each chunk's first record index); it also
-//                    lists the tiles too long for one wave's sort (three classes);
+//                    lists the tiles too long for one wave's sort (four classes);
 //   K3 tile_scatter  every chunk loads its cursors (tile start + chunk offset)
 //                    into LDS and scatters 64-bit keys (depth bits << 32 |
-//                    index) with LDS atomics; it also writes each Gaussian's
-//                    first record index;
+//                    index << 4) with LDS atomics (the low 4 bits of a tile-list
+//                    entry, its quadrant mask, are filled in by the forward
+//                    render); it also writes each Gaussian's first record index;
 //   K4 tile_sort     per tile, a bitonic network held in registers (exchanges
 //                    inside a lane, across lanes by swizzle/permute, across
 //                    waves through LDS), writing the Gaussian ids -- the tile
@@ -45,8 +46,11 @@ constexpr int kBinThreads = 1024;
 constexpr int kBinWaves = kBinThreads / 64;
 constexpr uint32_t kLdsTilesMax = 36864;  // K3 keeps one u32 per tile in LDS (144 KiB)
 constexpr uint32_t kSortWaveMax = 1024;   // longest list tile_sort_kernel sorts (one wave, 16 keys per lane)
-constexpr uint32_t kSortMidMax = 2048;    // class 1: (1024, 2048], 128 threads x 16 keys
-constexpr uint32_t kBigRegMax = 8192;     // class 2: (2048, 8192], 512 threads x 16 keys; class 3: longer
+// Longer lists go to persistent per-class kernels, T threads x 16 keys in registers:
+// class 0 (1024, 2048] T = 128, class 1 (2048, 4096] T = 256, class 2 (4096, 8192]
+// T = 512; class 3 (> 8192) sorts in global memory.
+constexpr int kSortClasses = 4;
+constexpr uint32_t kBigRegMax = 8192;
 
 typedef unsigned long long u64;
 
@@ -95,10 +99,11 @@ __device__ T block_exclusive_scan(T v, T* s_tmp, T* total) {
     return base + incl - v;
 }
 
-// Calls f(valid, owner, tile) once per step on every lane of the wave; over all
-// steps, the valid calls are exactly the (Gaussian, tile) instances of the wave's
-// 64 Gaussians (lane l: n tiles in rectangle r), each once; `owner` is the lane of
-// the instance's Gaussian.  f may shuffle from `owner` (all lanes are active).
+// Calls f(valid, owner, tile, tx, ty) once per step on every lane of the wave; over all
+// steps, the valid calls are exactly the (Gaussian, tile) instances of the wave's 64
+// Gaussians (lane l: n tiles in rectangle r), each once; `owner` is the lane of the
+// instance's Gaussian, (tx, ty) the tile's column and row.  f may shuffle from `owner`
+// (all lanes are active).
 template <class F>
 __device__ __forceinline__ void for_each_instance(uint32_t n, uint2 r, uint32_t gx, F&& f) {
     const int lane = threadIdx.x & 63;
@@ -122,12 +127,14 @@ __device__ __forceinline__ void for_each_instance(uint32_t n, uint2 r, uint32_t 
         const uint32_t k = s - __shfl(excl, owner);
         const uint32_t ow = __shfl(w, owner), org = __shfl(r.x, owner);
         const bool valid = s < total;
-        uint32_t tile = 0;
+        uint32_t tile = 0, tx = 0, ty = 0;
         if (valid) {
-            const uint32_t ty = k / ow, tx = k - ty * ow;
-            tile = ((org >> 16) + ty) * gx + (org & 0xffffu) + tx;
+            const uint32_t dy = k / ow;
+            tx = (org & 0xffffu) + (k - dy * ow);
+            ty = (org >> 16) + dy;
+            tile = ty * gx + tx;
         }
-        f(valid, owner, tile);
+        f(valid, owner, tile, tx, ty);
     }
 }
 
@@ -225,7 +232,7 @@ __global__ void __launch_bounds__(kBinThreads) tile_count_kernel(int P, int chun
         const uint32_t g = p < g1 ? order[p] : 0u;
         const uint32_t n = p < g1 ? tiles_touched[g] : 0u;
         const uint2 r = n ? rect[g] : make_uint2(0u, 0u);
-        for_each_instance(n, r, gx, [&](bool valid, int, uint32_t t) {
+        for_each_instance(n, r, gx, [&](bool valid, int, uint32_t t, uint32_t, uint32_t) {
             if (!valid) return;
             if (LDS)
                 atomicAdd(&s_hist[t >> 1], 1u << ((t & 1u) * 16));
@@ -260,8 +267,8 @@ __global__ void __launch_bounds__(kBinThreads) tile_scan_kernel(uint32_t tiles, 
                                                                 u64 cap, uint32_t* __restrict__ cls_list,
                                                                 uint32_t* __restrict__ cls_count) {
     __shared__ u64 s_tmp[kBinWaves];
-    __shared__ uint32_t s_cls[3];
-    if (threadIdx.x < 3) s_cls[threadIdx.x] = 0;  // published by the scan's barriers
+    __shared__ uint32_t s_cls[kSortClasses];
+    if (threadIdx.x < kSortClasses) s_cls[threadIdx.x] = 0;  // published by the scan's barriers
     const uint32_t T = blockDim.x;
     u64 carry = 0;
     for (uint32_t base = 0; base < tiles; base += T * kScanV) {
@@ -283,8 +290,8 @@ __global__ void __launch_bounds__(kBinThreads) tile_scan_kernel(uint32_t tiles, 
                 const u64 lo = at < cap ? at : cap, hi = at + v[i] < cap ? at + v[i] : cap;
                 ranges[b + i] = make_uint2((uint32_t)lo, (uint32_t)hi);
                 tile_base[b + i] = (uint32_t)at;
-                if (v[i] > kSortWaveMax) {  // long list: class 1, 2 or 3 (K4)
-                    const int c = v[i] <= kSortMidMax ? 0 : v[i] <= kBigRegMax ? 1 : 2;
+                if (v[i] > kSortWaveMax) {  // long list: one of the class kernels (K4)
+                    const int c = v[i] <= 2048u ? 0 : v[i] <= 4096u ? 1 : v[i] <= kBigRegMax ? 2 : 3;
                     cls_list[(size_t)c * tiles + atomicAdd(&s_cls[c], 1u)] = b + i;
                 }
             }
@@ -303,7 +310,7 @@ __global__ void __launch_bounds__(kBinThreads) tile_scan_kernel(uint32_t tiles, 
         carry += all;
     }
     __syncthreads();
-    if (threadIdx.x < 3) cls_count[threadIdx.x] = s_cls[threadIdx.x];
+    if (threadIdx.x < kSortClasses) cls_count[threadIdx.x] = s_cls[threadIdx.x];
 }
 
 // ---- K3 ---------------------------------------------------------------------
@@ -349,11 +356,11 @@ __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
         const uint32_t n = p < q1 ? tiles_touched[g] : 0u;
         const uint2 r = n ? rect[g] : make_uint2(0u, 0u);
         const uint32_t dk = n ? depth_key[g] : 0u;
-        for_each_instance(n, r, gx, [&](bool valid, int owner, uint32_t t) {
+        for_each_instance(n, r, gx, [&](bool valid, int owner, uint32_t t, uint32_t, uint32_t) {
             const uint32_t kh = __shfl(dk, owner), kg = __shfl(g, owner);
             if (!valid) return;
             const uint32_t pos = LDS ? atomicAdd(&s_cur[t], 1u) : atomicAdd(&tile_base[t], 1u);
-            if (pos < cap) keys[pos] = ((u64)kh << 32) | kg;  // cap: redone if exceeded
+            if (pos < cap) keys[pos] = ((u64)kh << 32) | (kg << kEntryMaskBits);  // cap: redone if exceeded
         });
     }
 #ifdef GSR_STAMPS
@@ -454,8 +461,9 @@ __device__ __forceinline__ void bitonic_regs(u64 (&a)[E], u64* s_x) {
     }
 }
 
-// Sort keys[lo, lo + n) (n <= T * E, T = the workgroup size) and write the Gaussian
-// ids (low key halves).
+// Sort keys[lo, lo + n) (n <= T * E, T = the workgroup size) and write the tile-list
+// entries (low key halves: Gaussian << 4; the Gaussian index is unique, so the order is the
+// reference's (depth, index) order).
 template <int T, int E>
 __device__ __forceinline__ void sort_list(const u64* __restrict__ keys, uint32_t lo, uint32_t n,
                                           uint32_t* __restrict__ gid_sorted, u64* s_x) {
@@ -645,10 +653,12 @@ hipError_t launch_tile_sort(uint32_t tiles, const uint2* ranges, const GeomState
     const auto grid = [&](uint32_t want) { return dim3(tiles < want ? tiles : want); };
     hipLaunchKernelGGL(tile_sort_class_kernel<128>, grid(2048), dim3(128), 0, stream, ranges, b.keys, c,
                        b.gid_sorted, g.cls_list, g.cls_count);
-    hipLaunchKernelGGL(tile_sort_class_kernel<512>, grid(512), dim3(512), 0, stream, ranges, b.keys, c,
+    hipLaunchKernelGGL(tile_sort_class_kernel<256>, grid(1024), dim3(256), 0, stream, ranges, b.keys, c,
                        b.gid_sorted, g.cls_list + tiles, g.cls_count + 1);
-    hipLaunchKernelGGL(tile_sort_global_kernel, grid(256), dim3(kBinThreads), 0, stream, ranges, b.keys, c,
+    hipLaunchKernelGGL(tile_sort_class_kernel<512>, grid(512), dim3(512), 0, stream, ranges, b.keys, c,
                        b.gid_sorted, g.cls_list + 2 * (size_t)tiles, g.cls_count + 2);
+    hipLaunchKernelGGL(tile_sort_global_kernel, grid(256), dim3(kBinThreads), 0, stream, ranges, b.keys, c,
+                       b.gid_sorted, g.cls_list + 3 * (size_t)tiles, g.cls_count + 3);
     return hipGetLastError();
 }
 

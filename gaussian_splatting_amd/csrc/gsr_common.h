@@ -44,6 +44,15 @@ constexpr float SH_C3_0 = -0.5900435899266435f, SH_C3_1 = 2.890611442640554f, SH
 // ---------------------------------------------------------------------------
 constexpr int kRecRows = 4;
 
+// Tile-list entries (BinningState::gid_sorted) are Gaussian << 4 | quadrant mask: bit k set
+// when the splat's alpha >= 1/255 footprint reaches a pixel centre of the tile's 8x8
+// quadrant k (footprint.h).  Binning writes the mask bits as 0; the forward render computes
+// the masks of the entries it stages and writes them back, and the backward, which only
+// visits entries the forward staged, reads them.  Hence P < 2^28.
+constexpr int kEntryMaskBits = 4;
+constexpr uint32_t kEntryMask = 0xfu;
+constexpr int kMaxGaussians = 1 << (32 - kEntryMaskBits);
+
 __host__ __device__ inline size_t align_up(size_t x, size_t a = kAlign) { return (x + a - 1) / a * a; }
 
 // Bump allocator over a caller-provided chunk (the three opaque uint8 tensors of
@@ -77,8 +86,8 @@ struct GeomState {
     uint32_t* n_visible;        // [1] entries of order
     uint32_t* tile_base;        // [tiles] first instance of each tile (scatter cursors without LDS)
     uint32_t* chunk_off;        // [chunks][tiles] each chunk's offset inside each tile's block
-    uint32_t* cls_list;         // [3][tiles] tiles whose lists are too long for one wave's sort, by class
-    uint32_t* cls_count;        // [3] entries of each class list
+    uint32_t* cls_list;         // [4][tiles] tiles whose lists are too long for one wave's sort, by class
+    uint32_t* cls_count;        // [4] entries of each class list
     unsigned long long* chunk_total;  // [chunks] tiles_touched per Gaussian chunk
     unsigned long long* chunk_base;   // [chunks] its exclusive scan
     unsigned long long* total;        // [1] number of instances (num_rendered)
@@ -90,12 +99,16 @@ struct ImageState {
     uint32_t* n_contrib;  // [N]
     float* accum;         // [4][N]: colour r,g,b and inverse depth, without background
     uint2* ranges;        // [tiles]
+    uint32_t* cost;       // [tiles] the forward's blend work per tile (slot-entries), the backward's
+                          // scheduling estimate
+    uint32_t* order;      // [tiles] the backward's tile order: heaviest first
 };
 
 // Binning state: per instance (R, or the capacity the buffer was requested for).
 struct BinningState {
-    unsigned long long* keys;  // per instance, grouped by tile: depth bits << 32 | Gaussian index
-    uint32_t* gid_sorted;      // Gaussian of each instance in (tile, depth, index) order: the tile lists
+    unsigned long long* keys;  // per instance, grouped by tile: depth bits << 32 | tile-list entry
+    uint32_t* gid_sorted;      // entry of each instance in (tile, depth, index) order: the tile lists
+                               // (Gaussian << kEntryMaskBits | quadrant mask)
 };
 
 // Per-instance gradient records (backward scratch), SoA so stores are aligned.

@@ -29,7 +29,7 @@ struct RenderFwdArgs {
     int W, H;
     uint32_t gx, gy;
     const uint2* ranges;
-    const uint32_t* gid_sorted;
+    uint32_t* gid_sorted;  // the forward writes each staged entry's quadrant mask into its low bits
     const float4* rec;
     const float* bg;
     float* out_color;
@@ -68,7 +68,7 @@ struct GaussBwdArgs {
     int antialiasing;
     const int* radii;
     GeomState geom;
-    GradRecs sums;  // per depth rank: summed render gradients
+    GradRecs sums;  // per Gaussian: summed render gradients (gauss_reduce_kernel)
     int have_invdepth;
     float* dL_dmean2D;    // [P,3]
     float* dL_dconic;     // [P,4] or null
@@ -97,6 +97,7 @@ hipError_t launch_tile_sort(uint32_t tiles, const uint2* ranges, const GeomState
 // render.hip
 hipError_t launch_render_fwd(const RenderFwdArgs& a, hipStream_t stream);
 hipError_t launch_render_bwd(const RenderBwdArgs& a, hipStream_t stream);
+hipError_t launch_tile_order(uint32_t tiles, const uint32_t* cost, uint32_t* order, hipStream_t stream);
 // backward.hip
 hipError_t launch_gauss_reduce(int P, const GeomState& g, uint32_t gx, const unsigned long long* lim_key,
                                const GradRecs& recs, const GradRecs& sums, hipStream_t stream);

@@ -31,6 +31,7 @@
 // (tile, Gaussian) instance -- and written with plain stores.  There are no
 // float atomics anywhere, so the result is bitwise reproducible (the reference
 // issues 10 global float atomics per pixel-Gaussian pair, CR/backward.cu:569-609).
+#include "footprint.h"
 #include "kernels.h"
 
 namespace gsr {
@@ -47,73 +48,6 @@ GSR_STAMP_BUFFER(g_st_rbwd);
 #else
 #define GSR_BWD_OCCUPANCY
 #endif
-
-// Quadrant mask of one splat's footprint box inside the tile at (tile_x0, tile_y0).
-__device__ __forceinline__ uint32_t quad_bits(float4 v1, float4 v2, int tile_x0, int tile_y0) {
-    const uint32_t bx = __float_as_uint(v1.w), by = __float_as_uint(v2.w);
-    const int x0 = unpack_lo(bx), x1 = unpack_hi(bx), y0 = unpack_lo(by), y1 = unpack_hi(by);
-    uint32_t q = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int qx0 = tile_x0 + (k & 1) * 8, qy0 = tile_y0 + (k >> 1) * 8;
-        if (x0 <= qx0 + 7 && x1 >= qx0 && y0 <= qy0 + 7 && y1 >= qy0) q |= 1u << k;
-    }
-    return q;
-}
-
-// Conic quadratic form Q(d) = a dx^2 + 2 b dx dy + c dy^2 (power = -Q/2), minimised over the
-// pixel-centre rectangle [x0,x1] x [y0,y1] of offsets d = p - mean.  For a positive-definite
-// conic the minimum is 0 if the mean is inside, otherwise on an edge, where Q is a 1-D
-// parabola minimised at the clamped vertex.
-__device__ __forceinline__ float rect_min_form(float a, float b, float c, float ra, float rc, float x0, float x1,
-                                               float y0, float y1) {
-    if (x0 <= 0.f && x1 >= 0.f && y0 <= 0.f && y1 >= 0.f) return 0.f;
-    float best = INFINITY;
-#pragma unroll
-    for (int k = 0; k < 2; k++) {
-        const float dx = k ? x1 : x0;
-        const float dy = fminf(y1, fmaxf(y0, -b * dx * rc));
-        best = fminf(best, a * dx * dx + (2.f * b * dx + c * dy) * dy);
-        const float ey = k ? y1 : y0;
-        const float ex = fminf(x1, fmaxf(x0, -b * ey * ra));
-        best = fminf(best, c * ey * ey + (2.f * b * ey + a * ex) * ex);
-    }
-    return best;
-}
-
-// Quadrant mask refined by the footprint ellipse itself: a quadrant the box overlaps is
-// dropped when no pixel centre of it lies inside the alpha >= 1/255 ellipse
-// Q <= 2 ln(255 o), with the same relative/absolute margin the box uses (preprocess.hip), so
-// the test stays conservative under fp32 rounding of the per-pixel evaluation.  Degenerate
-// conics keep the box result.  Runs while staging, one list entry per lane.
-__device__ __forceinline__ uint32_t quad_bits_exact(float4 v0, float4 v1, float4 v2, int tile_x0, int tile_y0) {
-    uint32_t q = quad_bits(v1, v2, tile_x0, tile_y0);
-    const float a = v0.z, b = v0.w, c = v1.x, o = v1.y;
-    if (q == 0 || !(a > 0.f && c > 0.f && a * c - b * b > 0.f) || !(o > 0.f)) return q;
-    const float tau = fmaxf(0.f, __logf(255.f * o)) * 1.001f + 0.01f;
-    const float lim = 2.f * tau;
-    const float ra = 1.f / a, rc = 1.f / c;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        if (!(q & (1u << k))) continue;
-        const float x0 = (float)(tile_x0 + (k & 1) * 8) - v0.x, y0 = (float)(tile_y0 + (k >> 1) * 8) - v0.y;
-        if (rect_min_form(a, b, c, ra, rc, x0, x0 + 7.f, y0, y0 + 7.f) > lim) q &= ~(1u << k);
-    }
-    return q;
-}
-
-// One quadrant's bit of quad_bits_exact: does the alpha >= 1/255 footprint (box, then
-// ellipse) reach a pixel centre of the 8x8 quadrant at (qx0, qy0)?
-__device__ __forceinline__ bool quad_hit(float4 v0, float4 v1, float4 v2, int qx0, int qy0) {
-    const uint32_t bx = __float_as_uint(v1.w), by = __float_as_uint(v2.w);
-    if (!(unpack_lo(bx) <= qx0 + 7 && unpack_hi(bx) >= qx0 && unpack_lo(by) <= qy0 + 7 && unpack_hi(by) >= qy0))
-        return false;
-    const float a = v0.z, b = v0.w, c = v1.x, o = v1.y;
-    if (!(a > 0.f && c > 0.f && a * c - b * b > 0.f) || !(o > 0.f)) return true;
-    const float tau = fmaxf(0.f, __logf(255.f * o)) * 1.001f + 0.01f;
-    const float x0 = (float)qx0 - v0.x, y0 = (float)qy0 - v0.y;
-    return rect_min_form(a, b, c, 1.f / a, 1.f / c, x0, x0 + 7.f, y0, y0 + 7.f) <= 2.f * tau;
-}
 
 __device__ __forceinline__ uint32_t uniform_u32(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
@@ -158,6 +92,7 @@ __global__ void __launch_bounds__(64) render_fwd_tile_kernel(RenderFwdArgs a) {
     float Tl[4], Tf[4], C0[4], C1[4], C2[4], D[4];
     uint32_t last[4];
     uint32_t alive = 0;  // wave-uniform: slots with at least one pixel still blending
+    uint32_t work = 0;   // wave-uniform: slot-entries blended (the backward's scheduling estimate)
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         const int px = tile_x0 + (q & 1) * 8 + lx, py = tile_y0 + (q >> 1) * 8 + ly;
@@ -172,12 +107,15 @@ __global__ void __launch_bounds__(64) render_fwd_tile_kernel(RenderFwdArgs a) {
     for (int b0 = 0; b0 < n && alive; b0 += kBatch) {
         uint32_t qm = 0;
         if (b0 + lane < n) {
-            const float4* rec = a.rec + (size_t)kRecRows * a.gid_sorted[range.x + b0 + lane];
+            uint32_t* ent = a.gid_sorted + range.x + b0 + lane;  // Gaussian << 4 | quadrant mask
+            const uint32_t gid = *ent >> kEntryMaskBits;
+            const float4* rec = a.rec + (size_t)kRecRows * gid;
             const float4 v0 = rec[0], v1 = rec[1], v2 = rec[2];
             s_xy[lane] = make_float4(v0.x, v0.y, v1.y, v1.z);
             s_col[lane] = v2;
             qm = quad_bits_exact(v0, v1, v2, tile_x0, tile_y0);
             s_cq[lane] = stage_conic(v0, v1, qm);
+            *ent = (gid << kEntryMaskBits) | qm;  // for the backward, which visits only staged entries
         }
         __syncthreads();
         unsigned long long todo = __ballot(qm != 0);
@@ -187,6 +125,7 @@ __global__ void __launch_bounds__(64) render_fwd_tile_kernel(RenderFwdArgs a) {
             const float4 xy = s_xy[j], cq = s_cq[j], col = s_col[j];
             const uint32_t m = uniform_u32(__float_as_uint(cq.w)) & alive;
             const uint32_t pos1 = (uint32_t)(b0 + j + 1);
+            work += (uint32_t)__builtin_popcount(m);
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 if (!(m & (1u << q))) continue;  // uniform: footprint misses this quadrant
@@ -218,6 +157,7 @@ __global__ void __launch_bounds__(64) render_fwd_tile_kernel(RenderFwdArgs a) {
     GSR_STAMP(g_st_rfwd, tile, 1);
     GSR_STAMP_RT(g_st_rfwd, tile, 5);
     GSR_STAMP_VAL(g_st_rfwd, tile, 2, n);
+    if (lane == 0) a.img.cost[tile] = work;
     const size_t N = (size_t)a.W * a.H;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
@@ -240,126 +180,20 @@ __global__ void __launch_bounds__(64) render_fwd_tile_kernel(RenderFwdArgs a) {
   }
 }
 
-// ---------------------------------------------------------------------------
-// Quadrant units.  One wave per (tile, 8x8 quadrant), one pixel per lane: four
-// independent waves per tile.  With one wave per tile (render_fwd_tile_kernel) a
-// SIMD holds ~8 tiles for the whole launch and the kernel ends with the SIMD whose
-// tiles happened to be slowest, running its last waves alone at a fraction of its
-// issue rate (measured: slowest wave ~2x the mean).  Four times as many, four times
-// shorter units let the workgroup dispatcher keep every SIMD full until the end.
-// Every unit stages its tile's list itself (the records of one tile are read by its
-// four units, close in time on the same XCD, so the repeats hit that XCD's L2) and
-// keeps only the entries whose alpha >= 1/255 footprint reaches its quadrant.
-__device__ __forceinline__ uint32_t unit_of_block(uint32_t b, uint32_t units) {
-    // blocks are dealt round-robin over the 8 XCDs: make XCD x run units [x U/8, (x+1) U/8)
-    // in order, so a tile's four units share an L2 and each L2 sees one band of the image
-    if (units % 8u) return b;
-    return (b % 8u) * (units / 8u) + b / 8u;
-}
-
-__global__ void __launch_bounds__(64) render_fwd_quad_kernel(RenderFwdArgs a) {
-    const uint32_t units = a.gx * a.gy * 4u;
-    const uint32_t u = unit_of_block(blockIdx.x, units);
-    const uint32_t tile = u >> 2, q = u & 3u;
-    const int lane = threadIdx.x;
-    const int qx0 = (int)(tile % a.gx) * kTile + (int)(q & 1u) * 8, qy0 = (int)(tile / a.gx) * kTile + (int)(q >> 1) * 8;
-    const int px = qx0 + (lane & 7), py = qy0 + (lane >> 3);
-    const float pxf = (float)px, pyf = (float)py;
-    GSR_STAMP(g_st_rfwd, u, 0);
-    GSR_STAMP_HWID(g_st_rfwd, u);
-    GSR_STAMP_RT(g_st_rfwd, u, 4);
-
-    __shared__ float4 s_xy[kBatch], s_cq[kBatch], s_col[kBatch];  // (x, y, o, 1/z), (A, B, C, -), rgb
-
-    float Tl = (px < a.W && py < a.H) ? 1.f : 0.f, Tf = 0.f, C0 = 0.f, C1 = 0.f, C2 = 0.f, D = 0.f;
-    uint32_t last = 0;
-    bool alive = __any(Tl > 0.f);
-
-    const uint2 range = a.ranges[tile];
-    const int n = (int)(range.y - range.x);
-    for (int b0 = 0; b0 < n && alive; b0 += kBatch) {
-        bool hit = false;
-        if (b0 + lane < n) {
-            const float4* rec = a.rec + (size_t)kRecRows * a.gid_sorted[range.x + b0 + lane];
-            const float4 v0 = rec[0], v1 = rec[1], v2 = rec[2];
-            s_xy[lane] = make_float4(v0.x, v0.y, v1.y, v1.z);
-            s_col[lane] = v2;
-            s_cq[lane] = stage_conic(v0, v1, 0u);
-            hit = quad_hit(v0, v1, v2, qx0, qy0);
-        }
-        __syncthreads();
-        unsigned long long todo = __ballot(hit);
-        while (todo) {
-            const int j = __builtin_ctzll(todo);
-            todo &= todo - 1;
-            const float4 xy = s_xy[j], cq = s_cq[j], col = s_col[j];
-            const float dx = xy.x - pxf, dy = xy.y - pyf;
-            const float p2 = dx * (cq.x * dx + cq.y * dy) + cq.z * dy * dy;
-            float G;
-            const float alpha = splat_alpha(p2, xy.z, G);
-            const float w0 = alpha * Tl;  // > 0 iff this pixel blends the splat
-            if (!__any(w0 > 0.f)) continue;  // uniform
-            const float test_T = Tl * (1.f - alpha);
-            const bool term = test_T < 0.0001f;  // live pixel: ends it, splat not added
-            const float w = term ? 0.f : w0;
-            // first termination wins (a finished pixel has Tl = 0); both are >= 0, so an integer max
-            Tf = __uint_as_float(max(__float_as_uint(Tf), term ? __float_as_uint(Tl) : 0u));
-            Tl = term ? 0.f : test_T;
-            C0 += col.x * w;
-            C1 += col.y * w;
-            C2 += col.z * w;
-            D += xy.w * w;
-            last = w > 0.f ? (uint32_t)(b0 + j + 1) : last;
-            if (!__any(Tl > 0.f)) {  // uniform: every pixel of the quadrant has terminated
-                alive = false;
-                break;
-            }
-        }
-        __syncthreads();
-    }
-    GSR_STAMP(g_st_rfwd, u, 1);
-    GSR_STAMP_RT(g_st_rfwd, u, 5);
-    GSR_STAMP_VAL(g_st_rfwd, u, 2, n);
-    if (px < a.W && py < a.H) {
-        const size_t N = (size_t)a.W * a.H;
-        const size_t pix = (size_t)py * a.W + px;
-        const float T = Tl > 0.f ? Tl : Tf;
-        a.img.final_T[pix] = T;
-        a.img.n_contrib[pix] = last;
-        a.img.accum[pix] = C0;
-        a.img.accum[N + pix] = C1;
-        a.img.accum[2 * N + pix] = C2;
-        a.img.accum[3 * N + pix] = D;
-        a.out_color[pix] = C0 + T * a.bg[0];
-        a.out_color[N + pix] = C1 + T * a.bg[1];
-        a.out_color[2 * N + pix] = C2 + T * a.bg[2];
-        a.out_invdepth[pix] = D;
-    }
-}
-
-static int render_variant() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("GSR_RENDER_FWD");
-        v = (e && e[0] == 't') ? 0 : 1;  // "tile": one wave per tile; default: quadrant units
-    }
-    return v;
-}
-
 hipError_t launch_render_fwd(const RenderFwdArgs& a, hipStream_t stream) {
     const uint32_t tiles = a.gx * a.gy;
     if (tiles == 0) return hipSuccess;
-    if (render_variant() == 0)
-        hipLaunchKernelGGL(render_fwd_tile_kernel, dim3(tiles), dim3(kWave), 0, stream, a);
-    else
-        hipLaunchKernelGGL(render_fwd_quad_kernel, dim3(tiles * 4), dim3(kWave), 0, stream, a);
+    hipLaunchKernelGGL(render_fwd_tile_kernel, dim3(tiles), dim3(kWave), 0, stream, a);
     return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(RenderBwdArgs a) {
   {
-    const uint32_t tile = blockIdx.x;
+    // heaviest tiles first (tile_order_kernel): the dispatcher deals them round-robin over
+    // the SIMDs, so every SIMD gets a similar share of the work, and the light tiles at the
+    // end of the order fill the slots that free up first
+    const uint32_t tile = a.img.order[blockIdx.x];
     const int tile_x0 = (int)(tile % a.gx) * kTile, tile_y0 = (int)(tile / a.gx) * kTile;
     const int lane = threadIdx.x;
     const int lx = lane & 7, ly = lane >> 3;
@@ -426,7 +260,7 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
     if (lane == 0) {
         unsigned long long lk = 0;
         if (limit > 0) {
-            const uint32_t gl = a.gid_sorted[range.x + limit - 1];
+            const uint32_t gl = a.gid_sorted[range.x + limit - 1] >> kEntryMaskBits;
             lk = ((unsigned long long)a.depth_key[gl] << 32) | gl;
         }
         a.lim_key[tile] = lk;
@@ -436,7 +270,8 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
         const bool has = b0 + lane < limit;
         uint32_t qm = 0, e = 0;
         if (has) {
-            const float4* rec = a.rec + (size_t)kRecRows * a.gid_sorted[range.x + b0 + lane];
+            const uint32_t ent = a.gid_sorted[range.x + b0 + lane];  // Gaussian << 4 | quadrant mask
+            const float4* rec = a.rec + (size_t)kRecRows * (ent >> kEntryMaskBits);
             const float4 v0 = rec[0], v1 = rec[1], v2 = rec[2], v3 = rec[3];
             // this instance's emission index (row 3: tile rectangle and first emission)
             e = __float_as_uint(v3.w) + (tty - __float_as_uint(v3.y)) * __float_as_uint(v3.z) +
@@ -444,7 +279,7 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
             s_xy[lane] = make_float4(v0.x, v0.y, v1.y, v1.z);
             s_col[lane] = v2;
             s_abc[lane] = make_float4(v0.z, v0.w, v1.x, 0.f);  // raw conic, for the flush
-            qm = quad_bits_exact(v0, v1, v2, tile_x0, tile_y0);
+            qm = ent & kEntryMask;
             s_cq[lane] = stage_conic(v0, v1, qm);
         }
         __syncthreads();
@@ -540,6 +375,47 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
     GSR_STAMP_VAL(g_st_rbwd, tile, 2, n);
     GSR_STAMP_VAL(g_st_rbwd, tile, 3, limit);
   }
+}
+
+// ---------------------------------------------------------------------------
+// Backward schedule: tiles in decreasing order of the forward's blend work (a counting sort
+// over 1024 cost buckets in one workgroup).  The order inside a bucket is whatever the LDS
+// atomics produce -- it only changes which SIMD runs which tile, never a result.
+constexpr int kOrderThreads = 1024, kOrderBuckets = 1024;
+
+__global__ void __launch_bounds__(kOrderThreads) tile_order_kernel(uint32_t tiles, const uint32_t* __restrict__ cost,
+                                                                   uint32_t* __restrict__ order) {
+    __shared__ uint32_t s_cnt[kOrderBuckets];
+    __shared__ uint32_t s_max;
+    if (threadIdx.x == 0) s_max = 0;
+    for (uint32_t i = threadIdx.x; i < kOrderBuckets; i += kOrderThreads) s_cnt[i] = 0;
+    __syncthreads();
+    uint32_t m = 0;
+    for (uint32_t t = threadIdx.x; t < tiles; t += kOrderThreads) m = max(m, cost[t]);
+    atomicMax(&s_max, m);
+    __syncthreads();
+    const unsigned long long cmax = (unsigned long long)s_max + 1;
+    auto bucket = [&](uint32_t c) {  // heaviest -> bucket 0
+        return (uint32_t)(((cmax - 1 - c) * (unsigned long long)kOrderBuckets) / cmax);
+    };
+    for (uint32_t t = threadIdx.x; t < tiles; t += kOrderThreads) atomicAdd(&s_cnt[bucket(cost[t])], 1u);
+    __syncthreads();
+    if (threadIdx.x == 0) {  // 1024 buckets: a serial scan is a few microseconds at most
+        uint32_t at = 0;
+        for (int b = 0; b < kOrderBuckets; b++) {
+            const uint32_t c = s_cnt[b];
+            s_cnt[b] = at;
+            at += c;
+        }
+    }
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < tiles; t += kOrderThreads) order[atomicAdd(&s_cnt[bucket(cost[t])], 1u)] = t;
+}
+
+hipError_t launch_tile_order(uint32_t tiles, const uint32_t* cost, uint32_t* order, hipStream_t stream) {
+    if (tiles == 0) return hipSuccess;
+    hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(kOrderThreads), 0, stream, tiles, cost, order);
+    return hipGetLastError();
 }
 
 hipError_t launch_render_bwd(const RenderBwdArgs& a, hipStream_t stream) {

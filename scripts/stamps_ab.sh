@@ -1,4 +1,4 @@
 mkdir -p gpurun_out/st2
-for v in quad tile; do
-GSR_RENDER_FWD=$v GSR_LIBRARY=$PWD/gaussian_splatting_amd/lib/libgsr_stamps.so timeout -k 10 300 python tools/stamps.py > gpurun_out/st2/stamps_$v.json 2>&1 || exit 1
+for v in tile; do
+GSR_RENDER=$v GSR_LIBRARY=$PWD/gaussian_splatting_amd/lib/libgsr_stamps.so timeout -k 10 300 python tools/stamps.py > gpurun_out/st2/stamps_$v.json 2>&1 || exit 1
 done

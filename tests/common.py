@@ -152,9 +152,11 @@ SMALL_CASES = [
     Case("scale_modifier", P=200, W=64, H=48, scale_modifier=0.7),
     Case("yawed_view", P=300, W=64, H=48, yaw=15.0),
     Case("dense_opaque", P=2000, W=64, H=64, opacity_std=3.0, scale_range=(0.05, 0.3)),
-    # tile lists past one wave's sort (binning.hip K4 classes): (1024, 2048], (2048, 8192], > 8192 entries
+    # tile lists past one wave's sort (binning.hip K4 classes): (1024, 2048], (2048, 4096], (4096, 8192],
+    # > 8192 entries
     Case("lists_1k_2k", P=1800, W=32, H=32, scale_range=(0.1, 0.4)),
-    Case("lists_2k_8k", P=5000, W=32, H=32, scale_range=(0.1, 0.4)),
+    Case("lists_2k_4k", P=5000, W=32, H=32, scale_range=(0.1, 0.4)),
+    Case("lists_4k_8k", P=10000, W=32, H=32, scale_range=(0.1, 0.4)),
     Case("lists_over_8k", P=10000, W=16, H=16, scale_range=(0.1, 0.4)),
 ]
 

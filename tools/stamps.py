@@ -124,13 +124,20 @@ def main():
         timeline("tile_count", read(fb, 0, nchunks), [0, 1, 2, 3]),
         timeline("tile_scatter", read(fb, 1, nchunks), [0, 1, 2]),
         timeline("tile_sort", read(fb, 2, tiles), [0, 1], extra={"n": 2}),
-        timeline("render_fwd", read(fr, 0, tiles * (1 if os.environ.get("GSR_RENDER_FWD", "q")[0] == "t" else 4)),
+        timeline("render_fwd", read(fr, 0, tiles),
                  [0, 1], extra={"n": 2}),
         timeline("render_bwd", read(fr, 1, tiles), [0, 1], extra={"n": 2, "limit": 3}),
     ]
     for r in res:
         print(json.dumps({k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items()}))
-    nf = tiles * (1 if os.environ.get("GSR_RENDER_FWD", "q")[0] == "t" else 4)
+    nf = tiles
+    sf, sb = read(fr, 0, nf), read(fr, 1, tiles)
+    fwd_tile = (sf[:, 1] - sf[:, 0]).reshape(tiles, -1).sum(1).astype(np.float64)
+    bwd_tile = (sb[:, 1] - sb[:, 0]).astype(np.float64)
+    print(json.dumps({"corr_fwd_bwd_tile_duration": float(np.corrcoef(fwd_tile, bwd_tile)[0, 1]),
+                      "corr_bwd_dur_limit": float(np.corrcoef(bwd_tile, sb[:, 3])[0, 1]),
+                      "bwd_dur_cv": float(bwd_tile.std() / bwd_tile.mean()),
+                      "fwd_dur_cv": float(fwd_tile.std() / fwd_tile.mean())}))
     for r in occupancy("render_fwd", read(fr, 0, nf))[:3] + occupancy("render_bwd", read(fr, 1, tiles))[:3]:
         print(json.dumps(r))
 
