@@ -127,8 +127,8 @@ gsr::GeomState carve_geom(char* base, int P, uint32_t gx, uint32_t gy, size_t* t
     g.n_visible = c.take<uint32_t>(1);
 
     g.chunk_off = c.take<uint32_t>(chunks * tiles);
-    g.cls_list = c.take<uint32_t>(4 * (size_t)tiles);
-    g.cls_count = c.take<uint32_t>(4);
+    g.cls_list = c.take<uint32_t>(2 * (size_t)tiles);
+    g.cls_count = c.take<uint32_t>(2);
     g.chunk_total = c.take<unsigned long long>(chunks);
     g.chunk_base = c.take<unsigned long long>(chunks);
     g.total = c.take<unsigned long long>(1);

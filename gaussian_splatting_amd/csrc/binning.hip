@@ -14,7 +14,7 @@
 //   K2 tile_scan     one workgroup: exclusive scans of the tile counts (-> the
 //                    per-tile ranges, identifyTileRanges' output) and of the
 //                    chunk totals (-> each chunk's first record index); it also
-//                    lists the tiles too long for one wave's sort (four classes);
+//                    lists the tiles too long for one wave's sort (two classes);
 //   K3 tile_scatter  every chunk loads its cursors (tile start + chunk offset)
 //                    into LDS and scatters 64-bit keys (depth bits << 32 |
 //                    index << 4) with LDS atomics (the low 4 bits of a tile-list
@@ -46,10 +46,10 @@ constexpr int kBinThreads = 1024;
 constexpr int kBinWaves = kBinThreads / 64;
 constexpr uint32_t kLdsTilesMax = 36864;  // K3 keeps one u32 per tile in LDS (144 KiB)
 constexpr uint32_t kSortWaveMax = 1024;   // longest list tile_sort_kernel sorts (one wave, 16 keys per lane)
-// Longer lists go to persistent per-class kernels, T threads x 16 keys in registers:
-// class 0 (1024, 2048] T = 128, class 1 (2048, 4096] T = 256, class 2 (4096, 8192]
-// T = 512; class 3 (> 8192) sorts in global memory.
-constexpr int kSortClasses = 4;
+// Longer lists go to two persistent kernels: class 0 (1024, 2048], 128 threads x 16 keys
+// in registers; class 1 (> 2048), 512 threads x 8 or 16 keys in registers up to 8192
+// keys, and a network in global memory beyond.
+constexpr int kSortClasses = 2;
 constexpr uint32_t kBigRegMax = 8192;
 
 typedef unsigned long long u64;
@@ -291,7 +291,7 @@ __global__ void __launch_bounds__(kBinThreads) tile_scan_kernel(uint32_t tiles, 
                 ranges[b + i] = make_uint2((uint32_t)lo, (uint32_t)hi);
                 tile_base[b + i] = (uint32_t)at;
                 if (v[i] > kSortWaveMax) {  // long list: one of the class kernels (K4)
-                    const int c = v[i] <= 2048u ? 0 : v[i] <= 4096u ? 1 : v[i] <= kBigRegMax ? 2 : 3;
+                    const int c = v[i] <= 2048u ? 0 : 1;
                     cls_list[(size_t)c * tiles + atomicAdd(&s_cls[c], 1u)] = b + i;
                 }
             }
@@ -526,40 +526,51 @@ __global__ void __launch_bounds__(T) tile_sort_class_kernel(const uint2* __restr
     }
 }
 
-// Lists beyond kBigRegMax: the network on the global keys, one workgroup per list
-// (any length; slow -- real scenes rarely produce such tiles).  "Flip" form: every
-// comparator is ascending; for block size k the first step pairs i with i ^ (k - 1),
-// the others with i ^ j, so keys past n behave as +infinity and are never touched.
-__global__ void __launch_bounds__(kBinThreads) tile_sort_global_kernel(const uint2* __restrict__ ranges,
-                                                                       u64* __restrict__ keys, u64 cap,
-                                                                       uint32_t* __restrict__ gid_sorted,
-                                                                       const uint32_t* __restrict__ list,
-                                                                       const uint32_t* __restrict__ count) {
+// Class 1: lists beyond 2048 keys, 512-thread workgroups walking K2's list.  Up to 8192
+// keys the registers hold them (8 or 16 per thread); beyond, a network on the global keys
+// (any length; slow -- real scenes rarely produce such tiles).  The global network uses
+// the "flip" form: every comparator is ascending; for block size k the first step pairs
+// i with i ^ (k - 1), the others with i ^ j, so keys past n behave as +infinity and are
+// never touched.
+constexpr int kBigThreads = 512;
+
+__global__ void __launch_bounds__(kBigThreads) tile_sort_big_kernel(const uint2* __restrict__ ranges,
+                                                                    u64* __restrict__ keys, u64 cap,
+                                                                    uint32_t* __restrict__ gid_sorted,
+                                                                    const uint32_t* __restrict__ list,
+                                                                    const uint32_t* __restrict__ count) {
+    __shared__ u64 s_x[kBigThreads * 16];
     const uint32_t nb = count[0];
     for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
         const uint2 r = ranges[list[b]];
-        const uint32_t n = tile_len(r, cap);
-        u64* k = keys + r.x;
-        uint32_t N2 = 1;
-        while (N2 < n) N2 <<= 1;
-        for (uint32_t kk = 2; kk <= N2; kk <<= 1) {
-            for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
-                for (uint32_t p = threadIdx.x; p < N2 / 2; p += blockDim.x) {
-                    const uint32_t lo = ((p & ~(j - 1)) << 1) | (p & (j - 1));  // p-th index with bit j clear
-                    const uint32_t hi = (j == (kk >> 1)) ? (lo ^ (kk - 1)) : (lo | j);
-                    if (hi < n) {
-                        const u64 x = k[lo], y = k[hi];
-                        if (y < x) {
-                            k[lo] = y;
-                            k[hi] = x;
+        const uint32_t n = tile_len(r, cap);  // may be shorter than its class when truncated by cap
+        if (n <= (uint32_t)kBigThreads * 8) {
+            sort_list<kBigThreads, 8>(keys, r.x, n, gid_sorted, s_x);
+        } else if (n <= kBigRegMax) {
+            sort_list<kBigThreads, 16>(keys, r.x, n, gid_sorted, s_x);
+        } else {
+            u64* k = keys + r.x;
+            uint32_t N2 = 1;
+            while (N2 < n) N2 <<= 1;
+            for (uint32_t kk = 2; kk <= N2; kk <<= 1) {
+                for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
+                    for (uint32_t p = threadIdx.x; p < N2 / 2; p += blockDim.x) {
+                        const uint32_t lo = ((p & ~(j - 1)) << 1) | (p & (j - 1));  // p-th index with bit j clear
+                        const uint32_t hi = (j == (kk >> 1)) ? (lo ^ (kk - 1)) : (lo | j);
+                        if (hi < n) {
+                            const u64 x = k[lo], y = k[hi];
+                            if (y < x) {
+                                k[lo] = y;
+                                k[hi] = x;
+                            }
                         }
                     }
+                    __syncthreads();
                 }
-                __syncthreads();
             }
+            for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) gid_sorted[r.x + i] = (uint32_t)k[i];
         }
-        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) gid_sorted[r.x + i] = (uint32_t)k[i];
-        __syncthreads();
+        __syncthreads();  // s_x is reused by the next tile
     }
 }
 
@@ -653,12 +664,8 @@ hipError_t launch_tile_sort(uint32_t tiles, const uint2* ranges, const GeomState
     const auto grid = [&](uint32_t want) { return dim3(tiles < want ? tiles : want); };
     hipLaunchKernelGGL(tile_sort_class_kernel<128>, grid(2048), dim3(128), 0, stream, ranges, b.keys, c,
                        b.gid_sorted, g.cls_list, g.cls_count);
-    hipLaunchKernelGGL(tile_sort_class_kernel<256>, grid(1024), dim3(256), 0, stream, ranges, b.keys, c,
+    hipLaunchKernelGGL(tile_sort_big_kernel, grid(512), dim3(kBigThreads), 0, stream, ranges, b.keys, c,
                        b.gid_sorted, g.cls_list + tiles, g.cls_count + 1);
-    hipLaunchKernelGGL(tile_sort_class_kernel<512>, grid(512), dim3(512), 0, stream, ranges, b.keys, c,
-                       b.gid_sorted, g.cls_list + 2 * (size_t)tiles, g.cls_count + 2);
-    hipLaunchKernelGGL(tile_sort_global_kernel, grid(256), dim3(kBinThreads), 0, stream, ranges, b.keys, c,
-                       b.gid_sorted, g.cls_list + 3 * (size_t)tiles, g.cls_count + 3);
     return hipGetLastError();
 }
 

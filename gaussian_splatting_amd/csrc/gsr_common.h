@@ -86,8 +86,8 @@ struct GeomState {
     uint32_t* n_visible;        // [1] entries of order
     uint32_t* tile_base;        // [tiles] first instance of each tile (scatter cursors without LDS)
     uint32_t* chunk_off;        // [chunks][tiles] each chunk's offset inside each tile's block
-    uint32_t* cls_list;         // [4][tiles] tiles whose lists are too long for one wave's sort, by class
-    uint32_t* cls_count;        // [4] entries of each class list
+    uint32_t* cls_list;         // [2][tiles] tiles whose lists are too long for one wave's sort, by class
+    uint32_t* cls_count;        // [2] entries of each class list
     unsigned long long* chunk_total;  // [chunks] tiles_touched per Gaussian chunk
     unsigned long long* chunk_base;   // [chunks] its exclusive scan
     unsigned long long* total;        // [1] number of instances (num_rendered)

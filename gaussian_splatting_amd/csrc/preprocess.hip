@@ -115,107 +115,187 @@ __device__ __forceinline__ void load_sh(const float* __restrict__ shs, int idx, 
 }
 
 
-template <bool SH_VEC4>
-__global__ void __launch_bounds__(256) preprocess_kernel(PreprocessArgs a) {
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= a.P) return;
-    a.radii[idx] = 0;
-    a.geom.tiles_touched[idx] = 0;
-    a.geom.depth_key[idx] = 0xffffffffu;
+// One wave per 64 consecutive Gaussians.  The geometry is per lane; two data paths are
+// cooperative so that every global access of the wave is a contiguous block:
+//  * SH (192 B per Gaussian at M = 16, most of the kernel's bytes): the wave's rows are
+//    staged through LDS in two halves of 32 rows (6 KiB each, 16-byte loads of one
+//    contiguous range), and lanes 0-31 / 32-63 evaluate their colours from LDS;
+//  * the 64-byte splat records are assembled in LDS and written as one 4 KiB block.
+// A culled Gaussian gets the reference's zero radius / tiles_touched, a 0xffffffff depth
+// key and an all-zero record (never read).
+constexpr int kPreThreads = 64;
+constexpr int kShHalfRows = 32;
+constexpr int kShRowF = 48;        // floats per SH row at M = 16
+constexpr int kShRowStride = 52;   // padded LDS row stride (16-byte aligned, conflict-free b128)
 
-    const float* V = a.viewmatrix;
-    const float3 p = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
-    const float3 p_view = xform_point_4x3(p, V);
-    if (p_view.z <= 0.2f) {  // in_frustum (CR/auxiliary.h:180-188); the reference traps when prefiltered
-        if (a.prefiltered) atomicOr(a.geom.status, 1u);
-        return;
+template <bool SH_LDS>
+__global__ void __launch_bounds__(kPreThreads) preprocess_kernel(PreprocessArgs a) {
+    __shared__ __attribute__((aligned(16))) float s_buf[SH_LDS ? kShHalfRows * kShRowStride : 64 * 16];
+    static_assert(kShHalfRows * kShRowStride >= 64 * 16, "the record block reuses the SH buffer");
+    const int lane = threadIdx.x;
+    const int g0 = blockIdx.x * kPreThreads;
+    const int idx = g0 + lane;
+    const bool valid = idx < a.P;
+    const int nvalid = min(kPreThreads, a.P - g0);
+
+    // ---- geometry (CR/forward.cu:255-326): `ok` replaces the reference's early returns
+    bool ok = valid;
+    float3 p = make_float3(0.f, 0.f, 0.f), p_view = p;
+    if (valid) {
+        p = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
+        p_view = xform_point_4x3(p, a.viewmatrix);
+        if (p_view.z <= 0.2f) {  // in_frustum (CR/auxiliary.h:180-188); the reference traps when prefiltered
+            if (a.prefiltered) atomicOr(a.geom.status, 1u);
+            ok = false;
+        }
     }
-    const float4 p_hom = xform_point_4x4(p, a.projmatrix);
-    const float p_w = 1.0f / (p_hom.w + 0.0000001f);
-    const float px_ndc = p_hom.x * p_w, py_ndc = p_hom.y * p_w;
-
-    float cov3[6];
-    if (a.cov3D_precomp) {
+    float px = 0.f, py = 0.f, ca = 0.f, cb = 0.f, cc = 0.f, h_scale = 1.f, det = 0.f;
+    float3 cov = make_float3(0.f, 0.f, 0.f);
+    int irad = 0;
+    uint2 rmin = make_uint2(0u, 0u), rmax = rmin;
+    uint32_t touched = 0;
+    if (ok) {
+        const float4 p_hom = xform_point_4x4(p, a.projmatrix);
+        const float p_w = 1.0f / (p_hom.w + 0.0000001f);
+        const float px_ndc = p_hom.x * p_w, py_ndc = p_hom.y * p_w;
+        float cov3[6];
+        if (a.cov3D_precomp) {
 #pragma unroll
-        for (int i = 0; i < 6; i++) cov3[i] = a.cov3D_precomp[6 * idx + i];
-    } else {
-        const float3 s = make_float3(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]);
-        const float4 q = reinterpret_cast<const float4*>(a.rotations)[idx];
-        cov3d_from_scale_rot(s, a.scale_modifier, q, cov3);
-    }
-    float3 cov = cov2d_project(p_view, a.focal_x, a.focal_y, a.tan_fovx, a.tan_fovy, V, cov3);
-
-    constexpr float h_var = 0.3f;
-    const float det_cov = cov.x * cov.z - cov.y * cov.y;
-    cov.x += h_var;
-    cov.z += h_var;
-    const float det = cov.x * cov.z - cov.y * cov.y;
-    float h_scale = 1.0f;
-    if (a.antialiasing) h_scale = sqrtf(fmaxf(0.000025f, det_cov / det));
-    if (det == 0.0f) return;
-    const float det_inv = 1.f / det;
-    const float ca = cov.z * det_inv, cb = -cov.y * det_inv, cc = cov.x * det_inv;
-
-    const float mid = 0.5f * (cov.x + cov.z);
-    const float lambda1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
-    const float lambda2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
-    const float my_radius = ceilf(3.f * sqrtf(fmaxf(lambda1, lambda2)));
-    const float px = ndc2pix(px_ndc, a.W), py = ndc2pix(py_ndc, a.H);
-    const int irad = (int)my_radius;
-    uint2 rmin, rmax;
-    get_rect(px, py, irad, a.gx, a.gy, rmin, rmax);
-    const uint32_t touched = (rmax.y - rmin.y) * (rmax.x - rmin.x);
-    if (touched == 0) return;
-
-    float3 rgb;
-    if (a.colors_precomp) {
-        rgb = make_float3(a.colors_precomp[3 * idx], a.colors_precomp[3 * idx + 1], a.colors_precomp[3 * idx + 2]);
-    } else {
-        float3 d = make_float3(p.x - a.campos[0], p.y - a.campos[1], p.z - a.campos[2]);
-        const float len = sqrtf(d.x * d.x + d.y * d.y + d.z * d.z);
-        d.x /= len; d.y /= len; d.z /= len;
-        float3 sh[16];
-        const int K = (a.D + 1) * (a.D + 1);
-        load_sh<SH_VEC4>(a.shs, idx, a.M, K, sh);
-        rgb = sh_to_rgb(a.D, sh, d.x, d.y, d.z);
-        a.geom.clamped[idx] = (uint8_t)((rgb.x < 0.f ? 1 : 0) | (rgb.y < 0.f ? 2 : 0) | (rgb.z < 0.f ? 4 : 0));
-        rgb.x = fmaxf(rgb.x, 0.f); rgb.y = fmaxf(rgb.y, 0.f); rgb.z = fmaxf(rgb.z, 0.f);
-    }
-
-    const float o_eff = a.opacities[idx] * h_scale;
-    // Conservative box of the alpha >= 1/255 footprint: o*exp(-q/2) >= 1/255 <=> q <= 2 ln(255 o).
-    uint32_t bbx = pack_i16x2(-32768, 32767), bby = pack_i16x2(-32768, 32767);
-    if (a.footprint_cull) {
-        if (o_eff * 255.f < 0.999f) {
-            bbx = pack_i16x2(1, 0);
-            bby = pack_i16x2(1, 0);
-        } else if (det > 0.f && cov.x > 0.f && cov.z > 0.f) {
-            const float tau = fmaxf(0.f, logf(255.f * o_eff)) * 1.001f + 0.01f;
-            const float ex = sqrtf(2.f * tau * cov.x) + 0.05f, ey = sqrtf(2.f * tau * cov.z) + 0.05f;
-            const float x0 = floorf(px - ex), x1 = ceilf(px + ex), y0 = floorf(py - ey), y1 = ceilf(py + ey);
-            if (isfinite(x0) && isfinite(x1) && isfinite(y0) && isfinite(y1)) {
-                bbx = pack_i16x2((int)fmaxf(x0, -32768.f), (int)fminf(x1, 32767.f));
-                bby = pack_i16x2((int)fmaxf(y0, -32768.f), (int)fminf(y1, 32767.f));
-            }
+            for (int i = 0; i < 6; i++) cov3[i] = a.cov3D_precomp[6 * idx + i];
+        } else {
+            const float3 sc = make_float3(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]);
+            const float4 q = reinterpret_cast<const float4*>(a.rotations)[idx];
+            cov3d_from_scale_rot(sc, a.scale_modifier, q, cov3);
+        }
+        cov = cov2d_project(p_view, a.focal_x, a.focal_y, a.tan_fovx, a.tan_fovy, a.viewmatrix, cov3);
+        constexpr float h_var = 0.3f;
+        const float det_cov = cov.x * cov.z - cov.y * cov.y;
+        cov.x += h_var;
+        cov.z += h_var;
+        det = cov.x * cov.z - cov.y * cov.y;
+        if (a.antialiasing) h_scale = sqrtf(fmaxf(0.000025f, det_cov / det));
+        if (det == 0.0f) {
+            ok = false;
+        } else {
+            const float det_inv = 1.f / det;
+            ca = cov.z * det_inv;
+            cb = -cov.y * det_inv;
+            cc = cov.x * det_inv;
+            const float mid = 0.5f * (cov.x + cov.z);
+            const float lambda1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
+            const float lambda2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
+            const float my_radius = ceilf(3.f * sqrtf(fmaxf(lambda1, lambda2)));
+            px = ndc2pix(px_ndc, a.W);
+            py = ndc2pix(py_ndc, a.H);
+            irad = (int)my_radius;
+            get_rect(px, py, irad, a.gx, a.gy, rmin, rmax);
+            touched = (rmax.y - rmin.y) * (rmax.x - rmin.x);
+            if (touched == 0) ok = false;
         }
     }
 
-    a.geom.depth_key[idx] = __float_as_uint(p_view.z);
-    a.radii[idx] = irad;
-    float4* rec = a.geom.rec + (size_t)kRecRows * idx;
-    rec[0] = make_float4(px, py, ca, cb);
-    rec[1] = make_float4(cc, o_eff, 1.0f / p_view.z, __uint_as_float(bbx));
-    rec[2] = make_float4(rgb.x, rgb.y, rgb.z, __uint_as_float(bby));
-    rec[3] = make_float4(__uint_as_float(rmin.x), __uint_as_float(rmin.y), __uint_as_float(rmax.x - rmin.x), 0.f);
-    a.geom.tiles_touched[idx] = touched;
-    a.geom.rect[idx] = make_uint2(rmin.x | (rmin.y << 16), rmax.x | (rmax.y << 16));
+    // ---- colour (CR/forward.cu:329-336)
+    float3 rgb = make_float3(0.f, 0.f, 0.f);
+    float3 dir = make_float3(0.f, 0.f, 0.f);
+    if (ok && !a.colors_precomp) {
+        float3 d = make_float3(p.x - a.campos[0], p.y - a.campos[1], p.z - a.campos[2]);
+        const float len = sqrtf(d.x * d.x + d.y * d.y + d.z * d.z);
+        dir = make_float3(d.x / len, d.y / len, d.z / len);
+    }
+    if (a.colors_precomp) {
+        if (ok) rgb = make_float3(a.colors_precomp[3 * idx], a.colors_precomp[3 * idx + 1], a.colors_precomp[3 * idx + 2]);
+    } else if constexpr (SH_LDS) {
+        const float4* src = reinterpret_cast<const float4*>(a.shs + (size_t)g0 * kShRowF);
+#pragma unroll
+        for (int half = 0; half < 2; half++) {
+            const int rows = min(kShHalfRows, nvalid - half * kShHalfRows);
+            if (rows > 0) {  // wave-uniform
+                const int n4 = rows * (kShRowF / 4);
+                const float4* hsrc = src + half * kShHalfRows * (kShRowF / 4);
+#pragma unroll
+                for (int k = 0; k < kShHalfRows * kShRowF / 4 / kPreThreads; k++) {
+                    const int i4 = k * kPreThreads + lane;
+                    if (i4 < n4) {
+                        const int d = i4 * 4, row = d / kShRowF, col = d - row * kShRowF;
+                        *reinterpret_cast<float4*>(&s_buf[row * kShRowStride + col]) = hsrc[i4];
+                    }
+                }
+                __syncthreads();
+                if ((lane >> 5) == half && ok) {
+                    const float* row = &s_buf[(lane & 31) * kShRowStride];
+                    float3 sh[16];
+#pragma unroll
+                    for (int k = 0; k < 16; k++) sh[k] = make_float3(row[3 * k], row[3 * k + 1], row[3 * k + 2]);
+                    rgb = sh_to_rgb(a.D, sh, dir.x, dir.y, dir.z);
+                }
+                __syncthreads();
+            }
+        }
+    } else if (ok) {
+        float3 sh[16];
+        const int K = (a.D + 1) * (a.D + 1);
+        load_sh<false>(a.shs, idx, a.M, K, sh);
+        rgb = sh_to_rgb(a.D, sh, dir.x, dir.y, dir.z);
+    }
+    if (ok && !a.colors_precomp) {
+        a.geom.clamped[idx] = (uint8_t)((rgb.x < 0.f ? 1 : 0) | (rgb.y < 0.f ? 2 : 0) | (rgb.z < 0.f ? 4 : 0));
+        rgb.x = fmaxf(rgb.x, 0.f);
+        rgb.y = fmaxf(rgb.y, 0.f);
+        rgb.z = fmaxf(rgb.z, 0.f);
+    }
+
+    // ---- footprint box and outputs
+    float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, r2 = r0, r3 = r0;
+    if (ok) {
+        const float o_eff = a.opacities[idx] * h_scale;
+        // Conservative box of the alpha >= 1/255 footprint: o*exp(-q/2) >= 1/255 <=> q <= 2 ln(255 o).
+        uint32_t bbx = pack_i16x2(-32768, 32767), bby = pack_i16x2(-32768, 32767);
+        if (a.footprint_cull) {
+            if (o_eff * 255.f < 0.999f) {
+                bbx = pack_i16x2(1, 0);
+                bby = pack_i16x2(1, 0);
+            } else if (det > 0.f && cov.x > 0.f && cov.z > 0.f) {
+                const float tau = fmaxf(0.f, logf(255.f * o_eff)) * 1.001f + 0.01f;
+                const float ex = sqrtf(2.f * tau * cov.x) + 0.05f, ey = sqrtf(2.f * tau * cov.z) + 0.05f;
+                const float x0 = floorf(px - ex), x1 = ceilf(px + ex), y0 = floorf(py - ey), y1 = ceilf(py + ey);
+                if (isfinite(x0) && isfinite(x1) && isfinite(y0) && isfinite(y1)) {
+                    bbx = pack_i16x2((int)fmaxf(x0, -32768.f), (int)fminf(x1, 32767.f));
+                    bby = pack_i16x2((int)fmaxf(y0, -32768.f), (int)fminf(y1, 32767.f));
+                }
+            }
+        }
+        r0 = make_float4(px, py, ca, cb);
+        r1 = make_float4(cc, o_eff, 1.0f / p_view.z, __uint_as_float(bbx));
+        r2 = make_float4(rgb.x, rgb.y, rgb.z, __uint_as_float(bby));
+        r3 = make_float4(__uint_as_float(rmin.x), __uint_as_float(rmin.y), __uint_as_float(rmax.x - rmin.x), 0.f);
+    }
+    if (valid) {
+        a.radii[idx] = ok ? irad : 0;
+        a.geom.tiles_touched[idx] = ok ? touched : 0u;
+        a.geom.depth_key[idx] = ok ? __float_as_uint(p_view.z) : 0xffffffffu;
+        a.geom.rect[idx] = make_uint2(rmin.x | (rmin.y << 16), rmax.x | (rmax.y << 16));
+    }
+    // the wave's 64 records as one contiguous 4 KiB store
+    float4* s_rec = reinterpret_cast<float4*>(s_buf);
+    s_rec[lane * kRecRows + 0] = r0;
+    s_rec[lane * kRecRows + 1] = r1;
+    s_rec[lane * kRecRows + 2] = r2;
+    s_rec[lane * kRecRows + 3] = r3;
+    __syncthreads();
+    float4* dst = a.geom.rec + (size_t)kRecRows * g0;
+#pragma unroll
+    for (int k = 0; k < kRecRows; k++) {
+        const int i = k * kPreThreads + lane;
+        if (i < nvalid * kRecRows) dst[i] = s_rec[i];
+    }
 }
 
 hipError_t launch_preprocess(const PreprocessArgs& a, hipStream_t stream) {
     if (a.P == 0) return hipSuccess;
-    const dim3 grid((a.P + 255) / 256), block(256);
-    const bool vec4 = a.shs && ((reinterpret_cast<uintptr_t>(a.shs) & 15) == 0) && ((a.M * 3) % 4 == 0);
-    if (vec4)
+    const dim3 grid((a.P + kPreThreads - 1) / kPreThreads), block(kPreThreads);
+    const bool lds = a.shs && !a.colors_precomp && a.M == 16 && a.D == 3 &&
+                     ((reinterpret_cast<uintptr_t>(a.shs) & 15) == 0);
+    if (lds)
         hipLaunchKernelGGL(preprocess_kernel<true>, grid, block, 0, stream, a);
     else
         hipLaunchKernelGGL(preprocess_kernel<false>, grid, block, 0, stream, a);
