@@ -123,7 +123,7 @@ gsr::GeomState carve_geom(char* base, int P, uint32_t gx, uint32_t gy, size_t* t
     g.tile_base = c.take<uint32_t>(tiles);
     const size_t chunks = bin_chunk_count(P);
     g.cell_off = c.take<uint32_t>(chunks * cells);
-    g.order = c.take<uint32_t>(P);
+    g.order = c.take<uint4>(P);
     g.n_visible = c.take<uint32_t>(1);
 
     g.chunk_off = c.take<uint32_t>(chunks * tiles);

@@ -65,6 +65,11 @@ __device__ __forceinline__ void unpack_rect(uint2 r, uint32_t& x0, uint32_t& y0,
     y1 = r.y >> 16;
 }
 
+// Tiles in a packed rectangle (= tiles_touched of its Gaussian).
+__device__ __forceinline__ uint32_t rect_tiles(uint2 r) {
+    return ((r.y & 0xffffu) - (r.x & 0xffffu)) * ((r.y >> 16) - (r.x >> 16));
+}
+
 // Sum over the workgroup (a multiple of 64 threads); result valid in every thread.
 template <typename T>
 __device__ T block_sum(T v, T* s_tmp) {
@@ -181,13 +186,16 @@ __global__ void __launch_bounds__(kBinThreads) cell_count_kernel(int P, int chun
 }
 
 // K0c: every chunk scans the cell counts (redundantly, cells are few), then scatters its
-// visible Gaussians' indices into their cells' blocks.  Block 0 publishes V.
+// visible Gaussians into their cells' blocks as 16-byte binning records (index, rect,
+// depth key), so that K1 and K3 read their chunk's Gaussians as one contiguous range
+// instead of gathering them.  Block 0 publishes V.
 __global__ void __launch_bounds__(kBinThreads) cell_scatter_kernel(int P, int chunk, const uint2* __restrict__ rect,
                                                                    const uint32_t* __restrict__ tiles_touched,
                                                                    uint32_t cells, uint32_t cgx,
                                                                    const uint32_t* __restrict__ cell_cnt,
                                                                    const uint32_t* __restrict__ cell_off,
-                                                                   uint32_t* __restrict__ order,
+                                                                   const uint32_t* __restrict__ depth_key,
+                                                                   uint4* __restrict__ order,
                                                                    uint32_t* __restrict__ n_visible) {
     extern __shared__ uint32_t s_c[];  // cells words
     __shared__ uint32_t s_tmp[kBinWaves];
@@ -205,14 +213,17 @@ __global__ void __launch_bounds__(kBinThreads) cell_scatter_kernel(int P, int ch
     if (blockIdx.x == 0 && threadIdx.x == 0) n_visible[0] = carry;
     __syncthreads();
     for (int g = g0 + (int)threadIdx.x; g < g1; g += kBinThreads)
-        if (tiles_touched[g]) order[atomicAdd(&s_c[cell_of(rect[g], cgx)], 1u)] = (uint32_t)g;
+        if (tiles_touched[g]) {
+            const uint2 r = rect[g];
+            order[atomicAdd(&s_c[cell_of(r, cgx)], 1u)] = make_uint4((uint32_t)g, r.x, r.y, depth_key[g]);
+        }
 }
 
 // ---- K1 ---------------------------------------------------------------------
 template <bool LDS>
 __global__ void __launch_bounds__(kBinThreads) tile_count_kernel(int P, int chunk, const uint2* __restrict__ rect,
                                                                  const uint32_t* __restrict__ tiles_touched,
-                                                                 const uint32_t* __restrict__ order,
+                                                                 const uint4* __restrict__ order,
                                                                  const uint32_t* __restrict__ n_visible,
                                                                  uint32_t tiles, uint32_t gx, uint32_t* __restrict__ cnt,
                                                                  uint32_t* __restrict__ chunk_off) {
@@ -229,9 +240,9 @@ __global__ void __launch_bounds__(kBinThreads) tile_count_kernel(int P, int chun
     GSR_STAMP(g_st_count, blockIdx.x, 1);
     for (int pb = g0 + wave * 64; pb < g1; pb += kBinThreads) {
         const int p = pb + lane;
-        const uint32_t g = p < g1 ? order[p] : 0u;
-        const uint32_t n = p < g1 ? tiles_touched[g] : 0u;
-        const uint2 r = n ? rect[g] : make_uint2(0u, 0u);
+        const uint4 o = p < g1 ? order[p] : make_uint4(0u, 0u, 0u, 0u);
+        const uint2 r = make_uint2(o.y, o.z);
+        const uint32_t n = rect_tiles(r);
         for_each_instance(n, r, gx, [&](bool valid, int, uint32_t t, uint32_t, uint32_t) {
             if (!valid) return;
             if (LDS)
@@ -317,7 +328,7 @@ __global__ void __launch_bounds__(kBinThreads) tile_scan_kernel(uint32_t tiles, 
 template <bool LDS>
 __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
     int P, int chunk, const uint2* __restrict__ rect, const uint32_t* __restrict__ tiles_touched,
-    const uint32_t* __restrict__ depth_key, const uint32_t* __restrict__ order, const uint32_t* __restrict__ n_visible,
+    const uint32_t* __restrict__ depth_key, const uint4* __restrict__ order, const uint32_t* __restrict__ n_visible,
     uint32_t tiles, uint32_t gx, uint32_t* __restrict__ tile_base,
     const uint32_t* __restrict__ chunk_off, const u64* __restrict__ chunk_base, u64* __restrict__ keys, u64 cap,
     uint32_t* __restrict__ rec_start, float4* __restrict__ rec) {
@@ -352,10 +363,10 @@ __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
     const int q0 = blockIdx.x * chunk, q1 = min(V, q0 + chunk);
     for (int pb = q0 + wave * 64; pb < q1; pb += kBinThreads) {
         const int p = pb + lane;
-        const uint32_t g = p < q1 ? order[p] : 0u;
-        const uint32_t n = p < q1 ? tiles_touched[g] : 0u;
-        const uint2 r = n ? rect[g] : make_uint2(0u, 0u);
-        const uint32_t dk = n ? depth_key[g] : 0u;
+        const uint4 o = p < q1 ? order[p] : make_uint4(0u, 0u, 0u, 0u);
+        const uint32_t g = o.x, dk = o.w;
+        const uint2 r = make_uint2(o.y, o.z);
+        const uint32_t n = rect_tiles(r);
         for_each_instance(n, r, gx, [&](bool valid, int owner, uint32_t t, uint32_t, uint32_t) {
             const uint32_t kh = __shfl(dk, owner), kg = __shfl(g, owner);
             if (!valid) return;
@@ -622,7 +633,7 @@ hipError_t launch_bin_count(int P, const GeomState& g, uint32_t gx, uint32_t gy,
     hipLaunchKernelGGL(cell_count_kernel, grid, block, cell_bytes, stream, P, chunk, g.rect, g.tiles_touched, cells,
                        cgx, g.cell_cnt, g.cell_off, g.chunk_total);
     hipLaunchKernelGGL(cell_scatter_kernel, grid, block, cell_bytes, stream, P, chunk, g.rect, g.tiles_touched,
-                       cells, cgx, g.cell_cnt, g.cell_off, g.order, g.n_visible);
+                       cells, cgx, g.cell_cnt, g.cell_off, g.depth_key, g.order, g.n_visible);
     const size_t hist_bytes = lds ? ((tiles + 1) / 2) * sizeof(uint32_t) : 0;
     if (lds)
         hipLaunchKernelGGL(tile_count_kernel<true>, grid, block, hist_bytes, stream, P, chunk, g.rect, g.tiles_touched,

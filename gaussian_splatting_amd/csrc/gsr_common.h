@@ -82,7 +82,7 @@ struct GeomState {
     uint32_t* tile_cnt;         // [tiles] instances per tile; cell_cnt follows it (one memset)
     uint32_t* cell_cnt;         // [cells] visible Gaussians per screen cell (spatial order, binning.hip K0)
     uint32_t* cell_off;         // [chunks][cells] each chunk's offset inside each cell's block
-    uint32_t* order;            // [P] visible Gaussians grouped by screen cell
+    uint4* order;               // [P] visible Gaussians grouped by screen cell: (index, rect, depth key)
     uint32_t* n_visible;        // [1] entries of order
     uint32_t* tile_base;        // [tiles] first instance of each tile (scatter cursors without LDS)
     uint32_t* chunk_off;        // [chunks][tiles] each chunk's offset inside each tile's block

@@ -386,6 +386,7 @@ constexpr int kOrderThreads = 1024, kOrderBuckets = 1024;
 __global__ void __launch_bounds__(kOrderThreads) tile_order_kernel(uint32_t tiles, const uint32_t* __restrict__ cost,
                                                                    uint32_t* __restrict__ order) {
     __shared__ uint32_t s_cnt[kOrderBuckets];
+    __shared__ uint32_t s_wsum[kOrderThreads / 64];
     __shared__ uint32_t s_max;
     if (threadIdx.x == 0) s_max = 0;
     for (uint32_t i = threadIdx.x; i < kOrderBuckets; i += kOrderThreads) s_cnt[i] = 0;
@@ -400,13 +401,20 @@ __global__ void __launch_bounds__(kOrderThreads) tile_order_kernel(uint32_t tile
     };
     for (uint32_t t = threadIdx.x; t < tiles; t += kOrderThreads) atomicAdd(&s_cnt[bucket(cost[t])], 1u);
     __syncthreads();
-    if (threadIdx.x == 0) {  // 1024 buckets: a serial scan is a few microseconds at most
-        uint32_t at = 0;
-        for (int b = 0; b < kOrderBuckets; b++) {
-            const uint32_t c = s_cnt[b];
-            s_cnt[b] = at;
-            at += c;
+    {  // exclusive scan, one bucket per thread
+        static_assert(kOrderBuckets == kOrderThreads, "one bucket per thread");
+        const uint32_t c = s_cnt[threadIdx.x];
+        uint32_t incl = c;
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t u = __shfl_up(incl, off);
+            if (lane >= off) incl += u;
         }
+        if (lane == 63) s_wsum[w] = incl;
+        __syncthreads();
+        uint32_t base = 0;
+        for (int i = 0; i < w; i++) base += s_wsum[i];
+        s_cnt[threadIdx.x] = base + incl - c;
     }
     __syncthreads();
     for (uint32_t t = threadIdx.x; t < tiles; t += kOrderThreads) order[atomicAdd(&s_cnt[bucket(cost[t])], 1u)] = t;
