@@ -72,7 +72,7 @@ def main():
         import json
 
         with open(a.json, "w") as f:
-            json.dump({"source": a.dir, "correction": "read = 2 x FETCH_SIZE KiB (gfx950), write = WRITE_SIZE KiB",
+            json.dump({"source": a.out or a.dir, "correction": "read = 2 x FETCH_SIZE KiB (gfx950), write = WRITE_SIZE KiB",
                        "kernels": table}, f, indent=1)
     if a.out:
         with open(a.out, "w") as f:
