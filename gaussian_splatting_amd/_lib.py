@@ -1,4 +1,4 @@
-"""ctypes binding of libgsr.so (the C ABI in include/gsr.h).
+"""ctypes binding of libgsr.so (the C ABI in include/gsr.h and include/gsr_knn.h).
 
 The library is built in-tree (``python -m gaussian_splatting_amd.build``) and
 loaded from ``gaussian_splatting_amd/lib/libgsr.so``.  There is no fallback: if
@@ -13,7 +13,9 @@ import threading
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GSR_LIBRARY", os.path.join(_PKG, "lib", "libgsr.so"))
-HEADER_PATH = os.path.join(os.path.dirname(_PKG), "include", "gsr.h")
+INCLUDE_DIR = os.path.join(os.path.dirname(_PKG), "include")
+HEADER_PATH = os.path.join(INCLUDE_DIR, "gsr.h")
+HEADERS = [os.path.join(INCLUDE_DIR, h) for h in ("gsr.h", "gsr_knn.h")]
 
 ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
 
@@ -42,6 +44,7 @@ SIGNATURES = {
     "gsr_profile_collect": (_i, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong), _i]),
     "gsr_profile_reset": (None, []),
     "gsr_profile_stage_name": (ctypes.c_char_p, [_i]),
+    "gsr_knn_mean_dist2": (_i, [_i, _vp, _vp, ALLOC_FN, _vp, _vp]),
 }
 
 _lock = threading.Lock()
@@ -52,11 +55,13 @@ class GsrError(RuntimeError):
     """A failure reported by libgsr (the reference raises RuntimeError / AT_ERROR too)."""
 
 
-def header_symbols(path: str = HEADER_PATH) -> list:
-    """Function names declared in include/gsr.h."""
-    with open(path) as f:
-        text = f.read()
-    return sorted(set(re.findall(r"\b(gsr_[a-z_]+)\s*\(", text)) - {"gsr_alloc_fn"})
+def header_symbols(paths=None) -> list:
+    """Function names declared in the C ABI headers (include/gsr.h, include/gsr_knn.h)."""
+    names = set()
+    for path in ([paths] if isinstance(paths, str) else (paths or HEADERS)):
+        with open(path) as f:
+            names |= set(re.findall(r"\b(gsr_[a-z0-9_]+)\s*\(", f.read()))
+    return sorted(names - {"gsr_alloc_fn"})
 
 
 def load():

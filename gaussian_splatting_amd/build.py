@@ -20,7 +20,7 @@ CSRC = os.path.join(PKG, "csrc")
 OBJ = os.path.join(PKG, "build")
 LIB_DIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIB_DIR, "libgsr.so")
-SOURCES = ["api.hip", "preprocess.hip", "binning.hip", "render.hip", "backward.hip"]
+SOURCES = ["api.hip", "preprocess.hip", "binning.hip", "render.hip", "backward.hip", "knn.hip"]
 HEADERS = ["gsr_common.h", "kernels.h", "footprint.h"]
 ARCH = os.environ.get("GSR_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -29,7 +29,8 @@ CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-W
 
 
 def _newest_input_mtime() -> float:
-    files = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(ROOT, "include", "gsr.h"), __file__]
+    files = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(ROOT, "include", h) for h in
+                                                                  ("gsr.h", "gsr_knn.h")] + [__file__]
     return max(os.path.getmtime(f) for f in files)
 
 

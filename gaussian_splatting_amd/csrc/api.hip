@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "../../include/gsr.h"
+#include "../../include/gsr_knn.h"
 #include "kernels.h"
 
 namespace {
@@ -188,6 +189,22 @@ extern "C" {
 const char* gsr_last_error(void) { return g_err; }
 
 const char* gsr_version(void) { return "gsr 0.1.0 gfx950"; }
+
+int gsr_knn_mean_dist2(int P, const float* points, float* mean_dists, gsr_alloc_fn scratch_alloc, void* scratch_ctx,
+                       void* stream_) {
+    g_err[0] = 0;
+    hipStream_t stream = (hipStream_t)stream_;
+    if (P < 0) return fail(GSR_ERR_ARGUMENT, "knn: P must be >= 0");
+    if (P == 0) return GSR_OK;
+    if (!points || !mean_dists) return fail(GSR_ERR_ARGUMENT, "knn: null pointer");
+    const size_t bytes = gsr::knn_scratch_bytes(P);
+    void* scratch = call_alloc(scratch_alloc, scratch_ctx, bytes);
+    if (!scratch) return fail(GSR_ERR_ALLOC, "knn: scratch allocation of %zu bytes failed", bytes);
+    HIP_TRY(gsr::launch_knn(P, points, mean_dists, scratch, stream), "knn");
+    // the caller frees the scratch after the call: finish the work first
+    HIP_TRY(hipStreamSynchronize(stream), "knn sync");
+    return GSR_OK;
+}
 
 int gsr_profile_enable(int stage_mask) {
     std::lock_guard<std::mutex> lk(g_prof.mu);

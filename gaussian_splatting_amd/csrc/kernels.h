@@ -98,6 +98,9 @@ hipError_t launch_tile_sort(uint32_t tiles, const uint2* ranges, const GeomState
 hipError_t launch_render_fwd(const RenderFwdArgs& a, hipStream_t stream);
 hipError_t launch_render_bwd(const RenderBwdArgs& a, hipStream_t stream);
 hipError_t launch_tile_order(uint32_t tiles, const uint32_t* cost, uint32_t* order, hipStream_t stream);
+// knn.hip
+size_t knn_scratch_bytes(int P);
+hipError_t launch_knn(int P, const float* pts, float* out, void* scratch, hipStream_t stream);
 // backward.hip
 hipError_t launch_gauss_reduce(int P, const GeomState& g, uint32_t gx, const unsigned long long* lim_key,
                                const GradRecs& recs, const GradRecs& sums, hipStream_t stream);
