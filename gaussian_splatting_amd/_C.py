@@ -20,7 +20,7 @@ import torch
 
 from . import _lib
 
-__all__ = ["rasterize_gaussians", "rasterize_gaussians_backward", "mark_visible"]
+__all__ = ["rasterize_gaussians", "rasterize_gaussians_backward", "mark_visible", "fusedssim", "fusedssim_backward"]
 
 
 # Sync-free forward (gsr_rasterize_forward_ex): the binning buffer is sized from a capacity
@@ -252,3 +252,28 @@ def mark_visible(means3D, viewmatrix, projmatrix) -> torch.Tensor:
                                   _stream_handle(device))
     _lib.check(rc, "mark_visible")
     return present
+
+
+# ---- fused SSIM as utils/loss_utils.py:16-37 expects it from this module ------------------
+# The reference's loss_utils tries ``from diff_gaussian_rasterization._C import fusedssim,
+# fusedssim_backward`` (the 3DGS-accel rasterizer's two-function variant: the forward returns
+# only the map, the backward takes the upstream gradient and recomputes what it needs).  Both
+# run on the same gfx950 kernels as fused_ssim_cuda (csrc/ssim.hip).
+def fusedssim(C1, C2, img1, img2):
+    """SSIM map of img1 vs img2 ([C,H,W] or [B,C,H,W], float32, HIP device), 'same' padding."""
+    import fused_ssim_cuda
+
+    a, b = (img1.unsqueeze(0), img2.unsqueeze(0)) if img1.dim() == 3 else (img1, img2)
+    ssim_map = fused_ssim_cuda.fusedssim(C1, C2, a, b, False)[0]
+    return ssim_map[0] if img1.dim() == 3 else ssim_map
+
+
+def fusedssim_backward(C1, C2, img1, img2, opt_grad):
+    """dL/dimg1 given dL/dmap; the derivative maps are recomputed (one extra forward pass)."""
+    import fused_ssim_cuda
+
+    squeeze = img1.dim() == 3
+    a, b, g = (t.unsqueeze(0) for t in (img1, img2, opt_grad)) if squeeze else (img1, img2, opt_grad)
+    _, d1, d2, d3 = fused_ssim_cuda.fusedssim(C1, C2, a, b, True)
+    grad = fused_ssim_cuda.fusedssim_backward(C1, C2, a, b, g, d1, d2, d3)
+    return grad[0] if squeeze else grad

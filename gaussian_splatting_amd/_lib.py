@@ -1,4 +1,4 @@
-"""ctypes binding of libgsr.so (the C ABI in include/gsr.h and include/gsr_knn.h).
+"""ctypes binding of libgsr.so (the C ABI in include/gsr.h, gsr_knn.h, gsr_ssim.h).
 
 The library is built in-tree (``python -m gaussian_splatting_amd.build``) and
 loaded from ``gaussian_splatting_amd/lib/libgsr.so``.  There is no fallback: if
@@ -15,7 +15,7 @@ _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GSR_LIBRARY", os.path.join(_PKG, "lib", "libgsr.so"))
 INCLUDE_DIR = os.path.join(os.path.dirname(_PKG), "include")
 HEADER_PATH = os.path.join(INCLUDE_DIR, "gsr.h")
-HEADERS = [os.path.join(INCLUDE_DIR, h) for h in ("gsr.h", "gsr_knn.h")]
+HEADERS = [os.path.join(INCLUDE_DIR, h) for h in ("gsr.h", "gsr_knn.h", "gsr_ssim.h")]
 
 ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
 
@@ -45,6 +45,8 @@ SIGNATURES = {
     "gsr_profile_reset": (None, []),
     "gsr_profile_stage_name": (ctypes.c_char_p, [_i]),
     "gsr_knn_mean_dist2": (_i, [_i, _vp, _vp, ALLOC_FN, _vp, _vp]),
+    "gsr_fused_ssim_forward": (_i, [_i, _i, _i, _i, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "gsr_fused_ssim_backward": (_i, [_i, _i, _i, _i, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
 }
 
 _lock = threading.Lock()

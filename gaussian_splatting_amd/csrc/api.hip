@@ -16,6 +16,7 @@
 
 #include "../../include/gsr.h"
 #include "../../include/gsr_knn.h"
+#include "../../include/gsr_ssim.h"
 #include "kernels.h"
 
 namespace {
@@ -189,6 +190,40 @@ extern "C" {
 const char* gsr_last_error(void) { return g_err; }
 
 const char* gsr_version(void) { return "gsr 0.1.0 gfx950"; }
+
+int gsr_fused_ssim_forward(int B, int CH, int H, int W, float C1, float C2, const float* img1, const float* img2,
+                           float* ssim_map, float* dm_dmu1, float* dm_dsigma1_sq, float* dm_dsigma12, void* stream) {
+    g_err[0] = 0;
+    if (B < 0 || CH < 0 || H < 0 || W < 0) return fail(GSR_ERR_ARGUMENT, "fused_ssim: negative size");
+    const long long planes = (long long)B * CH;
+    if (planes == 0 || H == 0 || W == 0) return GSR_OK;
+    if (planes > 65535) return fail(GSR_ERR_ARGUMENT, "fused_ssim: B*CH=%lld exceeds 65535 planes", planes);
+    if (!img1 || !img2 || !ssim_map) return fail(GSR_ERR_ARGUMENT, "fused_ssim: null pointer");
+    const int ndm = (dm_dmu1 != nullptr) + (dm_dsigma1_sq != nullptr) + (dm_dsigma12 != nullptr);
+    if (ndm != 0 && ndm != 3) return fail(GSR_ERR_ARGUMENT, "fused_ssim: pass all three derivative maps or none");
+    HIP_TRY(gsr::launch_ssim_fwd((int)planes, H, W, C1, C2, img1, img2, ssim_map, dm_dmu1, dm_dsigma1_sq, dm_dsigma12,
+                                 (hipStream_t)stream),
+            "fused_ssim forward");
+    return GSR_OK;
+}
+
+int gsr_fused_ssim_backward(int B, int CH, int H, int W, float C1, float C2, const float* img1, const float* img2,
+                            const float* dL_dmap, const float* dm_dmu1, const float* dm_dsigma1_sq,
+                            const float* dm_dsigma12, float* dL_dimg1, void* stream) {
+    (void)C1;  // the derivative maps already carry C1 and C2 (ssim.cu:315-366 does not use them either)
+    (void)C2;
+    g_err[0] = 0;
+    if (B < 0 || CH < 0 || H < 0 || W < 0) return fail(GSR_ERR_ARGUMENT, "fused_ssim: negative size");
+    const long long planes = (long long)B * CH;
+    if (planes == 0 || H == 0 || W == 0) return GSR_OK;
+    if (planes > 65535) return fail(GSR_ERR_ARGUMENT, "fused_ssim: B*CH=%lld exceeds 65535 planes", planes);
+    if (!img1 || !img2 || !dL_dmap || !dm_dmu1 || !dm_dsigma1_sq || !dm_dsigma12 || !dL_dimg1)
+        return fail(GSR_ERR_ARGUMENT, "fused_ssim backward: null pointer");
+    HIP_TRY(gsr::launch_ssim_bwd((int)planes, H, W, img1, img2, dL_dmap, dm_dmu1, dm_dsigma1_sq, dm_dsigma12, dL_dimg1,
+                                 (hipStream_t)stream),
+            "fused_ssim backward");
+    return GSR_OK;
+}
 
 int gsr_knn_mean_dist2(int P, const float* points, float* mean_dists, gsr_alloc_fn scratch_alloc, void* scratch_ctx,
                        void* stream_) {

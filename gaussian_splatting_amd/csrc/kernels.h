@@ -101,6 +101,12 @@ hipError_t launch_tile_order(uint32_t tiles, const uint32_t* cost, uint32_t* ord
 // knn.hip
 size_t knn_scratch_bytes(int P);
 hipError_t launch_knn(int P, const float* pts, float* out, void* scratch, hipStream_t stream);
+// ssim.hip
+hipError_t launch_ssim_fwd(int planes, int H, int W, float C1, float C2, const float* img1, const float* img2,
+                           float* map, float* dm_dmu1, float* dm_ds11, float* dm_ds12, hipStream_t stream);
+hipError_t launch_ssim_bwd(int planes, int H, int W, const float* img1, const float* img2, const float* dL_dmap,
+                           const float* dm_dmu1, const float* dm_ds11, const float* dm_ds12, float* dL_dimg1,
+                           hipStream_t stream);
 // backward.hip
 hipError_t launch_gauss_reduce(int P, const GeomState& g, uint32_t gx, const unsigned long long* lim_key,
                                const GradRecs& recs, const GradRecs& sums, hipStream_t stream);

@@ -12,6 +12,8 @@ Two kinds of vectors, both small .npz files of inputs and expected outputs:
                   (convert_SHs_python: colours = clamp_min(eval_sh(...) + 0.5, 0))
      l1_grad.npz  utils/loss_utils.py:16-19 l1_loss, its autograd gradient (the upstream-gradient
                   convention of train.py:155)
+     ssim.npz     utils/loss_utils.py ssim/_ssim (conv2d SSIM), mean and autograd gradient: pins
+                  oracle/ssim.py, the oracle of the fused-SSIM kernels
    These pin the camera conventions, the SH polynomial and the loss-gradient convention of the
    oracle and the HIP path.  The reference's rasterizer itself cannot run here (CUDA source,
    no nvcc, and BACKWARD::render is missing from the source; SURVEY.md section 8c).
@@ -107,6 +109,23 @@ def make_l1_vectors(loss_utils):
                         loss=np.array(loss.item()), grad=img.grad.numpy())
 
 
+def make_ssim_vectors(loss_utils):
+    """utils/loss_utils.py ssim (conv2d, 11x11 window, sigma 1.5) -- the function the reference's
+    fused-ssim test compares its kernels against (submodules/fused-ssim/tests/test.py:23-52,78-87) --
+    evaluated in float64 on CPU: the mean SSIM and its autograd gradient w.r.t. img1."""
+    out = {}
+    g = torch.Generator().manual_seed(9)
+    for i, shape in enumerate([(1, 3, 37, 53), (2, 2, 40, 45), (1, 1, 16, 9)]):
+        img1 = torch.rand(shape, generator=g, dtype=torch.float64)
+        img2 = (0.7 * img1 + 0.3 * torch.rand(shape, generator=g, dtype=torch.float64)).clamp(0, 1)
+        x = img1.clone().requires_grad_(True)
+        val = loss_utils.ssim(x, img2)
+        val.backward()
+        out[f"img1_{i}"], out[f"img2_{i}"] = img1.numpy(), img2.numpy()
+        out[f"value_{i}"], out[f"grad_{i}"] = np.array(val.item()), x.grad.numpy()
+    np.savez_compressed(os.path.join(HERE, "ssim.npz"), **out)
+
+
 def make_raster_vectors():
     from tests import common as C
     from gaussian_splatting_amd import synthetic as syn
@@ -153,6 +172,7 @@ def main():
 
     make_camera_vectors(gu)
     make_l1_vectors(loss_utils)
+    make_ssim_vectors(loss_utils)
     sys.path.remove(args.reference)
     make_sh_vectors(sh_utils)
     make_raster_vectors()
