@@ -63,7 +63,10 @@ __device__ __forceinline__ void reduce_records(int P, int g0, const uint32_t* __
     sa = make_float4(0.f, 0.f, 0.f, 0.f);
     sb = sa;
     sc = make_float2(0.f, 0.f);
-    for (uint32_t base = E0; base < E1; base += 64) {
+    // Whether slot e of a chunk has a record needs the tile's limit key: a dependent load.
+    // It is probed one chunk ahead, so the limit-key load of chunk c + 1 is in flight with
+    // the record loads of chunk c.
+    auto probe = [&](uint32_t base) -> bool {
         const uint32_t e = base + lane;
         // owner of slot e: the largest lane whose segment starts at or before it
         int owner = 0;
@@ -76,16 +79,21 @@ __device__ __forceinline__ void reduce_records(int P, int g0, const uint32_t* __
         const uint32_t o0 = __shfl(my0, owner), ow = __shfl(w, owner), ox = __shfl(x0, owner),
                        oy = __shfl(y0, owner);
         const unsigned long long okey = __shfl(key, owner);
+        if (e >= E1) return false;
+        const uint32_t k = e - o0, ty = k / ow, tile = (oy + ty) * gx + ox + (k - ty * ow);
+        return okey <= lim_key[tile];
+    };
+    bool has = E0 < E1 ? probe(E0) : false;
+    for (uint32_t base = E0; base < E1; base += 64) {
+        const uint32_t e = base + lane;
         float4 x = make_float4(0.f, 0.f, 0.f, 0.f), y = x;
         float2 z = make_float2(0.f, 0.f);
-        if (e < E1) {
-            const uint32_t k = e - o0, ty = k / ow, tile = (oy + ty) * gx + ox + (k - ty * ow);
-            if (okey <= lim_key[tile]) {
-                x = recs.a[e];
-                y = recs.b[e];
-                z = recs.c[e];
-            }
+        if (has) {
+            x = recs.a[e];
+            y = recs.b[e];
+            z = recs.c[e];
         }
+        const bool has_next = base + 64 < E1 ? probe(base + 64) : false;
         float4* row = reinterpret_cast<float4*>(&s_rec[lane * kRecStride]);
         row[0] = x;
         row[1] = y;
@@ -101,6 +109,7 @@ __device__ __forceinline__ void reduce_records(int P, int g0, const uint32_t* __
             sc.x += ww.x; sc.y += ww.y;
         }
         __syncthreads();
+        has = has_next;
     }
 }
 
