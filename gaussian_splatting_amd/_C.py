@@ -20,7 +20,8 @@ import torch
 
 from . import _lib
 
-__all__ = ["rasterize_gaussians", "rasterize_gaussians_backward", "mark_visible", "fusedssim", "fusedssim_backward"]
+__all__ = ["rasterize_gaussians", "rasterize_gaussians_backward", "mark_visible", "adamUpdate", "fusedssim",
+           "fusedssim_backward"]
 
 
 # Sync-free forward (gsr_rasterize_forward_ex): the binning buffer is sized from a capacity
@@ -116,14 +117,33 @@ class _Resizer:
             return None
 
 
-def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
-                        viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
-                        prefiltered, antialiasing, debug) -> Tuple[int, torch.Tensor, torch.Tensor, torch.Tensor,
-                                                                   torch.Tensor, torch.Tensor, torch.Tensor]:
+def _present(t) -> bool:
+    return t is not None and t.numel() != 0 and t.size(0) != 0
+
+
+def rasterize_gaussians(*args) -> Tuple[int, torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor,
+                                        torch.Tensor]:
     """RasterizeGaussiansCUDA (rasterize_points.cu:45-146).
+
+    Positional arguments, as the pybind function takes them:
+    ``(bg, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp, viewmatrix, projmatrix,
+    tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos, prefiltered, antialiasing, debug)``
+    -- the vendored rasterizer's 20 -- or the 3DGS-accel build's 21, which insert ``dc`` ([P,1,3]) before ``sh``
+    (then the rest coefficients [P,M,3]); see include/gsr.h gsr_rasterize_forward_dc.
 
     Returns ``(num_rendered, color[3,H,W], radii[P] int32, geomBuffer, binningBuffer, imgBuffer, invdepth[1,H,W])``.
     """
+    if len(args) == 21:
+        (background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp, viewmatrix,
+         projmatrix, tan_fovx, tan_fovy, image_height, image_width, dc, sh, degree, campos, prefiltered,
+         antialiasing, debug) = args
+    elif len(args) == 20:
+        (background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp, viewmatrix,
+         projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos, prefiltered, antialiasing,
+         debug) = args
+        dc = None
+    else:
+        raise TypeError(f"rasterize_gaussians(): expected 20 or 21 positional arguments, got {len(args)}")
     if means3D.ndimension() != 2 or means3D.size(1) != 3:
         raise RuntimeError("means3D must have dimensions (num_points, 3)")
     _require_device(means3D, "means3D")
@@ -142,49 +162,67 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     if P == 0:
         return 0, out_color, radii, geom, binning, img, out_invdepth
 
-    M = sh.size(1) if (sh is not None and sh.numel() != 0 and sh.size(0) != 0) else 0
+    M = sh.size(1) if _present(sh) else 0
+    split = dc is not None and _present(dc) and not _present(colors)
     ins = _Inputs(device)
     rg, rb, ri = _Resizer(geom), _Resizer(binning), _Resizer(img)
     nr = ctypes.c_int(0)
     cap = ctypes.c_int(0)
     key = (device.index, P, W, H)
+    common_head = (rg.cb, None, rb.cb, None, ri.cb, None, P, int(degree), M,
+                   ins.req(background, "bg", small=True), W, H, ins.req(means3D, "means3D"))
+    sh_args = ((ins.req(dc, "dc"), ins.opt(sh, "sh", align16=True)) if split else (ins.opt(sh, "sh", align16=True),))
+    common_tail = (
+        ins.opt(colors, "colors_precomp"), ins.req(opacity, "opacities"), ins.opt(scales, "scales"),
+        float(scale_modifier), ins.opt(rotations, "rotations", align16=True), ins.opt(cov3D_precomp, "cov3D_precomp"),
+        ins.req(viewmatrix, "viewmatrix", small=True), ins.req(projmatrix, "projmatrix", small=True),
+        ins.opt(campos if campos is not None and campos.device.type == "cuda" else
+                (campos.to(device) if campos is not None else None), "campos"),
+        float(tan_fovx), float(tan_fovy), int(bool(prefiltered)), out_color.data_ptr(), out_invdepth.data_ptr(),
+        int(bool(antialiasing)), radii.data_ptr(), int(bool(debug)), _stream_handle(device), ctypes.byref(nr),
+        _capacity_hint(key), ctypes.byref(cap))
+    fn = lib.gsr_rasterize_forward_dc if split else lib.gsr_rasterize_forward_ex
     with torch.cuda.device(device):
-        rc = lib.gsr_rasterize_forward_ex(
-            rg.cb, None, rb.cb, None, ri.cb, None, P, int(degree), M,
-            ins.req(background, "bg", small=True), W, H,
-            ins.req(means3D, "means3D"), ins.opt(sh, "sh", align16=True), ins.opt(colors, "colors_precomp"),
-            ins.req(opacity, "opacities"), ins.opt(scales, "scales"), float(scale_modifier),
-            ins.opt(rotations, "rotations", align16=True), ins.opt(cov3D_precomp, "cov3D_precomp"),
-            ins.req(viewmatrix, "viewmatrix", small=True), ins.req(projmatrix, "projmatrix", small=True),
-            ins.opt(campos if campos is not None and campos.device.type == "cuda" else
-                    (campos.to(device) if campos is not None else None), "campos"),
-            float(tan_fovx), float(tan_fovy), int(bool(prefiltered)), out_color.data_ptr(), out_invdepth.data_ptr(),
-            int(bool(antialiasing)), radii.data_ptr(), int(bool(debug)), _stream_handle(device), ctypes.byref(nr),
-            _capacity_hint(key), ctypes.byref(cap))
+        rc = fn(*common_head, *sh_args, *common_tail)
     _lib.check(rc, "rasterize_gaussians")
     _note_rendered(key, nr.value)
     binning._gsr_capacity = int(cap.value)  # the layout the backward must use (kept across save_for_backward)
     return int(nr.value), out_color, radii, geom, binning, img, out_invdepth
 
 
-def rasterize_gaussians_backward(background, means3D, radii, colors, opacities, scales, rotations, scale_modifier,
-                                 cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color,
-                                 dL_dout_invdepth, sh, degree, campos, geomBuffer, R, binningBuffer, imageBuffer,
-                                 antialiasing, debug, out=None):
+def rasterize_gaussians_backward(*args, out=None):
     """RasterizeGaussiansBackwardCUDA (rasterize_points.cu:149-248).
 
-    Returns ``(dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations)``.
-    ``out`` (an extension, not in the reference) may map any of the names
-    ``dL_dmeans3D, dL_dsh, dL_dopacity, dL_dscales, dL_drotations`` to preallocated
-    contiguous float32 tensors of the right shape -- e.g. views of one flat
-    gradient arena that is then all-reduced without a copy.
+    Positional arguments: the vendored rasterizer's 24 ``(bg, means3D, radii, colors, opacities, scales,
+    rotations, scale_modifier, cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color,
+    dL_dout_invdepth, sh, degree, campos, geomBuffer, R, binningBuffer, imageBuffer, antialiasing, debug)``,
+    or the 3DGS-accel build's 25 with ``dc`` before ``sh``.
+
+    Returns ``(dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations)``,
+    or, with ``dc``, ``(..., dL_dcov3D, dL_ddc, dL_dsh, ...)`` (9 tensors, as the accel build returns them).
+    ``out`` (an extension, not in the reference) may map any of the names ``dL_dmeans3D, dL_ddc, dL_dsh,
+    dL_dopacity, dL_dscales, dL_drotations`` to preallocated contiguous float32 tensors of the right shape --
+    e.g. views of one flat gradient arena that is then all-reduced without a copy.
     """
+    if len(args) == 25:
+        (background, means3D, radii, colors, opacities, scales, rotations, scale_modifier, cov3D_precomp, viewmatrix,
+         projmatrix, tan_fovx, tan_fovy, dL_dout_color, dL_dout_invdepth, dc, sh, degree, campos, geomBuffer, R,
+         binningBuffer, imageBuffer, antialiasing, debug) = args
+        accel = True
+    elif len(args) == 24:
+        (background, means3D, radii, colors, opacities, scales, rotations, scale_modifier, cov3D_precomp, viewmatrix,
+         projmatrix, tan_fovx, tan_fovy, dL_dout_color, dL_dout_invdepth, sh, degree, campos, geomBuffer, R,
+         binningBuffer, imageBuffer, antialiasing, debug) = args
+        dc, accel = None, False
+    else:
+        raise TypeError(f"rasterize_gaussians_backward(): expected 24 or 25 positional arguments, got {len(args)}")
     _require_device(means3D, "means3D")
     device = means3D.device
     lib = _lib.load()
     P = means3D.size(0)
     H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))
-    M = sh.size(1) if (sh is not None and sh.numel() != 0 and sh.size(0) != 0) else 0
+    M = sh.size(1) if _present(sh) else 0
+    split = accel and dc is not None and _present(dc) and not _present(colors)
     f32 = dict(dtype=torch.float32, device=device)
     alloc = _empty if P > 0 else torch.zeros
     out = dict(out or {})
@@ -202,36 +240,47 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, opacities, 
     dL_dopacity = buf("dL_dopacity", (P, 1))
     dL_dmeans3D = buf("dL_dmeans3D", (P, 3))
     dL_dcov3D = alloc((P, 6), **f32)
+    # the accel build always returns a [P,1,3] dc gradient (zeros when colours were precomputed)
+    dL_ddc = buf("dL_ddc", (P, 1, 3)) if accel else None
     dL_dsh = buf("dL_dsh", (P, M, 3))
     dL_dscales = buf("dL_dscales", (P, 3))
     dL_drotations = buf("dL_drotations", (P, 4))
     has_inv = dL_dout_invdepth is not None and dL_dout_invdepth.numel() != 0 and dL_dout_invdepth.size(0) != 0
     dL_dinvdepths = alloc((P, 1), **f32) if has_inv else None
-    result = (dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations)
+    if accel:
+        result = (dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_ddc, dL_dsh, dL_dscales,
+                  dL_drotations)
+    else:
+        result = (dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations)
     if P == 0:
         return result
+    if accel and not split:
+        dL_ddc.zero_()  # no SH evaluation: the dc gradient is zero, as the accel build's zero-initialised tensor
 
     ins = _Inputs(device)
     scratch = torch.empty(0, dtype=torch.uint8, device=device)
     rs = _Resizer(scratch)
+    head = (P, int(degree), M, int(R), ins.req(background, "bg", small=True), W, H, ins.req(means3D, "means3D"))
+    sh_args = ((ins.req(dc, "dc"), ins.opt(sh, "sh")) if split else (ins.opt(sh, "sh"),))
+    mid = (ins.opt(colors, "colors_precomp"),
+           ins.req(opacities, "opacities"), ins.opt(scales, "scales"), float(scale_modifier),
+           ins.opt(rotations, "rotations", align16=True), ins.opt(cov3D_precomp, "cov3D_precomp"),
+           ins.req(viewmatrix, "viewmatrix", small=True), ins.req(projmatrix, "projmatrix", small=True),
+           ins.opt(campos if campos is not None and campos.device.type == "cuda" else
+                   (campos.to(device) if campos is not None else None), "campos"),
+           float(tan_fovx), float(tan_fovy), radii.contiguous().data_ptr(), geomBuffer.data_ptr(),
+           binningBuffer.data_ptr() if binningBuffer.numel() else None, imageBuffer.data_ptr(),
+           ins.req(dL_dout_color, "dL_dout_color"),
+           ins.req(dL_dout_invdepth, "dL_dout_invdepth") if has_inv else None,
+           dL_dmeans2D.data_ptr(), None, dL_dopacity.data_ptr(), dL_dcolors.data_ptr(),
+           dL_dinvdepths.data_ptr() if has_inv else None, dL_dmeans3D.data_ptr(), dL_dcov3D.data_ptr())
+    sh_grads = ((dL_ddc.data_ptr(), dL_dsh.data_ptr() if M > 0 else None) if split else
+                (dL_dsh.data_ptr() if M > 0 else None,))
+    tail = (dL_dscales.data_ptr(), dL_drotations.data_ptr(), int(bool(antialiasing)), int(bool(debug)), rs.cb, None,
+            _stream_handle(device), int(getattr(binningBuffer, "_gsr_capacity", 0)), int(binningBuffer.numel()))
+    fn = lib.gsr_rasterize_backward_dc if split else lib.gsr_rasterize_backward_ex
     with torch.cuda.device(device):
-        rc = lib.gsr_rasterize_backward_ex(
-            P, int(degree), M, int(R), ins.req(background, "bg", small=True), W, H,
-            ins.req(means3D, "means3D"), ins.opt(sh, "sh"), ins.opt(colors, "colors_precomp"),
-            ins.req(opacities, "opacities"), ins.opt(scales, "scales"), float(scale_modifier),
-            ins.opt(rotations, "rotations", align16=True), ins.opt(cov3D_precomp, "cov3D_precomp"),
-            ins.req(viewmatrix, "viewmatrix", small=True), ins.req(projmatrix, "projmatrix", small=True),
-            ins.opt(campos if campos is not None and campos.device.type == "cuda" else
-                    (campos.to(device) if campos is not None else None), "campos"),
-            float(tan_fovx), float(tan_fovy), radii.contiguous().data_ptr(), geomBuffer.data_ptr(),
-            binningBuffer.data_ptr() if binningBuffer.numel() else None, imageBuffer.data_ptr(),
-            ins.req(dL_dout_color, "dL_dout_color"),
-            ins.req(dL_dout_invdepth, "dL_dout_invdepth") if has_inv else None,
-            dL_dmeans2D.data_ptr(), None, dL_dopacity.data_ptr(), dL_dcolors.data_ptr(),
-            dL_dinvdepths.data_ptr() if has_inv else None, dL_dmeans3D.data_ptr(), dL_dcov3D.data_ptr(),
-            dL_dsh.data_ptr() if M > 0 else None, dL_dscales.data_ptr(), dL_drotations.data_ptr(),
-            int(bool(antialiasing)), int(bool(debug)), rs.cb, None, _stream_handle(device),
-            int(getattr(binningBuffer, "_gsr_capacity", 0)), int(binningBuffer.numel()))
+        rc = fn(*head, *sh_args, *mid, *sh_grads, *tail)
     _lib.check(rc, "rasterize_gaussians_backward")
     return result
 
@@ -252,6 +301,13 @@ def mark_visible(means3D, viewmatrix, projmatrix) -> torch.Tensor:
                                   _stream_handle(device))
     _lib.check(rc, "mark_visible")
     return present
+
+
+def adamUpdate(param, param_grad, exp_avg, exp_avg_sq, visible, lr, b1, b2, eps, N, M):
+    """The 3DGS-accel build's ``_C.adamUpdate`` (SparseGaussianAdam's per-group call; include/gsr_adam.h)."""
+    from .optim import adam_update
+
+    adam_update(param, param_grad, exp_avg, exp_avg_sq, visible, lr, b1, b2, eps, N, M)
 
 
 # ---- fused SSIM as utils/loss_utils.py:16-37 expects it from this module ------------------

@@ -15,13 +15,21 @@ _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GSR_LIBRARY", os.path.join(_PKG, "lib", "libgsr.so"))
 INCLUDE_DIR = os.path.join(os.path.dirname(_PKG), "include")
 HEADER_PATH = os.path.join(INCLUDE_DIR, "gsr.h")
-HEADERS = [os.path.join(INCLUDE_DIR, h) for h in ("gsr.h", "gsr_knn.h", "gsr_ssim.h")]
+HEADERS = [os.path.join(INCLUDE_DIR, h) for h in ("gsr.h", "gsr_knn.h", "gsr_ssim.h", "gsr_adam.h")]
 
 ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
 
 _vp = ctypes.c_void_p
 _i = ctypes.c_int
 _f = ctypes.c_float
+
+class AdamGroup(ctypes.Structure):
+    """gsr_adam_group (include/gsr_adam.h)."""
+
+    _fields_ = [("param", ctypes.c_void_p), ("grad", ctypes.c_void_p), ("exp_avg", ctypes.c_void_p),
+                ("exp_avg_sq", ctypes.c_void_p), ("numel", ctypes.c_longlong), ("M", ctypes.c_int),
+                ("lr", ctypes.c_float), ("eps", ctypes.c_float)]
+
 
 # argument lists, in include/gsr.h order
 SIGNATURES = {
@@ -37,6 +45,12 @@ SIGNATURES = {
     "gsr_rasterize_backward_ex": (_i, [_i, _i, _i, _i, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp,
                                        _vp, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                        _vp, _vp, _vp, _i, _i, ALLOC_FN, _vp, _vp, _i, ctypes.c_size_t]),
+    "gsr_rasterize_forward_dc": (_i, [ALLOC_FN, _vp, ALLOC_FN, _vp, ALLOC_FN, _vp, _i, _i, _i, _vp, _i, _i, _vp, _vp,
+                                      _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp, _f, _f, _i, _vp, _vp, _i, _vp,
+                                      _i, _vp, ctypes.POINTER(_i), _i, ctypes.POINTER(_i)]),
+    "gsr_rasterize_backward_dc": (_i, [_i, _i, _i, _i, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp,
+                                       _vp, _vp, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                       _vp, _vp, _vp, _vp, _vp, _i, _i, ALLOC_FN, _vp, _vp, _i, ctypes.c_size_t]),
     "gsr_mark_visible": (_i, [_i, _vp, _vp, _vp, _vp, _vp]),
     "gsr_last_error": (ctypes.c_char_p, []),
     "gsr_version": (ctypes.c_char_p, []),
@@ -47,6 +61,8 @@ SIGNATURES = {
     "gsr_knn_mean_dist2": (_i, [_i, _vp, _vp, ALLOC_FN, _vp, _vp]),
     "gsr_fused_ssim_forward": (_i, [_i, _i, _i, _i, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gsr_fused_ssim_backward": (_i, [_i, _i, _i, _i, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "gsr_adam_update": (_i, [_vp, _vp, _vp, _vp, _vp, _f, _f, _f, _f, _i, _i, _vp]),
+    "gsr_adam_update_multi": (_i, [ctypes.POINTER(AdamGroup), _i, _vp, _i, _f, _f, _vp]),
 }
 
 _lock = threading.Lock()

@@ -20,7 +20,7 @@ CSRC = os.path.join(PKG, "csrc")
 OBJ = os.path.join(PKG, "build")
 LIB_DIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIB_DIR, "libgsr.so")
-SOURCES = ["api.hip", "preprocess.hip", "binning.hip", "render.hip", "backward.hip", "knn.hip", "ssim.hip"]
+SOURCES = ["api.hip", "preprocess.hip", "binning.hip", "render.hip", "backward.hip", "knn.hip", "ssim.hip", "adam.hip"]
 HEADERS = ["gsr_common.h", "kernels.h", "footprint.h"]
 ARCH = os.environ.get("GSR_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -30,7 +30,7 @@ CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-W
 
 def _newest_input_mtime() -> float:
     files = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(ROOT, "include", h) for h in
-                                                                  ("gsr.h", "gsr_knn.h", "gsr_ssim.h")] + [__file__]
+                                                                  ("gsr.h", "gsr_knn.h", "gsr_ssim.h", "gsr_adam.h")] + [__file__]
     return max(os.path.getmtime(f) for f in files)
 
 
@@ -69,6 +69,11 @@ def build(force: bool = False, jobs: int = 5, verbose: bool = True, variant: str
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
     os.replace(tmp, LIB_OUT)
+    # the offload bundler may leave per-object device images next to the output; nothing loads them
+    import glob
+
+    for stray in glob.glob(os.path.join(os.path.dirname(LIB_OUT), "*.hipv4-amdgcn-*")):
+        os.remove(stray)
     if verbose:
         print(f"[gsr] built {LIB_OUT}")
     return LIB_OUT

@@ -17,6 +17,7 @@
 #include "../../include/gsr.h"
 #include "../../include/gsr_knn.h"
 #include "../../include/gsr_ssim.h"
+#include "../../include/gsr_adam.h"
 #include "kernels.h"
 
 namespace {
@@ -241,6 +242,62 @@ int gsr_knn_mean_dist2(int P, const float* points, float* mean_dists, gsr_alloc_
     return GSR_OK;
 }
 
+// ---- SparseGaussianAdam's step (include/gsr_adam.h) -------------------------------
+static_assert(GSR_ADAM_MAX_GROUPS == gsr::kAdamMaxGroups, "group table size");
+
+static int adam_launch(const gsr_adam_group* groups, int n_groups, const unsigned char* visible, int N, float b1,
+                       float b2, void* stream) {
+    using namespace gsr;
+    g_err[0] = 0;
+    if (n_groups < 0 || n_groups > GSR_ADAM_MAX_GROUPS)
+        return fail(GSR_ERR_ARGUMENT, "adam_update: %d parameter groups (0..%d)", n_groups, GSR_ADAM_MAX_GROUPS);
+    if (N < 0) return fail(GSR_ERR_ARGUMENT, "adam_update: N must be >= 0");
+    if (N == 0 || n_groups == 0) return GSR_OK;
+    if (!visible || !groups) return fail(GSR_ERR_ARGUMENT, "adam_update: null pointer");
+    AdamArgs a{};
+    a.vis = visible;
+    a.b1 = b1;
+    a.b2 = b2;
+    uint32_t blocks = 0;
+    auto al16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+    for (int k = 0; k < n_groups; k++) {
+        const gsr_adam_group& s = groups[k];
+        if (s.M <= 0 || s.numel != (long long)N * s.M)
+            return fail(GSR_ERR_ARGUMENT, "adam_update: group %d has %lld values, expected N*M = %d*%d", k, s.numel, N,
+                        s.M);
+        if (s.numel > 0x7fffffffLL)
+            return fail(GSR_ERR_ARGUMENT, "adam_update: group %d has more than 2^31-1 values", k);
+        if (!s.param || !s.grad || !s.exp_avg || !s.exp_avg_sq)
+            return fail(GSR_ERR_ARGUMENT, "adam_update: group %d has a null parameter/state pointer", k);
+        AdamGroupDev& G = a.grp[a.n_groups++];
+        G.p = s.param; G.g = s.grad; G.m = s.exp_avg; G.v = s.exp_avg_sq;
+        G.n = (uint32_t)s.numel;
+        G.M = (uint32_t)s.M;
+        uint32_t l = 0;
+        while ((1u << l) < G.M) l++;
+        G.shift = 31 + l;
+        G.magic = ((1ull << G.shift) + G.M - 1) / G.M;  // ceil(2^(31+l) / M): exact i / M for i < 2^31
+        G.lr = s.lr;
+        G.eps = s.eps;
+        G.first_block = blocks;
+        G.vec = al16(s.param) && al16(s.grad) && al16(s.exp_avg) && al16(s.exp_avg_sq);
+        blocks += (G.n + kAdamBlockElems - 1) / kAdamBlockElems;
+    }
+    HIP_TRY(launch_adam(a, blocks, (hipStream_t)stream), "adam_update");
+    return GSR_OK;
+}
+
+int gsr_adam_update(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, const unsigned char* visible,
+                    float lr, float b1, float b2, float eps, int N, int M, void* stream) {
+    const gsr_adam_group g{param, grad, exp_avg, exp_avg_sq, (long long)N * M, M, lr, eps};
+    return adam_launch(&g, 1, visible, N, b1, b2, stream);
+}
+
+int gsr_adam_update_multi(const gsr_adam_group* groups, int n_groups, const unsigned char* visible, int N, float b1,
+                          float b2, void* stream) {
+    return adam_launch(groups, n_groups, visible, N, b1, b2, stream);
+}
+
 int gsr_profile_enable(int stage_mask) {
     std::lock_guard<std::mutex> lk(g_prof.mu);
     g_prof.mask = (unsigned)stage_mask;
@@ -299,7 +356,7 @@ int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const
 namespace {
 int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_alloc, void* binning_ctx,
                  gsr_alloc_fn image_alloc, void* image_ctx, int P, int D, int M, const float* background, int width,
-                 int height, const float* means3D, const float* shs, const float* colors_precomp,
+                 int height, const float* means3D, const float* dc, const float* shs, const float* colors_precomp,
                  const float* opacities, const float* scales, float scale_modifier, const float* rotations,
                  const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix, const float* cam_pos,
                  float tan_fovx, float tan_fovy, int prefiltered, float* out_color, float* out_invdepth,
@@ -318,8 +375,10 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
     if (P == 0) return GSR_OK;  // RI/rasterize_points.cu:108: nothing is launched
     if (!means3D || !opacities || !viewmatrix || !projmatrix || !background || !out_color || !out_invdepth || !radii)
         return fail(GSR_ERR_ARGUMENT, "rasterize_forward: missing required input");
-    if (!colors_precomp && !shs)
+    if (!colors_precomp && !shs && !dc)
         return fail(GSR_ERR_ARGUMENT, "rasterize_forward: provide either SHs or precomputed colours");
+    if (dc && M > 0 && !shs) return fail(GSR_ERR_ARGUMENT, "rasterize_forward: %d rest SH coefficients but no shs", M);
+    if (dc) M += 1;  // split layout: M counted the rest; the kernels see dc as coefficient 0
     if (!cov3D_precomp && (!scales || !rotations))
         return fail(GSR_ERR_ARGUMENT, "rasterize_forward: provide scales+rotations or a precomputed covariance");
     if (!colors_precomp && (D < 0 || D > 3 || (D + 1) * (D + 1) > M))
@@ -351,7 +410,8 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
         PreprocessArgs pa{};
         pa.P = P; pa.D = D; pa.M = M; pa.W = width; pa.H = height;
         pa.means3D = means3D; pa.scales = scales; pa.scale_modifier = scale_modifier; pa.rotations = rotations;
-        pa.opacities = opacities; pa.shs = colors_precomp ? nullptr : shs; pa.cov3D_precomp = cov3D_precomp;
+        pa.opacities = opacities; pa.shs = colors_precomp || M <= (dc ? 1 : 0) ? nullptr : shs;
+        pa.dc = colors_precomp ? nullptr : dc; pa.cov3D_precomp = cov3D_precomp;
         pa.colors_precomp = colors_precomp; pa.viewmatrix = viewmatrix; pa.projmatrix = projmatrix;
         pa.campos = cam_pos; pa.tan_fovx = tan_fovx; pa.tan_fovy = tan_fovy; pa.focal_x = focal_x;
         pa.focal_y = focal_y; pa.gx = gx; pa.gy = gy; pa.prefiltered = prefiltered; pa.antialiasing = antialiasing;
@@ -453,7 +513,7 @@ int gsr_rasterize_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn 
                           float* out_invdepth, int antialiasing, int* radii, int debug, void* stream,
                           int* num_rendered) {
     return forward_impl(geom_alloc, geom_ctx, binning_alloc, binning_ctx, image_alloc, image_ctx, P, D, M, background,
-                        width, height, means3D, shs, colors_precomp, opacities, scales, scale_modifier, rotations,
+                        width, height, means3D, nullptr, shs, colors_precomp, opacities, scales, scale_modifier, rotations,
                         cov3D_precomp, viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, prefiltered, out_color,
                         out_invdepth, antialiasing, radii, debug, stream, num_rendered, 0, nullptr);
 }
@@ -468,7 +528,7 @@ int gsr_rasterize_forward_ex(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_
                              int* radii, int debug, void* stream, int* num_rendered, int capacity_hint,
                              int* binning_capacity) {
     return forward_impl(geom_alloc, geom_ctx, binning_alloc, binning_ctx, image_alloc, image_ctx, P, D, M, background,
-                        width, height, means3D, shs, colors_precomp, opacities, scales, scale_modifier, rotations,
+                        width, height, means3D, nullptr, shs, colors_precomp, opacities, scales, scale_modifier, rotations,
                         cov3D_precomp, viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, prefiltered, out_color,
                         out_invdepth, antialiasing, radii, debug, stream, num_rendered, capacity_hint,
                         binning_capacity);
@@ -476,13 +536,13 @@ int gsr_rasterize_forward_ex(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_
 
 namespace {
 int backward_impl(int P, int D, int M, int R, const float* background, int width, int height, const float* means3D,
-                  const float* shs, const float* colors_precomp, const float* opacities, const float* scales,
+                  const float* dc, const float* shs, const float* colors_precomp, const float* opacities, const float* scales,
                   float scale_modifier, const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
                   const float* projmatrix, const float* campos, float tan_fovx, float tan_fovy, const int* radii,
                   void* geom_buffer, void* binning_buffer, void* image_buffer, const float* dL_dpix,
                   const float* dL_dinvdepths, float* dL_dmean2D, float* dL_dconic, float* dL_dopacity,
-                  float* dL_dcolor, float* dL_dinvdepth, float* dL_dmean3D, float* dL_dcov3D, float* dL_dsh,
-                  float* dL_dscale, float* dL_drot, int antialiasing, int debug, gsr_alloc_fn scratch_alloc,
+                  float* dL_dcolor, float* dL_dinvdepth, float* dL_dmean3D, float* dL_dcov3D, float* dL_ddc,
+                  float* dL_dsh, float* dL_dscale, float* dL_drot, int antialiasing, int debug, gsr_alloc_fn scratch_alloc,
                   void* scratch_ctx, void* stream_, int binning_capacity, size_t binning_bytes) {
     using namespace gsr;
     g_err[0] = 0;
@@ -495,7 +555,12 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
     if (!means3D || !opacities || !radii || !dL_dpix || !dL_dmean2D || !dL_dopacity || !dL_dcolor || !dL_dmean3D ||
         !dL_dcov3D || !viewmatrix || !projmatrix || !background)
         return fail(GSR_ERR_ARGUMENT, "rasterize_backward: missing required pointer");
-    if (shs && (!dL_dsh || !campos)) return fail(GSR_ERR_ARGUMENT, "rasterize_backward: SH gradient needs dL_dsh");
+    if (!colors_precomp && shs && (!dL_dsh || !campos))
+        return fail(GSR_ERR_ARGUMENT, "rasterize_backward: SH gradient needs dL_dsh");
+    if (!colors_precomp && dc && (!dL_ddc || !campos))
+        return fail(GSR_ERR_ARGUMENT, "rasterize_backward: dc gradient needs dL_ddc");
+    if (dc && M > 0 && !shs) return fail(GSR_ERR_ARGUMENT, "rasterize_backward: %d rest SH coefficients but no shs", M);
+    if (dc) M += 1;  // as in the forward
     if (scales && (!rotations || !dL_dscale || !dL_drot))
         return fail(GSR_ERR_ARGUMENT, "rasterize_backward: scale/rotation gradients need outputs");
     if ((dL_dinvdepths == nullptr) != (dL_dinvdepth == nullptr))
@@ -546,7 +611,8 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
         StageScope sc(ST_GAUSS_BWD, stream);
         GaussBwdArgs ga{};
         ga.P = P; ga.D = D; ga.M = M; ga.W = width; ga.H = height;
-        ga.means3D = means3D; ga.shs = colors_precomp ? nullptr : shs; ga.opacities = opacities; ga.scales = scales;
+        ga.means3D = means3D; ga.shs = colors_precomp || M <= (dc ? 1 : 0) ? nullptr : shs;
+        ga.dc = colors_precomp ? nullptr : dc; ga.opacities = opacities; ga.scales = scales;
         ga.rotations = rotations; ga.cov3D_precomp = cov3D_precomp; ga.scale_modifier = scale_modifier;
         ga.viewmatrix = viewmatrix; ga.projmatrix = projmatrix; ga.campos = campos;
         ga.tan_fovx = tan_fovx; ga.tan_fovy = tan_fovy; ga.focal_x = focal_x; ga.focal_y = focal_y;
@@ -554,7 +620,7 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
         ga.have_invdepth = dL_dinvdepths != nullptr;
         ga.dL_dmean2D = dL_dmean2D; ga.dL_dconic = dL_dconic; ga.dL_dopacity = dL_dopacity; ga.dL_dcolor = dL_dcolor;
         ga.dL_dinvdepth = dL_dinvdepth; ga.dL_dmean3D = dL_dmean3D; ga.dL_dcov3D = dL_dcov3D;
-        ga.dL_dsh = M > 0 ? dL_dsh : nullptr; ga.dL_dscale = dL_dscale; ga.dL_drot = dL_drot;
+        ga.dL_dsh = M > (dc ? 1 : 0) ? dL_dsh : nullptr; ga.dL_ddc = dc ? dL_ddc : nullptr; ga.dL_dscale = dL_dscale; ga.dL_drot = dL_drot;
         HIP_TRY(launch_gauss_bwd(ga, stream), "gauss_bwd");
     }
     if (int rc = check_debug(debug, stream, "gauss_bwd")) return rc;
@@ -572,10 +638,10 @@ int gsr_rasterize_backward(int P, int D, int M, int R, const float* background, 
                            float* dL_dinvdepth, float* dL_dmean3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscale,
                            float* dL_drot, int antialiasing, int debug, gsr_alloc_fn scratch_alloc,
                            void* scratch_ctx, void* stream) {
-    return backward_impl(P, D, M, R, background, width, height, means3D, shs, colors_precomp, opacities, scales,
+    return backward_impl(P, D, M, R, background, width, height, means3D, nullptr, shs, colors_precomp, opacities, scales,
                          scale_modifier, rotations, cov3D_precomp, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy,
                          radii, geom_buffer, binning_buffer, image_buffer, dL_dpix, dL_dinvdepths, dL_dmean2D,
-                         dL_dconic, dL_dopacity, dL_dcolor, dL_dinvdepth, dL_dmean3D, dL_dcov3D, dL_dsh, dL_dscale,
+                         dL_dconic, dL_dopacity, dL_dcolor, dL_dinvdepth, dL_dmean3D, dL_dcov3D, nullptr, dL_dsh, dL_dscale,
                          dL_drot, antialiasing, debug, scratch_alloc, scratch_ctx, stream, 0, 0);
 }
 
@@ -590,12 +656,51 @@ int gsr_rasterize_backward_ex(int P, int D, int M, int R, const float* backgroun
                               float* dL_dcov3D, float* dL_dsh, float* dL_dscale, float* dL_drot, int antialiasing,
                               int debug, gsr_alloc_fn scratch_alloc, void* scratch_ctx, void* stream,
                               int binning_capacity, size_t binning_bytes) {
-    return backward_impl(P, D, M, R, background, width, height, means3D, shs, colors_precomp, opacities, scales,
+    return backward_impl(P, D, M, R, background, width, height, means3D, nullptr, shs, colors_precomp, opacities, scales,
                          scale_modifier, rotations, cov3D_precomp, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy,
                          radii, geom_buffer, binning_buffer, image_buffer, dL_dpix, dL_dinvdepths, dL_dmean2D,
-                         dL_dconic, dL_dopacity, dL_dcolor, dL_dinvdepth, dL_dmean3D, dL_dcov3D, dL_dsh, dL_dscale,
+                         dL_dconic, dL_dopacity, dL_dcolor, dL_dinvdepth, dL_dmean3D, dL_dcov3D, nullptr, dL_dsh, dL_dscale,
                          dL_drot, antialiasing, debug, scratch_alloc, scratch_ctx, stream, binning_capacity,
                          binning_bytes);
+}
+
+int gsr_rasterize_forward_dc(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_alloc, void* binning_ctx,
+                             gsr_alloc_fn image_alloc, void* image_ctx, int P, int D, int M, const float* background,
+                             int width, int height, const float* means3D, const float* dc, const float* shs,
+                             const float* colors_precomp, const float* opacities, const float* scales,
+                             float scale_modifier, const float* rotations, const float* cov3D_precomp,
+                             const float* viewmatrix, const float* projmatrix, const float* cam_pos, float tan_fovx,
+                             float tan_fovy, int prefiltered, float* out_color, float* out_invdepth, int antialiasing,
+                             int* radii, int debug, void* stream, int* num_rendered, int capacity_hint,
+                             int* binning_capacity) {
+    if (!dc && !colors_precomp)
+        return fail(GSR_ERR_ARGUMENT, "rasterize_forward_dc: provide dc (+ shs) or precomputed colours");
+    return forward_impl(geom_alloc, geom_ctx, binning_alloc, binning_ctx, image_alloc, image_ctx, P, D, M, background,
+                        width, height, means3D, dc, shs, colors_precomp, opacities, scales, scale_modifier, rotations,
+                        cov3D_precomp, viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, prefiltered, out_color,
+                        out_invdepth, antialiasing, radii, debug, stream, num_rendered, capacity_hint,
+                        binning_capacity);
+}
+
+int gsr_rasterize_backward_dc(int P, int D, int M, int R, const float* background, int width, int height,
+                              const float* means3D, const float* dc, const float* shs, const float* colors_precomp,
+                              const float* opacities, const float* scales, float scale_modifier,
+                              const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
+                              const float* projmatrix, const float* campos, float tan_fovx, float tan_fovy,
+                              const int* radii, void* geom_buffer, void* binning_buffer, void* image_buffer,
+                              const float* dL_dpix, const float* dL_dinvdepths, float* dL_dmean2D, float* dL_dconic,
+                              float* dL_dopacity, float* dL_dcolor, float* dL_dinvdepth, float* dL_dmean3D,
+                              float* dL_dcov3D, float* dL_ddc, float* dL_dsh, float* dL_dscale, float* dL_drot,
+                              int antialiasing, int debug, gsr_alloc_fn scratch_alloc, void* scratch_ctx,
+                              void* stream, int binning_capacity, size_t binning_bytes) {
+    if (!dc && !colors_precomp)
+        return fail(GSR_ERR_ARGUMENT, "rasterize_backward_dc: provide dc (+ shs) or precomputed colours");
+    return backward_impl(P, D, M, R, background, width, height, means3D, dc, shs, colors_precomp, opacities, scales,
+                         scale_modifier, rotations, cov3D_precomp, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy,
+                         radii, geom_buffer, binning_buffer, image_buffer, dL_dpix, dL_dinvdepths, dL_dmean2D,
+                         dL_dconic, dL_dopacity, dL_dcolor, dL_dinvdepth, dL_dmean3D, dL_dcov3D, dL_ddc, dL_dsh,
+                         dL_dscale, dL_drot, antialiasing, debug, scratch_alloc, scratch_ctx, stream,
+                         binning_capacity, binning_bytes);
 }
 
 }  // extern "C"

@@ -152,13 +152,18 @@ struct ShLds {
     }
 };
 struct ShGlobal {
-    const float* src;
-    float* dst;
-    __device__ float3 load(int k) const { return make_float3(src[3 * k], src[3 * k + 1], src[3 * k + 2]); }
+    ShAddr src;
+    ShGradAddr dst;
+    int idx;
+    __device__ float3 load(int k) const {
+        const float* c = src.coef(idx, k);
+        return make_float3(c[0], c[1], c[2]);
+    }
     __device__ void store(int k, float3 v) const {
-        dst[3 * k] = v.x;
-        dst[3 * k + 1] = v.y;
-        dst[3 * k + 2] = v.z;
+        float* c = dst.coef(idx, k);
+        c[0] = v.x;
+        c[1] = v.y;
+        c[2] = v.z;
     }
 };
 
@@ -216,33 +221,25 @@ __device__ __forceinline__ void store3(float* p, int i, float x, float y, float 
     p[3 * i + 2] = z;
 }
 
-constexpr int kShRow = 48;     // floats per SH row staged through LDS (M = 16)
 constexpr int kShStride = 52;  // padded LDS row stride: conflict-free ds_read/write_b128
 
 // ---- 3. fused per-Gaussian backward ---------------------------------------------
 // (Folding the record sums into this kernel was measured slower: the sums' dependent loads
 // then run at this kernel's LDS-limited occupancy.)
-template <bool SH_LDS>
+template <int SH_MODE>
 __global__ void __launch_bounds__(64) gauss_bwd_kernel(GaussBwdArgs a) {
-    __shared__ __attribute__((aligned(16))) float s_sh[SH_LDS ? 64 * kShStride : 4];
+    __shared__ __attribute__((aligned(16))) float s_sh[SH_MODE != kShGlobal ? 64 * kShStride : 4];
     const int lane = threadIdx.x;
     const int g0 = blockIdx.x * 64;
     const int idx = g0 + lane;
     const int nvalid = min(64, a.P - g0);
     const int M = a.M;
 
-    if constexpr (SH_LDS) {
-        // coalesced stage-in of the wave's SH rows (64 x 48 floats)
-        const float4* src = reinterpret_cast<const float4*>(a.shs + (size_t)g0 * kShRow);
-        const int n4 = nvalid * (kShRow / 4);
-#pragma unroll
-        for (int k = 0; k < kShRow / 4; k++) {
-            const int i4 = k * 64 + lane;
-            if (i4 < n4) {
-                const int d = i4 * 4, row = d / kShRow, col = d - row * kShRow;
-                *reinterpret_cast<float4*>(&s_sh[row * kShStride + col]) = src[i4];
-            }
-        }
+    const ShAddr sh_src{a.shs, a.dc, M};
+    const ShGradAddr sh_dst{a.dL_dsh, a.dL_ddc, M};
+    if constexpr (SH_MODE != kShGlobal) {
+        // coalesced stage-in of the wave's SH rows (64 x 48 floats, either layout)
+        sh_stage_in<64, 64, SH_MODE == kShLdsSplit>(sh_src, g0, nvalid, s_sh, kShStride, lane);
         __syncthreads();
     }
 
@@ -258,12 +255,13 @@ __global__ void __launch_bounds__(64) gauss_bwd_kernel(GaussBwdArgs a) {
         for (int k = 0; k < 6; k++) a.dL_dcov3D[6 * idx + k] = 0.f;
         if (a.dL_dscale) store3(a.dL_dscale, idx, 0.f, 0.f, 0.f);
         if (a.dL_drot) reinterpret_cast<float4*>(a.dL_drot)[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (a.dL_dsh) {
-            if constexpr (SH_LDS) {
-                for (int k = 0; k < kShRow; k += 4)
+        if (a.dL_dsh || a.dL_ddc) {
+            if constexpr (SH_MODE != kShGlobal) {
+                for (int k = 0; k < kShRowF; k += 4)
                     *reinterpret_cast<float4*>(&s_sh[lane * kShStride + k]) = make_float4(0.f, 0.f, 0.f, 0.f);
             } else {
-                for (int k = 0; k < 3 * M; k++) a.dL_dsh[(size_t)idx * 3 * M + k] = 0.f;
+                const ShGlobal acc{sh_src, sh_dst, idx};
+                for (int k = 0; k < M; k++) acc.store(k, make_float3(0.f, 0.f, 0.f));
             }
         }
     }
@@ -410,18 +408,17 @@ __global__ void __launch_bounds__(64) gauss_bwd_kernel(GaussBwdArgs a) {
         dmean.z += (Pm[8] * m_w - Pm[11] * mul1) * m2x + (Pm[9] * m_w - Pm[11] * mul2) * m2y;
 
         // ---- SH colour backward (CR/backward.cu:12-146)
-        if (a.shs) {
+        if (a.shs || a.dc) {
             const float3 v = make_float3(mean.x - a.campos[0], mean.y - a.campos[1], mean.z - a.campos[2]);
             const float len = sqrtf(v.x * v.x + v.y * v.y + v.z * v.z);
             const uint8_t cm = a.geom.clamped[idx];
             const float3 g = make_float3((cm & 1) ? 0.f : dcol.x, (cm & 2) ? 0.f : dcol.y, (cm & 4) ? 0.f : dcol.z);
             float ddx, ddy, ddz;
-            if constexpr (SH_LDS) {
+            if constexpr (SH_MODE != kShGlobal) {
                 sh_backward(ShLds{&s_sh[lane * kShStride]}, a.D, M, v.x / len, v.y / len, v.z / len, g, ddx, ddy,
                             ddz);
             } else {
-                sh_backward(ShGlobal{a.shs + (size_t)idx * M * 3, a.dL_dsh + (size_t)idx * M * 3}, a.D, M, v.x / len,
-                            v.y / len, v.z / len, g, ddx, ddy, ddz);
+                sh_backward(ShGlobal{sh_src, sh_dst, idx}, a.D, M, v.x / len, v.y / len, v.z / len, g, ddx, ddy, ddz);
             }
             // dnormvdv (CR/auxiliary.h:129-139)
             const float sum2 = v.x * v.x + v.y * v.y + v.z * v.z;
@@ -429,8 +426,9 @@ __global__ void __launch_bounds__(64) gauss_bwd_kernel(GaussBwdArgs a) {
             dmean.x += ((sum2 - v.x * v.x) * ddx - v.y * v.x * ddy - v.z * v.x * ddz) * invsum32;
             dmean.y += (-v.x * v.y * ddx + (sum2 - v.y * v.y) * ddy - v.z * v.y * ddz) * invsum32;
             dmean.z += (-v.x * v.z * ddx - v.y * v.z * ddy + (sum2 - v.z * v.z) * ddz) * invsum32;
-        } else if (a.dL_dsh) {
-            for (int k = 0; k < 3 * M; k++) a.dL_dsh[(size_t)idx * 3 * M + k] = 0.f;
+        } else if (a.dL_dsh || a.dL_ddc) {
+            const ShGlobal acc{sh_src, sh_dst, idx};
+            for (int k = 0; k < M; k++) acc.store(k, make_float3(0.f, 0.f, 0.f));
         }
         store3(a.dL_dmean3D, idx, dmean.x, dmean.y, dmean.z);
 
@@ -473,31 +471,25 @@ __global__ void __launch_bounds__(64) gauss_bwd_kernel(GaussBwdArgs a) {
         }
     }
 
-    if constexpr (SH_LDS) {
+    if constexpr (SH_MODE != kShGlobal) {
         // coalesced write-back of the wave's dL/dSH rows
         __syncthreads();
-        float4* dst = reinterpret_cast<float4*>(a.dL_dsh + (size_t)g0 * kShRow);
-        const int n4 = nvalid * (kShRow / 4);
-#pragma unroll
-        for (int k = 0; k < kShRow / 4; k++) {
-            const int i4 = k * 64 + lane;
-            if (i4 < n4) {
-                const int d = i4 * 4, row = d / kShRow, col = d - row * kShRow;
-                dst[i4] = *reinterpret_cast<const float4*>(&s_sh[row * kShStride + col]);
-            }
-        }
+        sh_stage_out<64, 64, SH_MODE == kShLdsSplit>(sh_dst, g0, nvalid, s_sh, kShStride, lane);
     }
 }
 
 hipError_t launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t stream) {
     if (a.P == 0) return hipSuccess;
     const dim3 grid((a.P + 63) / 64), block(64);
-    const bool lds = a.shs && a.dL_dsh && a.M == 16 && ((reinterpret_cast<uintptr_t>(a.shs) & 15) == 0) &&
+    const bool lds = a.shs && a.dL_dsh && a.M == 16 && (!a.dc || a.dL_ddc) &&
+                     ((reinterpret_cast<uintptr_t>(a.shs) & 15) == 0) &&
                      ((reinterpret_cast<uintptr_t>(a.dL_dsh) & 15) == 0);
-    if (lds)
-        hipLaunchKernelGGL(gauss_bwd_kernel<true>, grid, block, 0, stream, a);
+    if (lds && a.dc)
+        hipLaunchKernelGGL(gauss_bwd_kernel<kShLdsSplit>, grid, block, 0, stream, a);
+    else if (lds)
+        hipLaunchKernelGGL(gauss_bwd_kernel<kShLdsCombined>, grid, block, 0, stream, a);
     else
-        hipLaunchKernelGGL(gauss_bwd_kernel<false>, grid, block, 0, stream, a);
+        hipLaunchKernelGGL(gauss_bwd_kernel<kShGlobal>, grid, block, 0, stream, a);
     return hipGetLastError();
 }
 

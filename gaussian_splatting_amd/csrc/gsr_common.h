@@ -119,6 +119,35 @@ struct GradRecs {
 };
 
 // ---------------------------------------------------------------------------
+// SH coefficient addressing.  Two layouts reach the kernels:
+//  * combined: shs [P, M, 3], coefficient k of Gaussian i at shs + (i M + k) 3
+//    (CR/forward.cu:29, the vendored rasterizer);
+//  * split (dc != nullptr): dc [P, 1, 3] holds coefficient 0 and shs [P, M-1, 3] the
+//    rest -- the 3DGS-accel rasterizer's (dc, shs) arguments, i.e. GaussianModel's
+//    _features_dc / _features_rest passed without a torch.cat
+//    (gaussian_renderer/__init__.py:106-125).
+// M is always the total coefficient count seen by the SH evaluation.
+// ---------------------------------------------------------------------------
+struct ShAddr {
+    const float* shs;
+    const float* dc;
+    int M;
+    __device__ __forceinline__ const float* coef(int idx, int k) const {
+        if (!dc) return shs + ((size_t)idx * M + k) * 3;
+        return k == 0 ? dc + (size_t)idx * 3 : shs + ((size_t)idx * (M - 1) + (k - 1)) * 3;
+    }
+};
+struct ShGradAddr {
+    float* dsh;
+    float* ddc;
+    int M;
+    __device__ __forceinline__ float* coef(int idx, int k) const {
+        if (!ddc) return dsh + ((size_t)idx * M + k) * 3;
+        return k == 0 ? ddc + (size_t)idx * 3 : dsh + ((size_t)idx * (M - 1) + (k - 1)) * 3;
+    }
+};
+
+// ---------------------------------------------------------------------------
 // Device math helpers (CR/auxiliary.h:43-117)
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ float3 xform_point_4x3(const float3& p, const float* m) {

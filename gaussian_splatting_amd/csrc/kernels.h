@@ -12,7 +12,8 @@ struct PreprocessArgs {
     float scale_modifier;
     const float* rotations;
     const float* opacities;
-    const float* shs;
+    const float* shs;  // combined [P,M,3], or the rest [P,M-1,3] when dc is set (ShAddr)
+    const float* dc;   // [P,1,3] or null
     const float* cov3D_precomp;
     const float* colors_precomp;
     const float* viewmatrix;
@@ -55,7 +56,8 @@ struct RenderBwdArgs {
 struct GaussBwdArgs {
     int P, D, M, W, H;
     const float* means3D;
-    const float* shs;
+    const float* shs;  // as PreprocessArgs::shs
+    const float* dc;   // [P,1,3] or null
     const float* opacities;
     const float* scales;
     const float* rotations;
@@ -77,10 +79,128 @@ struct GaussBwdArgs {
     float* dL_dinvdepth;  // [P] or null
     float* dL_dmean3D;    // [P,3]
     float* dL_dcov3D;     // [P,6]
-    float* dL_dsh;        // [P,M,3] or null (M == 0)
+    float* dL_dsh;        // [P,M,3] or null (M == 0); the rest [P,M-1,3] when dL_ddc is set
+    float* dL_ddc;        // [P,1,3] when the forward took dc, else null
     float* dL_dscale;     // [P,3] or null
     float* dL_drot;       // [P,4] or null
 };
+
+// ---- SH rows through LDS (preprocess and gauss_bwd, M = 16) -----------------------
+// LDS row r holds the 48 floats [coefficient 0..15][3] of Gaussian r0 + r at
+// lds[r * stride].  Combined layout: the block is one contiguous range of 48-float rows,
+// moved with 16-byte loads and 16-byte LDS stores.  Split layout (dc given): the rest
+// block is one contiguous range of 45-float rows, moved 16 bytes at a time and scattered
+// to LDS as scalars behind each row's 3 dc floats (the dc block is 3 floats a row).
+// Requires 16-byte aligned shs / dsh and r0 a multiple of 16.
+constexpr int kShRowF = 48;     // floats per staged SH row (M = 16)
+constexpr int kShRestF = 45;    // floats per rest row in the split layout
+
+template <int ROWS, int THREADS, bool SPLIT>
+__device__ __forceinline__ void sh_stage_in(const ShAddr& sa, int r0, int rows, float* lds, int stride, int tid) {
+    if constexpr (!SPLIT) {
+        const float4* src = reinterpret_cast<const float4*>(sa.shs + (size_t)r0 * kShRowF);
+        const int n4 = rows * (kShRowF / 4);
+#pragma unroll
+        for (int k = 0; k < ROWS * kShRowF / 4 / THREADS; k++) {
+            const int i4 = k * THREADS + tid;
+            if (i4 < n4) {
+                const int d = i4 * 4, row = d / kShRowF, col = d - row * kShRowF;
+                *reinterpret_cast<float4*>(&lds[row * stride + col]) = src[i4];
+            }
+        }
+        return;
+    } else {
+    const float* rest = sa.shs + (size_t)r0 * kShRestF;
+    const int nf = rows * kShRestF, n4 = nf >> 2;
+#pragma unroll
+    for (int k = 0; k < (ROWS * kShRestF / 4 + THREADS - 1) / THREADS; k++) {
+        const int i4 = k * THREADS + tid;
+        if (i4 < n4) {
+            const float4 v = reinterpret_cast<const float4*>(rest)[i4];
+            const float f[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const int d = i4 * 4 + c, row = d / kShRestF;
+                lds[row * stride + 3 + d - row * kShRestF] = f[c];
+            }
+        }
+    }
+    if (tid < (nf & 3)) {
+        const int d = n4 * 4 + tid, row = d / kShRestF;
+        lds[row * stride + 3 + d - row * kShRestF] = rest[d];
+    }
+    const float* dc = sa.dc + (size_t)r0 * 3;
+    for (int i = tid; i < rows * 3; i += THREADS) lds[(i / 3) * stride + i % 3] = dc[i];
+    }
+}
+
+template <int ROWS, int THREADS, bool SPLIT>
+__device__ __forceinline__ void sh_stage_out(const ShGradAddr& ga, int r0, int rows, const float* lds, int stride,
+                                             int tid) {
+    if constexpr (!SPLIT) {
+        float4* dst = reinterpret_cast<float4*>(ga.dsh + (size_t)r0 * kShRowF);
+        const int n4 = rows * (kShRowF / 4);
+#pragma unroll
+        for (int k = 0; k < ROWS * kShRowF / 4 / THREADS; k++) {
+            const int i4 = k * THREADS + tid;
+            if (i4 < n4) {
+                const int d = i4 * 4, row = d / kShRowF, col = d - row * kShRowF;
+                dst[i4] = *reinterpret_cast<const float4*>(&lds[row * stride + col]);
+            }
+        }
+        return;
+    } else {
+    float* rest = ga.dsh + (size_t)r0 * kShRestF;
+    const int nf = rows * kShRestF, n4 = nf >> 2;
+#pragma unroll
+    for (int k = 0; k < (ROWS * kShRestF / 4 + THREADS - 1) / THREADS; k++) {
+        const int i4 = k * THREADS + tid;
+        if (i4 < n4) {
+            float f[4];
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const int d = i4 * 4 + c, row = d / kShRestF;
+                f[c] = lds[row * stride + 3 + d - row * kShRestF];
+            }
+            reinterpret_cast<float4*>(rest)[i4] = make_float4(f[0], f[1], f[2], f[3]);
+        }
+    }
+    if (tid < (nf & 3)) {
+        const int d = n4 * 4 + tid, row = d / kShRestF;
+        rest[d] = lds[row * stride + 3 + d - row * kShRestF];
+    }
+    float* dc = ga.ddc + (size_t)r0 * 3;
+    for (int i = tid; i < rows * 3; i += THREADS) dc[i] = lds[(i / 3) * stride + i % 3];
+    }
+}
+// SH path of preprocess / gauss_bwd: per-lane global loads, or LDS staging of either layout
+enum ShMode { kShGlobal = 0, kShLdsCombined = 1, kShLdsSplit = 2 };
+
+// ---- sparse Adam (adam.hip) --------------------------------------------------------
+constexpr int kAdamMaxGroups = 8;  // GSR_ADAM_MAX_GROUPS
+struct AdamGroupDev {
+    float* p;
+    const float* g;
+    float* m;
+    float* v;
+    uint32_t n;                // N * M
+    uint32_t M;
+    unsigned long long magic;  // i / M == (i * magic) >> shift for i < 2^31
+    uint32_t shift;
+    float lr, eps;
+    uint32_t first_block;      // first workgroup of this group
+    int vec;                   // all four arrays 16-byte aligned
+};
+struct AdamArgs {
+    AdamGroupDev grp[kAdamMaxGroups];
+    int n_groups;
+    const uint8_t* vis;
+    float b1, b2;
+};
+constexpr int kAdamThreads = 256;
+constexpr int kAdamUnroll = 2;  // float4s per thread
+constexpr uint32_t kAdamBlockElems = kAdamThreads * kAdamUnroll * 4;
+hipError_t launch_adam(const AdamArgs& a, uint32_t blocks, hipStream_t stream);
 
 // preprocess.hip
 hipError_t launch_preprocess(const PreprocessArgs& a, hipStream_t stream);

@@ -88,33 +88,24 @@ __device__ __forceinline__ float3 sh_to_rgb(int deg, const float3* sh, float x, 
     return res;
 }
 
-// Load the first K = (deg+1)^2 coefficients (K <= 16) of Gaussian idx.
-template <bool VEC4>
-__device__ __forceinline__ void load_sh(const float* __restrict__ shs, int idx, int M, int K, float3 sh[16]) {
-    const float* base = shs + (size_t)idx * M * 3;
-    if constexpr (VEC4) {
-        float f[48];
-        const float4* b4 = reinterpret_cast<const float4*>(base);
-        const int n4 = (K * 3 + 3) >> 2;
+// Load the first K = (deg+1)^2 coefficients (K <= 16) of Gaussian idx, either layout.
+__device__ __forceinline__ void load_sh(const ShAddr& sa, int idx, int K, float3 sh[16]) {
 #pragma unroll
-        for (int i = 0; i < 12; i++) {
-            if (i < n4) {
-                float4 v = b4[i];
-                f[4 * i] = v.x; f[4 * i + 1] = v.y; f[4 * i + 2] = v.z; f[4 * i + 3] = v.w;
-            } else {
-                f[4 * i] = f[4 * i + 1] = f[4 * i + 2] = f[4 * i + 3] = 0.f;
-            }
+    for (int k = 0; k < 16; k++) {
+        if (k < K) {
+            const float* c = sa.coef(idx, k);
+            sh[k] = make_float3(c[0], c[1], c[2]);
+        } else {
+            sh[k] = make_float3(0.f, 0.f, 0.f);
         }
-#pragma unroll
-        for (int k = 0; k < 16; k++) sh[k] = make_float3(f[3 * k], f[3 * k + 1], f[3 * k + 2]);
-    } else {
-#pragma unroll
-        for (int k = 0; k < 16; k++)
-            sh[k] = k < K ? make_float3(base[3 * k], base[3 * k + 1], base[3 * k + 2]) : make_float3(0.f, 0.f, 0.f);
     }
 }
 
-
+// Stage rows [r0, r0 + rows) of the SH coefficients into LDS rows of kShRowStride floats
+// laid out [coefficient 0..15][3].  Combined layout: each row is 48 contiguous floats and
+// the block is one contiguous range (16-byte loads, 16-byte LDS stores).  Split layout: the
+// rest block (45 floats a row) is one contiguous range too, loaded 16 bytes at a time and
+// scattered to LDS as scalars behind the 3 dc floats of each row.
 // One wave per 64 consecutive Gaussians.  The geometry is per lane; two data paths are
 // cooperative so that every global access of the wave is a contiguous block:
 //  * SH (192 B per Gaussian at M = 16, most of the kernel's bytes): the wave's rows are
@@ -125,12 +116,11 @@ __device__ __forceinline__ void load_sh(const float* __restrict__ shs, int idx, 
 // key and an all-zero record (never read).
 constexpr int kPreThreads = 64;
 constexpr int kShHalfRows = 32;
-constexpr int kShRowF = 48;        // floats per SH row at M = 16
 constexpr int kShRowStride = 52;   // padded LDS row stride (16-byte aligned, conflict-free b128)
 
-template <bool SH_LDS>
+template <int SH_MODE>
 __global__ void __launch_bounds__(kPreThreads) preprocess_kernel(PreprocessArgs a) {
-    __shared__ __attribute__((aligned(16))) float s_buf[SH_LDS ? kShHalfRows * kShRowStride : 64 * 16];
+    __shared__ __attribute__((aligned(16))) float s_buf[SH_MODE != kShGlobal ? kShHalfRows * kShRowStride : 64 * 16];
     static_assert(kShHalfRows * kShRowStride >= 64 * 16, "the record block reuses the SH buffer");
     const int lane = threadIdx.x;
     const int g0 = blockIdx.x * kPreThreads;
@@ -204,22 +194,13 @@ __global__ void __launch_bounds__(kPreThreads) preprocess_kernel(PreprocessArgs 
     }
     if (a.colors_precomp) {
         if (ok) rgb = make_float3(a.colors_precomp[3 * idx], a.colors_precomp[3 * idx + 1], a.colors_precomp[3 * idx + 2]);
-    } else if constexpr (SH_LDS) {
-        const float4* src = reinterpret_cast<const float4*>(a.shs + (size_t)g0 * kShRowF);
+    } else if constexpr (SH_MODE != kShGlobal) {
+        const ShAddr sa{a.shs, a.dc, a.M};
 #pragma unroll
         for (int half = 0; half < 2; half++) {
             const int rows = min(kShHalfRows, nvalid - half * kShHalfRows);
             if (rows > 0) {  // wave-uniform
-                const int n4 = rows * (kShRowF / 4);
-                const float4* hsrc = src + half * kShHalfRows * (kShRowF / 4);
-#pragma unroll
-                for (int k = 0; k < kShHalfRows * kShRowF / 4 / kPreThreads; k++) {
-                    const int i4 = k * kPreThreads + lane;
-                    if (i4 < n4) {
-                        const int d = i4 * 4, row = d / kShRowF, col = d - row * kShRowF;
-                        *reinterpret_cast<float4*>(&s_buf[row * kShRowStride + col]) = hsrc[i4];
-                    }
-                }
+                sh_stage_in<kShHalfRows, kPreThreads, SH_MODE == kShLdsSplit>(sa, g0 + half * kShHalfRows, rows, s_buf, kShRowStride, lane);
                 __syncthreads();
                 if ((lane >> 5) == half && ok) {
                     const float* row = &s_buf[(lane & 31) * kShRowStride];
@@ -234,7 +215,7 @@ __global__ void __launch_bounds__(kPreThreads) preprocess_kernel(PreprocessArgs 
     } else if (ok) {
         float3 sh[16];
         const int K = (a.D + 1) * (a.D + 1);
-        load_sh<false>(a.shs, idx, a.M, K, sh);
+        load_sh(ShAddr{a.shs, a.dc, a.M}, idx, K, sh);
         rgb = sh_to_rgb(a.D, sh, dir.x, dir.y, dir.z);
     }
     if (ok && !a.colors_precomp) {
@@ -293,12 +274,15 @@ __global__ void __launch_bounds__(kPreThreads) preprocess_kernel(PreprocessArgs 
 hipError_t launch_preprocess(const PreprocessArgs& a, hipStream_t stream) {
     if (a.P == 0) return hipSuccess;
     const dim3 grid((a.P + kPreThreads - 1) / kPreThreads), block(kPreThreads);
+    // LDS staging for the full SH3 row, either layout (combined [P,16,3] or dc + rest [P,15,3])
     const bool lds = a.shs && !a.colors_precomp && a.M == 16 && a.D == 3 &&
                      ((reinterpret_cast<uintptr_t>(a.shs) & 15) == 0);
-    if (lds)
-        hipLaunchKernelGGL(preprocess_kernel<true>, grid, block, 0, stream, a);
+    if (lds && a.dc)
+        hipLaunchKernelGGL(preprocess_kernel<kShLdsSplit>, grid, block, 0, stream, a);
+    else if (lds)
+        hipLaunchKernelGGL(preprocess_kernel<kShLdsCombined>, grid, block, 0, stream, a);
     else
-        hipLaunchKernelGGL(preprocess_kernel<false>, grid, block, 0, stream, a);
+        hipLaunchKernelGGL(preprocess_kernel<kShGlobal>, grid, block, 0, stream, a);
     return hipGetLastError();
 }
 

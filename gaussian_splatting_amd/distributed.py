@@ -20,27 +20,48 @@ import torch.distributed as dist
 # block order inside the arena; shapes are per-Gaussian
 _BLOCKS = (("dL_dmeans3D", (3,)), ("dL_dsh", None), ("dL_dopacity", (1,)), ("dL_dscales", (3,)),
            ("dL_drotations", (4,)))
+# separate-SH arena: exactly GaussianModel's parameter groups, in its order (gaussian_model.py:235-242)
+_BLOCKS_SEPARATE = (("dL_dmeans3D", (3,)), ("dL_ddc", (1, 3)), ("dL_dsh", None), ("dL_dopacity", (1,)),
+                    ("dL_dscales", (3,)), ("dL_drotations", (4,)))
+_GROUP_OF = {"dL_dmeans3D": "xyz", "dL_ddc": "f_dc", "dL_dopacity": "opacity", "dL_dscales": "scaling",
+             "dL_drotations": "rotation"}
 
 
 class GradArena:
-    """Flat gradient buffer with per-parameter views, reduced by a single collective."""
+    """Flat gradient buffer with per-parameter views, reduced by a single collective.
 
-    def __init__(self, P: int, M: int, device, dtype=torch.float32):
-        self.P, self.M = P, M
-        per = {"dL_dmeans3D": 3, "dL_dsh": 3 * M, "dL_dopacity": 1, "dL_dscales": 3, "dL_drotations": 4}
-        self.floats_per_gaussian = sum(per.values())
+    ``separate_sh=False``: the vendored rasterizer's outputs (one ``dL_dsh`` [P,M,3] block).
+    ``separate_sh=True``: the 3DGS-accel outputs -- ``dL_ddc`` [P,1,3] and ``dL_dsh`` [P,M-1,3] as two
+    contiguous blocks, so every block is exactly one GaussianModel parameter's gradient and can be
+    handed to the optimizer without a copy (``param_grads()``)."""
+
+    def __init__(self, P: int, M: int, device, dtype=torch.float32, separate_sh: bool = False):
+        self.P, self.M, self.separate_sh = P, M, separate_sh
+        rest = M - 1 if separate_sh else M
+        per = {"dL_dmeans3D": 3, "dL_ddc": 3, "dL_dsh": 3 * rest, "dL_dopacity": 1, "dL_dscales": 3,
+               "dL_drotations": 4}
+        blocks = _BLOCKS_SEPARATE if separate_sh else _BLOCKS
+        self.floats_per_gaussian = sum(per[name] for name, _ in blocks)
         self.flat = torch.empty(P * self.floats_per_gaussian, device=device, dtype=dtype)
         self._views: Dict[str, torch.Tensor] = {}
         off = 0
-        for name, shape in _BLOCKS:
+        for name, shape in blocks:
             n = P * per[name]
-            shp = (P, M, 3) if name == "dL_dsh" else (P,) + shape
+            shp = (P, rest, 3) if name == "dL_dsh" else (P,) + shape
             self._views[name] = self.flat[off:off + n].view(shp)
             off += n
 
     def views(self) -> Dict[str, torch.Tensor]:
         """Output tensors for ``_C.rasterize_gaussians_backward(..., out=...)``."""
         return self._views
+
+    def param_grads(self) -> Dict[str, torch.Tensor]:
+        """Gradient of each GaussianModel parameter group, by group name (separate-SH arena only)."""
+        if not self.separate_sh:
+            raise RuntimeError("param_grads() needs separate_sh=True (f_dc / f_rest as their own blocks)")
+        out = {_GROUP_OF[k]: v for k, v in self._views.items() if k in _GROUP_OF}
+        out["f_rest"] = self._views["dL_dsh"]
+        return out
 
     def all_reduce(self, op=None, group: Optional[dist.ProcessGroup] = None, average: bool = False) -> None:
         """Sum (or average) the arena over all ranks in one collective."""
@@ -52,6 +73,8 @@ class GradArena:
 
     def split_features(self):
         """(f_dc, f_rest) gradient views, matching GaussianModel._features_dc / _features_rest."""
+        if self.separate_sh:
+            return self._views["dL_ddc"], self._views["dL_dsh"]
         sh = self._views["dL_dsh"]
         return sh[:, :1, :], sh[:, 1:, :]
 

@@ -39,51 +39,70 @@ class GaussianRasterizationSettings(NamedTuple):
     antialiasing: bool
 
 
-def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
-                        raster_settings):
-    return _RasterizeGaussians.apply(means3D, means2D, sh, colors_precomp, opacities, scales, rotations,
-                                     cov3Ds_precomp, raster_settings)
+def rasterize_gaussians(*args):
+    """``rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
+    raster_settings)`` (vendored, :24-46), or the 3DGS-accel form with ``dc`` before ``sh``."""
+    if len(args) not in (9, 10):
+        raise TypeError(f"rasterize_gaussians(): expected 9 or 10 arguments, got {len(args)}")
+    return _RasterizeGaussians.apply(*args)
 
 
 class _RasterizeGaussians(torch.autograd.Function):
     """Autograd node: forward = _C.rasterize_gaussians, backward = _C.rasterize_gaussians_backward.
 
-    ``means2D`` only carries the screen-space gradient (the reference's trick for
-    densification statistics); its value is never read.
+    Inputs ``(means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp, raster_settings)``
+    as in the vendored rasterizer (:48-148), or ``(means3D, means2D, dc, sh, ...)`` as in the 3DGS-accel build
+    (separate_sh=True callers, gaussian_renderer/__init__.py:106-125): ``dc`` is ``_features_dc`` [P,1,3] and
+    ``sh`` then ``_features_rest`` [P,M,3]; the two get their own gradients, with no concatenation.
+    ``means2D`` only carries the screen-space gradient (the reference's trick for densification statistics);
+    its value is never read.
     """
 
     @staticmethod
-    def forward(ctx, means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
-                raster_settings):
-        s = raster_settings
-        num_rendered, color, radii, geom, binning, img, invdepths = _C.rasterize_gaussians(
-            s.bg, means3D, colors_precomp, opacities, scales, rotations, s.scale_modifier, cov3Ds_precomp,
-            s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, s.image_height, s.image_width, sh, s.sh_degree,
-            s.campos, s.prefiltered, s.antialiasing, s.debug)
+    def forward(ctx, *args):
+        if len(args) == 10:
+            means3D, means2D, dc, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp, s = args
+        else:
+            means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp, s = args
+            dc = None
+        head = (s.bg, means3D, colors_precomp, opacities, scales, rotations, s.scale_modifier, cov3Ds_precomp,
+                s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, s.image_height, s.image_width)
+        tail = (s.sh_degree, s.campos, s.prefiltered, s.antialiasing, s.debug)
+        sh_args = (sh,) if dc is None else (dc, sh)
+        num_rendered, color, radii, geom, binning, img, invdepths = _C.rasterize_gaussians(*head, *sh_args, *tail)
         ctx.raster_settings = s
         ctx.num_rendered = num_rendered
-        ctx.save_for_backward(colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, opacities, geom,
-                              binning, img)
+        ctx.separate_sh = dc is not None
+        saved = (colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, opacities, geom, binning, img)
+        ctx.save_for_backward(*saved, *(() if dc is None else (dc,)))
         ctx.mark_non_differentiable(radii)
         return color, radii, invdepths
 
     @staticmethod
     def backward(ctx, grad_out_color, _grad_radii, grad_out_depth):
         s = ctx.raster_settings
+        saved = ctx.saved_tensors
         (colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, opacities, geom, binning,
-         img) = ctx.saved_tensors
-        (grad_means2D, grad_colors_precomp, grad_opacities, grad_means3D, grad_cov3Ds_precomp, grad_sh, grad_scales,
-         grad_rotations) = _C.rasterize_gaussians_backward(
-            s.bg, means3D, radii, colors_precomp, opacities, scales, rotations, s.scale_modifier, cov3Ds_precomp,
-            s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, grad_out_color, grad_out_depth, sh, s.sh_degree,
-            s.campos, geom, ctx.num_rendered, binning, img, s.antialiasing, s.debug)
+         img) = saved[:11]
+        dc = saved[11] if ctx.separate_sh else None
+        head = (s.bg, means3D, radii, colors_precomp, opacities, scales, rotations, s.scale_modifier, cov3Ds_precomp,
+                s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, grad_out_color, grad_out_depth)
+        tail = (s.sh_degree, s.campos, geom, ctx.num_rendered, binning, img, s.antialiasing, s.debug)
 
         def fit(g, like):  # inputs given as empty tensors get no gradient
             return None if like is None or like.numel() == 0 else g
 
-        return (grad_means3D, grad_means2D, fit(grad_sh, sh), fit(grad_colors_precomp, colors_precomp),
-                grad_opacities, fit(grad_scales, scales), fit(grad_rotations, rotations),
-                fit(grad_cov3Ds_precomp, cov3Ds_precomp), None)
+        if dc is None:
+            (grad_means2D, grad_colors_precomp, grad_opacities, grad_means3D, grad_cov3Ds_precomp, grad_sh,
+             grad_scales, grad_rotations) = _C.rasterize_gaussians_backward(*head, sh, *tail)
+            return (grad_means3D, grad_means2D, fit(grad_sh, sh), fit(grad_colors_precomp, colors_precomp),
+                    grad_opacities, fit(grad_scales, scales), fit(grad_rotations, rotations),
+                    fit(grad_cov3Ds_precomp, cov3Ds_precomp), None)
+        (grad_means2D, grad_colors_precomp, grad_opacities, grad_means3D, grad_cov3Ds_precomp, grad_dc, grad_sh,
+         grad_scales, grad_rotations) = _C.rasterize_gaussians_backward(*head, dc, sh, *tail)
+        return (grad_means3D, grad_means2D, fit(grad_dc, dc), fit(grad_sh, sh),
+                fit(grad_colors_precomp, colors_precomp), grad_opacities, fit(grad_scales, scales),
+                fit(grad_rotations, rotations), fit(grad_cov3Ds_precomp, cov3Ds_precomp), None)
 
 
 class GaussianRasterizer(nn.Module):
@@ -99,7 +118,10 @@ class GaussianRasterizer(nn.Module):
             return _C.mark_visible(positions, s.viewmatrix, s.projmatrix)
 
     def forward(self, means3D, means2D, opacities, shs=None, colors_precomp=None, scales=None, rotations=None,
-                cov3D_precomp=None):
+                cov3D_precomp=None, dc=None):
+        """Same checks as the reference (:242-261).  ``dc=`` (keyword) selects the 3DGS-accel separate-SH
+        input: ``dc`` = ``_features_dc`` [P,1,3] and ``shs`` = ``_features_rest`` [P,M,3]
+        (gaussian_renderer/__init__.py:115-125)."""
         s = self.raster_settings
         if (shs is None and colors_precomp is None) or (shs is not None and colors_precomp is not None):
             raise Exception("Please provide exactly one of either SHs or precomputed colors!")
@@ -112,5 +134,9 @@ class GaussianRasterizer(nn.Module):
         scales = empty if scales is None else scales
         rotations = empty if rotations is None else rotations
         cov3D_precomp = empty if cov3D_precomp is None else cov3D_precomp
-        return rasterize_gaussians(means3D, means2D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp,
-                                   s)
+        if dc is None:
+            return rasterize_gaussians(means3D, means2D, shs, colors_precomp, opacities, scales, rotations,
+                                       cov3D_precomp, s)
+        dc = empty if colors_precomp.numel() != 0 else dc
+        return rasterize_gaussians(means3D, means2D, dc, shs, colors_precomp, opacities, scales, rotations,
+                                   cov3D_precomp, s)

@@ -121,6 +121,38 @@ int gsr_rasterize_backward_ex(int P, int D, int M, int R, const float* backgroun
                               int debug, gsr_alloc_fn scratch_alloc, void* scratch_ctx, void* stream,
                               int binning_capacity, size_t binning_bytes);
 
+/* Separate-DC variants: the 3DGS-accel rasterizer's interface (the build that ships
+ * SparseGaussianAdam), which the reference's callers select with separate_sh=True
+ * (train.py:41-45,105,144; gaussian_renderer/__init__.py:106-125 passes dc= and
+ * shs= = GaussianModel._features_dc / _features_rest).  Its _C.rasterize_gaussians /
+ * _C.rasterize_gaussians_backward take `dc` right before `sh`, and the backward returns
+ * dL_ddc before dL_dsh.  Here: dc is [P,1,3] (coefficient 0), shs is [P,M,3] with M
+ * the number of REST coefficients (15 at SH degree 3; shs may be NULL when M == 0), and
+ * the colour is the same polynomial as with one combined [P,M+1,3] array.  dL_ddc
+ * ([P,1,3]) and dL_dsh ([P,M,3]) are written for every element.  Everything else is
+ * gsr_rasterize_forward_ex / gsr_rasterize_backward_ex. */
+int gsr_rasterize_forward_dc(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_alloc, void* binning_ctx,
+                             gsr_alloc_fn image_alloc, void* image_ctx, int P, int D, int M, const float* background,
+                             int width, int height, const float* means3D, const float* dc, const float* shs,
+                             const float* colors_precomp, const float* opacities, const float* scales,
+                             float scale_modifier, const float* rotations, const float* cov3D_precomp,
+                             const float* viewmatrix, const float* projmatrix, const float* cam_pos, float tan_fovx,
+                             float tan_fovy, int prefiltered, float* out_color, float* out_invdepth, int antialiasing,
+                             int* radii, int debug, void* stream, int* num_rendered, int capacity_hint,
+                             int* binning_capacity);
+
+int gsr_rasterize_backward_dc(int P, int D, int M, int R, const float* background, int width, int height,
+                              const float* means3D, const float* dc, const float* shs, const float* colors_precomp,
+                              const float* opacities, const float* scales, float scale_modifier,
+                              const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
+                              const float* projmatrix, const float* campos, float tan_fovx, float tan_fovy,
+                              const int* radii, void* geom_buffer, void* binning_buffer, void* image_buffer,
+                              const float* dL_dpix, const float* dL_dinvdepths, float* dL_dmean2D, float* dL_dconic,
+                              float* dL_dopacity, float* dL_dcolor, float* dL_dinvdepth, float* dL_dmean3D,
+                              float* dL_dcov3D, float* dL_ddc, float* dL_dsh, float* dL_dscale, float* dL_drot,
+                              int antialiasing, int debug, gsr_alloc_fn scratch_alloc, void* scratch_ctx,
+                              void* stream, int binning_capacity, size_t binning_bytes);
+
 /* Frustum test, view-space z > 0.2 (CudaRasterizer::Rasterizer::markVisible).
  * `present` is P bytes (bool). */
 int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,

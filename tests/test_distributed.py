@@ -92,3 +92,27 @@ def test_view_sharded_allreduce_equals_sum_of_views():
         np.testing.assert_allclose(s[:P], norms, rtol=1e-5)
         np.testing.assert_array_equal(s[P:2 * P], counts)
         np.testing.assert_array_equal(s[2 * P:], maxr)
+
+
+def test_separate_sh_arena_is_gaussian_model_groups():
+    """The separate-SH arena holds GaussianModel's six parameter groups back to back, in training_setup's order
+    (gaussian_model.py:235-242), each one contiguous -- the 3DGS-accel backward writes them in place."""
+    from gaussian_splatting_amd.distributed import GradArena
+
+    P = 10
+    a = GradArena(P, 16, "cpu", separate_sh=True)
+    assert a.floats_per_gaussian == 59
+    g = a.param_grads()
+    assert list(g) == ["xyz", "f_dc", "f_rest", "opacity", "scaling", "rotation"] or \
+        sorted(g) == sorted(["xyz", "f_dc", "f_rest", "opacity", "scaling", "rotation"])
+    shapes = {"xyz": (P, 3), "f_dc": (P, 1, 3), "f_rest": (P, 15, 3), "opacity": (P, 1), "scaling": (P, 3),
+              "rotation": (P, 4)}
+    off = 0
+    for name in ("xyz", "f_dc", "f_rest", "opacity", "scaling", "rotation"):
+        t = g[name]
+        assert tuple(t.shape) == shapes[name] and t.is_contiguous()
+        assert t.data_ptr() == a.flat.data_ptr() + 4 * off, name
+        off += t.numel()
+    assert off == a.flat.numel()
+    dc, rest = a.split_features()
+    assert dc.data_ptr() == g["f_dc"].data_ptr() and rest.data_ptr() == g["f_rest"].data_ptr()

@@ -121,15 +121,18 @@ def test_rasterizer_argument_validation():
 
 
 def test_drop_in_package_surface():
-    """diff_gaussian_rasterization exports what gaussian_renderer imports, and NOT SparseGaussianAdam
-    (its absence keeps train.py on the dense path)."""
+    """diff_gaussian_rasterization exports what gaussian_renderer imports, plus the 3DGS-accel surface:
+    SparseGaussianAdam (train.py:41-45 then passes dc=/shs= separately, which GaussianRasterizer.forward accepts)."""
     import diff_gaussian_rasterization as d
 
     for name in ("GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians", "_RasterizeGaussians",
                  "_C"):
         assert hasattr(d, name), name
-    assert not hasattr(d, "SparseGaussianAdam")
-    for fn in ("rasterize_gaussians", "rasterize_gaussians_backward", "mark_visible"):
+    assert hasattr(d, "SparseGaussianAdam")
+    import inspect
+
+    assert "dc" in inspect.signature(d.GaussianRasterizer.forward).parameters
+    for fn in ("rasterize_gaussians", "rasterize_gaussians_backward", "mark_visible", "adamUpdate"):
         assert callable(getattr(d._C, fn))
 
 
