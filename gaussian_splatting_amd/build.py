@@ -72,7 +72,8 @@ def build(force: bool = False, jobs: int = 5, verbose: bool = True, variant: str
     # the offload bundler may leave per-object device images next to the output; nothing loads them
     import glob
 
-    for stray in glob.glob(os.path.join(os.path.dirname(LIB_OUT), "*.hipv4-amdgcn-*")):
+    for stray in glob.glob(os.path.join(os.path.dirname(LIB_OUT), "*.hipv4-amdgcn-*")) + \
+            glob.glob(os.path.join(os.path.dirname(LIB_OUT), "*.host-x86_64-*")):
         os.remove(stray)
     if verbose:
         print(f"[gsr] built {LIB_OUT}")

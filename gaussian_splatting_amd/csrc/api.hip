@@ -135,6 +135,8 @@ gsr::GeomState carve_geom(char* base, int P, uint32_t gx, uint32_t gy, size_t* t
     g.chunk_total = c.take<unsigned long long>(chunks);
     g.chunk_base = c.take<unsigned long long>(chunks);
     g.total = c.take<unsigned long long>(1);
+    g.unit_cnt = c.take<uint32_t>((size_t)kUnitLists * kUnitShards * kUnitCntStride);
+    g.unit_part = c.take<uint2>((size_t)(kUnitLists - 1) * kUnitShards * unit_part_cap(tiles));
     *total = align_up(c.off);
     return g;
 }
@@ -149,7 +151,8 @@ gsr::ImageState carve_image(char* base, int W, int H, uint32_t tiles, size_t* to
     im.accum = c.take<float>(4 * N);
     im.ranges = c.take<uint2>(tiles);
     im.cost = c.take<uint32_t>(tiles);
-    im.order = c.take<uint32_t>(tiles);
+    im.tile_limit = c.take<uint32_t>(tiles);
+    im.lim_key = c.take<unsigned long long>(tiles);
     *total = align_up(c.off);
     return im;
 }
@@ -160,16 +163,16 @@ gsr::BinningState carve_binning(char* base, size_t C, size_t* total) {
     BinningState b{};
     b.keys = c.take<unsigned long long>(C);
     b.gid_sorted = c.take<uint32_t>(C);
+    b.ckpt = c.take<float>((C / kCkStride + 1) * (size_t)kCkFloats);
+    b.unit_full = c.take<uint2>(kUnitShards * unit_full_cap(C));
     *total = align_up(c.off);
     return b;
 }
 
 // Backward scratch: per-tile limit keys, R per-instance records, P per-Gaussian sums.
-void carve_recs(char* base, size_t R, size_t P, size_t tiles, gsr::GradRecs* recs, gsr::GradRecs* sums,
-                unsigned long long** lim_key, size_t* total) {
+void carve_recs(char* base, size_t R, size_t P, gsr::GradRecs* recs, gsr::GradRecs* sums, size_t* total) {
     using namespace gsr;
     Carver c{base, 0};
-    *lim_key = c.take<unsigned long long>(tiles);
     recs->a = c.take<float4>(R);
     recs->b = c.take<float4>(R);
     recs->c = c.take<float2>(R);
@@ -177,6 +180,17 @@ void carve_recs(char* base, size_t R, size_t P, size_t tiles, gsr::GradRecs* rec
     sums->b = c.take<float4>(P);
     sums->c = c.take<float2>(P);
     *total = align_up(c.off);
+}
+
+// Backward segment length in checkpoints (GSR_BWD_SEG_CK, default 1 = kCkStride entries per wave;
+// a large value gives one wave per tile, the schedule before checkpoints, for A/B runs).
+int bwd_segment_checkpoints() {
+    static const int v = [] {
+        const char* e = getenv("GSR_BWD_SEG_CK");
+        const int x = e ? atoi(e) : 1;
+        return x >= 1 ? (x > (1 << 20) ? (1 << 20) : x) : 1;
+    }();
+    return v;
 }
 
 void* call_alloc(gsr_alloc_fn fn, void* ctx, size_t bytes) {
@@ -404,7 +418,7 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
     if (!ibase) return fail(GSR_ERR_ALLOC, "rasterize_forward: image buffer allocation failed");
     ImageState img = carve_image(ibase, width, height, tiles, &img_bytes);
 
-    HIP_TRY(hipMemsetAsync(geom.status, 0, 4 * sizeof(uint32_t), stream), "status init");
+    if (prefiltered) HIP_TRY(hipMemsetAsync(geom.status, 0, 4 * sizeof(uint32_t), stream), "status init");
     {
         StageScope sc(ST_PREPROCESS, stream);
         PreprocessArgs pa{};
@@ -417,6 +431,8 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
         pa.focal_y = focal_y; pa.gx = gx; pa.gy = gy; pa.prefiltered = prefiltered; pa.antialiasing = antialiasing;
         pa.footprint_cull = (width < 32000 && height < 32000) ? 1 : 0;
         pa.radii = radii; pa.geom = geom;
+        pa.zero = geom.tile_cnt;  // tile and cell counters (binning.hip K0/K1), contiguous
+        pa.zero_n = tiles + (uint32_t)bin_cell_count(gx, gy);
         HIP_TRY(launch_preprocess(pa, stream), "preprocess");
     }
     if (int rc = check_debug(debug, stream, "preprocess")) return rc;
@@ -476,7 +492,10 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
             RenderFwdArgs ra{};
             ra.W = width; ra.H = height; ra.gx = gx; ra.gy = gy; ra.ranges = img.ranges;
             ra.gid_sorted = bin.gid_sorted; ra.rec = geom.rec; ra.bg = background;
-            ra.out_color = out_color; ra.out_invdepth = out_invdepth; ra.img = img;
+            ra.out_color = out_color; ra.out_invdepth = out_invdepth; ra.ckpt = bin.ckpt; ra.img = img;
+            ra.unit_cnt = geom.unit_cnt; ra.unit_part = geom.unit_part; ra.unit_full = bin.unit_full;
+            ra.full_cap = (uint32_t)unit_full_cap(C);
+            ra.seg_ck = bwd_segment_checkpoints();
             HIP_TRY(launch_render_fwd(ra, stream), "render_fwd");
         }
         return check_debug(debug, stream, "render_fwd");
@@ -585,11 +604,12 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
     BinningState bin = carve_binning((char*)binning_buffer, C, &tmp);
     size_t rec_bytes = 0;
     GradRecs recs{}, sums{};
-    unsigned long long* lim_key = nullptr;
-    carve_recs(nullptr, (size_t)R, (size_t)P, tiles, &recs, &sums, &lim_key, &rec_bytes);
+    const int seg_ck = bwd_segment_checkpoints();
+    const size_t max_units = R > 0 ? bwd_max_units((size_t)R, tiles, seg_ck) : 0;
+    carve_recs(nullptr, (size_t)R, (size_t)P, &recs, &sums, &rec_bytes);
     char* rbase = (char*)call_alloc(scratch_alloc, scratch_ctx, rec_bytes);
     if (!rbase) return fail(GSR_ERR_ALLOC, "rasterize_backward: scratch allocation failed");
-    carve_recs(rbase, (size_t)R, (size_t)P, tiles, &recs, &sums, &lim_key, &rec_bytes);
+    carve_recs(rbase, (size_t)R, (size_t)P, &recs, &sums, &rec_bytes);
 
     if (R > 0) {
         StageScope sc(ST_RENDER_BWD, stream);
@@ -597,14 +617,15 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
         ra.W = width; ra.H = height; ra.gx = gx; ra.gy = gy; ra.ranges = img.ranges; ra.gid_sorted = bin.gid_sorted;
         ra.rec = geom.rec;
         ra.bg = background; ra.dL_dpix = dL_dpix; ra.dL_dinvdepth = dL_dinvdepths; ra.img = img; ra.recs = recs;
-        ra.depth_key = geom.depth_key; ra.lim_key = lim_key;
-        HIP_TRY(launch_tile_order(tiles, img.cost, img.order, stream), "tile_order");
-        HIP_TRY(launch_render_bwd(ra, stream), "render_bwd");
+        ra.ckpt = bin.ckpt; ra.depth_key = geom.depth_key; ra.seg_ck = seg_ck;
+        ra.unit_cnt = geom.unit_cnt; ra.unit_part = geom.unit_part; ra.unit_full = bin.unit_full;
+        ra.full_cap = (uint32_t)unit_full_cap(C);
+        HIP_TRY(launch_render_bwd(ra, max_units, stream), "render_bwd");
     }
     if (int rc = check_debug(debug, stream, "render_bwd")) return rc;
     {
         StageScope sc(ST_GAUSS_REDUCE, stream);
-        HIP_TRY(launch_gauss_reduce(P, geom, gx, lim_key, recs, sums, stream), "gauss_reduce");
+        HIP_TRY(launch_gauss_reduce(P, geom, gx, img.lim_key, recs, sums, stream), "gauss_reduce");
     }
     if (int rc = check_debug(debug, stream, "gauss_reduce")) return rc;
     {

@@ -270,7 +270,8 @@ __global__ void __launch_bounds__(kBinThreads) tile_count_kernel(int P, int chun
 // counts (independent loads), then one block scan per round.
 constexpr int kScanV = 8;
 
-__global__ void __launch_bounds__(kBinThreads) tile_scan_kernel(uint32_t tiles, const uint32_t* __restrict__ cnt,
+__global__ void __launch_bounds__(kBinThreads) tile_scan_kernel(uint32_t tiles, uint32_t* __restrict__ cnt,
+                                                                uint32_t n_counters, uint32_t* __restrict__ unit_cnt,
                                                                 uint2* __restrict__ ranges,
                                                                 uint32_t* __restrict__ tile_base, int nchunks,
                                                                 const u64* __restrict__ chunk_total,
@@ -280,6 +281,7 @@ __global__ void __launch_bounds__(kBinThreads) tile_scan_kernel(uint32_t tiles, 
     __shared__ u64 s_tmp[kBinWaves];
     __shared__ uint32_t s_cls[kSortClasses];
     if (threadIdx.x < kSortClasses) s_cls[threadIdx.x] = 0;  // published by the scan's barriers
+    if (threadIdx.x < kUnitLists * kUnitShards) unit_cnt[threadIdx.x * kUnitCntStride] = 0u;  // render work lists
     const uint32_t T = blockDim.x;
     u64 carry = 0;
     for (uint32_t base = 0; base < tiles; base += T * kScanV) {
@@ -322,6 +324,10 @@ __global__ void __launch_bounds__(kBinThreads) tile_scan_kernel(uint32_t tiles, 
     }
     __syncthreads();
     if (threadIdx.x < kSortClasses) cls_count[threadIdx.x] = s_cls[threadIdx.x];
+    // Leave the tile and cell counters zeroed (all reads of them are done): a rebuild of the
+    // lists (capacity hint too small, api.hip) counts again without a memset.  preprocess
+    // zeroes them for the first count of a call.
+    for (uint32_t i = threadIdx.x; i < n_counters; i += T) cnt[i] = 0u;
 }
 
 // ---- K3 ---------------------------------------------------------------------
@@ -627,8 +633,7 @@ hipError_t launch_bin_count(int P, const GeomState& g, uint32_t gx, uint32_t gy,
     const bool lds = tiles <= kLdsTilesMax;
     const dim3 grid(nchunks), block(kBinThreads);
     if (cells > kLdsTilesMax) return hipErrorInvalidValue;  // > 589k tiles: far beyond any image size
-    hipError_t e = hipMemsetAsync(g.tile_cnt, 0, (tiles + cells) * sizeof(uint32_t), stream);  // + cell_cnt
-    if (e != hipSuccess) return e;
+    // g.tile_cnt / g.cell_cnt are zero here: preprocess zeroes them, tile_scan_kernel re-zeroes them
     const size_t cell_bytes = cells * sizeof(uint32_t);
     hipLaunchKernelGGL(cell_count_kernel, grid, block, cell_bytes, stream, P, chunk, g.rect, g.tiles_touched, cells,
                        cgx, g.cell_cnt, g.cell_off, g.chunk_total);
@@ -641,7 +646,8 @@ hipError_t launch_bin_count(int P, const GeomState& g, uint32_t gx, uint32_t gy,
     else
         hipLaunchKernelGGL(tile_count_kernel<false>, grid, block, 0, stream, P, chunk, g.rect, g.tiles_touched,
                            g.order, g.n_visible, tiles, gx, g.tile_cnt, g.chunk_off);
-    hipLaunchKernelGGL(tile_scan_kernel, dim3(1), block, 0, stream, tiles, g.tile_cnt, ranges, g.tile_base, nchunks,
+    hipLaunchKernelGGL(tile_scan_kernel, dim3(1), block, 0, stream, tiles, g.tile_cnt, tiles + cells, g.unit_cnt,
+                       ranges, g.tile_base, nchunks,
                        g.chunk_total, g.chunk_base, g.total, (u64)cap, g.cls_list, g.cls_count);
     return hipGetLastError();
 }

@@ -91,6 +91,10 @@ struct GeomState {
     unsigned long long* chunk_total;  // [chunks] tiles_touched per Gaussian chunk
     unsigned long long* chunk_base;   // [chunks] its exclusive scan
     unsigned long long* total;        // [1] number of instances (num_rendered)
+    // backward work list (render.hip, see kUnitLists): counters [list][shard] one per 128-B line,
+    // zeroed by K2 before each forward render; the partial-segment lists, [4][shard][unit_part_cap]
+    uint32_t* unit_cnt;
+    uint2* unit_part;
 };
 
 // Image state: per pixel (N) and per tile.
@@ -99,9 +103,10 @@ struct ImageState {
     uint32_t* n_contrib;  // [N]
     float* accum;         // [4][N]: colour r,g,b and inverse depth, without background
     uint2* ranges;        // [tiles]
-    uint32_t* cost;       // [tiles] the forward's blend work per tile (slot-entries), the backward's
-                          // scheduling estimate
-    uint32_t* order;      // [tiles] the backward's tile order: heaviest first
+    uint32_t* cost;       // [tiles] the forward's blend work per tile (slot-entries; diagnostics)
+    uint32_t* tile_limit; // [tiles] max n_contrib over the tile's pixels: the backward walks [0, limit)
+    unsigned long long* lim_key;  // [tiles] key (depth bits << 32 | index) of the entry at limit - 1, 0 if
+                                  // none: entries past it have no gradient record (backward.hip)
 };
 
 // Binning state: per instance (R, or the capacity the buffer was requested for).
@@ -109,7 +114,39 @@ struct BinningState {
     unsigned long long* keys;  // per instance, grouped by tile: depth bits << 32 | tile-list entry
     uint32_t* gid_sorted;      // entry of each instance in (tile, depth, index) order: the tile lists
                                // (Gaussian << kEntryMaskBits | quadrant mask)
+    float* ckpt;               // blend checkpoints, [C / kCkStride + 1][kCkFloats] (see below)
+    uint2* unit_full;          // backward units covering full segments, [shard][unit_full_cap(C)]
 };
+
+// ---------------------------------------------------------------------------
+// Blend checkpoints.  Every kCkStride list entries the forward render stores each
+// pixel's blend state (live transmittance, accumulated colour, accumulated inverse
+// depth) -- checkpoint c of a tile is the state after its first c * kCkStride entries.
+// The backward then walks a tile's list in independent segments of kCkStride entries
+// (one wave each) instead of one wave per tile, which bounds the work of a wave and
+// removes the launch's tail.  Slot of the checkpoint at list position p (absolute,
+// p = range.x + c * kCkStride, c >= 1): p / kCkStride -- unique because checkpoints of
+// one tile are kCkStride apart and the next tile's first one is kCkStride past its start.
+// Layout of a slot: [5 values][4 quadrant slots][64 lanes] floats, the values being
+// T, C.r, C.g, C.b, invdepth.
+// ---------------------------------------------------------------------------
+constexpr int kCkStride = 256;
+constexpr int kCkFloats = 5 * 4 * 64;
+
+// ---------------------------------------------------------------------------
+// The backward's work list.  The forward render appends, per tile, one unit (tile, first
+// checkpoint) for each full segment below the tile's limit and one for the partial last
+// segment; the backward runs one wave per unit in list order: full segments, then the
+// partial ones by length quarter, longest first.  Every list is sharded by tile % 8 (the
+// XCD the dispatcher deals the tile's workgroup to): appends are returning atomics, and one
+// counter word shared by all tiles saturates (~88 adds/us chip-wide) and stalls the
+// forward's waves at their ends.
+// ---------------------------------------------------------------------------
+constexpr int kUnitLists = 5;       // full, partial quarters 0..3 (longest first)
+constexpr int kUnitShards = 8;
+constexpr int kUnitCntStride = 32;  // counter words, one per 128-B line
+__host__ __device__ inline uint32_t unit_part_cap(uint32_t tiles) { return (tiles + kUnitShards - 1) / kUnitShards; }
+__host__ __device__ inline size_t unit_full_cap(size_t C) { return C / kCkStride + 1; }
 
 // Per-instance gradient records (backward scratch), SoA so stores are aligned.
 struct GradRecs {

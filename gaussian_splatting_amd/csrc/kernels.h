@@ -24,6 +24,8 @@ struct PreprocessArgs {
     int prefiltered, antialiasing, footprint_cull;
     int* radii;
     GeomState geom;
+    uint32_t* zero;   // counters the binning accumulates into, zeroed here (no memset launch)
+    uint32_t zero_n;
 };
 
 struct RenderFwdArgs {
@@ -35,7 +37,14 @@ struct RenderFwdArgs {
     const float* bg;
     float* out_color;
     float* out_invdepth;
+    float* ckpt;           // blend checkpoints (BinningState::ckpt)
     ImageState img;
+    // the backward's work list, appended per tile (GeomState::unit_cnt / unit_part, BinningState::unit_full)
+    uint32_t* unit_cnt;
+    uint2* unit_part;
+    uint2* unit_full;
+    uint32_t full_cap;     // unit_full_cap(binning capacity): stride of unit_full's shards
+    int seg_ck;
 };
 
 struct RenderBwdArgs {
@@ -49,8 +58,14 @@ struct RenderBwdArgs {
     const float* dL_dinvdepth;  // [H,W] or null
     ImageState img;
     GradRecs recs;
-    const uint32_t* depth_key;          // per Gaussian
-    unsigned long long* lim_key;        // [tiles] out: key of the last entry that has a record (0: none)
+    const float* ckpt;                  // blend checkpoints written by the forward
+    const uint32_t* depth_key;          // per Gaussian (for the tile's lim_key)
+    // work list: (tile, first checkpoint index) of each wave, written by the forward render
+    const uint32_t* unit_cnt;
+    const uint2* unit_part;
+    const uint2* unit_full;
+    uint32_t full_cap;
+    int seg_ck;                         // checkpoints per backward segment (segment = seg_ck * kCkStride)
 };
 
 struct GaussBwdArgs {
@@ -216,8 +231,10 @@ hipError_t launch_tile_sort(uint32_t tiles, const uint2* ranges, const GeomState
                             size_t cap, hipStream_t stream);
 // render.hip
 hipError_t launch_render_fwd(const RenderFwdArgs& a, hipStream_t stream);
-hipError_t launch_render_bwd(const RenderBwdArgs& a, hipStream_t stream);
-hipError_t launch_tile_order(uint32_t tiles, const uint32_t* cost, uint32_t* order, hipStream_t stream);
+hipError_t launch_render_bwd(const RenderBwdArgs& a, size_t max_units, hipStream_t stream);
+// backward work list: one unit per (tile, segment of seg_ck * kCkStride entries below the tile's limit),
+// written by the forward render; at most R / (seg_ck kCkStride) + tiles of them
+size_t bwd_max_units(size_t R, uint32_t tiles, int seg_ck);
 // knn.hip
 size_t knn_scratch_bytes(int P);
 hipError_t launch_knn(int P, const float* pts, float* out, void* scratch, hipStream_t stream);

@@ -127,6 +127,7 @@ __global__ void __launch_bounds__(kPreThreads) preprocess_kernel(PreprocessArgs 
     const int idx = g0 + lane;
     const bool valid = idx < a.P;
     const int nvalid = min(kPreThreads, a.P - g0);
+    for (uint32_t i = blockIdx.x * kPreThreads + lane; i < a.zero_n; i += gridDim.x * kPreThreads) a.zero[i] = 0u;
 
     // ---- geometry (CR/forward.cu:255-326): `ok` replaces the reference's early returns
     bool ok = valid;

@@ -118,6 +118,20 @@ __global__ void __launch_bounds__(64) render_fwd_tile_kernel(RenderFwdArgs a) {
             *ent = (gid << kEntryMaskBits) | qm;  // for the backward, which visits only staged entries
         }
         __syncthreads();
+        // Blend checkpoint (gsr_common.h): the state before entry b0, stored after this batch's
+        // loads have landed.  vmcnt counts stores too, so stores issued ahead of the loads would
+        // make the staging wait for them; here they drain while the batch blends.
+        if (b0 > 0 && (b0 & (kCkStride - 1)) == 0) {  // uniform
+            float* ck = a.ckpt + (size_t)((range.x + (uint32_t)b0) / kCkStride) * kCkFloats + lane;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                ck[(0 * 4 + q) * 64] = Tl[q];
+                ck[(1 * 4 + q) * 64] = C0[q];
+                ck[(2 * 4 + q) * 64] = C1[q];
+                ck[(3 * 4 + q) * 64] = C2[q];
+                ck[(4 * 4 + q) * 64] = D[q];
+            }
+        }
         unsigned long long todo = __ballot(qm != 0);
         while (todo && alive) {
             const int j = __builtin_ctzll(todo);
@@ -157,7 +171,34 @@ __global__ void __launch_bounds__(64) render_fwd_tile_kernel(RenderFwdArgs a) {
     GSR_STAMP(g_st_rfwd, tile, 1);
     GSR_STAMP_RT(g_st_rfwd, tile, 5);
     GSR_STAMP_VAL(g_st_rfwd, tile, 2, n);
-    if (lane == 0) a.img.cost[tile] = work;
+    {  // the tile's limit for the backward: its largest n_contrib
+        uint32_t lm = max(max(last[0], last[1]), max(last[2], last[3]));
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) lm = max(lm, (uint32_t)__shfl_xor((int)lm, off));
+        if (lane == 0) {
+            a.img.cost[tile] = work;
+            a.img.tile_limit[tile] = lm;
+            if (lm == 0) a.img.lim_key[tile] = 0ull;  // (otherwise the backward's first unit writes it)
+        }
+        // The backward's work list: units (tile, k * seg_ck) for the full segments of S entries below
+        // the limit, then the last partial segment into one of four lists by length quarter.
+        // Lanes 0 and 1 append in parallel (separate counters, gsr_common.h "work list").
+        const uint32_t S = (uint32_t)a.seg_ck * kCkStride;
+        const uint32_t nf = lm / S, rem = lm % S;
+        const uint32_t shard = tile % kUnitShards;
+        const uint32_t b = min(3u, (uint32_t)(((unsigned long long)(S - rem) * 4) / S));  // longest -> 0
+        uint32_t base = 0;
+        if ((lane == 0 && nf) || (lane == 1 && rem)) {
+            const uint32_t list = lane == 0 ? 0u : 1u + b;
+            base = atomicAdd(&a.unit_cnt[(list * kUnitShards + shard) * kUnitCntStride], lane == 0 ? nf : 1u);
+        }
+        const uint32_t fbase = __shfl(base, 0);
+        uint2* full = a.unit_full + (size_t)shard * a.full_cap;
+        for (uint32_t k = lane; k < nf; k += kWave) full[fbase + k] = make_uint2(tile, k * (uint32_t)a.seg_ck);
+        if (lane == 1 && rem)
+            a.unit_part[((size_t)b * kUnitShards + shard) * unit_part_cap(a.gx * a.gy) + base] =
+                make_uint2(tile, nf * (uint32_t)a.seg_ck);
+    }
     const size_t N = (size_t)a.W * a.H;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
@@ -190,10 +231,27 @@ hipError_t launch_render_fwd(const RenderFwdArgs& a, hipStream_t stream) {
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(RenderBwdArgs a) {
   {
-    // heaviest tiles first (tile_order_kernel): the dispatcher deals them round-robin over
-    // the SIMDs, so every SIMD gets a similar share of the work, and the light tiles at the
-    // end of the order fill the slots that free up first
-    const uint32_t tile = a.img.order[blockIdx.x];
+    // One wave per unit = (tile, segment): the entries [start, end) of the tile's list, start a
+    // multiple of the checkpoint stride.  Units come longest first (bwd_units_kernel), so the
+    // dispatcher deals equal-sized pieces of work round-robin over the SIMDs and the short ones
+    // fill the slots that free up last -- no tile's full list ever sits on one SIMD.
+    uint2 unit;
+    {  // full segments first, then the partial ones, longest quarter first; shards in order
+        uint32_t i = blockIdx.x;
+        int l = 0;
+        for (; l < kUnitLists * kUnitShards; l++) {
+            const uint32_t c = uniform_u32(a.unit_cnt[l * kUnitCntStride]);
+            if (i < c) break;
+            i -= c;
+        }
+        if (l == kUnitLists * kUnitShards) return;  // past the list (the grid is sized for the worst case)
+        if (l < kUnitShards)
+            unit = a.unit_full[(size_t)l * a.full_cap + i];
+        else
+            unit = a.unit_part[(size_t)(l - kUnitShards) * unit_part_cap(a.gx * a.gy) + i];
+    }
+    const uint32_t tile = unit.x;
+    const int start = (int)unit.y * kCkStride;
     const int tile_x0 = (int)(tile % a.gx) * kTile, tile_y0 = (int)(tile / a.gx) * kTile;
     const int lane = threadIdx.x;
     const int lx = lane & 7, ly = lane >> 3;
@@ -202,11 +260,15 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
     __shared__ float4 s_xy[kBatch], s_cq[kBatch], s_col[kBatch];  // as in the forward
     __shared__ float4 s_abc[kBatch];                              // raw conic (a, b, c) for the flush
     __shared__ float4 s_acc[kBatch][3];                           // per entry: the 10 reduced sums (+2 pad)
-    GSR_STAMP(g_st_rbwd, tile, 0);
-    GSR_STAMP_HWID(g_st_rbwd, tile);
-    GSR_STAMP_RT(g_st_rbwd, tile, 4);
+    GSR_STAMP(g_st_rbwd, blockIdx.x, 0);
+    GSR_STAMP_HWID(g_st_rbwd, blockIdx.x);
+    GSR_STAMP_RT(g_st_rbwd, blockIdx.x, 4);
 
+    const uint2 range = a.ranges[tile];
     const size_t N = (size_t)a.W * a.H;
+    // blend state at `start`: the forward's checkpoint (gsr_common.h), or the empty state
+    const float* ck = start > 0 ? a.ckpt + (size_t)((range.x + (uint32_t)start) / kCkStride) * kCkFloats + lane
+                                : nullptr;
     float T[4], gB[4], g0[4], g1[4], g2[4], gi[4];
     int nc[4];
 #pragma unroll
@@ -222,10 +284,18 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
             g1[q] = a.dL_dpix[N + pix];
             g2[q] = a.dL_dpix[2 * N + pix];
             if (a.dL_dinvdepth) gi[q] = a.dL_dinvdepth[pix];
-            // dL/dpix . (everything the forward accumulated + the background term of dL/dalpha,
-            // CR/backward.cu:587-590); shrinks to "behind this entry" as the walk proceeds
-            gB[q] = g0[q] * a.img.accum[pix] + g1[q] * a.img.accum[N + pix] + g2[q] * a.img.accum[2 * N + pix] +
-                    gi[q] * a.img.accum[3 * N + pix] +
+            // dL/dpix . (what the forward accumulated from `start` on) + the background term of
+            // dL/dalpha (CR/backward.cu:587-590); shrinks to "behind this entry" as the walk proceeds
+            float c0 = a.img.accum[pix], c1 = a.img.accum[N + pix], c2 = a.img.accum[2 * N + pix],
+                  cd = a.img.accum[3 * N + pix];
+            if (ck) {
+                T[q] = ck[(0 * 4 + q) * 64];
+                c0 -= ck[(1 * 4 + q) * 64];
+                c1 -= ck[(2 * 4 + q) * 64];
+                c2 -= ck[(3 * 4 + q) * 64];
+                cd -= ck[(4 * 4 + q) * 64];
+            }
+            gB[q] = g0[q] * c0 + g1[q] * c1 + g2[q] * c2 + gi[q] * cd +
                     a.img.final_T[pix] * (a.bg[0] * g0[q] + a.bg[1] * g1[q] + a.bg[2] * g2[q]);
         }
     }
@@ -240,34 +310,28 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
         slim[q] = (int)uniform_u32((uint32_t)v);
     }
     const int limit = max(max(slim[0], slim[1]), max(slim[2], slim[3]));
-    uint32_t live = 0;  // slots still reachable at the current position (uniform)
+    const int end = min(limit, start + a.seg_ck * kCkStride);
+    uint32_t live = 0;     // slots still reachable at the current position (uniform)
     int next_lim = limit;  // smallest slot limit among live slots
 #pragma unroll
     for (int q = 0; q < 4; q++)
-        if (slim[q] > 0) {
+        if (slim[q] > start) {
             live |= 1u << q;
             next_lim = min(next_lim, slim[q]);
         }
     // where this lane's row of the reduce-scatter lands in s_acc (see below)
     const int row = lane >> 4, slot_k = ((row & 1) << 1) | (row >> 1);
 
-    const uint2 range = a.ranges[tile];
-    const int n = (int)(range.y - range.x);
-    // Entries at positions >= limit get no gradient record at all.  The per-Gaussian
-    // reduction recognises them by key (tile lists are sorted by depth bits << 32 |
-    // index): lim_key[tile] = key of the entry at position limit - 1, 0 if none (a
-    // visible Gaussian's depth bits are never 0).
-    if (lane == 0) {
-        unsigned long long lk = 0;
-        if (limit > 0) {
-            const uint32_t gl = a.gid_sorted[range.x + limit - 1] >> kEntryMaskBits;
-            lk = ((unsigned long long)a.depth_key[gl] << 32) | gl;
-        }
-        a.lim_key[tile] = lk;
+    if (start == 0 && lane == 0) {
+        // the key of the entry at limit - 1 (tiles with limit 0 get 0 from bwd_units_kernel): entries
+        // past it get no gradient record, and the per-Gaussian reduction recognises them by key (tile
+        // lists are sorted by depth bits << 32 | index; a visible Gaussian's depth bits are never 0)
+        const uint32_t gl = a.gid_sorted[range.x + limit - 1] >> kEntryMaskBits;
+        a.img.lim_key[tile] = ((unsigned long long)a.depth_key[gl] << 32) | gl;
     }
     const uint32_t ttx = tile % a.gx, tty = tile / a.gx;
-    for (int b0 = 0; b0 < limit; b0 += kBatch) {
-        const bool has = b0 + lane < limit;
+    for (int b0 = start; b0 < end; b0 += kBatch) {
+        const bool has = b0 + lane < end;
         uint32_t qm = 0, e = 0;
         if (has) {
             const uint32_t ent = a.gid_sorted[range.x + b0 + lane];  // Gaussian << 4 | quadrant mask
@@ -370,66 +434,18 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
         }
         __syncthreads();
     }
-    GSR_STAMP(g_st_rbwd, tile, 1);
-    GSR_STAMP_RT(g_st_rbwd, tile, 5);
-    GSR_STAMP_VAL(g_st_rbwd, tile, 2, n);
-    GSR_STAMP_VAL(g_st_rbwd, tile, 3, limit);
+    GSR_STAMP(g_st_rbwd, blockIdx.x, 1);
+    GSR_STAMP_RT(g_st_rbwd, blockIdx.x, 5);
+    GSR_STAMP_VAL(g_st_rbwd, blockIdx.x, 2, tile);
+    GSR_STAMP_VAL(g_st_rbwd, blockIdx.x, 3, end - start);
   }
 }
 
-// ---------------------------------------------------------------------------
-// Backward schedule: tiles in decreasing order of the forward's blend work (a counting sort
-// over 1024 cost buckets in one workgroup).  The order inside a bucket is whatever the LDS
-// atomics produce -- it only changes which SIMD runs which tile, never a result.
-constexpr int kOrderThreads = 1024, kOrderBuckets = 1024;
+size_t bwd_max_units(size_t R, uint32_t tiles, int seg_ck) { return R / ((size_t)seg_ck * kCkStride) + tiles; }
 
-__global__ void __launch_bounds__(kOrderThreads) tile_order_kernel(uint32_t tiles, const uint32_t* __restrict__ cost,
-                                                                   uint32_t* __restrict__ order) {
-    __shared__ uint32_t s_cnt[kOrderBuckets];
-    __shared__ uint32_t s_wsum[kOrderThreads / 64];
-    __shared__ uint32_t s_max;
-    if (threadIdx.x == 0) s_max = 0;
-    for (uint32_t i = threadIdx.x; i < kOrderBuckets; i += kOrderThreads) s_cnt[i] = 0;
-    __syncthreads();
-    uint32_t m = 0;
-    for (uint32_t t = threadIdx.x; t < tiles; t += kOrderThreads) m = max(m, cost[t]);
-    atomicMax(&s_max, m);
-    __syncthreads();
-    const unsigned long long cmax = (unsigned long long)s_max + 1;
-    auto bucket = [&](uint32_t c) {  // heaviest -> bucket 0
-        return (uint32_t)(((cmax - 1 - c) * (unsigned long long)kOrderBuckets) / cmax);
-    };
-    for (uint32_t t = threadIdx.x; t < tiles; t += kOrderThreads) atomicAdd(&s_cnt[bucket(cost[t])], 1u);
-    __syncthreads();
-    {  // exclusive scan, one bucket per thread
-        static_assert(kOrderBuckets == kOrderThreads, "one bucket per thread");
-        const uint32_t c = s_cnt[threadIdx.x];
-        uint32_t incl = c;
-        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-        for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t u = __shfl_up(incl, off);
-            if (lane >= off) incl += u;
-        }
-        if (lane == 63) s_wsum[w] = incl;
-        __syncthreads();
-        uint32_t base = 0;
-        for (int i = 0; i < w; i++) base += s_wsum[i];
-        s_cnt[threadIdx.x] = base + incl - c;
-    }
-    __syncthreads();
-    for (uint32_t t = threadIdx.x; t < tiles; t += kOrderThreads) order[atomicAdd(&s_cnt[bucket(cost[t])], 1u)] = t;
-}
-
-hipError_t launch_tile_order(uint32_t tiles, const uint32_t* cost, uint32_t* order, hipStream_t stream) {
-    if (tiles == 0) return hipSuccess;
-    hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(kOrderThreads), 0, stream, tiles, cost, order);
-    return hipGetLastError();
-}
-
-hipError_t launch_render_bwd(const RenderBwdArgs& a, hipStream_t stream) {
-    const uint32_t tiles = a.gx * a.gy;
-    if (tiles == 0) return hipSuccess;
-    hipLaunchKernelGGL(render_bwd_kernel, dim3(tiles), dim3(kWave), 0, stream, a);
+hipError_t launch_render_bwd(const RenderBwdArgs& a, size_t max_units, hipStream_t stream) {
+    if (max_units == 0) return hipSuccess;
+    hipLaunchKernelGGL(render_bwd_kernel, dim3((uint32_t)max_units), dim3(kWave), 0, stream, a);
     return hipGetLastError();
 }
 
