@@ -137,6 +137,7 @@ gsr::GeomState carve_geom(char* base, int P, uint32_t gx, uint32_t gy, size_t* t
     g.total = c.take<unsigned long long>(1);
     g.unit_cnt = c.take<uint32_t>((size_t)kUnitLists * kUnitShards * kUnitCntStride);
     g.unit_part = c.take<uint2>((size_t)(kUnitLists - 1) * kUnitShards * unit_part_cap(tiles));
+    g.tile_join = c.take<unsigned long long>(tiles);
     *total = align_up(c.off);
     return g;
 }
@@ -150,8 +151,6 @@ gsr::ImageState carve_image(char* base, int W, int H, uint32_t tiles, size_t* to
     im.n_contrib = c.take<uint32_t>(N);
     im.accum = c.take<float>(4 * N);
     im.ranges = c.take<uint2>(tiles);
-    im.cost = c.take<uint32_t>(tiles);
-    im.tile_limit = c.take<uint32_t>(tiles);
     im.lim_key = c.take<unsigned long long>(tiles);
     *total = align_up(c.off);
     return im;
@@ -495,6 +494,7 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
             ra.out_color = out_color; ra.out_invdepth = out_invdepth; ra.ckpt = bin.ckpt; ra.img = img;
             ra.unit_cnt = geom.unit_cnt; ra.unit_part = geom.unit_part; ra.unit_full = bin.unit_full;
             ra.full_cap = (uint32_t)unit_full_cap(C);
+            ra.tile_join = geom.tile_join;
             ra.seg_ck = bwd_segment_checkpoints();
             HIP_TRY(launch_render_fwd(ra, stream), "render_fwd");
         }

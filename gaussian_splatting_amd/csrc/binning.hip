@@ -272,6 +272,7 @@ constexpr int kScanV = 8;
 
 __global__ void __launch_bounds__(kBinThreads) tile_scan_kernel(uint32_t tiles, uint32_t* __restrict__ cnt,
                                                                 uint32_t n_counters, uint32_t* __restrict__ unit_cnt,
+                                                                unsigned long long* __restrict__ tile_join,
                                                                 uint2* __restrict__ ranges,
                                                                 uint32_t* __restrict__ tile_base, int nchunks,
                                                                 const u64* __restrict__ chunk_total,
@@ -328,6 +329,7 @@ __global__ void __launch_bounds__(kBinThreads) tile_scan_kernel(uint32_t tiles, 
     // lists (capacity hint too small, api.hip) counts again without a memset.  preprocess
     // zeroes them for the first count of a call.
     for (uint32_t i = threadIdx.x; i < n_counters; i += T) cnt[i] = 0u;
+    for (uint32_t i = threadIdx.x; i < tiles; i += T) tile_join[i] = 0ull;  // render_fwd's half-tile join
 }
 
 // ---- K3 ---------------------------------------------------------------------
@@ -646,7 +648,7 @@ hipError_t launch_bin_count(int P, const GeomState& g, uint32_t gx, uint32_t gy,
     else
         hipLaunchKernelGGL(tile_count_kernel<false>, grid, block, 0, stream, P, chunk, g.rect, g.tiles_touched,
                            g.order, g.n_visible, tiles, gx, g.tile_cnt, g.chunk_off);
-    hipLaunchKernelGGL(tile_scan_kernel, dim3(1), block, 0, stream, tiles, g.tile_cnt, tiles + cells, g.unit_cnt,
+    hipLaunchKernelGGL(tile_scan_kernel, dim3(1), block, 0, stream, tiles, g.tile_cnt, tiles + cells, g.unit_cnt, g.tile_join,
                        ranges, g.tile_base, nchunks,
                        g.chunk_total, g.chunk_base, g.total, (u64)cap, g.cls_list, g.cls_count);
     return hipGetLastError();

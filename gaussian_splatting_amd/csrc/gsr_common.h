@@ -95,6 +95,7 @@ struct GeomState {
     // zeroed by K2 before each forward render; the partial-segment lists, [4][shard][unit_part_cap]
     uint32_t* unit_cnt;
     uint2* unit_part;
+    unsigned long long* tile_join;  // [tiles] the forward's half-tile waves combine their limits here (K2 zeroes)
 };
 
 // Image state: per pixel (N) and per tile.
@@ -103,8 +104,6 @@ struct ImageState {
     uint32_t* n_contrib;  // [N]
     float* accum;         // [4][N]: colour r,g,b and inverse depth, without background
     uint2* ranges;        // [tiles]
-    uint32_t* cost;       // [tiles] the forward's blend work per tile (slot-entries; diagnostics)
-    uint32_t* tile_limit; // [tiles] max n_contrib over the tile's pixels: the backward walks [0, limit)
     unsigned long long* lim_key;  // [tiles] key (depth bits << 32 | index) of the entry at limit - 1, 0 if
                                   // none: entries past it have no gradient record (backward.hip)
 };
@@ -130,7 +129,10 @@ struct BinningState {
 // Layout of a slot: [5 values][4 quadrant slots][64 lanes] floats, the values being
 // T, C.r, C.g, C.b, invdepth.
 // ---------------------------------------------------------------------------
-constexpr int kCkStride = 256;
+#ifndef GSR_CK_STRIDE
+#define GSR_CK_STRIDE 256  // a multiple of the render batch (64); A/B builds override it
+#endif
+constexpr int kCkStride = GSR_CK_STRIDE;
 constexpr int kCkFloats = 5 * 4 * 64;
 
 // ---------------------------------------------------------------------------

@@ -44,6 +44,7 @@ struct RenderFwdArgs {
     uint2* unit_part;
     uint2* unit_full;
     uint32_t full_cap;     // unit_full_cap(binning capacity): stride of unit_full's shards
+    unsigned long long* tile_join;  // GeomState::tile_join
     int seg_ck;
 };
 

@@ -31,6 +31,8 @@
 // (tile, Gaussian) instance -- and written with plain stores.  There are no
 // float atomics anywhere, so the result is bitwise reproducible (the reference
 // issues 10 global float atomics per pixel-Gaussian pair, CR/backward.cu:569-609).
+#include <cstdlib>
+
 #include "footprint.h"
 #include "kernels.h"
 
@@ -76,30 +78,51 @@ __device__ __forceinline__ float splat_alpha(float p2, float opacity, float& G) 
 // transmittance at termination.  A finished pixel therefore blends with weight 0
 // without any mask bookkeeping, and the only wave-level decisions are "does any
 // lane of this slot blend this splat" and "is any pixel of this slot still live".
-__global__ void __launch_bounds__(64) render_fwd_tile_kernel(RenderFwdArgs a) {
+#ifdef GSR_FWD_WAVES
+#define GSR_FWD_OCCUPANCY __attribute__((amdgpu_waves_per_eu(GSR_FWD_WAVES, GSR_FWD_WAVES)))
+#else
+#define GSR_FWD_OCCUPANCY
+#endif
+// One wave per PART of a tile: NQ = 4 quadrants (the whole 16x16 tile) or NQ = 2 (its top or
+// bottom half).  Each lane owns one pixel in each of the part's NQ quadrants ("slots").  With
+// half tiles the 8160 tiles of a 1080p view become 16320 waves of half the blend work each, so
+// the launch no longer ends with SIMDs finishing their second whole tile alone; the price is
+// that both halves stage the same entries.  Grid: groups of 8 consecutive tiles x NPART parts,
+// block b -> tile 8 (b / (8 NPART)) + b % 8, part (b / 8) % NPART: the parts of a tile sit on
+// the same XCD (blocks are dealt round-robin over the 8 XCDs) and share its L2.
+template <int NQ>
+__global__ void __launch_bounds__(64) GSR_FWD_OCCUPANCY render_fwd_kernel(RenderFwdArgs a) {
   {
-    const uint32_t tile = blockIdx.x;
+    constexpr int NPART = 4 / NQ;
+    constexpr uint32_t kPartMask = (1u << NQ) - 1u;
+    const uint32_t tiles = a.gx * a.gy;
+    const uint32_t tile = (blockIdx.x / (8 * NPART)) * 8 + blockIdx.x % 8;
+    const int part = NPART == 1 ? 0 : (int)((blockIdx.x / 8) % NPART);
+    if (tile >= tiles) return;
+    const int qbase = part * NQ;  // first quadrant of this part
     const int tile_x0 = (int)(tile % a.gx) * kTile, tile_y0 = (int)(tile / a.gx) * kTile;
     const int lane = threadIdx.x;
     const int lx = lane & 7, ly = lane >> 3;
     const float pxf0 = (float)(tile_x0 + lx), pyf0 = (float)(tile_y0 + ly);  // this lane's pixel in quadrant 0
-    GSR_STAMP(g_st_rfwd, tile, 0);  // (stamp slots are per tile here, per unit in the quad kernel)
-    GSR_STAMP_HWID(g_st_rfwd, tile);
-    GSR_STAMP_RT(g_st_rfwd, tile, 4);
+    if (part == 0) {
+        GSR_STAMP(g_st_rfwd, tile, 0);
+        GSR_STAMP_HWID(g_st_rfwd, tile);
+        GSR_STAMP_RT(g_st_rfwd, tile, 4);
+    }
 
     __shared__ float4 s_xy[kBatch], s_cq[kBatch], s_col[kBatch];  // (x, y, o, 1/z), (A, B, C, quads), rgb
 
-    float Tl[4], Tf[4], C0[4], C1[4], C2[4], D[4];
-    uint32_t last[4];
+    float Tl[NQ], Tf[NQ], C0[NQ], C1[NQ], C2[NQ], D[NQ];
+    uint32_t last[NQ];
     uint32_t alive = 0;  // wave-uniform: slots with at least one pixel still blending
-    uint32_t work = 0;   // wave-uniform: slot-entries blended (the backward's scheduling estimate)
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
+    for (int k = 0; k < NQ; k++) {
+        const int q = qbase + k;
         const int px = tile_x0 + (q & 1) * 8 + lx, py = tile_y0 + (q >> 1) * 8 + ly;
-        Tl[q] = (px < a.W && py < a.H) ? 1.f : 0.f;
-        Tf[q] = C0[q] = C1[q] = C2[q] = D[q] = 0.f;
-        last[q] = 0;
-        if (__any(Tl[q] > 0.f)) alive |= 1u << q;
+        Tl[k] = (px < a.W && py < a.H) ? 1.f : 0.f;
+        Tf[k] = C0[k] = C1[k] = C2[k] = D[k] = 0.f;
+        last[k] = 0;
+        if (__any(Tl[k] > 0.f)) alive |= 1u << k;
     }
 
     const uint2 range = a.ranges[tile];
@@ -114,117 +137,146 @@ __global__ void __launch_bounds__(64) render_fwd_tile_kernel(RenderFwdArgs a) {
             s_xy[lane] = make_float4(v0.x, v0.y, v1.y, v1.z);
             s_col[lane] = v2;
             qm = quad_bits_exact(v0, v1, v2, tile_x0, tile_y0);
-            s_cq[lane] = stage_conic(v0, v1, qm);
-            *ent = (gid << kEntryMaskBits) | qm;  // for the backward, which visits only staged entries
+            s_cq[lane] = stage_conic(v0, v1, (qm >> qbase) & kPartMask);
+            // all four bits, for the backward (which visits only staged entries); with two parts
+            // both may store the entry, the same value
+            *ent = (gid << kEntryMaskBits) | qm;
         }
         __syncthreads();
         // Blend checkpoint (gsr_common.h): the state before entry b0, stored after this batch's
         // loads have landed.  vmcnt counts stores too, so stores issued ahead of the loads would
-        // make the staging wait for them; here they drain while the batch blends.
+        // make the staging wait for them; here they drain while the batch blends.  A part writes
+        // its own quadrants' slots while it is alive: a backward slot that reaches past b0 has a
+        // pixel that blended past b0, so its part was alive here.
         if (b0 > 0 && (b0 & (kCkStride - 1)) == 0) {  // uniform
             float* ck = a.ckpt + (size_t)((range.x + (uint32_t)b0) / kCkStride) * kCkFloats + lane;
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                ck[(0 * 4 + q) * 64] = Tl[q];
-                ck[(1 * 4 + q) * 64] = C0[q];
-                ck[(2 * 4 + q) * 64] = C1[q];
-                ck[(3 * 4 + q) * 64] = C2[q];
-                ck[(4 * 4 + q) * 64] = D[q];
+            for (int k = 0; k < NQ; k++) {
+                const int q = qbase + k;
+                ck[(0 * 4 + q) * 64] = Tl[k];
+                ck[(1 * 4 + q) * 64] = C0[k];
+                ck[(2 * 4 + q) * 64] = C1[k];
+                ck[(3 * 4 + q) * 64] = C2[k];
+                ck[(4 * 4 + q) * 64] = D[k];
             }
         }
-        unsigned long long todo = __ballot(qm != 0);
+        unsigned long long todo = __ballot((qm >> qbase) & kPartMask);
         while (todo && alive) {
             const int j = __builtin_ctzll(todo);
             todo &= todo - 1;
             const float4 xy = s_xy[j], cq = s_cq[j], col = s_col[j];
             const uint32_t m = uniform_u32(__float_as_uint(cq.w)) & alive;
             const uint32_t pos1 = (uint32_t)(b0 + j + 1);
-            work += (uint32_t)__builtin_popcount(m);
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                if (!(m & (1u << q))) continue;  // uniform: footprint misses this quadrant
+            for (int k = 0; k < NQ; k++) {
+                if (!(m & (1u << k))) continue;  // uniform: footprint misses this quadrant
+                const int q = qbase + k;
                 const float dx = xy.x - (pxf0 + (float)((q & 1) * 8)), dy = xy.y - (pyf0 + (float)((q >> 1) * 8));
                 const float p2 = dx * (cq.x * dx + cq.y * dy) + cq.z * dy * dy;
                 float G;
                 const float alpha = splat_alpha(p2, xy.z, G);
-                const float w0 = alpha * Tl[q];  // > 0 iff this pixel blends the splat
+                const float w0 = alpha * Tl[k];  // > 0 iff this pixel blends the splat
                 if (!__any(w0 > 0.f)) continue;  // uniform
-                const float test_T = Tl[q] * (1.f - alpha);
+                const float test_T = Tl[k] * (1.f - alpha);
                 const bool term = test_T < 0.0001f;  // live pixel: ends it, splat not added
                 const float w = term ? 0.f : w0;
                 // first termination wins (later ones see Tl = 0); both are >= 0, so an integer max
-                Tf[q] = __uint_as_float(max(__float_as_uint(Tf[q]), term ? __float_as_uint(Tl[q]) : 0u));
-                Tl[q] = term ? 0.f : test_T;
-                C0[q] += col.x * w;
-                C1[q] += col.y * w;
-                C2[q] += col.z * w;
-                D[q] += xy.w * w;
-                last[q] = w > 0.f ? pos1 : last[q];
-                if (!__any(Tl[q] > 0.f)) alive &= ~(1u << q);
+                Tf[k] = __uint_as_float(max(__float_as_uint(Tf[k]), term ? __float_as_uint(Tl[k]) : 0u));
+                Tl[k] = term ? 0.f : test_T;
+                C0[k] += col.x * w;
+                C1[k] += col.y * w;
+                C2[k] += col.z * w;
+                D[k] += xy.w * w;
+                last[k] = w > 0.f ? pos1 : last[k];
+                if (!__any(Tl[k] > 0.f)) alive &= ~(1u << k);
             }
         }
         __syncthreads();
 #ifdef GSR_STAMPS
-        if (threadIdx.x == 0) g_st_rfwd[(size_t)tile * kStampSlots + 3] = (unsigned long long)(b0 + kBatch);
+        if (threadIdx.x == 0 && part == 0) g_st_rfwd[(size_t)tile * kStampSlots + 3] = (unsigned long long)(b0 + kBatch);
 #endif
     }
-    GSR_STAMP(g_st_rfwd, tile, 1);
-    GSR_STAMP_RT(g_st_rfwd, tile, 5);
-    GSR_STAMP_VAL(g_st_rfwd, tile, 2, n);
-    {  // the tile's limit for the backward: its largest n_contrib
-        uint32_t lm = max(max(last[0], last[1]), max(last[2], last[3]));
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) lm = max(lm, (uint32_t)__shfl_xor((int)lm, off));
-        if (lane == 0) {
-            a.img.cost[tile] = work;
-            a.img.tile_limit[tile] = lm;
-            if (lm == 0) a.img.lim_key[tile] = 0ull;  // (otherwise the backward's first unit writes it)
-        }
-        // The backward's work list: units (tile, k * seg_ck) for the full segments of S entries below
-        // the limit, then the last partial segment into one of four lists by length quarter.
-        // Lanes 0 and 1 append in parallel (separate counters, gsr_common.h "work list").
-        const uint32_t S = (uint32_t)a.seg_ck * kCkStride;
-        const uint32_t nf = lm / S, rem = lm % S;
-        const uint32_t shard = tile % kUnitShards;
-        const uint32_t b = min(3u, (uint32_t)(((unsigned long long)(S - rem) * 4) / S));  // longest -> 0
-        uint32_t base = 0;
-        if ((lane == 0 && nf) || (lane == 1 && rem)) {
-            const uint32_t list = lane == 0 ? 0u : 1u + b;
-            base = atomicAdd(&a.unit_cnt[(list * kUnitShards + shard) * kUnitCntStride], lane == 0 ? nf : 1u);
-        }
-        const uint32_t fbase = __shfl(base, 0);
-        uint2* full = a.unit_full + (size_t)shard * a.full_cap;
-        for (uint32_t k = lane; k < nf; k += kWave) full[fbase + k] = make_uint2(tile, k * (uint32_t)a.seg_ck);
-        if (lane == 1 && rem)
-            a.unit_part[((size_t)b * kUnitShards + shard) * unit_part_cap(a.gx * a.gy) + base] =
-                make_uint2(tile, nf * (uint32_t)a.seg_ck);
+    if (part == 0) {
+        GSR_STAMP(g_st_rfwd, tile, 1);
+        GSR_STAMP_RT(g_st_rfwd, tile, 5);
+        GSR_STAMP_VAL(g_st_rfwd, tile, 2, n);
     }
     const size_t N = (size_t)a.W * a.H;
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
+    for (int k = 0; k < NQ; k++) {
+        const int q = qbase + k;
         const int px = tile_x0 + (q & 1) * 8 + lx, py = tile_y0 + (q >> 1) * 8 + ly;
         if (px < a.W && py < a.H) {
             const size_t pix = (size_t)py * a.W + px;
-            const float T = Tl[q] > 0.f ? Tl[q] : Tf[q];
+            const float T = Tl[k] > 0.f ? Tl[k] : Tf[k];
             a.img.final_T[pix] = T;
-            a.img.n_contrib[pix] = last[q];
-            a.img.accum[pix] = C0[q];
-            a.img.accum[N + pix] = C1[q];
-            a.img.accum[2 * N + pix] = C2[q];
-            a.img.accum[3 * N + pix] = D[q];
-            a.out_color[pix] = C0[q] + T * a.bg[0];
-            a.out_color[N + pix] = C1[q] + T * a.bg[1];
-            a.out_color[2 * N + pix] = C2[q] + T * a.bg[2];
-            a.out_invdepth[pix] = D[q];
+            a.img.n_contrib[pix] = last[k];
+            a.img.accum[pix] = C0[k];
+            a.img.accum[N + pix] = C1[k];
+            a.img.accum[2 * N + pix] = C2[k];
+            a.img.accum[3 * N + pix] = D[k];
+            a.out_color[pix] = C0[k] + T * a.bg[0];
+            a.out_color[N + pix] = C1[k] + T * a.bg[1];
+            a.out_color[2 * N + pix] = C2[k] + T * a.bg[2];
+            a.out_invdepth[pix] = D[k];
         }
     }
+
+    // The tile's limit for the backward: its largest n_contrib.  With two parts the second part
+    // to finish combines them: each adds (1 << 62) + (its limit << 31 part) to the tile's join
+    // word (zeroed by K2), so the second add returns the first part's limit -- no fence needed.
+    uint32_t lm = last[0];
+#pragma unroll
+    for (int k = 1; k < NQ; k++) lm = max(lm, last[k]);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) lm = max(lm, (uint32_t)__shfl_xor((int)lm, off));
+    if (NPART == 2) {
+        unsigned long long old = 0;
+        if (lane == 0)
+            old = atomicAdd(&a.tile_join[tile], (1ull << 62) + ((unsigned long long)lm << (31 * part)));
+        old = __shfl(old, 0);
+        if ((old >> 62) == 0) return;  // the other part finishes the tile
+        lm = max(lm, (uint32_t)((old >> (31 * (part ^ 1))) & 0x7fffffffull));
+    }
+    if (lane == 0 && lm == 0) a.img.lim_key[tile] = 0ull;  // (otherwise the backward's first unit writes it)
+    // The backward's work list: units (tile, k * seg_ck) for the full segments of S entries below
+    // the limit, then the last partial segment into one of four lists by length quarter.
+    // Lanes 0 and 1 append in parallel (separate counters, gsr_common.h "work list").
+    const uint32_t S = (uint32_t)a.seg_ck * kCkStride;
+    const uint32_t nf = lm / S, rem = lm % S;
+    const uint32_t shard = tile % kUnitShards;
+    const uint32_t b = min(3u, (uint32_t)(((unsigned long long)(S - rem) * 4) / S));  // longest -> 0
+    uint32_t base = 0;
+    if ((lane == 0 && nf) || (lane == 1 && rem)) {
+        const uint32_t list = lane == 0 ? 0u : 1u + b;
+        base = atomicAdd(&a.unit_cnt[(list * kUnitShards + shard) * kUnitCntStride], lane == 0 ? nf : 1u);
+    }
+    const uint32_t fbase = __shfl(base, 0);
+    uint2* full = a.unit_full + (size_t)shard * a.full_cap;
+    for (uint32_t k = lane; k < nf; k += kWave) full[fbase + k] = make_uint2(tile, k * (uint32_t)a.seg_ck);
+    if (lane == 1 && rem)
+        a.unit_part[((size_t)b * kUnitShards + shard) * unit_part_cap(tiles) + base] =
+            make_uint2(tile, nf * (uint32_t)a.seg_ck);
   }
+}
+
+// Quadrants per forward wave: 2 (half tiles) unless GSR_FWD_QUADS=4 (whole tiles, for A/B runs).
+static int fwd_quads_per_wave() {
+    static const int v = [] {
+        const char* e = getenv("GSR_FWD_QUADS");
+        return (e && atoi(e) == 4) ? 4 : 2;
+    }();
+    return v;
 }
 
 hipError_t launch_render_fwd(const RenderFwdArgs& a, hipStream_t stream) {
     const uint32_t tiles = a.gx * a.gy;
     if (tiles == 0) return hipSuccess;
-    hipLaunchKernelGGL(render_fwd_tile_kernel, dim3(tiles), dim3(kWave), 0, stream, a);
+    const uint32_t groups = (tiles + 7) / 8;
+    if (fwd_quads_per_wave() == 4)
+        hipLaunchKernelGGL(render_fwd_kernel<4>, dim3(groups * 8), dim3(kWave), 0, stream, a);
+    else
+        hipLaunchKernelGGL(render_fwd_kernel<2>, dim3(groups * 16), dim3(kWave), 0, stream, a);
     return hipGetLastError();
 }
 

@@ -114,6 +114,7 @@ def main():
     torch.cuda.synchronize()
     tiles = ((cam.width + 15) // 16) * ((cam.height + 15) // 16)
     P = cfg["P"]
+    units = int(nr) // 256 + tiles  # bwd_max_units (render.hip), checkpoint stride 256
     nchunks = min(256, max(1, (P + 1023) // 1024))
     fb = lib.gsr_diag_stamps_binning
     fr = lib.gsr_diag_stamps_render
@@ -126,19 +127,20 @@ def main():
         timeline("tile_sort", read(fb, 2, tiles), [0, 1], extra={"n": 2}),
         timeline("render_fwd", read(fr, 0, tiles),
                  [0, 1], extra={"n": 2}),
-        timeline("render_bwd", read(fr, 1, tiles), [0, 1], extra={"n": 2, "limit": 3}),
+        timeline("render_bwd", read(fr, 1, units), [0, 1], extra={"len": 3}),
     ]
     for r in res:
         print(json.dumps({k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items()}))
-    nf = tiles
-    sf, sb = read(fr, 0, nf), read(fr, 1, tiles)
-    fwd_tile = (sf[:, 1] - sf[:, 0]).reshape(tiles, -1).sum(1).astype(np.float64)
-    bwd_tile = (sb[:, 1] - sb[:, 0]).astype(np.float64)
-    print(json.dumps({"corr_fwd_bwd_tile_duration": float(np.corrcoef(fwd_tile, bwd_tile)[0, 1]),
-                      "corr_bwd_dur_limit": float(np.corrcoef(bwd_tile, sb[:, 3])[0, 1]),
-                      "bwd_dur_cv": float(bwd_tile.std() / bwd_tile.mean()),
+    # backward: one workgroup per (tile, segment) unit; per-tile sums of the unit durations
+    sf, sb = read(fr, 0, tiles), read(fr, 1, units)
+    okb = (sb[:, 0] > 0) & (sb[:, 1] >= sb[:, 0])
+    fwd_tile = (sf[:, 1] - sf[:, 0]).astype(np.float64)
+    bwd_tile = np.bincount(sb[okb, 2], weights=(sb[okb, 1] - sb[okb, 0]).astype(np.float64), minlength=tiles)
+    print(json.dumps({"bwd_units": int(okb.sum()),
+                      "corr_fwd_bwd_tile_duration": float(np.corrcoef(fwd_tile, bwd_tile[:tiles])[0, 1]),
+                      "bwd_tile_cv": float(bwd_tile.std() / bwd_tile.mean()),
                       "fwd_dur_cv": float(fwd_tile.std() / fwd_tile.mean())}))
-    for r in occupancy("render_fwd", read(fr, 0, nf))[:3] + occupancy("render_bwd", read(fr, 1, tiles))[:3]:
+    for r in occupancy("render_fwd", sf)[:3] + occupancy("render_bwd", sb)[:3]:
         print(json.dumps(r))
 
 
