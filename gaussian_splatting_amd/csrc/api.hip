@@ -192,6 +192,35 @@ int bwd_segment_checkpoints() {
     return v;
 }
 
+// Per (host thread, device): a pinned 8-byte slot that num_rendered is copied into and the
+// event recorded behind that copy.  The host waits on the event -- i.e. for the binning
+// counts -- and not for the whole stream, so the render kernels queued behind the copy keep
+// the GPU busy while the host returns to Python and queues the backward.
+struct TotalReadback {
+    unsigned long long* host = nullptr;
+    hipEvent_t ev = nullptr;
+};
+int total_readback(TotalReadback** out) {
+    constexpr int kMaxDevices = 64;
+    thread_local TotalReadback slots[kMaxDevices];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices)
+        return fail(GSR_ERR_HIP, "num_rendered readback: no current device");
+    TotalReadback& r = slots[dev];
+    if (!r.host) {
+        void* h = nullptr;
+        if (hipHostMalloc(&h, sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess)
+            return fail(GSR_ERR_HIP, "num_rendered readback: hipHostMalloc failed");
+        if (hipEventCreateWithFlags(&r.ev, hipEventDisableTiming) != hipSuccess) {
+            (void)hipHostFree(h);
+            return fail(GSR_ERR_HIP, "num_rendered readback: hipEventCreate failed");
+        }
+        r.host = (unsigned long long*)h;
+    }
+    *out = &r;
+    return GSR_OK;
+}
+
 void* call_alloc(gsr_alloc_fn fn, void* ctx, size_t bytes) {
     if (!fn) return nullptr;
     return fn(ctx, bytes ? bytes : 1);
@@ -456,11 +485,21 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
     // Scatter + tile sort + render into a binning buffer of capacity C.  In exact mode
     // C = R is read back first -- the reference's one host synchronisation
     // (CR/rasterizer_impl.cu:313).  In capacity mode (capacity_hint > 0) nothing waits
-    // for the host: R is read once at the end, and if it exceeds C the lists are
+    // for the host: every stage is queued, then the host waits for the copy of R queued
+    // right behind K2 (not for the render behind it), and if R exceeds C the lists are
     // rebuilt into a buffer of exactly R.
-    auto read_total = [&](unsigned long long* total) -> int {
-        HIP_TRY(hipMemcpyAsync(total, geom.total, sizeof(*total), hipMemcpyDeviceToHost, stream), "num_rendered copy");
-        HIP_TRY(hipStreamSynchronize(stream), "num_rendered sync");
+    TotalReadback* rb = nullptr;
+    if (int rc = total_readback(&rb)) return rc;
+    // queue the copy of num_rendered (written by K2) and mark it; wait_total() waits for it only
+    auto queue_total = [&]() -> int {
+        HIP_TRY(hipMemcpyAsync(rb->host, geom.total, sizeof(*rb->host), hipMemcpyDeviceToHost, stream),
+                "num_rendered copy");
+        HIP_TRY(hipEventRecord(rb->ev, stream), "num_rendered event");
+        return GSR_OK;
+    };
+    auto wait_total = [&](unsigned long long* total) -> int {
+        HIP_TRY(hipEventSynchronize(rb->ev), "num_rendered sync");
+        *total = *rb->host;
         if (*total > (unsigned long long)INT_MAX)
             return fail(GSR_ERR_OVERFLOW, "rasterize_forward: %llu tile instances exceed INT_MAX", *total);
         return GSR_OK;
@@ -503,14 +542,16 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
 
     unsigned long long total = 0;
     size_t C = 0;
+    if (int rc = queue_total()) return rc;
     if (capacity_hint <= 0) {
-        if (int rc = read_total(&total)) return rc;
+        if (int rc = wait_total(&total)) return rc;
         C = (size_t)total;
         if (int rc = bin_and_render(C)) return rc;
     } else {
+        // everything is queued before the host waits, and it waits for the counts only
         C = (size_t)capacity_hint;
         if (int rc = bin_and_render(C)) return rc;
-        if (int rc = read_total(&total)) return rc;
+        if (int rc = wait_total(&total)) return rc;
         if (total > C) {  // the hint was too small: recount (resets the cursors) and rebuild exactly
             C = (size_t)total;
             HIP_TRY(launch_bin_count(P, geom, gx, gy, img.ranges, C, stream), "bin_count");
