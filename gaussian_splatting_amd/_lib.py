@@ -15,7 +15,7 @@ _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GSR_LIBRARY", os.path.join(_PKG, "lib", "libgsr.so"))
 INCLUDE_DIR = os.path.join(os.path.dirname(_PKG), "include")
 HEADER_PATH = os.path.join(INCLUDE_DIR, "gsr.h")
-HEADERS = [os.path.join(INCLUDE_DIR, h) for h in ("gsr.h", "gsr_knn.h", "gsr_ssim.h", "gsr_adam.h")]
+HEADERS = [os.path.join(INCLUDE_DIR, h) for h in ("gsr.h", "gsr_knn.h", "gsr_ssim.h", "gsr_adam.h", "gsr_densify.h")]
 
 ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
 
@@ -29,6 +29,22 @@ class AdamGroup(ctypes.Structure):
     _fields_ = [("param", ctypes.c_void_p), ("grad", ctypes.c_void_p), ("exp_avg", ctypes.c_void_p),
                 ("exp_avg_sq", ctypes.c_void_p), ("numel", ctypes.c_longlong), ("M", ctypes.c_int),
                 ("lr", ctypes.c_float), ("eps", ctypes.c_float)]
+
+
+class DensifyGroup(ctypes.Structure):
+    """gsr_densify_group (include/gsr_densify.h)."""
+
+    _fields_ = [("src", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("src_exp_avg", ctypes.c_void_p),
+                ("src_exp_avg_sq", ctypes.c_void_p), ("dst_exp_avg", ctypes.c_void_p),
+                ("dst_exp_avg_sq", ctypes.c_void_p), ("width", ctypes.c_int), ("role", ctypes.c_int)]
+
+
+class DensifyParams(ctypes.Structure):
+    """gsr_densify_params (include/gsr_densify.h)."""
+
+    _fields_ = [("grad_threshold", ctypes.c_float), ("clone_extent", ctypes.c_float),
+                ("min_opacity", ctypes.c_float), ("big_extent", ctypes.c_float), ("use_screen_size", ctypes.c_int),
+                ("split_n", ctypes.c_int), ("split_div", ctypes.c_float)]
 
 
 # argument lists, in include/gsr.h order
@@ -63,6 +79,12 @@ SIGNATURES = {
     "gsr_fused_ssim_backward": (_i, [_i, _i, _i, _i, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gsr_adam_update": (_i, [_vp, _vp, _vp, _vp, _vp, _f, _f, _f, _f, _i, _i, _vp]),
     "gsr_adam_update_multi": (_i, [ctypes.POINTER(AdamGroup), _i, _vp, _i, _f, _f, _vp]),
+    "gsr_densify_stats": (_i, [_i, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "gsr_densify_scratch_bytes": (ctypes.c_ulonglong, [_i]),
+    "gsr_densify_plan": (_i, [_i, _vp, _vp, _vp, _vp, ctypes.POINTER(DensifyParams), _vp, _vp,
+                              ctypes.POINTER(ctypes.c_longlong), _vp]),
+    "gsr_densify_apply": (_i, [_i, _vp, ctypes.POINTER(DensifyGroup), _i, _vp, _vp, _vp, _vp,
+                               ctypes.POINTER(DensifyParams), _vp]),
 }
 
 _lock = threading.Lock()

@@ -20,7 +20,7 @@ CSRC = os.path.join(PKG, "csrc")
 OBJ = os.path.join(PKG, "build")
 LIB_DIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIB_DIR, "libgsr.so")
-SOURCES = ["api.hip", "preprocess.hip", "binning.hip", "render.hip", "backward.hip", "knn.hip", "ssim.hip", "adam.hip"]
+SOURCES = ["api.hip", "preprocess.hip", "binning.hip", "render.hip", "backward.hip", "knn.hip", "ssim.hip", "adam.hip", "densify.hip"]
 HEADERS = ["gsr_common.h", "kernels.h", "footprint.h"]
 ARCH = os.environ.get("GSR_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -30,7 +30,7 @@ CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-W
 
 def _newest_input_mtime() -> float:
     files = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(ROOT, "include", h) for h in
-                                                                  ("gsr.h", "gsr_knn.h", "gsr_ssim.h", "gsr_adam.h")] + [__file__]
+                                                                  ("gsr.h", "gsr_knn.h", "gsr_ssim.h", "gsr_adam.h", "gsr_densify.h")] + [__file__]
     return max(os.path.getmtime(f) for f in files)
 
 

@@ -18,6 +18,7 @@
 #include "../../include/gsr_knn.h"
 #include "../../include/gsr_ssim.h"
 #include "../../include/gsr_adam.h"
+#include "../../include/gsr_densify.h"
 #include "kernels.h"
 
 namespace {
@@ -338,6 +339,129 @@ int gsr_adam_update(float* param, const float* grad, float* exp_avg, float* exp_
 int gsr_adam_update_multi(const gsr_adam_group* groups, int n_groups, const unsigned char* visible, int N, float b1,
                           float b2, void* stream) {
     return adam_launch(groups, n_groups, visible, N, b1, b2, stream);
+}
+
+// ---- adaptive density control (include/gsr_densify.h) ------------------------------
+int gsr_densify_stats(int P, const float* viewspace_grad, const int* radii, const unsigned char* visible,
+                      float* grad_accum, float* denom, float* max_radii2D, void* stream) {
+    using namespace gsr;
+    g_err[0] = 0;
+    if (P < 0) return fail(GSR_ERR_ARGUMENT, "densify_stats: P must be >= 0");
+    if (P == 0) return GSR_OK;
+    if (viewspace_grad && (!grad_accum || !denom)) return fail(GSR_ERR_ARGUMENT, "densify_stats: null accumulator");
+    if (!viewspace_grad && !(radii && max_radii2D))
+        return fail(GSR_ERR_ARGUMENT, "densify_stats: nothing to update");
+    if (!radii && !visible) return fail(GSR_ERR_ARGUMENT, "densify_stats: need radii or a visibility mask");
+    HIP_TRY(launch_densify_stats(P, viewspace_grad, radii, visible, grad_accum, denom, max_radii2D,
+                                 (hipStream_t)stream),
+            "densify_stats");
+    return GSR_OK;
+}
+
+unsigned long long gsr_densify_scratch_bytes(int P) { return P > 0 ? gsr::densify_scratch_bytes(P) : 0ull; }
+
+int gsr_densify_plan(int P, const float* grad_accum, const float* denom, const float* opacity, const float* scaling,
+                     const gsr_densify_params* prm, void* scratch, unsigned char* split_mask, long long* counts,
+                     void* stream) {
+    using namespace gsr;
+    g_err[0] = 0;
+    if (!prm || !counts) return fail(GSR_ERR_ARGUMENT, "densify_plan: null params/counts");
+    if (P < 0) return fail(GSR_ERR_ARGUMENT, "densify_plan: P must be >= 0");
+    for (int k = 0; k < GSR_DENSIFY_NCOUNTS; k++) counts[k] = 0;
+    if (P == 0) return GSR_OK;
+    if (!grad_accum || !denom || !opacity || !scaling || !scratch)
+        return fail(GSR_ERR_ARGUMENT, "densify_plan: null pointer");
+    if (prm->split_n < 1 || prm->split_n > 64) return fail(GSR_ERR_ARGUMENT, "densify_plan: split N = %d", prm->split_n);
+    DensifyArgs a{};
+    a.P = P;
+    a.accum = grad_accum; a.denom = denom; a.opacity = opacity; a.scaling = scaling;
+    a.grad_threshold = prm->grad_threshold; a.clone_extent = prm->clone_extent; a.min_opacity = prm->min_opacity;
+    a.big_extent = prm->big_extent; a.split_div = prm->split_div; a.use_screen_size = prm->use_screen_size;
+    a.split_mask = split_mask;
+    densify_carve(scratch, P, a);
+    const hipStream_t s = (hipStream_t)stream;
+    HIP_TRY(launch_densify_plan(a, s), "densify_plan");
+    uint32_t tot[4] = {0, 0, 0, 0};
+    HIP_TRY(hipMemcpyAsync(tot, a.totals, sizeof(tot), hipMemcpyDeviceToHost, s), "densify_plan counts");
+    HIP_TRY(hipStreamSynchronize(s), "densify_plan sync");
+    counts[GSR_DENSIFY_KEPT] = tot[0];
+    counts[GSR_DENSIFY_CLONES] = tot[1];
+    counts[GSR_DENSIFY_CHILDREN] = tot[2];
+    counts[GSR_DENSIFY_SPLIT] = tot[3];
+    counts[GSR_DENSIFY_TOTAL] = (long long)tot[0] + tot[1] + (long long)prm->split_n * tot[2];
+    if (counts[GSR_DENSIFY_TOTAL] > 0x7fffffffLL)
+        return fail(GSR_ERR_OVERFLOW, "densify_plan: %lld Gaussians after densification", counts[GSR_DENSIFY_TOTAL]);
+    return GSR_OK;
+}
+
+int gsr_densify_apply(int P, const void* scratch, const gsr_densify_group* groups, int n_groups,
+                      const float* rotation, const float* samples, const int* tmp_radii_in, int* tmp_radii_out,
+                      const gsr_densify_params* prm, void* stream) {
+    using namespace gsr;
+    g_err[0] = 0;
+    if (!prm) return fail(GSR_ERR_ARGUMENT, "densify_apply: null params");
+    if (P < 0 || n_groups < 0 || n_groups > GSR_DENSIFY_MAX_GROUPS)
+        return fail(GSR_ERR_ARGUMENT, "densify_apply: P = %d, %d groups (0..%d)", P, n_groups, GSR_DENSIFY_MAX_GROUPS);
+    if (P == 0) return GSR_OK;
+    if (!scratch || (n_groups > 0 && !groups)) return fail(GSR_ERR_ARGUMENT, "densify_apply: null pointer");
+    if ((tmp_radii_in == nullptr) != (tmp_radii_out == nullptr))
+        return fail(GSR_ERR_ARGUMENT, "densify_apply: tmp_radii in and out must both be given or both be null");
+    DensifyArgs d{};
+    densify_carve(const_cast<void*>(scratch), P, d);
+    const hipStream_t s = (hipStream_t)stream;
+    uint32_t tot[4] = {0, 0, 0, 0};  // the plan's totals (a tiny synchronous read; the plan already synchronised)
+    HIP_TRY(hipMemcpyAsync(tot, d.totals, sizeof(tot), hipMemcpyDeviceToHost, s), "densify_apply counts");
+    HIP_TRY(hipStreamSynchronize(s), "densify_apply sync");
+    if ((unsigned long long)tot[0] + tot[1] + (unsigned long long)prm->split_n * tot[2] == 0)
+        return GSR_OK;  // everything pruned: the new arrays are empty
+    if (tot[3] > 0 && tot[2] > 0 && !samples)
+        return fail(GSR_ERR_ARGUMENT, "densify_apply: %u split Gaussians but no samples", tot[3]);
+    auto launch = [&](const void* src, void* dst, const void* sm, const void* sv, void* dm, void* dv, int width,
+                      int role, const char* what) -> int {
+        if (width <= 0) return fail(GSR_ERR_ARGUMENT, "densify_apply: %s width %d", what, width);
+        if ((size_t)P * (size_t)width > 0x7fffffffull)
+            return fail(GSR_ERR_ARGUMENT, "densify_apply: %s has more than 2^31-1 values", what);
+        if (!src || !dst) return fail(GSR_ERR_ARGUMENT, "densify_apply: %s null array", what);
+        if ((sm == nullptr) != (dm == nullptr) || (sv == nullptr) != (dv == nullptr) || (sm == nullptr) != (sv == nullptr))
+            return fail(GSR_ERR_ARGUMENT, "densify_apply: %s Adam state pointers must all be given or all be null",
+                        what);
+        if (role == GSR_DENSIFY_XYZ && (width != 3 || !rotation))
+            return fail(GSR_ERR_ARGUMENT, "densify_apply: the xyz group needs width 3 and the rotations");
+        if (role == GSR_DENSIFY_SCALING && width != 3)
+            return fail(GSR_ERR_ARGUMENT, "densify_apply: the scaling group needs width 3");
+        if (role < GSR_DENSIFY_COPY || role > GSR_DENSIFY_SCALING)
+            return fail(GSR_ERR_ARGUMENT, "densify_apply: %s role %d", what, role);
+        DensifyApplyArgs a{};
+        a.src = (const uint32_t*)src; a.dst = (uint32_t*)dst;
+        a.src_m = (const uint32_t*)sm; a.src_v = (const uint32_t*)sv; a.dst_m = (uint32_t*)dm; a.dst_v = (uint32_t*)dv;
+        a.n = (uint32_t)((size_t)P * width);
+        a.width = (uint32_t)width;
+        uint32_t l = 0;
+        while ((1u << l) < a.width) l++;
+        a.shift = 31 + l;
+        a.magic = ((1ull << a.shift) + a.width - 1) / a.width;  // exact t / width for t < 2^31
+        a.role = role;
+        a.rows = d.rows;
+        a.rotation = rotation;
+        a.samples = samples;
+        a.n_split = tot[3];
+        a.n_children = tot[2];
+        a.split_n = prm->split_n;
+        a.split_div = prm->split_div;
+        HIP_TRY(launch_densify_apply(a, s), "densify_apply");
+        return GSR_OK;
+    };
+    for (int k = 0; k < n_groups; k++) {
+        const gsr_densify_group& g = groups[k];
+        if (int rc = launch(g.src, g.dst, g.src_exp_avg, g.src_exp_avg_sq, g.dst_exp_avg, g.dst_exp_avg_sq, g.width,
+                            g.role, "group"))
+            return rc;
+    }
+    if (tmp_radii_in)
+        if (int rc = launch(tmp_radii_in, tmp_radii_out, nullptr, nullptr, nullptr, nullptr, 1, GSR_DENSIFY_COPY,
+                            "tmp_radii"))
+            return rc;
+    return GSR_OK;
 }
 
 int gsr_profile_enable(int stage_mask) {

@@ -2,6 +2,7 @@
 #pragma once
 
 #include "gsr_common.h"
+#include "../../include/gsr_densify.h"
 
 namespace gsr {
 
@@ -217,6 +218,48 @@ constexpr int kAdamThreads = 256;
 constexpr int kAdamUnroll = 2;  // float4s per thread
 constexpr uint32_t kAdamBlockElems = kAdamThreads * kAdamUnroll * 4;
 hipError_t launch_adam(const AdamArgs& a, uint32_t blocks, hipStream_t stream);
+
+// ---- adaptive density control (densify.hip) ------------------------------------------
+struct DensifyArgs {
+    int P;
+    const float* accum;
+    const float* denom;
+    const float* opacity;
+    const float* scaling;
+    float grad_threshold, clone_extent, min_opacity, big_extent, split_div;
+    int use_screen_size;
+    uint8_t* split_mask;  // may be null
+    // scratch (densify_carve)
+    int4* rows;           // [P] kept row, clone row, first child row, split rank (-1: none)
+    uint8_t* flags;       // [P]
+    uint32_t* blk;        // [blocks][4] counts, then exclusive offsets
+    uint32_t* totals;     // [4] kept, clones, children per copy, splits
+};
+struct DensifyApplyArgs {
+    const uint32_t* src;
+    uint32_t* dst;
+    const uint32_t* src_m;
+    const uint32_t* src_v;
+    uint32_t* dst_m;  // null: the group has no Adam state
+    uint32_t* dst_v;
+    uint32_t n;       // P * width
+    uint32_t width;
+    unsigned long long magic;  // t / width == (t * magic) >> shift for t < 2^31
+    uint32_t shift;
+    int role;
+    const int4* rows;
+    const float* rotation;
+    const float* samples;
+    uint32_t n_split, n_children;
+    int split_n;
+    float split_div;
+};
+size_t densify_scratch_bytes(int P);
+void densify_carve(void* scratch, int P, DensifyArgs& a);
+hipError_t launch_densify_stats(int P, const float* vgrad, const int* radii, const uint8_t* visible, float* accum,
+                                float* denom, float* max_r, hipStream_t stream);
+hipError_t launch_densify_plan(const DensifyArgs& a, hipStream_t stream);
+hipError_t launch_densify_apply(const DensifyApplyArgs& a, hipStream_t stream);
 
 // preprocess.hip
 hipError_t launch_preprocess(const PreprocessArgs& a, hipStream_t stream);
