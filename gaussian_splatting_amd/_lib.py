@@ -15,7 +15,7 @@ _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GSR_LIBRARY", os.path.join(_PKG, "lib", "libgsr.so"))
 INCLUDE_DIR = os.path.join(os.path.dirname(_PKG), "include")
 HEADER_PATH = os.path.join(INCLUDE_DIR, "gsr.h")
-HEADERS = [os.path.join(INCLUDE_DIR, h) for h in ("gsr.h", "gsr_knn.h", "gsr_ssim.h", "gsr_adam.h", "gsr_densify.h")]
+HEADERS = [os.path.join(INCLUDE_DIR, h) for h in ("gsr.h", "gsr_knn.h", "gsr_ssim.h", "gsr_adam.h", "gsr_densify.h", "gsr_ply.h")]
 
 ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
 
@@ -85,6 +85,15 @@ SIGNATURES = {
                               ctypes.POINTER(ctypes.c_longlong), _vp]),
     "gsr_densify_apply": (_i, [_i, _vp, ctypes.POINTER(DensifyGroup), _i, _vp, _vp, _vp, _vp,
                                ctypes.POINTER(DensifyParams), _vp]),
+    "gsr_ply_open": (_i, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p)]),
+    "gsr_ply_close": (None, [_vp]),
+    "gsr_ply_vertex_count": (ctypes.c_longlong, [_vp]),
+    "gsr_ply_property_count": (_i, [_vp]),
+    "gsr_ply_property_name": (ctypes.c_char_p, [_vp, _i]),
+    "gsr_ply_read_float": (_i, [_vp, _i, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_void_p),
+                                ctypes.POINTER(ctypes.c_longlong)]),
+    "gsr_ply_write": (_i, [ctypes.c_char_p, ctypes.c_longlong, _i, ctypes.POINTER(ctypes.c_char_p), ctypes.c_char_p,
+                           ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_longlong)]),
 }
 
 _lock = threading.Lock()

@@ -20,7 +20,7 @@ CSRC = os.path.join(PKG, "csrc")
 OBJ = os.path.join(PKG, "build")
 LIB_DIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIB_DIR, "libgsr.so")
-SOURCES = ["api.hip", "preprocess.hip", "binning.hip", "render.hip", "backward.hip", "knn.hip", "ssim.hip", "adam.hip", "densify.hip"]
+SOURCES = ["api.hip", "preprocess.hip", "binning.hip", "render.hip", "backward.hip", "knn.hip", "ssim.hip", "adam.hip", "densify.hip", "ply.cpp"]
 HEADERS = ["gsr_common.h", "kernels.h", "footprint.h"]
 ARCH = os.environ.get("GSR_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -30,7 +30,7 @@ CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-W
 
 def _newest_input_mtime() -> float:
     files = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(ROOT, "include", h) for h in
-                                                                  ("gsr.h", "gsr_knn.h", "gsr_ssim.h", "gsr_adam.h", "gsr_densify.h")] + [__file__]
+                                                                  ("gsr.h", "gsr_knn.h", "gsr_ssim.h", "gsr_adam.h", "gsr_densify.h", "gsr_ply.h")] + [__file__]
     return max(os.path.getmtime(f) for f in files)
 
 
@@ -41,7 +41,7 @@ FILE_FLAGS = {"render.hip": ["-fno-slp-vectorize"], "preprocess.hip": ["-fno-slp
 
 
 def _compile(src: str, objdir: str = OBJ, extra=()) -> str:
-    obj = os.path.join(objdir, src.replace(".hip", ".o"))
+    obj = os.path.join(objdir, os.path.splitext(src)[0] + ".o")
     cmd = [HIPCC, *CXXFLAGS, *FILE_FLAGS.get(src, []), *extra, "-c", os.path.join(CSRC, src), "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:

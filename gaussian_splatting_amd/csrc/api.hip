@@ -34,6 +34,21 @@ int fail(int code, const char* fmt, ...) {
     return code;
 }
 
+}  // namespace
+
+namespace gsr {
+// for host-only translation units (ply.cpp): set gsr_last_error()'s message, return `code`
+int set_error(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+}  // namespace gsr
+
+namespace {
+
 #define HIP_TRY(expr, stage)                                                                                    \
     do {                                                                                                        \
         hipError_t _e = (expr);                                                                                 \
