@@ -90,6 +90,9 @@ SIGNATURES = {
     "gsr_ply_vertex_count": (ctypes.c_longlong, [_vp]),
     "gsr_ply_property_count": (_i, [_vp]),
     "gsr_ply_property_name": (ctypes.c_char_p, [_vp, _i]),
+    "gsr_ply_property_type": (_i, [_vp, _i, ctypes.POINTER(_i), ctypes.POINTER(ctypes.c_char)]),
+    "gsr_ply_read_raw": (_i, [_vp, _i, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_void_p),
+                              ctypes.POINTER(ctypes.c_longlong)]),
     "gsr_ply_read_float": (_i, [_vp, _i, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_void_p),
                                 ctypes.POINTER(ctypes.c_longlong)]),
     "gsr_ply_write": (_i, [ctypes.c_char_p, ctypes.c_longlong, _i, ctypes.POINTER(ctypes.c_char_p), ctypes.c_char_p,

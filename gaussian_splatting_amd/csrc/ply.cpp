@@ -213,9 +213,45 @@ extern "C" const char* gsr_ply_property_name(const gsr_ply* ply, int i) {
     return ply->elems[ply->vertex].props[i].name.c_str();
 }
 
-extern "C" int gsr_ply_read_float(gsr_ply* ply, int n, const char* const* names, float* const* out,
-                                  const long long* out_stride) {
-    if (!ply || n < 0 || (n > 0 && (!names || !out || !out_stride))) return fail("ply_read: null argument");
+namespace {
+
+// store one value of column k, row v: as float32, or in the property's own type (raw)
+struct Sink {
+    void* const* out;
+    const long long* stride;
+    bool raw;
+    void from_bytes(int k, long long v, const unsigned char* p, int bytes, char kind, bool swap) const {
+        char* dst = (char*)out[k] + v * stride[k];
+        if (!raw) {
+            const float x = (float)decode(p, bytes, kind, swap);
+            memcpy(dst, &x, 4);
+        } else if (!swap) {
+            memcpy(dst, p, bytes);
+        } else {
+            for (int i = 0; i < bytes; i++) dst[i] = (char)p[bytes - 1 - i];
+        }
+    }
+    void from_double(int k, long long v, double x, int bytes, char kind) const {
+        char* dst = (char*)out[k] + v * stride[k];
+        if (!raw) {
+            const float f = (float)x;
+            memcpy(dst, &f, 4);
+            return;
+        }
+        switch (kind == 'f' ? bytes * 10 : kind == 'i' ? bytes : bytes + 100) {
+            case 40: { const float f = (float)x; memcpy(dst, &f, 4); break; }
+            case 80: memcpy(dst, &x, 8); break;
+            case 1: { const int8_t t = (int8_t)x; memcpy(dst, &t, 1); break; }
+            case 2: { const int16_t t = (int16_t)x; memcpy(dst, &t, 2); break; }
+            case 4: { const int32_t t = (int32_t)x; memcpy(dst, &t, 4); break; }
+            case 101: { const uint8_t t = (uint8_t)x; memcpy(dst, &t, 1); break; }
+            case 102: { const uint16_t t = (uint16_t)x; memcpy(dst, &t, 2); break; }
+            default: { const uint32_t t = (uint32_t)x; memcpy(dst, &t, 4); break; }
+        }
+    }
+};
+
+int read_impl(gsr_ply* ply, int n, const char* const* names, const Sink& sink) {
     const Element& V = ply->elems[ply->vertex];
     std::vector<int> col(n);
     std::vector<size_t> coff(n, 0);
@@ -235,9 +271,6 @@ extern "C" int gsr_ply_read_float(gsr_ply* ply, int n, const char* const* names,
     std::unique_ptr<FILE, FileCloser> f(fopen(ply->path.c_str(), "rb"));
     if (!f || fseek(f.get(), ply->body, SEEK_SET) != 0) return fail("ply_read: cannot reopen %s", ply->path.c_str());
     const long long N = V.count;
-    auto store = [&](int k, long long v, double x) {
-        *(float*)((char*)out[k] + v * out_stride[k]) = (float)x;
-    };
 
     if (ply->fmt == kAscii) {
         std::string line;
@@ -260,7 +293,10 @@ extern "C" int gsr_ply_read_float(gsr_ply* ply, int n, const char* const* names,
                 if (end == p) return fail("ply_read: bad ascii value at vertex %lld", v);
                 p = end;
             }
-            for (int k = 0; k < n; k++) store(k, v, vals[col[k]]);
+            for (int k = 0; k < n; k++) {
+                const Prop& pr = V.props[col[k]];
+                sink.from_double(k, v, vals[col[k]], pr.type, pr.kind);
+            }
         }
         return GSR_OK;
     }
@@ -289,10 +325,10 @@ extern "C" int gsr_ply_read_float(gsr_ply* ply, int n, const char* const* names,
     }
     if (!V.fixed()) {  // a vertex element with list properties: row by row
         std::vector<unsigned char> row;
+        std::vector<size_t> poff(V.props.size());
         for (long long v = 0; v < N; v++) {
             row.clear();
             size_t off = 0;
-            std::vector<size_t> poff(V.props.size());
             for (size_t j = 0; j < V.props.size(); j++) {
                 const Prop& p = V.props[j];
                 poff[j] = off;
@@ -311,7 +347,7 @@ extern "C" int gsr_ply_read_float(gsr_ply* ply, int n, const char* const* names,
             }
             for (int k = 0; k < n; k++) {
                 const Prop& p = V.props[col[k]];
-                store(k, v, decode(row.data() + poff[col[k]], p.type, p.kind, swap));
+                sink.from_bytes(k, v, row.data() + poff[col[k]], p.type, p.kind, swap);
             }
         }
         return GSR_OK;
@@ -326,16 +362,38 @@ extern "C" int gsr_ply_read_float(gsr_ply* ply, int n, const char* const* names,
         for (int k = 0; k < n; k++) {
             const Prop& p = V.props[col[k]];
             const unsigned char* src = buf.data() + coff[k];
-            char* dst = (char*)out[k] + v0 * out_stride[k];
-            if (p.kind == 'f' && p.type == 4 && !swap) {  // the common case: float32 little-endian
-                for (long long r = 0; r < nr; r++)
-                    memcpy(dst + r * out_stride[k], src + (size_t)r * rb, 4);
+            const long long st = sink.stride[k];
+            char* dst = (char*)sink.out[k] + v0 * st;
+            if (!swap && p.type == 4 && (sink.raw || p.kind == 'f')) {  // float32 / any 4-byte raw: moves
+                for (long long r = 0; r < nr; r++) memcpy(dst + r * st, src + (size_t)r * rb, 4);
             } else {
-                for (long long r = 0; r < nr; r++)
-                    *(float*)(dst + r * out_stride[k]) = (float)decode(src + (size_t)r * rb, p.type, p.kind, swap);
+                for (long long r = 0; r < nr; r++) sink.from_bytes(k, v0 + r, src + (size_t)r * rb, p.type, p.kind, swap);
             }
         }
     }
+    return GSR_OK;
+}
+
+}  // namespace
+
+extern "C" int gsr_ply_read_float(gsr_ply* ply, int n, const char* const* names, float* const* out,
+                                  const long long* out_stride) {
+    if (!ply || n < 0 || (n > 0 && (!names || !out || !out_stride))) return fail("ply_read: null argument");
+    return read_impl(ply, n, names, Sink{(void* const*)out, out_stride, false});
+}
+
+extern "C" int gsr_ply_read_raw(gsr_ply* ply, int n, const char* const* names, void* const* out,
+                                const long long* out_stride) {
+    if (!ply || n < 0 || (n > 0 && (!names || !out || !out_stride))) return fail("ply_read: null argument");
+    return read_impl(ply, n, names, Sink{out, out_stride, true});
+}
+
+extern "C" int gsr_ply_property_type(const gsr_ply* ply, int i, int* bytes, char* kind) {
+    if (!ply || !bytes || !kind || i < 0 || i >= (int)ply->elems[ply->vertex].props.size())
+        return fail("ply_property_type: bad argument");
+    const Prop& p = ply->elems[ply->vertex].props[i];
+    *bytes = p.type;
+    *kind = p.list ? 'l' : p.kind;
     return GSR_OK;
 }
 
@@ -346,18 +404,21 @@ extern "C" int gsr_ply_write(const char* path, long long N, int n, const char* c
     std::vector<int> bytes(n);
     size_t rb = 0;
     std::string header = "ply\nformat binary_little_endian 1.0\nelement vertex " + std::to_string(N) + "\n";
+    // column type codes as Python's struct module spells them; header names as plyfile writes them
+    static const struct { char code; int b; const char* name; } tab[] = {
+        {'b', 1, "char"}, {'B', 1, "uchar"}, {'h', 2, "short"}, {'H', 2, "ushort"},
+        {'i', 4, "int"},  {'I', 4, "uint"},  {'f', 4, "float"}, {'d', 8, "double"}};
     for (int k = 0; k < n; k++) {
         if (!names[k] || !names[k][0]) return fail("ply_write: empty property name");
-        if (types[k] == 'f') {
-            bytes[k] = 4;
-            header += std::string("property float ") + names[k] + "\n";
-        } else if (types[k] == 'B') {
-            bytes[k] = 1;
-            header += std::string("property uchar ") + names[k] + "\n";
-        } else {
-            return fail("ply_write: type '%c' of '%s' (expected 'f' or 'B')", types[k], names[k]);
-        }
-        rb += bytes[k];
+        int b = 0;
+        for (const auto& t : tab)
+            if (t.code == types[k]) {
+                b = t.b;
+                header += std::string("property ") + t.name + " " + names[k] + "\n";
+            }
+        if (!b) return fail("ply_write: type '%c' of '%s' (one of bBhHiIfd)", types[k], names[k]);
+        bytes[k] = b;
+        rb += b;
     }
     header += "end_header\n";
     std::unique_ptr<FILE, FileCloser> f(fopen(path, "wb"));
@@ -372,10 +433,12 @@ extern "C" int gsr_ply_write(const char* path, long long N, int n, const char* c
             const char* src = (const char*)columns[k] + v0 * strides[k];
             unsigned char* dst = buf.data() + off;
             const long long st = strides[k];
-            if (bytes[k] == 4)  // constant-size copies: inlined moves, not library calls
-                for (long long r = 0; r < nr; r++) memcpy(dst + (size_t)r * rb, src + r * st, 4);
-            else
-                for (long long r = 0; r < nr; r++) dst[(size_t)r * rb] = (unsigned char)src[r * st];
+            switch (bytes[k]) {  // constant-size copies: inlined moves, not library calls
+                case 1: for (long long r = 0; r < nr; r++) dst[(size_t)r * rb] = (unsigned char)src[r * st]; break;
+                case 2: for (long long r = 0; r < nr; r++) memcpy(dst + (size_t)r * rb, src + r * st, 2); break;
+                case 4: for (long long r = 0; r < nr; r++) memcpy(dst + (size_t)r * rb, src + r * st, 4); break;
+                default: for (long long r = 0; r < nr; r++) memcpy(dst + (size_t)r * rb, src + r * st, 8); break;
+            }
             off += bytes[k];
         }
         if (fwrite(buf.data(), rb, (size_t)nr, f.get()) != (size_t)nr) return fail("ply_write: write failed");

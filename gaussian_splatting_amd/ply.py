@@ -26,7 +26,7 @@ import numpy as np
 
 from . import _lib
 
-__all__ = ["read_vertex", "vertex_properties", "write_vertex", "construct_list_of_attributes", "save_ply", "load_ply",
+__all__ = ["read_vertex", "read_vertex_raw", "vertex_properties", "vertex_schema", "write_vertex", "construct_list_of_attributes", "save_ply", "load_ply",
            "store_ply", "fetch_ply", "BasicPointCloud", "install", "install_dataset_readers"]
 
 
@@ -54,6 +54,41 @@ def vertex_properties(path: str) -> Tuple[int, List[str]]:
         lib.gsr_ply_close(h)
 
 
+def vertex_schema(path: str) -> Tuple[int, List[str], List[Tuple[int, str]]]:
+    """(vertex count, property names, (bytes, kind) per property: kind 'i' / 'u' / 'f', or
+    'l' for a list property)."""
+    lib, h = _open(path)
+    try:
+        n = int(lib.gsr_ply_vertex_count(h))
+        names, types = [], []
+        for i in range(lib.gsr_ply_property_count(h)):
+            names.append(lib.gsr_ply_property_name(h, i).decode())
+            b, k = ctypes.c_int(), ctypes.c_char()
+            _lib.check(lib.gsr_ply_property_type(h, i, ctypes.byref(b), ctypes.byref(k)), "ply property type")
+            types.append((b.value, k.value.decode()))
+        return n, names, types
+    finally:
+        lib.gsr_ply_close(h)
+
+
+def read_vertex_raw(path: str, names: Sequence[str], out: Dict[str, np.ndarray]) -> None:
+    """Fill ``out[name]`` (1-D arrays, possibly strided, of the property's own size) with the
+    named vertex properties in their file types, host byte order."""
+    lib, h = _open(path)
+    try:
+        N = int(lib.gsr_ply_vertex_count(h))
+        k = len(names)
+        for n in names:
+            if out[n].ndim != 1 or out[n].shape[0] != N:
+                raise ValueError(f"output for '{n}' must be a vector of {N}")
+        c_names = (ctypes.c_char_p * k)(*[n.encode() for n in names])
+        ptrs = (ctypes.c_void_p * k)(*[out[n].ctypes.data for n in names])
+        strides = (ctypes.c_longlong * k)(*[out[n].strides[0] for n in names])
+        _lib.check(lib.gsr_ply_read_raw(h, k, c_names, ptrs, strides), f"ply read {path}")
+    finally:
+        lib.gsr_ply_close(h)
+
+
 def read_vertex(path: str, names: Sequence[str], out: Dict[str, np.ndarray] = None) -> Dict[str, np.ndarray]:
     """The named vertex properties as float32 columns (``out[name]`` may supply strided float32
     views of length N to fill in place)."""
@@ -76,9 +111,14 @@ def read_vertex(path: str, names: Sequence[str], out: Dict[str, np.ndarray] = No
         lib.gsr_ply_close(h)
 
 
-def write_vertex(path: str, columns: Sequence[Tuple[str, np.ndarray]]) -> None:
-    """One vertex element; each column a 1-D float32 ('float') or uint8 ('uchar') array (strided
-    views are fine)."""
+_CODES = {"i1": b"b", "u1": b"B", "i2": b"h", "u2": b"H", "i4": b"i", "u4": b"I", "f4": b"f", "f8": b"d"}
+
+
+def write_vertex(path: str, columns: Sequence[Tuple[str, np.ndarray]], element: str = "vertex") -> None:
+    """One vertex element; each column a 1-D numeric array of a PLY scalar type (int8 ... float64;
+    strided views such as structured-array fields are fine)."""
+    if element != "vertex":
+        raise NotImplementedError(f"only a 'vertex' element can be written, not '{element}'")
     if not columns:
         raise ValueError("write_vertex: no columns")
     N = columns[0][1].shape[0]
@@ -86,12 +126,10 @@ def write_vertex(path: str, columns: Sequence[Tuple[str, np.ndarray]]) -> None:
     for name, a in columns:
         if a.ndim != 1 or a.shape[0] != N:
             raise ValueError(f"column '{name}' must be 1-D of length {N}")
-        if a.dtype == np.float32:
-            types += b"f"
-        elif a.dtype == np.uint8:
-            types += b"B"
-        else:
-            raise ValueError(f"column '{name}': dtype {a.dtype} (float32 or uint8)")
+        code = _CODES.get(a.dtype.str[1:]) if a.dtype.byteorder in "=<|" else None
+        if code is None:
+            raise ValueError(f"column '{name}': dtype {a.dtype} is not a little-endian PLY scalar type")
+        types += code
         keep.append(a)
         names.append(name.encode())
         ptrs.append(a.ctypes.data)

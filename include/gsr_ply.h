@@ -36,13 +36,23 @@ int gsr_ply_property_count(const gsr_ply* ply);
 /* name of vertex property i (valid until gsr_ply_close) */
 const char* gsr_ply_property_name(const gsr_ply* ply, int i);
 
+/* type of vertex property i: *bytes = 1, 2, 4 or 8 and *kind = 'i' (signed), 'u' (unsigned),
+   'f' (float), or 'l' for a list property */
+int gsr_ply_property_type(const gsr_ply* ply, int i, int* bytes, char* kind);
+
+/* Read n scalar vertex properties in their own types (host byte order) */
+int gsr_ply_read_raw(gsr_ply* ply, int n, const char* const* names, void* const* out,
+                     const long long* out_stride);
+
 /* Read n vertex properties by name into float32 arrays: element v of property k goes to
    (char*)out[k] + v * out_stride[k] (bytes). */
 int gsr_ply_read_float(gsr_ply* ply, int n, const char* const* names, float* const* out,
                        const long long* out_stride);
 
 /* Write a binary little-endian PLY with one vertex element of N rows and n properties.
-   types[k]: 'f' = float32 (column of float), 'B' = uint8 (column of unsigned char).
+   types[k] (Python struct codes): 'b' int8, 'B' uint8, 'h' int16, 'H' uint16, 'i' int32, 'I' uint32,
+   'f' float32, 'd' float64; the header names them char, uchar, short, ushort, int, uint, float,
+   double, as plyfile does.
    Element v of column k is read from (const char*)columns[k] + v * strides[k] (bytes). */
 int gsr_ply_write(const char* path, long long N, int n, const char* const* names, const char* types,
                   const void* const* columns, const long long* strides);

@@ -19,8 +19,10 @@ The split's normal samples are an input (the reference draws them with torch.nor
 tests draw the same numbers for both sides).  numpy float32 arithmetic rounds every
 operation; exp/log may differ from the GPU's by an ulp, so the tests compare copies
 bitwise and computed values (children's xyz and scaling) within 1e-6.  The reference's
-own tests cover none of this: parity unpinned by reference tests; pinned by the
-reference's code as restated here and by the known-answer cases in tests/test_densify.py.
+own tests cover none of this.  Pinned (tests/test_densify.py, CPU, in the container where
+the reference is mounted) against the reference's OWN GaussianModel.densify_and_prune /
+add_densification_stats, compiled from its source with the device literal "cuda" read as
+"cpu", on the same inputs and the same torch.normal samples; and by known-answer cases.
 """
 from __future__ import annotations
 

@@ -243,3 +243,104 @@ def test_densification_stats_match_oracle(use_index_filter):
     np.testing.assert_array_equal(model.xyz_gradient_accum.cpu().numpy(), accum)
     np.testing.assert_array_equal(model.denom.cpu().numpy(), denom)
     np.testing.assert_array_equal(model.max_radii2D.cpu().numpy(), maxr)
+
+
+# ---- the reference's own densification code (this container only) ------------------------
+REF = "/root/reference"
+
+
+class _CudaToCpu(__import__("ast").NodeTransformer):
+    def visit_Constant(self, node):
+        if node.value == "cuda":
+            node.value = "cpu"
+        return node
+
+
+def _reference_gaussian_model():
+    """GaussianModel (scene/gaussian_model.py) and build_rotation / strip_symmetric / ...
+    (utils/general_utils.py) compiled from the reference's source with the literal device
+    "cuda" read as "cpu" -- the only change -- so its densification runs on this CPU-only
+    host.  (The scene package does not import here: scene/cameras.py needs cv2.)  Skipped
+    where the reference is not mounted."""
+    import ast
+    import os
+
+    if not os.path.isdir(os.path.join(REF, "scene")):
+        pytest.skip("reference not mounted")
+    from torch import nn
+
+    from gaussian_splatting_amd.ply import BasicPointCloud
+
+    ns = {"torch": torch, "nn": nn, "np": np, "os": os, "BasicPointCloud": BasicPointCloud}
+    gu = ast.parse(open(os.path.join(REF, "utils/general_utils.py")).read())
+    funcs = [n for n in gu.body if isinstance(n, ast.FunctionDef)]
+    exec(compile(_CudaToCpu().visit(ast.Module(body=funcs, type_ignores=[])), "general_utils", "exec"), ns)
+    gm = ast.parse(open(os.path.join(REF, "scene/gaussian_model.py")).read())
+    cls = [n for n in gm.body if isinstance(n, ast.ClassDef) and n.name == "GaussianModel"]
+    exec(compile(_CudaToCpu().visit(ast.Module(body=cls, type_ignores=[])), "gaussian_model", "exec"), ns)
+    return ns["GaussianModel"]
+
+
+@pytest.mark.parametrize("max_screen,moments", [(20, True), (None, True), (20, False)])
+def test_oracle_matches_reference_code(max_screen, moments):
+    """oracle/densify.py against the reference's own densify_and_prune / add_densification_stats
+    on the same inputs and the same normal samples (CPU generator, same seed, same draw)."""
+    from torch import nn
+
+    GM = _reference_gaussian_model()
+    P = 3000
+    params, mom, accum, denom = _case(P, 11, moments)
+    m = GM(3)
+    for k, a in ATTR.items():
+        setattr(m, a, nn.Parameter(torch.tensor(params[k]).requires_grad_(True)))
+    m.optimizer = torch.optim.Adam([{"params": [getattr(m, ATTR[k])], "lr": 1e-3, "name": k} for k in ATTR],
+                                   lr=0.0, eps=1e-15)
+    if mom is not None:
+        for k, a in ATTR.items():
+            m.optimizer.state[getattr(m, a)] = {"step": torch.tensor(3.0), "exp_avg": torch.tensor(mom[k][0]),
+                                                "exp_avg_sq": torch.tensor(mom[k][1])}
+    m.percent_dense = 0.01
+    # the statistics through the reference's add_densification_stats and train.py:212-213
+    rng = np.random.default_rng(12)
+    vg = rng.standard_normal((P, 3)).astype(np.float32) * 1e-3
+    radii = rng.integers(-1, 9, P).astype(np.int32)
+    m.xyz_gradient_accum = torch.tensor(accum).reshape(P, 1).clone()
+    m.denom = torch.tensor(denom).reshape(P, 1).clone()
+    m.max_radii2D = torch.zeros(P)
+    vpt = torch.zeros(P, 3, requires_grad=True)
+    vpt.grad = torch.tensor(vg)
+    vis = torch.tensor(radii) > 0
+    m.max_radii2D[vis] = torch.max(m.max_radii2D[vis], torch.tensor(radii)[vis])
+    m.add_densification_stats(vpt, vis)
+    acc_o, den_o, maxr_o = accum.reshape(P, 1).copy(), denom.reshape(P, 1).copy(), np.zeros(P, np.float32)
+    od.densification_stats(vg, acc_o, den_o, maxr_o, radii)
+    np.testing.assert_allclose(m.xyz_gradient_accum.numpy(), acc_o, rtol=1e-6, atol=0)
+    np.testing.assert_array_equal(m.denom.numpy(), den_o)
+    np.testing.assert_array_equal(m.max_radii2D.numpy(), maxr_o)
+
+    st = od.State(params, mom or {}, m.xyz_gradient_accum.numpy(), m.denom.numpy())
+    # the samples the reference will draw: same seed, same stds, same call
+    with np.errstate(divide="ignore", invalid="ignore"):
+        grads = st.accum / st.denom
+    grads[np.isnan(grads)] = 0
+    st_c = od.State(params, mom or {}, st.accum, st.denom)
+    od.densify_and_clone(st_c, grads, 2e-4, 2.0, 0.01)
+    sel = od.split_mask(st_c, grads, 2e-4, 2.0, 0.01)
+    stds = torch.exp(torch.tensor(st_c.params["scaling"][sel])).repeat(2, 1)
+    torch.manual_seed(123)
+    samples = torch.normal(mean=torch.zeros((stds.size(0), 3)), std=stds).numpy()
+    torch.manual_seed(123)
+    m.densify_and_prune(2e-4, 0.005, 2.0, max_screen, torch.ones(P, dtype=torch.int32))
+    od.densify_and_prune(st, 2e-4, 0.005, 2.0, max_screen, 0.01, samples)
+    assert m._xyz.shape[0] == st.P
+    for k, a in ATTR.items():
+        got = getattr(m, a).detach().numpy()
+        if k in ("xyz", "scaling"):
+            np.testing.assert_allclose(got, st.params[k], rtol=1e-6, atol=1e-6, err_msg=k)
+        else:
+            np.testing.assert_array_equal(got, st.params[k], err_msg=k)
+        state = m.optimizer.state.get(getattr(m, a))
+        if mom is not None:
+            np.testing.assert_array_equal(state["exp_avg"].numpy(), st.moments[k][0], err_msg=k)
+            np.testing.assert_array_equal(state["exp_avg_sq"].numpy(), st.moments[k][1], err_msg=k)
+    assert m.tmp_radii is None

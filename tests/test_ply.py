@@ -2,12 +2,15 @@
 
 The reference writes and reads its scenes with `plyfile` (scene/gaussian_model.py:288-376,
 scene/dataset_readers.py:120-143), which this image lacks, and its tests hold no PLY file:
-parity unpinned by reference fixtures.  Pinned here by the PLY 1.0 format itself (header
+no reference fixture exists.  Pinned here by the PLY 1.0 format itself (header
 bytes as plyfile emits them: "ply", "format binary_little_endian 1.0", "element vertex N",
 "property float <name>" / "property uchar <name>", "end_header"), by hand-built files in the
 other encodings the reader must accept (ascii with comments, big-endian with mixed types,
 an element with a list property before "vertex"), and by the reference's attribute order and
-SH layout.  The reader/writer is host code, so these run on the CPU except the load_ply test,
+SH layout.  Where the reference is mounted (this container), its own storePly / fetchPly /
+save_ply / construct_list_of_attributes, compiled from its source with the drop-in
+``plyfile`` package of this repository, must produce byte-identical files and identical
+arrays.  The reader/writer is host code, so these run on the CPU except the load_ply test,
 which creates the parameters on the GPU as the reference does.
 """
 import os
@@ -145,3 +148,72 @@ def test_load_ply_roundtrip(tmp_path):
         assert got.is_cuda and got.requires_grad and got.is_contiguous()
         assert torch.equal(got.detach().cpu(), getattr(src, a)), a
     assert dst.active_sh_degree == 3
+
+
+# ---- the reference's own PLY code, run through the drop-in plyfile (this container only) ----
+REF = "/root/reference"
+
+
+def _reference_functions():
+    """The reference's PLY functions, compiled from its source files with this repository's
+    drop-in ``plyfile`` in their globals: ``storePly`` / ``fetchPly``
+    (scene/dataset_readers.py:120-143) and ``GaussianModel.construct_list_of_attributes`` /
+    ``save_ply`` (scene/gaussian_model.py:288-321).  (The ``scene`` package itself does not
+    import here: scene/cameras.py needs cv2.)  Skipped where the reference is not mounted
+    (the GPU box)."""
+    import ast
+    import sys
+
+    if not os.path.isdir(os.path.join(REF, "scene")):
+        pytest.skip("reference not mounted")
+    import plyfile
+
+    assert os.path.dirname(os.path.dirname(plyfile.__file__)) == os.path.dirname(os.path.dirname(__file__))
+    ns = {"np": np, "os": os, "PlyData": plyfile.PlyData, "PlyElement": plyfile.PlyElement,
+          "BasicPointCloud": ply.BasicPointCloud, "mkdir_p": lambda d: os.makedirs(d, exist_ok=True)}
+    wanted = {"storePly", "fetchPly", "construct_list_of_attributes", "save_ply"}
+    for f in ("scene/dataset_readers.py", "scene/gaussian_model.py"):
+        tree = ast.parse(open(os.path.join(REF, f)).read())
+        for node in ast.walk(tree):
+            if isinstance(node, ast.FunctionDef) and node.name in wanted and node.name not in ns:
+                mod = ast.Module(body=[node], type_ignores=[])
+                exec(compile(mod, os.path.join(REF, f), "exec"), ns)
+    assert wanted <= set(ns), wanted - set(ns)
+    return ns
+
+
+def test_reference_store_fetch_through_dropin(tmp_path):
+    """scene/dataset_readers.py storePly / fetchPly (the reference's code) against ours."""
+    ref = _reference_functions()
+    rng = np.random.default_rng(4)
+    xyz = rng.standard_normal((500, 3))
+    rgb = rng.integers(0, 256, (500, 3)).astype(np.uint8)
+    a, b = str(tmp_path / "ref.ply"), str(tmp_path / "ours.ply")
+    ref["storePly"](a, xyz, rgb)
+    ply.store_ply(b, xyz, rgb)
+    assert open(a, "rb").read() == open(b, "rb").read()
+    ra, rb = ref["fetchPly"](a), ply.fetch_ply(a)
+    for x, y in zip(ra, rb):
+        assert x.dtype == y.dtype
+        np.testing.assert_array_equal(x, y)
+
+
+def test_reference_save_ply_through_dropin(tmp_path):
+    """GaussianModel.save_ply (the reference's code, CPU tensors) writes the same bytes as
+    ply.save_ply, and plyfile.PlyData.read sees what load_ply expects."""
+    ref = _reference_functions()
+    rng = np.random.default_rng(5)
+    src = _CpuModel(257, 3, rng)
+    src.construct_list_of_attributes = lambda: ref["construct_list_of_attributes"](src)
+    a, b = str(tmp_path / "ref" / "point_cloud.ply"), str(tmp_path / "ours.ply")
+    ref["save_ply"](src, a)
+    ply.save_ply(src, b)
+    assert open(a, "rb").read() == open(b, "rb").read()
+    assert ref["construct_list_of_attributes"](src) == ply.construct_list_of_attributes(src)
+    from plyfile import PlyData
+
+    pd = PlyData.read(a)
+    el = pd.elements[0]
+    assert len(el) == 257 and el["f_rest_44"].dtype == np.float32
+    np.testing.assert_array_equal(el["f_rest_44"], src._features_rest.numpy()[:, 14, 2])
+    assert [p.name for p in el.properties] == ply.construct_list_of_attributes(src)
