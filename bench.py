@@ -31,7 +31,7 @@ sys.path.insert(0, ROOT)
 
 from gaussian_splatting_amd import _C, _lib  # noqa: E402
 from gaussian_splatting_amd import synthetic as syn  # noqa: E402
-from gaussian_splatting_amd.distributed import GradArena  # noqa: E402
+from gaussian_splatting_amd.distributed import GradArena, ViewExchange  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 # HBM bytes per launch measured with rocprofv3 PMC passes (scripts/pmc_session.sh -> tools/pmc_summary.py);
@@ -96,6 +96,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="1m_1080p_sh3", choices=sorted(syn.CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--exchange", choices=("auto", "views", "allreduce"), default="auto",
+                    help="N > 1: all-gather the view blocks or all-reduce the parameter gradients; auto = views "
+                         "up to 4 ranks, all-reduce beyond (DESIGN.md section 7)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--ramp-seconds", type=float, default=0.3,
                     help="untimed steps before the warmup, until the GPU clock has ramped up (DVFS)")
@@ -104,10 +107,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # GSR_BENCH_SHARE_GPU=1 (rehearsal on a one-GPU box only): every rank on cuda:0, gloo
+    # collectives -- exercises the N > 1 code path, not its speed
+    rehearse = os.environ.get("GSR_BENCH_SHARE_GPU", "0") == "1"
+    gpu = 0 if rehearse else local_rank
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     cfg = syn.CONFIGS[args.config]
     P, W, H, Kdeg = cfg["P"], cfg["width"], cfg["height"], cfg["sh_degree"]
@@ -119,18 +129,26 @@ def main():
     bg = torch.zeros(3, device=dev)
     empty = torch.empty(0, device=dev)
     arena = GradArena(P, scene.shs.shape[1], dev)
+    views = world > 1 and (args.exchange == "views" or (args.exchange == "auto" and world <= 4))
+    ex = ViewExchange(P, dev) if views else None
 
     def step():
         fwd = _C.rasterize_gaussians(bg, scene.means3D, empty, scene.opacities, scene.scales, scene.rotations, 1.0,
                                      empty, cam.viewmatrix, cam.projmatrix, cam.tanfovx, cam.tanfovy, H, W, scene.shs,
                                      Kdeg, cam.campos, False, False, False)
         nr, color, radii, geom, binning, img, invd = fwd
-        _C.rasterize_gaussians_backward(bg, scene.means3D, radii, empty, scene.opacities, scene.scales,
-                                        scene.rotations, 1.0, empty, cam.viewmatrix, cam.projmatrix, cam.tanfovx,
-                                        cam.tanfovy, gc, gd, scene.shs, Kdeg, cam.campos, geom, nr, binning, img,
-                                        False, False, out=arena.views())
-        if world > 1:
-            arena.all_reduce()
+        bwd = (bg, scene.means3D, radii, empty, scene.opacities, scene.scales, scene.rotations, 1.0, empty,
+               cam.viewmatrix, cam.projmatrix, cam.tanfovx, cam.tanfovy, gc, gd, scene.shs, Kdeg, cam.campos, geom, nr,
+               binning, img, False, False)
+        if views:  # N > 1: exchange the 44-B view blocks, every rank sums all views' gradients
+            _C.rasterize_gaussians_backward_screen(*bwd, view_block=ex.local_block())
+            ex.exchange()
+            _C.gauss_backward_views(scene.means3D, None, scene.shs, Kdeg, scene.opacities, scene.scales,
+                                    scene.rotations, 1.0, ex.gathered, out=arena.views())
+        else:
+            _C.rasterize_gaussians_backward(*bwd, out=arena.views())
+            if world > 1:
+                arena.all_reduce()
         return nr
 
     # Untimed clock ramp: the GPU lowers its clock when idle and takes ~0.1 s of load to come back
@@ -203,7 +221,8 @@ def main():
             "data": "synthetic (frustum-uniform Gaussians, SURVEY.md 8d; seed 0)",
             "config": {"workload": args.config, "gaussians": P, "width": W, "height": H, "sh_degree": Kdeg,
                        "num_rendered": nr, "views": "one per GPU, yaw 5 deg x rank",
-                       "parallelism": f"view-sharded x{world}" + (" + RCCL all-reduce" if world > 1 else "")},
+                       "parallelism": f"view-sharded x{world}" + (
+                           "" if world == 1 else " + RCCL all-gather of view blocks" if views else " + RCCL all-reduce")},
             "roofline": {"kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "algorithmic_bytes_per_launch": alg, "mean_launch_ms": dom_ms},

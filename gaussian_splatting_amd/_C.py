@@ -20,7 +20,8 @@ import torch
 
 from . import _lib
 
-__all__ = ["rasterize_gaussians", "rasterize_gaussians_backward", "mark_visible", "adamUpdate", "fusedssim",
+__all__ = ["rasterize_gaussians", "rasterize_gaussians_backward", "rasterize_gaussians_backward_screen",
+           "gauss_backward_views", "view_block_floats", "mark_visible", "adamUpdate", "fusedssim",
            "fusedssim_backward"]
 
 
@@ -283,6 +284,100 @@ def rasterize_gaussians_backward(*args, out=None):
         rc = fn(*head, *sh_args, *mid, *sh_grads, *tail)
     _lib.check(rc, "rasterize_gaussians_backward")
     return result
+
+
+def view_block_floats(P: int) -> int:
+    """Floats in one view block (include/gsr.h, multi-GPU view exchange)."""
+    return int(_lib.load().gsr_view_block_floats(int(P)))
+
+
+def rasterize_gaussians_backward_screen(*args, view_block: torch.Tensor) -> None:
+    """The backward of ``rasterize_gaussians_backward`` up to the per-Gaussian render-gradient
+    sums, written with the camera into ``view_block`` (a float32 tensor of
+    ``view_block_floats(P)`` values; include/gsr.h ``gsr_rasterize_backward_screen``).
+    Arguments as ``rasterize_gaussians_backward`` (24, or 25 with ``dc``); colours from SH and
+    cov3D from scales / rotations.  The rest of the backward, over any number of gathered
+    views, is ``gauss_backward_views``."""
+    if len(args) == 25:
+        (background, means3D, radii, colors, opacities, scales, rotations, scale_modifier, cov3D_precomp, viewmatrix,
+         projmatrix, tan_fovx, tan_fovy, dL_dout_color, dL_dout_invdepth, dc, sh, degree, campos, geomBuffer, R,
+         binningBuffer, imageBuffer, antialiasing, debug) = args
+    elif len(args) == 24:
+        (background, means3D, radii, colors, opacities, scales, rotations, scale_modifier, cov3D_precomp, viewmatrix,
+         projmatrix, tan_fovx, tan_fovy, dL_dout_color, dL_dout_invdepth, sh, degree, campos, geomBuffer, R,
+         binningBuffer, imageBuffer, antialiasing, debug) = args
+        dc = None
+    else:
+        raise TypeError(f"rasterize_gaussians_backward_screen(): expected 24 or 25 positional arguments, got {len(args)}")
+    if _present(colors) or _present(cov3D_precomp):
+        raise RuntimeError("rasterize_gaussians_backward_screen: precomputed colours / cov3D are per view; "
+                           "use rasterize_gaussians_backward")
+    _require_device(means3D, "means3D")
+    device = means3D.device
+    P = means3D.size(0)
+    nb = view_block_floats(P)
+    if (view_block.dtype != torch.float32 or not view_block.is_contiguous() or view_block.numel() != nb
+            or view_block.device != device):
+        raise RuntimeError(f"view_block must be a contiguous float32 tensor of {nb} values on {device}")
+    if P == 0:
+        return
+    lib = _lib.load()
+    H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))
+    M = sh.size(1) if _present(sh) else 0
+    has_inv = dL_dout_invdepth is not None and dL_dout_invdepth.numel() != 0 and dL_dout_invdepth.size(0) != 0
+    ins = _Inputs(device)
+    scratch = torch.empty(0, dtype=torch.uint8, device=device)
+    rs = _Resizer(scratch)
+    with torch.cuda.device(device):
+        rc = lib.gsr_rasterize_backward_screen(
+            P, int(degree), M, int(R), ins.req(background, "bg", small=True), W, H, ins.req(means3D, "means3D"),
+            ins.opt(dc, "dc") if _present(dc) else None, ins.opt(sh, "sh"), ins.req(opacities, "opacities"),
+            ins.req(scales, "scales"), float(scale_modifier), ins.req(rotations, "rotations", align16=True),
+            ins.req(viewmatrix, "viewmatrix", small=True), ins.req(projmatrix, "projmatrix", small=True),
+            ins.req(campos if campos.device.type == "cuda" else campos.to(device), "campos"),
+            float(tan_fovx), float(tan_fovy), radii.contiguous().data_ptr(), geomBuffer.data_ptr(),
+            binningBuffer.data_ptr() if binningBuffer.numel() else None, imageBuffer.data_ptr(),
+            ins.req(dL_dout_color, "dL_dout_color"),
+            ins.req(dL_dout_invdepth, "dL_dout_invdepth") if has_inv else None,
+            int(bool(antialiasing)), int(bool(debug)), rs.cb, None, _stream_handle(device),
+            int(getattr(binningBuffer, "_gsr_capacity", 0)), int(binningBuffer.numel()), view_block.data_ptr())
+    _lib.check(rc, "rasterize_gaussians_backward_screen")
+
+
+def gauss_backward_views(means3D, dc, sh, degree, opacities, scales, rotations, scale_modifier, blocks, out) -> None:
+    """The per-Gaussian backward summed over ``blocks`` ([n_views, view_block_floats(P)] float32,
+    e.g. an all-gathered exchange buffer), written into ``out`` (names as the ``out=`` of
+    ``rasterize_gaussians_backward``: dL_dmeans3D, dL_ddc (when dc is given), dL_dsh,
+    dL_dopacity, dL_dscales, dL_drotations; contiguous float32)."""
+    _require_device(means3D, "means3D")
+    device = means3D.device
+    P = means3D.size(0)
+    nb = view_block_floats(P)
+    if blocks.dim() != 2 or blocks.size(1) != nb or blocks.dtype != torch.float32 or not blocks.is_contiguous():
+        raise RuntimeError(f"blocks must be a contiguous float32 [n_views, {nb}] tensor")
+    M = sh.size(1) if _present(sh) else 0
+    need = {"dL_dmeans3D": (P, 3), "dL_dsh": (P, M, 3), "dL_dopacity": (P, 1), "dL_dscales": (P, 3),
+            "dL_drotations": (P, 4)}
+    if _present(dc):
+        need["dL_ddc"] = (P, 1, 3)
+    for k, shp in need.items():
+        t = out.get(k)
+        if t is None or tuple(t.shape) != shp or t.dtype != torch.float32 or not t.is_contiguous() or t.device != device:
+            raise RuntimeError(f"out[{k}] must be a contiguous float32 {shp} tensor on {device}")
+    if P == 0:
+        return
+    lib = _lib.load()
+    ins = _Inputs(device)
+    with torch.cuda.device(device):
+        rc = lib.gsr_gauss_backward_views(
+            P, int(degree), M, ins.req(means3D, "means3D"), ins.opt(dc, "dc") if _present(dc) else None,
+            ins.opt(sh, "sh"), ins.req(opacities, "opacities"), ins.req(scales, "scales"),
+            ins.req(rotations, "rotations", align16=True), float(scale_modifier), int(blocks.size(0)),
+            blocks.data_ptr(), nb, out["dL_dmeans3D"].data_ptr(),
+            out["dL_ddc"].data_ptr() if _present(dc) else None, out["dL_dsh"].data_ptr() if M > 0 else None,
+            out["dL_dopacity"].data_ptr(), out["dL_dscales"].data_ptr(), out["dL_drotations"].data_ptr(),
+            _stream_handle(device))
+    _lib.check(rc, "gauss_backward_views")
 
 
 def mark_visible(means3D, viewmatrix, projmatrix) -> torch.Tensor:

@@ -68,6 +68,12 @@ SIGNATURES = {
                                        _vp, _vp, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                        _vp, _vp, _vp, _vp, _vp, _i, _i, ALLOC_FN, _vp, _vp, _i, ctypes.c_size_t]),
     "gsr_mark_visible": (_i, [_i, _vp, _vp, _vp, _vp, _vp]),
+    "gsr_view_block_floats": (ctypes.c_ulonglong, [_i]),
+    "gsr_rasterize_backward_screen": (_i, [_i, _i, _i, _i, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp,
+                                           _vp, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, ALLOC_FN, _vp, _vp, _i,
+                                           ctypes.c_size_t, _vp]),
+    "gsr_gauss_backward_views": (_i, [_i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _f, _i, _vp, ctypes.c_longlong, _vp,
+                                      _vp, _vp, _vp, _vp, _vp, _vp]),
     "gsr_last_error": (ctypes.c_char_p, []),
     "gsr_version": (ctypes.c_char_p, []),
     "gsr_profile_enable": (_i, [_i]),

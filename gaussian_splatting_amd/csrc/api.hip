@@ -742,28 +742,35 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
                   const float* dL_dinvdepths, float* dL_dmean2D, float* dL_dconic, float* dL_dopacity,
                   float* dL_dcolor, float* dL_dinvdepth, float* dL_dmean3D, float* dL_dcov3D, float* dL_ddc,
                   float* dL_dsh, float* dL_dscale, float* dL_drot, int antialiasing, int debug, gsr_alloc_fn scratch_alloc,
-                  void* scratch_ctx, void* stream_, int binning_capacity, size_t binning_bytes) {
+                  void* scratch_ctx, void* stream_, int binning_capacity, size_t binning_bytes,
+                  float* view_block = nullptr) {
     using namespace gsr;
     g_err[0] = 0;
     hipStream_t stream = (hipStream_t)stream_;
+    // view_block: screen-space backward only -- the render-gradient sums, flags and camera go
+    // into the block (gsr_rasterize_backward_screen) and the per-Gaussian backward is skipped
+    const bool screen = view_block != nullptr;
     if (P < 0 || R < 0 || width <= 0 || height <= 0)
         return fail(GSR_ERR_ARGUMENT, "rasterize_backward: invalid sizes P=%d R=%d W=%d H=%d", P, R, width, height);
     if (P == 0) return GSR_OK;
     if (!geom_buffer || !image_buffer || (R > 0 && !binning_buffer))
         return fail(GSR_ERR_ARGUMENT, "rasterize_backward: missing forward buffers");
-    if (!means3D || !opacities || !radii || !dL_dpix || !dL_dmean2D || !dL_dopacity || !dL_dcolor || !dL_dmean3D ||
-        !dL_dcov3D || !viewmatrix || !projmatrix || !background)
+    if (!means3D || !opacities || !radii || !dL_dpix || !viewmatrix || !projmatrix || !background || !campos)
         return fail(GSR_ERR_ARGUMENT, "rasterize_backward: missing required pointer");
-    if (!colors_precomp && shs && (!dL_dsh || !campos))
-        return fail(GSR_ERR_ARGUMENT, "rasterize_backward: SH gradient needs dL_dsh");
-    if (!colors_precomp && dc && (!dL_ddc || !campos))
-        return fail(GSR_ERR_ARGUMENT, "rasterize_backward: dc gradient needs dL_ddc");
+    if (!screen) {
+        if (!dL_dmean2D || !dL_dopacity || !dL_dcolor || !dL_dmean3D || !dL_dcov3D)
+            return fail(GSR_ERR_ARGUMENT, "rasterize_backward: missing required output");
+        if (!colors_precomp && shs && !dL_dsh)
+            return fail(GSR_ERR_ARGUMENT, "rasterize_backward: SH gradient needs dL_dsh");
+        if (!colors_precomp && dc && !dL_ddc)
+            return fail(GSR_ERR_ARGUMENT, "rasterize_backward: dc gradient needs dL_ddc");
+        if (scales && (!rotations || !dL_dscale || !dL_drot))
+            return fail(GSR_ERR_ARGUMENT, "rasterize_backward: scale/rotation gradients need outputs");
+        if ((dL_dinvdepths == nullptr) != (dL_dinvdepth == nullptr))
+            return fail(GSR_ERR_ARGUMENT, "rasterize_backward: dL_dinvdepths and dL_dinvdepth go together");
+    }
     if (dc && M > 0 && !shs) return fail(GSR_ERR_ARGUMENT, "rasterize_backward: %d rest SH coefficients but no shs", M);
     if (dc) M += 1;  // as in the forward
-    if (scales && (!rotations || !dL_dscale || !dL_drot))
-        return fail(GSR_ERR_ARGUMENT, "rasterize_backward: scale/rotation gradients need outputs");
-    if ((dL_dinvdepths == nullptr) != (dL_dinvdepth == nullptr))
-        return fail(GSR_ERR_ARGUMENT, "rasterize_backward: dL_dinvdepths and dL_dinvdepth go together");
 
     const float focal_y = height / (2.0f * tan_fovy);
     const float focal_x = width / (2.0f * tan_fovx);
@@ -790,6 +797,14 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
     char* rbase = (char*)call_alloc(scratch_alloc, scratch_ctx, rec_bytes);
     if (!rbase) return fail(GSR_ERR_ALLOC, "rasterize_backward: scratch allocation failed");
     carve_recs(rbase, (size_t)R, (size_t)P, &recs, &sums, &rec_bytes);
+    uint32_t* flags = nullptr;
+    if (screen) {  // the sums and flags go to the view block (gsr_common.h "View block")
+        float* body = view_block + kViewBlockHeader;
+        sums.a = reinterpret_cast<float4*>(body);
+        sums.b = reinterpret_cast<float4*>(body + 4 * (size_t)P);
+        sums.c = reinterpret_cast<float2*>(body + 8 * (size_t)P);
+        flags = reinterpret_cast<uint32_t*>(body + 10 * (size_t)P);
+    }
 
     if (R > 0) {
         StageScope sc(ST_RENDER_BWD, stream);
@@ -805,9 +820,15 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
     if (int rc = check_debug(debug, stream, "render_bwd")) return rc;
     {
         StageScope sc(ST_GAUSS_REDUCE, stream);
-        HIP_TRY(launch_gauss_reduce(P, geom, gx, img.lim_key, recs, sums, stream), "gauss_reduce");
+        HIP_TRY(launch_gauss_reduce(P, geom, gx, img.lim_key, recs, sums, flags, radii, stream), "gauss_reduce");
     }
     if (int rc = check_debug(debug, stream, "gauss_reduce")) return rc;
+    if (screen) {
+        HIP_TRY(launch_view_header(view_block, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, focal_x, focal_y,
+                                   antialiasing, dL_dinvdepths != nullptr, stream),
+                "view header");
+        return check_debug(debug, stream, "view header");
+    }
     {
         StageScope sc(ST_GAUSS_BWD, stream);
         GaussBwdArgs ga{};
@@ -905,3 +926,58 @@ int gsr_rasterize_backward_dc(int P, int D, int M, int R, const float* backgroun
 }
 
 }  // extern "C"
+
+// ---- multi-GPU view exchange (include/gsr.h) -----------------------------------------
+unsigned long long gsr_view_block_floats(int P) { return P > 0 ? gsr::view_block_floats((size_t)P) : 0ull; }
+
+int gsr_rasterize_backward_screen(int P, int D, int M, int R, const float* background, int width, int height,
+                                  const float* means3D, const float* dc, const float* shs, const float* opacities,
+                                  const float* scales, float scale_modifier, const float* rotations,
+                                  const float* viewmatrix, const float* projmatrix, const float* campos,
+                                  float tan_fovx, float tan_fovy, const int* radii, void* geom_buffer,
+                                  void* binning_buffer, void* image_buffer, const float* dL_dpix,
+                                  const float* dL_dinvdepths, int antialiasing, int debug, gsr_alloc_fn scratch_alloc,
+                                  void* scratch_ctx, void* stream, int binning_capacity, size_t binning_bytes,
+                                  float* view_block) {
+    if (!view_block) return fail(GSR_ERR_ARGUMENT, "rasterize_backward_screen: null view block");
+    if ((reinterpret_cast<uintptr_t>(view_block) & 15) != 0)
+        return fail(GSR_ERR_ARGUMENT, "rasterize_backward_screen: view block must be 16-byte aligned");
+    return backward_impl(P, D, M, R, background, width, height, means3D, dc, shs, nullptr, opacities, scales,
+                         scale_modifier, rotations, nullptr, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, radii,
+                         geom_buffer, binning_buffer, image_buffer, dL_dpix, dL_dinvdepths, nullptr, nullptr, nullptr,
+                         nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, antialiasing, debug,
+                         scratch_alloc, scratch_ctx, stream, binning_capacity, binning_bytes, view_block);
+}
+
+int gsr_gauss_backward_views(int P, int D, int M, const float* means3D, const float* dc, const float* shs,
+                             const float* opacities, const float* scales, const float* rotations, float scale_modifier,
+                             int n_views, const float* blocks, long long block_floats, float* dL_dmean3D,
+                             float* dL_ddc, float* dL_dsh, float* dL_dopacity, float* dL_dscale, float* dL_drot,
+                             void* stream) {
+    using namespace gsr;
+    g_err[0] = 0;
+    if (P < 0 || n_views < 0) return fail(GSR_ERR_ARGUMENT, "gauss_backward_views: P=%d views=%d", P, n_views);
+    if (P == 0) return GSR_OK;
+    if ((size_t)block_floats != view_block_floats((size_t)P))
+        return fail(GSR_ERR_ARGUMENT, "gauss_backward_views: block of %lld floats, expected %zu", block_floats,
+                    view_block_floats((size_t)P));
+    if (!means3D || !opacities || !scales || !rotations || (n_views > 0 && !blocks) || !dL_dmean3D || !dL_dopacity ||
+        !dL_dscale || !dL_drot)
+        return fail(GSR_ERR_ARGUMENT, "gauss_backward_views: null pointer");
+    if (D < 0 || D > 3) return fail(GSR_ERR_ARGUMENT, "gauss_backward_views: SH degree %d", D);
+    if (dc && M > 0 && !shs) return fail(GSR_ERR_ARGUMENT, "gauss_backward_views: rest SH without shs");
+    if ((shs && !dL_dsh) || (dc && !dL_ddc)) return fail(GSR_ERR_ARGUMENT, "gauss_backward_views: missing SH outputs");
+    if (!dc && !shs) return fail(GSR_ERR_ARGUMENT, "gauss_backward_views: needs SH (precomputed colours are per view)");
+    ViewsBwdArgs a{};
+    a.P = P; a.D = D; a.M = dc ? M + 1 : M;
+    a.means3D = means3D; a.shs = (dc && M == 0) ? nullptr : shs; a.dc = dc; a.opacities = opacities; a.scales = scales;
+    a.rotations = rotations; a.scale_modifier = scale_modifier; a.n_views = n_views; a.blocks = blocks;
+    a.block_floats = (size_t)block_floats;
+    a.dL_dmean3D = dL_dmean3D; a.dL_dsh = a.shs ? dL_dsh : nullptr; a.dL_ddc = dc ? dL_ddc : nullptr;
+    a.dL_dopacity = dL_dopacity; a.dL_dscale = dL_dscale; a.dL_drot = dL_drot;
+    {
+        StageScope sc(ST_GAUSS_BWD, (hipStream_t)stream);
+        HIP_TRY(launch_gauss_bwd_views(a, (hipStream_t)stream), "gauss_backward_views");
+    }
+    return GSR_OK;
+}

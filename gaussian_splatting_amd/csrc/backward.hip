@@ -118,7 +118,9 @@ __global__ void __launch_bounds__(64) gauss_reduce_kernel(int P, const uint32_t*
                                                           const uint2* __restrict__ rect,
                                                           const uint32_t* __restrict__ depth_key, uint32_t gx,
                                                           const unsigned long long* __restrict__ lim_key,
-                                                          GradRecs recs, GradRecs sums) {
+                                                          GradRecs recs, GradRecs sums, uint32_t* __restrict__ flags,
+                                                          const int* __restrict__ radii,
+                                                          const uint8_t* __restrict__ clamped) {
     __shared__ __attribute__((aligned(16))) float s_rec[64 * kRecStride];
     const int g = blockIdx.x * 64 + (int)threadIdx.x;
     float4 sa, sb;
@@ -129,14 +131,17 @@ __global__ void __launch_bounds__(64) gauss_reduce_kernel(int P, const uint32_t*
         sums.a[g] = sa;
         sums.b[g] = sb;
         sums.c[g] = sc;
+        // view-block flag word (gauss_bwd_views_kernel): bit 0 visible, bits 1-3 the SH clamp mask
+        if (flags) flags[g] = (radii[g] > 0 ? 1u : 0u) | ((uint32_t)(clamped[g] & 7u) << 1);
     }
 }
 
 hipError_t launch_gauss_reduce(int P, const GeomState& g, uint32_t gx, const unsigned long long* lim_key,
-                               const GradRecs& recs, const GradRecs& sums, hipStream_t stream) {
+                               const GradRecs& recs, const GradRecs& sums, uint32_t* flags, const int* radii,
+                               hipStream_t stream) {
     if (P == 0) return hipSuccess;
     hipLaunchKernelGGL(gauss_reduce_kernel, dim3((P + 63) / 64), dim3(64), 0, stream, P, g.rec_start, g.tiles_touched,
-                       g.rect, g.depth_key, gx, lim_key, recs, sums);
+                       g.rect, g.depth_key, gx, lim_key, recs, sums, flags, radii, g.clamped);
     return hipGetLastError();
 }
 
@@ -222,6 +227,223 @@ __device__ __forceinline__ void store3(float* p, int i, float x, float y, float 
 }
 
 constexpr int kShStride = 52;  // padded LDS row stride: conflict-free ds_read/write_b128
+
+// ---- per-view gradient math (one Gaussian, one view) ----------------------------
+// computeCov2DCUDA with its re-derived tail, the screen-space mean chain, the SH colour
+// backward and the scale/rotation backward, from the view's summed render gradients.
+// Used once per (Gaussian, view) by gauss_bwd_views_kernel.  It is the same math as
+// gauss_bwd_kernel's body, which keeps its own inline copy: there the outputs are stored as
+// soon as they are formed, and routing the single-view kernel through this function
+// measured 118 -> 124 us (r1af).  Keep the two in step.
+struct ViewCam {
+    const float* V;       // viewmatrix, 16 floats (column-major)
+    const float* Pm;      // projmatrix
+    const float* campos;  // 3
+    float tan_fovx, tan_fovy, focal_x, focal_y;
+    int antialiasing, have_invdepth;
+};
+struct GaussIn {
+    float3 mean;
+    bool have_scales;
+    float3 sc3;            // scales (when have_scales)
+    float4 q;              // rotation (when have_scales)
+    const float* cov3D;    // 6 floats, or null
+    float scale_modifier;
+    float opacity;         // for the AA chain
+};
+struct ViewOut {
+    float3 dmean;
+    float dop;
+    float dcov[6];
+    float3 dscale;
+    float4 drot;
+};
+
+template <class ShAcc>
+__device__ __forceinline__ void view_backward(const ViewCam& c, const GaussIn& gi, float4 sa, float4 sb, float2 sc,
+                                              uint8_t cm, bool do_sh, int D, int M, const ShAcc& sh, ViewOut& o) {
+    const float3 dcol = make_float3(sa.x, sa.y, sa.z);
+    const float dinvd = sa.w;
+    const float m2x = sb.x, m2y = sb.y;
+    float dop = sb.z;
+    const float dca = sc.x, dcb = sb.w, dcc = sc.y;  // dL/dconic, the reference's convention
+    // ---- computeCov2DCUDA
+    const float* V = c.V;
+    const float3 mean = gi.mean;
+    float3 t = xform_point_4x3(mean, V);
+    const float limx = 1.3f * c.tan_fovx, limy = 1.3f * c.tan_fovy;
+    const float txtz = t.x / t.z, tytz = t.y / t.z;
+    t.x = fminf(limx, fmaxf(-limx, txtz)) * t.z;
+    t.y = fminf(limy, fmaxf(-limy, tytz)) * t.z;
+    const float x_grad_mul = txtz < -limx || txtz > limx ? 0.f : 1.f;
+    const float y_grad_mul = tytz < -limy || tytz > limy ? 0.f : 1.f;
+    const float fx = c.focal_x, fy = c.focal_y;
+    const float j00 = fx / t.z, j02 = -(fx * t.x) / (t.z * t.z);
+    const float j11 = fy / t.z, j12 = -(fy * t.y) / (t.z * t.z);
+    // A = J * Rv, rows A0 (x) and A1 (y); Rv rows (V0,V4,V8) (V1,V5,V9) (V2,V6,V10)
+    const float A0[3] = {j00 * V[0] + j02 * V[2], j00 * V[4] + j02 * V[6], j00 * V[8] + j02 * V[10]};
+    const float A1[3] = {j11 * V[1] + j12 * V[2], j11 * V[5] + j12 * V[6], j11 * V[9] + j12 * V[10]};
+
+    float cov[6];
+    const float3 sc3 = gi.sc3;
+    const float4 q = gi.q;
+    if (gi.cov3D) {
+        for (int k = 0; k < 6; k++) cov[k] = gi.cov3D[k];
+    } else {
+        const float r_ = q.x, x = q.y, y = q.z, z = q.w;
+        const float sx = gi.scale_modifier * sc3.x, sy = gi.scale_modifier * sc3.y, sz = gi.scale_modifier * sc3.z;
+        const float L00 = (1.f - 2.f * (y * y + z * z)) * sx, L01 = 2.f * (x * y - r_ * z) * sy,
+                    L02 = 2.f * (x * z + r_ * y) * sz;
+        const float L10 = 2.f * (x * y + r_ * z) * sx, L11 = (1.f - 2.f * (x * x + z * z)) * sy,
+                    L12 = 2.f * (y * z - r_ * x) * sz;
+        const float L20 = 2.f * (x * z - r_ * y) * sx, L21 = 2.f * (y * z + r_ * x) * sy,
+                    L22 = (1.f - 2.f * (x * x + y * y)) * sz;
+        cov[0] = L00 * L00 + L01 * L01 + L02 * L02;
+        cov[1] = L00 * L10 + L01 * L11 + L02 * L12;
+        cov[2] = L00 * L20 + L01 * L21 + L02 * L22;
+        cov[3] = L10 * L10 + L11 * L11 + L12 * L12;
+        cov[4] = L10 * L20 + L11 * L21 + L12 * L22;
+        cov[5] = L20 * L20 + L21 * L21 + L22 * L22;
+    }
+    const float SA0[3] = {cov[0] * A0[0] + cov[1] * A0[1] + cov[2] * A0[2],
+                          cov[1] * A0[0] + cov[3] * A0[1] + cov[4] * A0[2],
+                          cov[2] * A0[0] + cov[4] * A0[1] + cov[5] * A0[2]};
+    const float SA1[3] = {cov[0] * A1[0] + cov[1] * A1[1] + cov[2] * A1[2],
+                          cov[1] * A1[0] + cov[3] * A1[1] + cov[4] * A1[2],
+                          cov[2] * A1[0] + cov[4] * A1[1] + cov[5] * A1[2]};
+    float c_xx = A0[0] * SA0[0] + A0[1] * SA0[1] + A0[2] * SA0[2];
+    const float c_xy = A0[0] * SA1[0] + A0[1] * SA1[1] + A0[2] * SA1[2];
+    float c_yy = A1[0] * SA1[0] + A1[1] * SA1[1] + A1[2] * SA1[2];
+
+    constexpr float h_var = 0.3f;
+    float d_inside_root = 0.f;
+    if (c.antialiasing) {
+        const float det_cov = c_xx * c_yy - c_xy * c_xy;
+        c_xx += h_var;
+        c_yy += h_var;
+        const float det_cov_plus_h_cov = c_xx * c_yy - c_xy * c_xy;
+        const float h = sqrtf(fmaxf(0.000025f, det_cov / det_cov_plus_h_cov));
+        const float d_h = dop * gi.opacity;
+        dop = dop * h;
+        d_inside_root = (det_cov / det_cov_plus_h_cov) <= 0.000025f ? 0.f : d_h / (2.f * h);
+    } else {
+        c_xx += h_var;
+        c_yy += h_var;
+    }
+    float dL_dc_xx = 0.f, dL_dc_xy = 0.f, dL_dc_yy = 0.f;
+    if (c.antialiasing) {
+        // the reference's formula (CR/backward.cu:256-270), at the dilated x, y as written there
+        const float x = c_xx, y = c_yy, z = c_xy, w = h_var;
+        const float qd = w * w + w * (x + y) + x * y - z * z;
+        const float denom_f = d_inside_root / (qd * qd);
+        dL_dc_xx = w * (w * y + y * y + z * z) * denom_f;
+        dL_dc_yy = w * (w * x + x * x + z * z) * denom_f;
+        dL_dc_xy = -2.f * w * z * (w + x + y) * denom_f;
+    }
+    const float denom = c_xx * c_yy - c_xy * c_xy;
+    const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
+    if (denom2inv != 0.f) {
+        dL_dc_xx += denom2inv * (-c_yy * c_yy * dca + 2.f * c_xy * c_yy * dcb + (denom - c_xx * c_yy) * dcc);
+        dL_dc_yy += denom2inv * (-c_xx * c_xx * dcc + 2.f * c_xx * c_xy * dcb + (denom - c_xx * c_yy) * dca);
+        dL_dc_xy += denom2inv * 2.f * (c_xy * c_yy * dca - (denom + 2.f * c_xy * c_xy) * dcb + c_xx * c_xy * dcc);
+    }
+    o.dop = dop;
+
+    // tail: cov2D = A Sigma A^T  ->  dL/dcov3D (6 stored entries) and dL/dA
+    const float ga = dL_dc_xx, gb = dL_dc_xy, gc = dL_dc_yy;
+    float dcov[6];
+    dcov[0] = A0[0] * A0[0] * ga + A0[0] * A1[0] * gb + A1[0] * A1[0] * gc;
+    dcov[3] = A0[1] * A0[1] * ga + A0[1] * A1[1] * gb + A1[1] * A1[1] * gc;
+    dcov[5] = A0[2] * A0[2] * ga + A0[2] * A1[2] * gb + A1[2] * A1[2] * gc;
+    dcov[1] = 2.f * A0[0] * A0[1] * ga + (A0[0] * A1[1] + A0[1] * A1[0]) * gb + 2.f * A1[0] * A1[1] * gc;
+    dcov[2] = 2.f * A0[0] * A0[2] * ga + (A0[0] * A1[2] + A0[2] * A1[0]) * gb + 2.f * A1[0] * A1[2] * gc;
+    dcov[4] = 2.f * A0[2] * A0[1] * ga + (A0[1] * A1[2] + A0[2] * A1[1]) * gb + 2.f * A1[1] * A1[2] * gc;
+    for (int k = 0; k < 6; k++) o.dcov[k] = dcov[k];
+
+    float dA0[3], dA1[3];
+    for (int k = 0; k < 3; k++) {
+        dA0[k] = 2.f * ga * SA0[k] + gb * SA1[k];
+        dA1[k] = 2.f * gc * SA1[k] + gb * SA0[k];
+    }
+    const float dJ00 = dA0[0] * V[0] + dA0[1] * V[4] + dA0[2] * V[8];
+    const float dJ02 = dA0[0] * V[2] + dA0[1] * V[6] + dA0[2] * V[10];
+    const float dJ11 = dA1[0] * V[1] + dA1[1] * V[5] + dA1[2] * V[9];
+    const float dJ12 = dA1[0] * V[2] + dA1[1] * V[6] + dA1[2] * V[10];
+    const float tz = 1.f / t.z, tz2 = tz * tz, tz3 = tz2 * tz;
+    const float dL_dtx = x_grad_mul * -fx * tz2 * dJ02;
+    const float dL_dty = y_grad_mul * -fy * tz2 * dJ12;
+    float dL_dtz =
+        -fx * tz2 * dJ00 - fy * tz2 * dJ11 + (2.f * fx * t.x) * tz3 * dJ02 + (2.f * fy * t.y) * tz3 * dJ12;
+    if (c.have_invdepth) dL_dtz -= dinvd / (t.z * t.z);
+    // transformVec4x3Transpose (CR/auxiliary.h:109-117)
+    float3 dmean = make_float3(V[0] * dL_dtx + V[1] * dL_dty + V[2] * dL_dtz,
+                               V[4] * dL_dtx + V[5] * dL_dty + V[6] * dL_dtz,
+                               V[8] * dL_dtx + V[9] * dL_dty + V[10] * dL_dtz);
+
+    // ---- screen-space mean -> 3-D mean through the projection (CR/backward.cu:403-420)
+    const float* Pm = c.Pm;
+    const float4 m_hom = xform_point_4x4(mean, Pm);
+    const float m_w = 1.0f / (m_hom.w + 0.0000001f);
+    const float mul1 = m_hom.x * m_w * m_w, mul2 = m_hom.y * m_w * m_w;
+    dmean.x += (Pm[0] * m_w - Pm[3] * mul1) * m2x + (Pm[1] * m_w - Pm[3] * mul2) * m2y;
+    dmean.y += (Pm[4] * m_w - Pm[7] * mul1) * m2x + (Pm[5] * m_w - Pm[7] * mul2) * m2y;
+    dmean.z += (Pm[8] * m_w - Pm[11] * mul1) * m2x + (Pm[9] * m_w - Pm[11] * mul2) * m2y;
+
+    // ---- SH colour backward (CR/backward.cu:12-146)
+    if (do_sh) {
+        const float3 v = make_float3(mean.x - c.campos[0], mean.y - c.campos[1], mean.z - c.campos[2]);
+        const float len = sqrtf(v.x * v.x + v.y * v.y + v.z * v.z);
+        const float3 g = make_float3((cm & 1) ? 0.f : dcol.x, (cm & 2) ? 0.f : dcol.y, (cm & 4) ? 0.f : dcol.z);
+        float ddx, ddy, ddz;
+        sh_backward(sh, D, M, v.x / len, v.y / len, v.z / len, g, ddx, ddy, ddz);
+        // dnormvdv (CR/auxiliary.h:129-139)
+        const float sum2 = v.x * v.x + v.y * v.y + v.z * v.z;
+        const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
+        dmean.x += ((sum2 - v.x * v.x) * ddx - v.y * v.x * ddy - v.z * v.x * ddz) * invsum32;
+        dmean.y += (-v.x * v.y * ddx + (sum2 - v.y * v.y) * ddy - v.z * v.y * ddz) * invsum32;
+        dmean.z += (-v.x * v.z * ddx - v.y * v.z * ddy + (sum2 - v.z * v.z) * ddz) * invsum32;
+    }
+    o.dmean = dmean;
+
+    // ---- scale / rotation backward (CR/backward.cu:296-365, called when scales are given, :427-428)
+    if (gi.have_scales) {
+        const float r_ = q.x, x = q.y, y = q.z, z = q.w;
+        // Rg[col][row] = the reference's GLM rotation (R_std transposed)
+        const float Rg[3][3] = {{1.f - 2.f * (y * y + z * z), 2.f * (x * y - r_ * z), 2.f * (x * z + r_ * y)},
+                                {2.f * (x * y + r_ * z), 1.f - 2.f * (x * x + z * z), 2.f * (y * z - r_ * x)},
+                                {2.f * (x * z - r_ * y), 2.f * (y * z + r_ * x), 1.f - 2.f * (x * x + y * y)}};
+        const float s[3] = {gi.scale_modifier * sc3.x, gi.scale_modifier * sc3.y, gi.scale_modifier * sc3.z};
+        const float dS[3][3] = {{dcov[0], 0.5f * dcov[1], 0.5f * dcov[2]},
+                                {0.5f * dcov[1], dcov[3], 0.5f * dcov[4]},
+                                {0.5f * dcov[2], 0.5f * dcov[4], dcov[5]}};
+        // dMt[r][c] = dL_dM[c][r], dL_dM = 2 M dSigma (GLM product), M[k][r] = s_r Rg[k][r]
+        float dMt[3][3];
+        for (int c = 0; c < 3; c++)
+            for (int rr = 0; rr < 3; rr++)
+                dMt[rr][c] = 2.f * s[rr] * (Rg[0][rr] * dS[c][0] + Rg[1][rr] * dS[c][1] + Rg[2][rr] * dS[c][2]);
+        // dot(Rt[i], dL_dMt[i]) -- the reference leaves the scale modifier out here
+        const float ds0 = Rg[0][0] * dMt[0][0] + Rg[1][0] * dMt[0][1] + Rg[2][0] * dMt[0][2];
+        const float ds1 = Rg[0][1] * dMt[1][0] + Rg[1][1] * dMt[1][1] + Rg[2][1] * dMt[1][2];
+        const float ds2 = Rg[0][2] * dMt[2][0] + Rg[1][2] * dMt[2][1] + Rg[2][2] * dMt[2][2];
+        o.dscale = make_float3(ds0, ds1, ds2);
+        for (int i = 0; i < 3; i++)
+            for (int kk = 0; kk < 3; kk++) dMt[i][kk] *= s[i];
+        float4 dq;
+        dq.x = 2.f * z * (dMt[0][1] - dMt[1][0]) + 2.f * y * (dMt[2][0] - dMt[0][2]) +
+               2.f * x * (dMt[1][2] - dMt[2][1]);
+        dq.y = 2.f * y * (dMt[1][0] + dMt[0][1]) + 2.f * z * (dMt[2][0] + dMt[0][2]) +
+               2.f * r_ * (dMt[1][2] - dMt[2][1]) - 4.f * x * (dMt[2][2] + dMt[1][1]);
+        dq.z = 2.f * x * (dMt[1][0] + dMt[0][1]) + 2.f * r_ * (dMt[2][0] - dMt[0][2]) +
+               2.f * z * (dMt[1][2] + dMt[2][1]) - 4.f * y * (dMt[2][2] + dMt[0][0]);
+        dq.w = 2.f * r_ * (dMt[0][1] - dMt[1][0]) + 2.f * x * (dMt[2][0] + dMt[0][2]) +
+               2.f * y * (dMt[1][2] + dMt[2][1]) - 4.f * z * (dMt[1][1] + dMt[0][0]);
+        o.drot = dq;
+    } else {
+        o.dscale = make_float3(0.f, 0.f, 0.f);
+        o.drot = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+}
+
 
 // ---- 3. fused per-Gaussian backward ---------------------------------------------
 // (Folding the record sums into this kernel was measured slower: the sums' dependent loads
@@ -476,6 +698,212 @@ __global__ void __launch_bounds__(64) gauss_bwd_kernel(GaussBwdArgs a) {
         __syncthreads();
         sh_stage_out<64, 64, SH_MODE == kShLdsSplit>(sh_dst, g0, nvalid, s_sh, kShStride, lane);
     }
+}
+
+// ---- 4. the same backward over several views' summed render gradients -----------
+// Multi-GPU (distributed.py ViewExchange): every rank all-gathers the
+// other ranks' per-Gaussian render-gradient sums (a "view block": camera header, 10 floats
+// and a flag word per Gaussian, kViewBlock* in gsr_common.h) instead of all-reducing the
+// 59-float parameter gradients, and runs this kernel once: one lane per Gaussian loops over
+// the views, evaluates view_backward for each view in which the Gaussian is visible, and
+// sums the parameter gradients in registers.  Every rank runs it on the same gathered bytes,
+// so the replicas' gradients are bitwise identical.
+// Phase 1 reads the staged (or global) SH rows for the view-direction gradient and drops
+// the per-coefficient products; phase 2 forms dL/dSH_k = sum over views of B_k(dir_v) g_v
+// one SH band at a time (bands are compile-time, so the band's accumulators stay in
+// registers), recomputing dir_v and g_v from the view blocks -- dL/dSH does not depend on
+// the SH values, so the 48 accumulators of all coefficients are never live at once.
+template <bool LDS>
+struct ShReadOnly {
+    const float* lds_row;  // staged row (LDS variants)
+    ShAddr src;            // global rows otherwise
+    int idx;
+    __device__ __forceinline__ float3 load(int k) const {
+        if constexpr (LDS) return make_float3(lds_row[3 * k], lds_row[3 * k + 1], lds_row[3 * k + 2]);
+        const float* c = src.coef(idx, k);
+        return make_float3(c[0], c[1], c[2]);
+    }
+    __device__ __forceinline__ void store(int, float3) const {}
+};
+template <int K0, int K1>
+struct ShBand {  // accumulates B_k g for K0 <= k < K1; SH values are not needed (read as 0)
+    float* acc;
+    __device__ __forceinline__ float3 load(int) const { return make_float3(0.f, 0.f, 0.f); }
+    __device__ __forceinline__ void store(int k, float3 v) const {
+        if (k >= K0 && k < K1) {
+            acc[3 * (k - K0)] += v.x;
+            acc[3 * (k - K0) + 1] += v.y;
+            acc[3 * (k - K0) + 2] += v.z;
+        }
+    }
+};
+
+// dL/dSH of band [K0, K1) for lane idx, summed over the views it is visible in; written to
+// the lane's LDS row (LDS variants) or straight to global memory
+template <int K0, int K1, int SH_MODE>
+__device__ __forceinline__ void views_sh_band(const ViewsBwdArgs& a, int idx, float3 mean, float* row,
+                                              const ShGradAddr& dst) {
+    float acc[3 * (K1 - K0)];
+#pragma unroll
+    for (int i = 0; i < 3 * (K1 - K0); i++) acc[i] = 0.f;
+#pragma unroll 1
+    for (int v = 0; v < a.n_views; v++) {
+        const float* blk = a.blocks + (size_t)v * a.block_floats;
+        const uint32_t flags = reinterpret_cast<const uint32_t*>(blk + kViewBlockHeader + 10 * (size_t)a.P)[idx];
+        if (!(flags & 1u)) continue;
+        const float* cp = blk + kViewCamPos;
+        const float3 d = make_float3(mean.x - cp[0], mean.y - cp[1], mean.z - cp[2]);
+        const float len = sqrtf(d.x * d.x + d.y * d.y + d.z * d.z);
+        const float4 sa = reinterpret_cast<const float4*>(blk + kViewBlockHeader)[idx];
+        const float3 g = make_float3((flags & 2u) ? 0.f : sa.x, (flags & 4u) ? 0.f : sa.y, (flags & 8u) ? 0.f : sa.z);
+        float ddx, ddy, ddz;
+        sh_backward(ShBand<K0, K1>{acc}, a.D, a.M, d.x / len, d.y / len, d.z / len, g, ddx, ddy, ddz);
+    }
+#pragma unroll
+    for (int k = K0; k < K1; k++) {
+        const float x = acc[3 * (k - K0)], y = acc[3 * (k - K0) + 1], z = acc[3 * (k - K0) + 2];
+        if constexpr (SH_MODE != kShGlobal) {
+            row[3 * k] = x;
+            row[3 * k + 1] = y;
+            row[3 * k + 2] = z;
+        } else if (k < a.M) {
+            float* c = dst.coef(idx, k);
+            c[0] = x;
+            c[1] = y;
+            c[2] = z;
+        }
+    }
+}
+
+template <int SH_MODE>
+// 3 waves per SIMD (the LDS limit of the SH staging): the register allocator then spills a
+// few values but the per-view latency chains overlap better (8 views: 0.50 -> 0.44 ms, r1af)
+#ifndef GSR_VIEWS_WAVES
+#define GSR_VIEWS_WAVES 3
+#endif
+#ifdef GSR_VIEWS_WAVES
+#define GSR_VIEWS_OCCUPANCY __attribute__((amdgpu_waves_per_eu(GSR_VIEWS_WAVES, GSR_VIEWS_WAVES)))
+#else
+#define GSR_VIEWS_OCCUPANCY
+#endif
+__global__ void __launch_bounds__(64) GSR_VIEWS_OCCUPANCY gauss_bwd_views_kernel(ViewsBwdArgs a) {
+    __shared__ __attribute__((aligned(16))) float s_sh[SH_MODE != kShGlobal ? 64 * kShStride : 4];
+    const int lane = threadIdx.x;
+    const int g0 = blockIdx.x * 64;
+    const int idx = g0 + lane;
+    const int nvalid = min(64, a.P - g0);
+    const int M = a.M;
+    const ShAddr sh_src{a.shs, a.dc, M};
+    const ShGradAddr sh_dst{a.dL_dsh, a.dL_ddc, M};
+    if constexpr (SH_MODE != kShGlobal) {
+        sh_stage_in<64, 64, SH_MODE == kShLdsSplit>(sh_src, g0, nvalid, s_sh, kShStride, lane);
+        __syncthreads();
+    }
+    const bool valid = idx < a.P;
+    float3 mean = make_float3(0.f, 0.f, 0.f);
+    // ---- phase 1: geometry gradients, summed over views
+    if (valid) {
+        GaussIn gi;
+        gi.mean = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
+        mean = gi.mean;
+        gi.have_scales = true;
+        gi.sc3 = make_float3(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]);
+        gi.q = reinterpret_cast<const float4*>(a.rotations)[idx];
+        gi.cov3D = nullptr;
+        gi.scale_modifier = a.scale_modifier;
+        gi.opacity = a.opacities[idx];
+        const ShReadOnly<SH_MODE != kShGlobal> shr{SH_MODE != kShGlobal ? &s_sh[lane * kShStride] : nullptr, sh_src,
+                                                   idx};
+        float3 dmean = make_float3(0.f, 0.f, 0.f), dscale = dmean;
+        float4 drot = make_float4(0.f, 0.f, 0.f, 0.f);
+        float dop = 0.f;
+#pragma unroll 1
+        for (int v = 0; v < a.n_views; v++) {
+            const float* blk = a.blocks + (size_t)v * a.block_floats;
+            const uint32_t flags = reinterpret_cast<const uint32_t*>(blk + kViewBlockHeader + 10 * (size_t)a.P)[idx];
+            if (!(flags & 1u)) continue;  // not visible in view v: no gradient from it
+            const ViewCam cam{blk + kViewCamView, blk + kViewCamProj, blk + kViewCamPos, blk[kViewCamTanX],
+                              blk[kViewCamTanY],  blk[kViewCamFocalX], blk[kViewCamFocalY],
+                              (int)__float_as_uint(blk[kViewCamAA]), (int)__float_as_uint(blk[kViewCamInvDepth])};
+            const float* sums = blk + kViewBlockHeader;
+            const float4 sa = reinterpret_cast<const float4*>(sums)[idx];
+            const float4 sb = reinterpret_cast<const float4*>(sums + 4 * (size_t)a.P)[idx];
+            const float2 sc = reinterpret_cast<const float2*>(sums + 8 * (size_t)a.P)[idx];
+            ViewOut o;
+            view_backward(cam, gi, sa, sb, sc, (uint8_t)((flags >> 1) & 7u), true, a.D, M, shr, o);
+            dmean.x += o.dmean.x; dmean.y += o.dmean.y; dmean.z += o.dmean.z;
+            dop += o.dop;
+            dscale.x += o.dscale.x; dscale.y += o.dscale.y; dscale.z += o.dscale.z;
+            drot.x += o.drot.x; drot.y += o.drot.y; drot.z += o.drot.z; drot.w += o.drot.w;
+        }
+        store3(a.dL_dmean3D, idx, dmean.x, dmean.y, dmean.z);
+        a.dL_dopacity[idx] = dop;
+        store3(a.dL_dscale, idx, dscale.x, dscale.y, dscale.z);
+        reinterpret_cast<float4*>(a.dL_drot)[idx] = drot;
+    }
+    // ---- phase 2: dL/dSH band by band (CR/backward.cu:43-127 products, summed over views)
+    if constexpr (SH_MODE != kShGlobal) __syncthreads();  // the staged SH rows are read for the last time
+    float* row = SH_MODE != kShGlobal ? &s_sh[lane * kShStride] : nullptr;
+    if (valid) {
+        views_sh_band<0, 1, SH_MODE>(a, idx, mean, row, sh_dst);
+        if (a.D > 0) views_sh_band<1, 4, SH_MODE>(a, idx, mean, row, sh_dst);
+        if (a.D > 1) views_sh_band<4, 9, SH_MODE>(a, idx, mean, row, sh_dst);
+        if (a.D > 2) views_sh_band<9, 16, SH_MODE>(a, idx, mean, row, sh_dst);
+        const int K = (a.D + 1) * (a.D + 1);
+        if constexpr (SH_MODE != kShGlobal) {
+            for (int k = K; k < 16; k++) row[3 * k] = row[3 * k + 1] = row[3 * k + 2] = 0.f;
+        } else {
+            for (int k = K; k < M; k++) {
+                float* c = sh_dst.coef(idx, k);
+                c[0] = c[1] = c[2] = 0.f;
+            }
+        }
+    }
+    if constexpr (SH_MODE != kShGlobal) {
+        __syncthreads();
+        sh_stage_out<64, 64, SH_MODE == kShLdsSplit>(sh_dst, g0, nvalid, s_sh, kShStride, lane);
+    }
+}
+
+hipError_t launch_gauss_bwd_views(const ViewsBwdArgs& a, hipStream_t stream) {
+    if (a.P == 0) return hipSuccess;
+    const dim3 grid((a.P + 63) / 64), block(64);
+    const bool lds = a.shs && a.dL_dsh && a.M == 16 && (!a.dc || a.dL_ddc) &&
+                     ((reinterpret_cast<uintptr_t>(a.shs) & 15) == 0) &&
+                     ((reinterpret_cast<uintptr_t>(a.dL_dsh) & 15) == 0);
+    if (lds && a.dc)
+        hipLaunchKernelGGL(gauss_bwd_views_kernel<kShLdsSplit>, grid, block, 0, stream, a);
+    else if (lds)
+        hipLaunchKernelGGL(gauss_bwd_views_kernel<kShLdsCombined>, grid, block, 0, stream, a);
+    else
+        hipLaunchKernelGGL(gauss_bwd_views_kernel<kShGlobal>, grid, block, 0, stream, a);
+    return hipGetLastError();
+}
+
+// The header of a view block: the camera, as gauss_bwd_views_kernel reads it.
+__global__ void view_header_kernel(float* blk, const float* view, const float* proj, const float* campos,
+                                   float tan_fovx, float tan_fovy, float focal_x, float focal_y, int antialiasing,
+                                   int have_invdepth) {
+    const int t = threadIdx.x;
+    if (t < 16) blk[kViewCamView + t] = view[t];
+    else if (t < 32) blk[kViewCamProj + t - 16] = proj[t - 16];
+    else if (t < 35) blk[kViewCamPos + t - 32] = campos[t - 32];
+    else if (t == 35) {
+        blk[kViewCamTanX] = tan_fovx;
+        blk[kViewCamTanY] = tan_fovy;
+        blk[kViewCamFocalX] = focal_x;
+        blk[kViewCamFocalY] = focal_y;
+        blk[kViewCamAA] = __uint_as_float((uint32_t)antialiasing);
+        blk[kViewCamInvDepth] = __uint_as_float((uint32_t)have_invdepth);
+    }
+}
+
+hipError_t launch_view_header(float* blk, const float* view, const float* proj, const float* campos, float tan_fovx,
+                              float tan_fovy, float focal_x, float focal_y, int antialiasing, int have_invdepth,
+                              hipStream_t stream) {
+    hipLaunchKernelGGL(view_header_kernel, dim3(1), dim3(64), 0, stream, blk, view, proj, campos, tan_fovx, tan_fovy,
+                       focal_x, focal_y, antialiasing, have_invdepth);
+    return hipGetLastError();
 }
 
 hipError_t launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t stream) {

@@ -150,6 +150,20 @@ constexpr int kUnitCntStride = 32;  // counter words, one per 128-B line
 __host__ __device__ inline uint32_t unit_part_cap(uint32_t tiles) { return (tiles + kUnitShards - 1) / kUnitShards; }
 __host__ __device__ inline size_t unit_full_cap(size_t C) { return C / kCkStride + 1; }
 
+// ---------------------------------------------------------------------------
+// View block (multi-GPU exchange, include/gsr.h gsr_rasterize_backward_screen /
+// gsr_gauss_backward_views): one view's camera and per-Gaussian render-gradient sums,
+// in floats: [0, 64) header (the camera, offsets below), then sums.a [P][4], sums.b [P][4],
+// sums.c [P][2] and the flag word [P] (bit 0 visible, bits 1-3 SH clamp mask); the block
+// is padded to a multiple of 64 floats so the next view's block stays 256-byte aligned.
+// ---------------------------------------------------------------------------
+constexpr int kViewBlockHeader = 64;
+constexpr int kViewCamView = 0, kViewCamProj = 16, kViewCamPos = 32, kViewCamTanX = 35, kViewCamTanY = 36,
+              kViewCamFocalX = 37, kViewCamFocalY = 38, kViewCamAA = 39, kViewCamInvDepth = 40;
+__host__ __device__ inline size_t view_block_floats(size_t P) {
+    return (kViewBlockHeader + 11 * P + 63) / 64 * 64;
+}
+
 // Per-instance gradient records (backward scratch), SoA so stores are aligned.
 struct GradRecs {
     float4* a;  // (dcolor.r, dcolor.g, dcolor.b, dinvdepth)

@@ -290,7 +290,32 @@ hipError_t launch_ssim_bwd(int planes, int H, int W, const float* img1, const fl
                            hipStream_t stream);
 // backward.hip
 hipError_t launch_gauss_reduce(int P, const GeomState& g, uint32_t gx, const unsigned long long* lim_key,
-                               const GradRecs& recs, const GradRecs& sums, hipStream_t stream);
+                               const GradRecs& recs, const GradRecs& sums, uint32_t* flags, const int* radii,
+                               hipStream_t stream);
+// multi-view backward over gathered view blocks (backward.hip section 4)
+struct ViewsBwdArgs {
+    int P, D, M;
+    const float* means3D;
+    const float* shs;
+    const float* dc;
+    const float* opacities;
+    const float* scales;
+    const float* rotations;
+    float scale_modifier;
+    int n_views;
+    const float* blocks;  // [n_views][block_floats]
+    size_t block_floats;
+    float* dL_dmean3D;
+    float* dL_dsh;
+    float* dL_ddc;
+    float* dL_dopacity;
+    float* dL_dscale;
+    float* dL_drot;
+};
+hipError_t launch_gauss_bwd_views(const ViewsBwdArgs& a, hipStream_t stream);
+hipError_t launch_view_header(float* blk, const float* view, const float* proj, const float* campos, float tan_fovx,
+                              float tan_fovy, float focal_x, float focal_y, int antialiasing, int have_invdepth,
+                              hipStream_t stream);
 hipError_t launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t stream);
 
 }  // namespace gsr

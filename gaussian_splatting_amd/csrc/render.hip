@@ -74,8 +74,9 @@ __device__ __forceinline__ float splat_alpha(float p2, float opacity, float& G) 
 
 // ---------------------------------------------------------------------------
 // Per-pixel state is arithmetic, not boolean: Tl is the live transmittance and
-// drops to 0 when the pixel terminates (CR/forward.cu:477-482); Tf then holds the
-// transmittance at termination.  A finished pixel therefore blends with weight 0
+// drops to 0 when the pixel terminates (CR/forward.cu:477-482); Tc is T after the
+// pixel's last contributor, which is the reference's final_T whether or not the pixel
+// terminated (skipped entries leave T alone).  A finished pixel therefore blends with weight 0
 // without any mask bookkeeping, and the only wave-level decisions are "does any
 // lane of this slot blend this splat" and "is any pixel of this slot still live".
 #ifdef GSR_FWD_WAVES
@@ -112,7 +113,7 @@ __global__ void __launch_bounds__(64) GSR_FWD_OCCUPANCY render_fwd_kernel(Render
 
     __shared__ float4 s_xy[kBatch], s_cq[kBatch], s_col[kBatch];  // (x, y, o, 1/z), (A, B, C, quads), rgb
 
-    float Tl[NQ], Tf[NQ], C0[NQ], C1[NQ], C2[NQ], D[NQ];
+    float Tl[NQ], Tc[NQ], C0[NQ], C1[NQ], C2[NQ], D[NQ];
     uint32_t last[NQ];
     uint32_t alive = 0;  // wave-uniform: slots with at least one pixel still blending
 #pragma unroll
@@ -120,7 +121,8 @@ __global__ void __launch_bounds__(64) GSR_FWD_OCCUPANCY render_fwd_kernel(Render
         const int q = qbase + k;
         const int px = tile_x0 + (q & 1) * 8 + lx, py = tile_y0 + (q >> 1) * 8 + ly;
         Tl[k] = (px < a.W && py < a.H) ? 1.f : 0.f;
-        Tf[k] = C0[k] = C1[k] = C2[k] = D[k] = 0.f;
+        Tc[k] = 1.f;
+        C0[k] = C1[k] = C2[k] = D[k] = 0.f;
         last[k] = 0;
         if (__any(Tl[k] > 0.f)) alive |= 1u << k;
     }
@@ -180,15 +182,16 @@ __global__ void __launch_bounds__(64) GSR_FWD_OCCUPANCY render_fwd_kernel(Render
                 const float test_T = Tl[k] * (1.f - alpha);
                 const bool term = test_T < 0.0001f;  // live pixel: ends it, splat not added
                 const float w = term ? 0.f : w0;
-                // first termination wins (later ones see Tl = 0); both are >= 0, so an integer max
-                Tf[k] = __uint_as_float(max(__float_as_uint(Tf[k]), term ? __float_as_uint(Tl[k]) : 0u));
+                const bool blended = w > 0.f;
                 Tl[k] = term ? 0.f : test_T;
                 C0[k] += col.x * w;
                 C1[k] += col.y * w;
                 C2[k] += col.z * w;
                 D[k] += xy.w * w;
-                last[k] = w > 0.f ? pos1 : last[k];
-                if (!__any(Tl[k] > 0.f)) alive &= ~(1u << k);
+                last[k] = blended ? pos1 : last[k];
+                Tc[k] = blended ? test_T : Tc[k];  // T after the last contributor = final_T
+                // a slot can only die where one of its pixels terminated just now (mask logic, SALU)
+                if (__any(term && w0 > 0.f) && !__any(Tl[k] > 0.f)) alive &= ~(1u << k);
             }
         }
         __syncthreads();
@@ -208,7 +211,9 @@ __global__ void __launch_bounds__(64) GSR_FWD_OCCUPANCY render_fwd_kernel(Render
         const int px = tile_x0 + (q & 1) * 8 + lx, py = tile_y0 + (q >> 1) * 8 + ly;
         if (px < a.W && py < a.H) {
             const size_t pix = (size_t)py * a.W + px;
-            const float T = Tl[k] > 0.f ? Tl[k] : Tf[k];
+            // the reference's final_T is T after the pixel's last contributor: entries after it
+            // either do not blend (T unchanged) or end the pixel without blending
+            const float T = Tc[k];
             a.img.final_T[pix] = T;
             a.img.n_contrib[pix] = last[k];
             a.img.accum[pix] = C0[k];

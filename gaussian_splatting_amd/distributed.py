@@ -91,3 +91,45 @@ def reduce_densification_stats(grad_norm_sum: torch.Tensor, denom: torch.Tensor,
     grad_norm_sum.copy_(stats[:n].view_as(grad_norm_sum))
     denom.copy_(stats[n:].view_as(denom))
     dist.all_reduce(max_radii2D, op=dist.ReduceOp.MAX, group=group)
+
+
+class ViewExchange:
+    """The multi-GPU exchange of view blocks (include/gsr.h, "Multi-GPU view exchange").
+
+    Instead of all-reducing the parameter gradients (``GradArena.all_reduce``: 2 (N-1)/N x 59
+    floats per Gaussian through every rank's xGMI links), each rank writes its view's
+    per-Gaussian render-gradient sums into its block of ``gathered`` (``[N, block_floats]``,
+    ~44 B per Gaussian), ONE ``all_gather_into_tensor`` (in place) gives every rank all N
+    blocks, and ``_C.gauss_backward_views`` turns them into the summed parameter gradients on
+    every rank -- the same bytes in, the same kernel, so the replicas agree bit for bit.  At
+    N = 2 a rank receives 11 floats per Gaussian instead of 59; at N = 8, 77 instead of 103.
+
+        ex = ViewExchange(P, device)
+        _C.rasterize_gaussians_backward_screen(*backward_args, view_block=ex.local_block())
+        ex.exchange()
+        _C.gauss_backward_views(means3D, dc, sh, degree, opacities, scales, rotations, 1.0,
+                                ex.gathered, out=arena.views())
+    """
+
+    def __init__(self, P: int, device, group: Optional[dist.ProcessGroup] = None):
+        from . import _C
+
+        self.P, self.group = P, group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.block_floats = _C.view_block_floats(P) if P > 0 else 0
+        self.gathered = torch.empty(self.world, self.block_floats, dtype=torch.float32, device=device)
+
+    def local_block(self) -> torch.Tensor:
+        return self.gathered[self.rank]
+
+    def exchange(self) -> None:
+        """All-gather the blocks (in place: this rank's block is already at its slot)."""
+        if self.world > 1:
+            dist.all_gather_into_tensor(self.gathered.view(-1), self.local_block(), group=self.group)
+
+    def means2D_grad(self, rank: Optional[int] = None) -> torch.Tensor:
+        """dL/dmeans2D (x, y) of a rank's view, [P, 2] (a strided view of its block): the
+        densification statistics' input (train.py:215)."""
+        b = self.gathered[self.rank if rank is None else rank]
+        return b[64 + 4 * self.P: 64 + 8 * self.P].view(self.P, 4)[:, :2]

@@ -153,6 +153,44 @@ int gsr_rasterize_backward_dc(int P, int D, int M, int R, const float* backgroun
                               int antialiasing, int debug, gsr_alloc_fn scratch_alloc, void* scratch_ctx,
                               void* stream, int binning_capacity, size_t binning_bytes);
 
+/* Multi-GPU view exchange (gaussian_splatting_amd/distributed.py
+ * ViewExchange).  The reference trains on one GPU; sharding views over N ranks needs the
+ * N views' parameter gradients summed on every rank.  Instead of all-reducing the 59-float
+ * parameter gradients (2 (N-1)/N x 236 B per Gaussian per rank over xGMI), each rank
+ * all-gathers the other ranks' "view blocks" -- a camera header and, per Gaussian, the 10
+ * summed render gradients (dL/dcolour, dL/dinvdepth, dL/dmean2D, dL/dopacity, dL/dconic)
+ * plus a visibility / SH-clamp word, 44 B -- and every rank runs the per-Gaussian backward
+ * over all views at once (10 (N-1) floats received per Gaussian instead of 118 (N-1)/N).
+ *
+ * gsr_view_block_floats(P): floats in one view block (padded to 256 B).
+ * gsr_rasterize_backward_screen: the backward of gsr_rasterize_backward_dc up to the
+ *   per-Gaussian sums (CR/backward.cu:433-612 = renderCUDA backward), written with the
+ *   camera into view_block (device, 16-byte aligned, gsr_view_block_floats(P) floats);
+ *   colours from SH (dc + shs, or shs alone with dc NULL), cov3D from scales/rotations.
+ *   dL/dmeans2D of this view is the block's float pair at [64 + 4P + 2g] (densification).
+ * gsr_gauss_backward_views: the rest of the backward (CR/backward.cu:153-429,
+ *   computeCov2DCUDA + preprocessCUDA, as gsr_rasterize_backward_dc's last stage) for all
+ *   n_views gathered blocks (blocks[v * block_floats ...]), writing the SUM over views of
+ *   dL/dmeans3D, dL/ddc, dL/dsh, dL/dopacity, dL/dscales, dL/drotations.  With one view it
+ *   equals the single-view backward bit for bit. */
+unsigned long long gsr_view_block_floats(int P);
+
+int gsr_rasterize_backward_screen(int P, int D, int M, int R, const float* background, int width, int height,
+                                  const float* means3D, const float* dc, const float* shs, const float* opacities,
+                                  const float* scales, float scale_modifier, const float* rotations,
+                                  const float* viewmatrix, const float* projmatrix, const float* campos,
+                                  float tan_fovx, float tan_fovy, const int* radii, void* geom_buffer,
+                                  void* binning_buffer, void* image_buffer, const float* dL_dpix,
+                                  const float* dL_dinvdepths, int antialiasing, int debug, gsr_alloc_fn scratch_alloc,
+                                  void* scratch_ctx, void* stream, int binning_capacity, size_t binning_bytes,
+                                  float* view_block);
+
+int gsr_gauss_backward_views(int P, int D, int M, const float* means3D, const float* dc, const float* shs,
+                             const float* opacities, const float* scales, const float* rotations, float scale_modifier,
+                             int n_views, const float* blocks, long long block_floats, float* dL_dmean3D,
+                             float* dL_ddc, float* dL_dsh, float* dL_dopacity, float* dL_dscale, float* dL_drot,
+                             void* stream);
+
 /* Frustum test, view-space z > 0.2 (CudaRasterizer::Rasterizer::markVisible).
  * `present` is P bytes (bool). */
 int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,

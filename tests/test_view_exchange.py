@@ -1,0 +1,149 @@
+"""Multi-GPU view exchange (include/gsr.h "Multi-GPU view exchange", distributed.ViewExchange).
+
+The exchange replaces the all-reduce of parameter gradients by an all-gather of per-view
+render-gradient sums; every rank then runs the per-Gaussian backward over all views.  On one
+GPU the views are rendered one after another, so this checks the arithmetic the ranks do:
+* one view through the exchange path equals the single-view backward to float32 rounding
+  (the same formulas; the compiler may contract them into FMAs differently in the two
+  kernels);
+* several views equal the sum of the single-view backwards (different summation order:
+  float32 tolerance), for the combined and the separate-SH (dc) layouts;
+* a view block's dL/dmeans2D equals the backward's;
+* the CPU gloo test checks the in-place all-gather layout of the exchange buffer.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from tests import common as C
+
+GROUPS = ("dL_dmeans3D", "dL_dsh", "dL_dopacity", "dL_dscales", "dL_drotations")
+
+
+def _view_inputs(case_kw, yaw, dev):
+    case = C.Case("views", yaw=yaw, **case_kw)
+    return C.build(case), case
+
+
+def _single_and_block(inp, case, dev, split):
+    """Single-view backward grads, and the same view's block."""
+    from gaussian_splatting_amd import _C
+
+    fwd = C.run_gpu_forward(inp, device=dev)
+    gc, gd = C.l1_grads(case.H, case.W)
+    gc, gd = gc.to(dev), gd.to(dev)
+    nr, color, radii, geom, binning, img, invd = fwd
+    t = {k: (v.to(dev) if isinstance(v, torch.Tensor) else v) for k, v in inp.items()}
+    empty = torch.empty(0, device=dev)
+    sh = t["shs"]
+    if split:
+        dc, rest = sh[:, :1].contiguous(), sh[:, 1:].contiguous()
+        args = (t["bg"], t["means3D"], radii, empty, t["opacities"], t["scales"], t["rotations"], t["scale_modifier"],
+                empty, t["viewmatrix"], t["projmatrix"], t["tanfovx"], t["tanfovy"], gc, gd, dc, rest, t["sh_degree"],
+                t["campos"], geom, nr, binning, img, bool(t["antialiasing"]), False)
+    else:
+        args = (t["bg"], t["means3D"], radii, empty, t["opacities"], t["scales"], t["rotations"], t["scale_modifier"],
+                empty, t["viewmatrix"], t["projmatrix"], t["tanfovx"], t["tanfovy"], gc, gd, sh, t["sh_degree"],
+                t["campos"], geom, nr, binning, img, bool(t["antialiasing"]), False)
+    out = _C.rasterize_gaussians_backward(*args)
+    P = t["means3D"].shape[0]
+    block = torch.empty(_C.view_block_floats(P), device=dev)
+    _C.rasterize_gaussians_backward_screen(*args, view_block=block)
+    if split:
+        names = ("dL_dmeans2D", "dL_dcolors", "dL_dopacity", "dL_dmeans3D", "dL_dcov3D", "dL_ddc", "dL_dsh",
+                 "dL_dscales", "dL_drotations")
+    else:
+        names = ("dL_dmeans2D", "dL_dcolors", "dL_dopacity", "dL_dmeans3D", "dL_dcov3D", "dL_dsh", "dL_dscales",
+                 "dL_drotations")
+    return dict(zip(names, out)), block, t
+
+
+def _views_backward(t, blocks, split, dev):
+    from gaussian_splatting_amd import _C
+
+    P = t["means3D"].shape[0]
+    sh = t["shs"]
+    M = sh.shape[1]
+    out = {"dL_dmeans3D": torch.empty(P, 3, device=dev), "dL_dopacity": torch.empty(P, 1, device=dev),
+           "dL_dscales": torch.empty(P, 3, device=dev), "dL_drotations": torch.empty(P, 4, device=dev)}
+    if split:
+        dc, rest = sh[:, :1].contiguous(), sh[:, 1:].contiguous()
+        out["dL_ddc"] = torch.empty(P, 1, 3, device=dev)
+        out["dL_dsh"] = torch.empty(P, M - 1, 3, device=dev)
+        _C.gauss_backward_views(t["means3D"], dc, rest, t["sh_degree"], t["opacities"], t["scales"], t["rotations"],
+                                t["scale_modifier"], blocks, out)
+    else:
+        out["dL_dsh"] = torch.empty(P, M, 3, device=dev)
+        _C.gauss_backward_views(t["means3D"], None, sh, t["sh_degree"], t["opacities"], t["scales"], t["rotations"],
+                                t["scale_modifier"], blocks, out)
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("split", [False, True])
+@pytest.mark.parametrize("case_kw", [dict(P=300, W=64, H=48), dict(P=250, W=48, H=40, sh_degree=1),
+                                     dict(P=300, W=64, H=48, antialiasing=True)])
+def test_one_view_equals_single_view(case_kw, split):
+    dev = torch.device("cuda", 0)
+    inp, case = _view_inputs(case_kw, 0.0, dev)
+    single, block, t = _single_and_block(inp, case, dev, split)
+    got = _views_backward(t, block.view(1, -1), split, dev)
+    torch.cuda.synchronize()
+    for k in got:
+        err = (got[k] - single[k]).abs().max().item()
+        assert err <= 1e-5 * max(single[k].abs().max().item(), 1e-3), (k, err)
+    P = t["means3D"].shape[0]
+    m2 = block[64 + 4 * P: 64 + 8 * P].view(P, 4)[:, :2]
+    assert torch.equal(m2, single["dL_dmeans2D"][:, :2])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("split", [False, True])
+def test_views_sum_equals_sum_of_single_views(split):
+    dev = torch.device("cuda", 0)
+    blocks, sums = [], None
+    for v, yaw in enumerate((0.0, 7.0, -12.0, 20.0)):
+        inp, case = _view_inputs(dict(P=2000, W=96, H=80), yaw, dev)
+        single, block, t = _single_and_block(inp, case, dev, split)
+        blocks.append(block)
+        sums = {k: single[k].clone() for k in single} if sums is None else {k: sums[k] + single[k] for k in sums}
+    got = _views_backward(t, torch.stack(blocks), split, dev)
+    torch.cuda.synchronize()
+    for k in got:
+        ref = sums[k]
+        err = (got[k] - ref).abs().max().item()
+        scale = ref.abs().max().item()
+        assert err <= 2e-6 * max(scale, 1e-3) + 1e-9, (k, err, scale)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    try:
+        buf = torch.empty(2, 5)  # the exchange buffer's layout, without the library
+        buf[rank] = torch.arange(5, dtype=torch.float32) + 10 * rank
+        dist.all_gather_into_tensor(buf.view(-1), buf[rank])
+        np.save(os.path.join(out, f"g{rank}.npy"), buf.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_exchange_layout_gloo(tmp_path):
+    """All-gather in place into [world, block] puts rank r's block at row r on every rank."""
+    mp.spawn(_worker, args=(_free_port(), str(tmp_path)), nprocs=2, join=True)
+    expect = np.stack([np.arange(5) + 10 * r for r in range(2)]).astype(np.float32)
+    for r in range(2):
+        np.testing.assert_array_equal(np.load(tmp_path / f"g{r}.npy"), expect)

@@ -1,0 +1,84 @@
+#!/usr/bin/env python3
+"""Cost of the multi-GPU view exchange's compute side on one MI355X (development tool).
+
+    python tools/bench_views.py [--config 1m_1080p_sh3]
+
+Renders one view, copies its view block N times (N = 1, 2, 4, 8: the gathered buffer an
+N-rank job holds after the all-gather) and times gauss_backward_views over it, next to the
+single-view backward's gauss_bwd stage.  Also prints the exchange volumes per rank:
+all-gather of view blocks vs all-reduce of the 59-float parameter gradients.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from gaussian_splatting_amd import _C, _lib  # noqa: E402
+from gaussian_splatting_amd import synthetic as syn  # noqa: E402
+from gaussian_splatting_amd.distributed import GradArena  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="1m_1080p_sh3")
+    ap.add_argument("--reps", type=int, default=20)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    cfg = syn.CONFIGS[a.config]
+    P, W, H, D = cfg["P"], cfg["width"], cfg["height"], cfg["sh_degree"]
+    scene, cam = syn.config_scene(a.config, seed=0)
+    scene, cam = scene.to(dev), cam.to(dev)
+    gc, gd = syn.upstream_grads(H, W)
+    gc, gd = gc.to(dev), gd.to(dev)
+    bg, empty = torch.zeros(3, device=dev), torch.empty(0, device=dev)
+    arena = GradArena(P, scene.shs.shape[1], dev)
+    fwd = _C.rasterize_gaussians(bg, scene.means3D, empty, scene.opacities, scene.scales, scene.rotations, 1.0, empty,
+                                 cam.viewmatrix, cam.projmatrix, cam.tanfovx, cam.tanfovy, H, W, scene.shs, D,
+                                 cam.campos, False, False, False)
+    nr, color, radii, geom, binning, img, invd = fwd
+    bwd = (bg, scene.means3D, radii, empty, scene.opacities, scene.scales, scene.rotations, 1.0, empty, cam.viewmatrix,
+           cam.projmatrix, cam.tanfovx, cam.tanfovy, gc, gd, scene.shs, D, cam.campos, geom, nr, binning, img, False,
+           False)
+    nb = _C.view_block_floats(P)
+    block = torch.empty(nb, device=dev)
+    _C.rasterize_gaussians_backward_screen(*bwd, view_block=block)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+
+    def timed(fn):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(a.reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / a.reps
+
+    _lib.profile_reset()
+    _lib.profile_enable(True, stages=["gauss_bwd"])
+    for _ in range(a.reps):
+        _C.rasterize_gaussians_backward(*bwd, out=arena.views())
+    torch.cuda.synchronize()
+    _lib.profile_enable(False)
+    t, n = _lib.profile_collect()["gauss_bwd"]
+    res = {"config": a.config, "P": P, "gauss_bwd_single_ms": t / n, "views_ms": {}, "exchange_MB_per_rank": {}}
+    for N in (1, 2, 4, 8):
+        blocks = block.unsqueeze(0).repeat(N, 1).contiguous()
+        res["views_ms"][N] = timed(lambda: _C.gauss_backward_views(scene.means3D, None, scene.shs, D, scene.opacities,
+                                                                  scene.scales, scene.rotations, 1.0, blocks,
+                                                                  arena.views()))
+        res["exchange_MB_per_rank"][N] = {"allgather_view_blocks": (N - 1) * nb * 4 / 1e6,
+                                          "allreduce_param_grads": 2 * (N - 1) / N * arena.flat.numel() * 4 / 1e6}
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
