@@ -25,14 +25,14 @@ namespace gsr {
 // ---- 1. segmented sums of the per-instance records ------------------------------
 // One wave per 64 consecutive Gaussians.  Their records form one contiguous range
 // [E0, E1) (record index = rec_start[g] + k, k = the tile's row-major index in g's
-// rectangle); it is streamed through LDS 64 records at a time with fully coalesced
-// loads, and every lane sums the rows of its own segment from LDS in order, so the
-// result does not depend on scheduling.  The render backward writes records only
+// rectangle); it is read 64 records at a time with fully coalesced loads (one record
+// per lane) and each Gaussian's run is summed by a segmented scan over the wave, in a
+// fixed order, so the result does not depend on scheduling.  The render backward writes records only
 // for entries before each tile's last contributor; instance (g, tile t) has one iff
 // key(g) = depth bits << 32 | g <= lim_key[t] (tile lists are sorted by key), and
 // the others are read as zeros without touching memory (render.hip, "Entries at
 // positions >= limit").
-constexpr int kRecStride = 12;  // floats per staged record row (10 used), 48 B
+constexpr int kRecStride = 12;  // floats per Gaussian in the LDS hand-off of chunk totals (10 used), 48 B
 
 // Sums of the records of the wave's 64 consecutive Gaussians [g0, g0 + 64), one
 // Gaussian per lane (zeros for lanes past P).  s_rec: 64 * kRecStride floats of LDS.
@@ -64,11 +64,19 @@ __device__ __forceinline__ void reduce_records(int P, int g0, const uint32_t* __
     sb = sa;
     sc = make_float2(0.f, 0.f);
     // Whether slot e of a chunk has a record needs the tile's limit key: a dependent load.
-    // It is probed one chunk ahead, so the limit-key load of chunk c + 1 is in flight with
-    // the record loads of chunk c.
-    auto probe = [&](uint32_t base) -> bool {
+    // Wave-parallel segmented sums: the chunk's 64 records stay in registers (one per lane);
+    // a segmented inclusive scan over the wave (DPP row shifts and row broadcasts, the add
+    // masked where the source lane belongs to another Gaussian) leaves each Gaussian's chunk
+    // total in the last lane of its run, which hands it to the owner lane through LDS.  The
+    // cost no longer depends on the longest run in the chunk (a Gaussian touching hundreds
+    // of tiles made 63 lanes wait).  Chunk c + 1's records and limit keys load while chunk
+    // c is reduced.
+    struct Slot {
+        bool has;
+        int owner, seg0;
+    };
+    auto probe2 = [&](uint32_t base) -> Slot {
         const uint32_t e = base + lane;
-        // owner of slot e: the largest lane whose segment starts at or before it
         int owner = 0;
 #pragma unroll
         for (int step = 32; step > 0; step >>= 1) {
@@ -79,37 +87,70 @@ __device__ __forceinline__ void reduce_records(int P, int g0, const uint32_t* __
         const uint32_t o0 = __shfl(my0, owner), ow = __shfl(w, owner), ox = __shfl(x0, owner),
                        oy = __shfl(y0, owner);
         const unsigned long long okey = __shfl(key, owner);
-        if (e >= E1) return false;
+        if (e >= E1) return Slot{false, -1, lane};
+        const int seg0 = o0 > base ? (int)(o0 - base) : 0;
         const uint32_t k = e - o0, ty = k / ow, tile = (oy + ty) * gx + ox + (k - ty * ow);
-        return okey <= lim_key[tile];
+        return Slot{okey <= lim_key[tile], owner, seg0};
     };
-    bool has = E0 < E1 ? probe(E0) : false;
+    float4* part = reinterpret_cast<float4*>(s_rec);  // [64][3] float4: a Gaussian's chunk total
+    Slot cur = E0 < E1 ? probe2(E0) : Slot{false, -1, lane};
+    float4 x = make_float4(0.f, 0.f, 0.f, 0.f), y = x;
+    float2 z = make_float2(0.f, 0.f);
+    if (cur.has) {
+        x = recs.a[E0 + lane];
+        y = recs.b[E0 + lane];
+        z = recs.c[E0 + lane];
+    }
     for (uint32_t base = E0; base < E1; base += 64) {
-        const uint32_t e = base + lane;
-        float4 x = make_float4(0.f, 0.f, 0.f, 0.f), y = x;
-        float2 z = make_float2(0.f, 0.f);
-        if (has) {
-            x = recs.a[e];
-            y = recs.b[e];
-            z = recs.c[e];
+        const Slot nxt = base + 64 < E1 ? probe2(base + 64) : Slot{false, -1, lane};
+        float4 nx = make_float4(0.f, 0.f, 0.f, 0.f), ny = nx;
+        float2 nz = make_float2(0.f, 0.f);
+        if (nxt.has) {
+            nx = recs.a[base + 64 + lane];
+            ny = recs.b[base + 64 + lane];
+            nz = recs.c[base + 64 + lane];
         }
-        const bool has_next = base + 64 < E1 ? probe(base + 64) : false;
-        float4* row = reinterpret_cast<float4*>(&s_rec[lane * kRecStride]);
-        row[0] = x;
-        row[1] = y;
-        row[2] = make_float4(z.x, z.y, 0.f, 0.f);
+        // segmented inclusive scan, one DPP step per distance (gsr_common.h wave_sum_to_lane63)
+        const int r = lane & 15, row = lane >> 4;
+        const bool t1 = lane - 1 >= cur.seg0 && r >= 1, t2 = lane - 2 >= cur.seg0 && r >= 2,
+                   t4 = lane - 4 >= cur.seg0 && r >= 4, t8 = lane - 8 >= cur.seg0 && r >= 8,
+                   tb15 = (row & 1) && row * 16 - 1 >= cur.seg0, tb31 = row >= 2 && 31 >= cur.seg0;
+        float v[10] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w, z.x, z.y};
+#pragma unroll
+        for (int i = 0; i < 10; i++) {
+            float t;
+            t = dpp_f32<0x111, 0xf, true>(v[i]);
+            v[i] += t1 ? t : 0.f;
+            t = dpp_f32<0x112, 0xf, true>(v[i]);
+            v[i] += t2 ? t : 0.f;
+            t = dpp_f32<0x114, 0xf, true>(v[i]);
+            v[i] += t4 ? t : 0.f;
+            t = dpp_f32<0x118, 0xf, true>(v[i]);
+            v[i] += t8 ? t : 0.f;
+            t = dpp_f32<0x142, 0xa, false>(v[i]);
+            v[i] += tb15 ? t : 0.f;
+            t = dpp_f32<0x143, 0xc, false>(v[i]);
+            v[i] += tb31 ? t : 0.f;
+        }
+        // the last lane of each run hands the total to its owner
+        const int next_owner = __shfl_down(cur.owner, 1);
+        if (cur.owner >= 0 && (lane == 63 || next_owner != cur.owner)) {
+            part[cur.owner * 3 + 0] = make_float4(v[0], v[1], v[2], v[3]);
+            part[cur.owner * 3 + 1] = make_float4(v[4], v[5], v[6], v[7]);
+            part[cur.owner * 3 + 2] = make_float4(v[8], v[9], 0.f, 0.f);
+        }
         __syncthreads();
-        const uint32_t lo = my0 > base ? my0 : base;
-        const uint32_t hi = my1 < base + 64 ? my1 : base + 64;
-        for (uint32_t k = lo; k < hi; k++) {
-            const float4* rr = reinterpret_cast<const float4*>(&s_rec[(int)(k - base) * kRecStride]);
-            const float4 p = rr[0], q = rr[1], ww = rr[2];
+        if ((my0 > base ? my0 : base) < (my1 < base + 64 ? my1 : base + 64)) {  // this Gaussian has records here
+            const float4 p = part[lane * 3 + 0], q = part[lane * 3 + 1], ww = part[lane * 3 + 2];
             sa.x += p.x; sa.y += p.y; sa.z += p.z; sa.w += p.w;
             sb.x += q.x; sb.y += q.y; sb.z += q.z; sb.w += q.w;
             sc.x += ww.x; sc.y += ww.y;
         }
         __syncthreads();
-        has = has_next;
+        cur = nxt;
+        x = nx;
+        y = ny;
+        z = nz;
     }
 }
 

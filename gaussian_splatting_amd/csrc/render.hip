@@ -6,9 +6,11 @@
 // (T * (1 - alpha) < 1e-4 ends the pixel without adding that Gaussian), and the
 // same outputs (colour + T * bg, inverse depth, final T, last contributor).
 //
-// CDNA4 structure (DESIGN.md "render"):
-//  * ONE wave64 per 16x16 tile.  Lane l owns pixel (l & 7, l >> 3) of each of the
-//    four 8x8 quadrants ("slots" 0..3), so a lane carries four pixels' state;
+// CDNA4 structure:
+//  * forward: one wave64 per half tile (16x8 pixels); lane l owns pixel (l & 7, l >> 3)
+//    of each of the half's two 8x8 quadrants ("slots"); the backward: one wave64 per
+//    (tile, 256-entry segment) unit with all four quadrants, started from the forward's
+//    blend checkpoint;
 //  * list entries are staged 64 at a time (one per lane) into LDS as 48-byte
 //    splat records; while loading, each entry's alpha >= 1/255 footprint (its
 //    box, then the ellipse itself) is tested against the four quadrants (4-bit
