@@ -212,10 +212,20 @@ int bwd_segment_checkpoints() {
 // event recorded behind that copy.  The host waits on the event -- i.e. for the binning
 // counts -- and not for the whole stream, so the render kernels queued behind the copy keep
 // the GPU busy while the host returns to Python and queues the backward.
+// By default the slot is coherent and mapped, and K2 stores the count into it itself
+// (`dev`), so no copy is queued behind K2; GSR_HOST_TOTAL=0 selects the copy (A/B runs).
 struct TotalReadback {
     unsigned long long* host = nullptr;
+    unsigned long long* dev = nullptr;  // device view of `host`, or null: copy instead
     hipEvent_t ev = nullptr;
 };
+bool host_total_store() {
+    static const bool v = [] {
+        const char* e = getenv("GSR_HOST_TOTAL");
+        return !e || atoi(e) != 0;
+    }();
+    return v;
+}
 int total_readback(TotalReadback** out) {
     constexpr int kMaxDevices = 64;
     thread_local TotalReadback slots[kMaxDevices];
@@ -225,13 +235,21 @@ int total_readback(TotalReadback** out) {
     TotalReadback& r = slots[dev];
     if (!r.host) {
         void* h = nullptr;
-        if (hipHostMalloc(&h, sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess)
+        const bool mapped = host_total_store();
+        if (hipHostMalloc(&h, sizeof(unsigned long long),
+                          mapped ? hipHostMallocMapped | hipHostMallocCoherent : hipHostMallocDefault) != hipSuccess)
             return fail(GSR_ERR_HIP, "num_rendered readback: hipHostMalloc failed");
+        void* d = nullptr;
+        if (mapped && hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+            (void)hipHostFree(h);
+            return fail(GSR_ERR_HIP, "num_rendered readback: hipHostGetDevicePointer failed");
+        }
         if (hipEventCreateWithFlags(&r.ev, hipEventDisableTiming) != hipSuccess) {
             (void)hipHostFree(h);
             return fail(GSR_ERR_HIP, "num_rendered readback: hipEventCreate failed");
         }
         r.host = (unsigned long long*)h;
+        r.dev = (unsigned long long*)d;
     }
     *out = &r;
     return GSR_OK;
@@ -613,10 +631,12 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
     }
     // exact mode: counts first (ranges unclamped), then the host reads R
     const size_t kNoCap = ~(size_t)0;
+    TotalReadback* rb = nullptr;
+    if (int rc = total_readback(&rb)) return rc;
     {
         StageScope sc(ST_BIN_COUNT, stream);
         HIP_TRY(launch_bin_count(P, geom, gx, gy, img.ranges, capacity_hint > 0 ? (size_t)capacity_hint : kNoCap,
-                                 stream),
+                                 rb->dev, stream),
                 "bin_count");
     }
     if (int rc = check_debug(debug, stream, "bin_count")) return rc;
@@ -627,12 +647,12 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
     // for the host: every stage is queued, then the host waits for the copy of R queued
     // right behind K2 (not for the render behind it), and if R exceeds C the lists are
     // rebuilt into a buffer of exactly R.
-    TotalReadback* rb = nullptr;
-    if (int rc = total_readback(&rb)) return rc;
-    // queue the copy of num_rendered (written by K2) and mark it; wait_total() waits for it only
+    // mark num_rendered (K2 stores it into the host slot, or a copy is queued); wait_total()
+    // waits for that mark only
     auto queue_total = [&]() -> int {
-        HIP_TRY(hipMemcpyAsync(rb->host, geom.total, sizeof(*rb->host), hipMemcpyDeviceToHost, stream),
-                "num_rendered copy");
+        if (!rb->dev)
+            HIP_TRY(hipMemcpyAsync(rb->host, geom.total, sizeof(*rb->host), hipMemcpyDeviceToHost, stream),
+                    "num_rendered copy");
         HIP_TRY(hipEventRecord(rb->ev, stream), "num_rendered event");
         return GSR_OK;
     };
@@ -693,7 +713,7 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
         if (int rc = wait_total(&total)) return rc;
         if (total > C) {  // the hint was too small: recount (resets the cursors) and rebuild exactly
             C = (size_t)total;
-            HIP_TRY(launch_bin_count(P, geom, gx, gy, img.ranges, C, stream), "bin_count");
+            HIP_TRY(launch_bin_count(P, geom, gx, gy, img.ranges, C, nullptr, stream), "bin_count");
             if (int rc = bin_and_render(C)) return rc;
         }
     }

@@ -277,7 +277,7 @@ __global__ void __launch_bounds__(kBinThreads) tile_scan_kernel(uint32_t tiles, 
                                                                 uint32_t* __restrict__ tile_base, int nchunks,
                                                                 const u64* __restrict__ chunk_total,
                                                                 u64* __restrict__ chunk_base, u64* __restrict__ total,
-                                                                u64 cap, uint32_t* __restrict__ cls_list,
+                                                                u64* host_total, u64 cap, uint32_t* __restrict__ cls_list,
                                                                 uint32_t* __restrict__ cls_count) {
     __shared__ u64 s_tmp[kBinWaves];
     __shared__ uint32_t s_cls[kSortClasses];
@@ -313,7 +313,11 @@ __global__ void __launch_bounds__(kBinThreads) tile_scan_kernel(uint32_t tiles, 
         }
         carry += all;
     }
-    if (threadIdx.x == 0) total[0] = carry;
+    if (threadIdx.x == 0) {
+        total[0] = carry;
+        // the host's copy (coherent pinned memory, mapped): no copy launch behind this kernel
+        if (host_total) __hip_atomic_store(host_total, carry, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     carry = 0;
     for (uint32_t base = 0; base < (uint32_t)nchunks; base += T) {
         const uint32_t c = base + threadIdx.x;
@@ -626,7 +630,7 @@ size_t bin_cell_count(uint32_t gx, uint32_t gy) {
 // K0 + K1 + K2: spatial order, tile counts, ranges, tile starts, chunk offsets, record
 // bases, the long-list class lists and the instance count (g.total).
 hipError_t launch_bin_count(int P, const GeomState& g, uint32_t gx, uint32_t gy, uint2* ranges, size_t cap,
-                            hipStream_t stream) {
+                            unsigned long long* host_total, hipStream_t stream) {
     const uint32_t tiles = gx * gy;
     int chunk = 0;
     const int nchunks = bin_chunks(P, &chunk);
@@ -650,7 +654,7 @@ hipError_t launch_bin_count(int P, const GeomState& g, uint32_t gx, uint32_t gy,
                            g.order, g.n_visible, tiles, gx, g.tile_cnt, g.chunk_off);
     hipLaunchKernelGGL(tile_scan_kernel, dim3(1), block, 0, stream, tiles, g.tile_cnt, tiles + cells, g.unit_cnt, g.tile_join,
                        ranges, g.tile_base, nchunks,
-                       g.chunk_total, g.chunk_base, g.total, (u64)cap, g.cls_list, g.cls_count);
+                       g.chunk_total, g.chunk_base, g.total, (u64*)host_total, (u64)cap, g.cls_list, g.cls_count);
     return hipGetLastError();
 }
 

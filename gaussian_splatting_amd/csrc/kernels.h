@@ -267,8 +267,9 @@ hipError_t launch_mark_visible(int P, const float* means3D, const float* view, b
 // binning.hip
 size_t bin_chunk_count(int P);
 size_t bin_cell_count(uint32_t gx, uint32_t gy);
+// host_total: mapped coherent host memory K2 also writes the instance count to, or null
 hipError_t launch_bin_count(int P, const GeomState& g, uint32_t gx, uint32_t gy, uint2* ranges, size_t cap,
-                            hipStream_t stream);
+                            unsigned long long* host_total, hipStream_t stream);
 hipError_t launch_bin_scatter(int P, const GeomState& g, uint32_t gx, uint32_t gy, const BinningState& b, size_t cap,
                               hipStream_t stream);
 hipError_t launch_tile_sort(uint32_t tiles, const uint2* ranges, const GeomState& g, const BinningState& b,
