@@ -317,7 +317,6 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
     const float pxf0 = (float)(tile_x0 + lx), pyf0 = (float)(tile_y0 + ly);  // this lane's pixel in quadrant 0
 
     __shared__ float4 s_xy[kBatch], s_cq[kBatch], s_col[kBatch];  // as in the forward
-    __shared__ float4 s_abc[kBatch];                              // raw conic (a, b, c) for the flush
     __shared__ float4 s_acc[kBatch][3];                           // per entry: the 10 reduced sums (+2 pad)
     GSR_STAMP(g_st_rbwd, blockIdx.x, 0);
     GSR_STAMP_HWID(g_st_rbwd, blockIdx.x);
@@ -392,6 +391,7 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
     for (int b0 = start; b0 < end; b0 += kBatch) {
         const bool has = b0 + lane < end;
         uint32_t qm = 0, e = 0;
+        float ca = 0.f, cb = 0.f, cc = 0.f, o = 0.f;  // this lane's entry: raw conic and opacity, for the flush
         if (has) {
             const uint32_t ent = a.gid_sorted[range.x + b0 + lane];  // Gaussian << 4 | quadrant mask
             const float4* rec = a.rec + (size_t)kRecRows * (ent >> kEntryMaskBits);
@@ -401,7 +401,10 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
                 (ttx - __float_as_uint(v3.x));
             s_xy[lane] = make_float4(v0.x, v0.y, v1.y, v1.z);
             s_col[lane] = v2;
-            s_abc[lane] = make_float4(v0.z, v0.w, v1.x, 0.f);  // raw conic, for the flush
+            ca = v0.z;
+            cb = v0.w;
+            cc = v1.x;
+            o = v1.y;
             qm = ent & kEntryMask;
             s_cq[lane] = stage_conic(v0, v1, qm);
         }
@@ -478,8 +481,6 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
             float2 rc = make_float2(0.f, 0.f);
             if ((written >> lane) & 1ull) {
                 const float4 A = s_acc[lane][0], B = s_acc[lane][1], Cc = s_acc[lane][2];
-                const float4 abc = s_abc[lane];
-                const float ca = abc.x, cb = abc.y, cc = abc.z, o = s_xy[lane].z;
                 // dL/dmean2D in NDC units (x 0.5 W, 0.5 H, CR/backward.cu:509-510,600-601);
                 // dL/dconic with the reference's -0.5 factors (CR/backward.cu:604-606)
                 ra = A;
