@@ -489,9 +489,15 @@ __device__ __forceinline__ void view_backward(const ViewCam& c, const GaussIn& g
 // ---- 3. fused per-Gaussian backward ---------------------------------------------
 // (Folding the record sums into this kernel was measured slower: the sums' dependent loads
 // then run at this kernel's LDS-limited occupancy.)
+#ifndef GSR_GB_HALVES
+#define GSR_GB_HALVES 1
+#endif
+// With GSR_GB_HALVES the SH rows go through LDS 32 at a time at the end of the kernel
+// (lanes 0-31, then 32-63): 6.6 KiB of LDS per wave instead of 13, twice the waves per CU.
+constexpr int kGbShRows = GSR_GB_HALVES ? 32 : 64;
 template <int SH_MODE>
 __global__ void __launch_bounds__(64) gauss_bwd_kernel(GaussBwdArgs a) {
-    __shared__ __attribute__((aligned(16))) float s_sh[SH_MODE != kShGlobal ? 64 * kShStride : 4];
+    __shared__ __attribute__((aligned(16))) float s_sh[SH_MODE != kShGlobal ? kGbShRows * kShStride : 4];
     const int lane = threadIdx.x;
     const int g0 = blockIdx.x * 64;
     const int idx = g0 + lane;
@@ -500,11 +506,15 @@ __global__ void __launch_bounds__(64) gauss_bwd_kernel(GaussBwdArgs a) {
 
     const ShAddr sh_src{a.shs, a.dc, M};
     const ShGradAddr sh_dst{a.dL_dsh, a.dL_ddc, M};
-    if constexpr (SH_MODE != kShGlobal) {
+    constexpr bool kShLate = SH_MODE != kShGlobal && GSR_GB_HALVES;
+    if constexpr (SH_MODE != kShGlobal && !kShLate) {
         // coalesced stage-in of the wave's SH rows (64 x 48 floats, either layout)
         sh_stage_in<64, 64, SH_MODE == kShLdsSplit>(sh_src, g0, nvalid, s_sh, kShStride, lane);
         __syncthreads();
     }
+    // deferred SH backward (kShLate): its inputs, and the 3-D mean gradient it adds to
+    bool sh_late = false;
+    float3 sh_v = make_float3(0.f, 0.f, 0.f), sh_g = sh_v, dmean_late = sh_v;
 
     const bool valid = idx < a.P;
     const bool visible = valid && a.radii[idx] > 0;
@@ -519,7 +529,9 @@ __global__ void __launch_bounds__(64) gauss_bwd_kernel(GaussBwdArgs a) {
         if (a.dL_dscale) store3(a.dL_dscale, idx, 0.f, 0.f, 0.f);
         if (a.dL_drot) reinterpret_cast<float4*>(a.dL_drot)[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
         if (a.dL_dsh || a.dL_ddc) {
-            if constexpr (SH_MODE != kShGlobal) {
+            if constexpr (kShLate) {
+                // rows zeroed in the SH pass below
+            } else if constexpr (SH_MODE != kShGlobal) {
                 for (int k = 0; k < kShRowF; k += 4)
                     *reinterpret_cast<float4*>(&s_sh[lane * kShStride + k]) = make_float4(0.f, 0.f, 0.f, 0.f);
             } else {
@@ -671,7 +683,12 @@ __global__ void __launch_bounds__(64) gauss_bwd_kernel(GaussBwdArgs a) {
         dmean.z += (Pm[8] * m_w - Pm[11] * mul1) * m2x + (Pm[9] * m_w - Pm[11] * mul2) * m2y;
 
         // ---- SH colour backward (CR/backward.cu:12-146)
-        if (a.shs || a.dc) {
+        if (kShLate && (a.shs || a.dc)) {
+            sh_late = true;
+            sh_v = make_float3(mean.x - a.campos[0], mean.y - a.campos[1], mean.z - a.campos[2]);
+            const uint8_t cm = a.geom.clamped[idx];
+            sh_g = make_float3((cm & 1) ? 0.f : dcol.x, (cm & 2) ? 0.f : dcol.y, (cm & 4) ? 0.f : dcol.z);
+        } else if (a.shs || a.dc) {
             const float3 v = make_float3(mean.x - a.campos[0], mean.y - a.campos[1], mean.z - a.campos[2]);
             const float len = sqrtf(v.x * v.x + v.y * v.y + v.z * v.z);
             const uint8_t cm = a.geom.clamped[idx];
@@ -693,7 +710,10 @@ __global__ void __launch_bounds__(64) gauss_bwd_kernel(GaussBwdArgs a) {
             const ShGlobal acc{sh_src, sh_dst, idx};
             for (int k = 0; k < M; k++) acc.store(k, make_float3(0.f, 0.f, 0.f));
         }
-        store3(a.dL_dmean3D, idx, dmean.x, dmean.y, dmean.z);
+        if (sh_late)
+            dmean_late = dmean;  // stored after the SH pass adds the direction term
+        else
+            store3(a.dL_dmean3D, idx, dmean.x, dmean.y, dmean.z);
 
         // ---- scale / rotation backward (CR/backward.cu:296-365, called when scales are given, :427-428)
         if (a.scales) {
@@ -734,7 +754,41 @@ __global__ void __launch_bounds__(64) gauss_bwd_kernel(GaussBwdArgs a) {
         }
     }
 
-    if constexpr (SH_MODE != kShGlobal) {
+    if constexpr (kShLate) {
+        // SH backward, half a wave at a time through LDS: coalesced stage-in of 32 rows,
+        // their lanes evaluate it in place, coalesced write-back of the 32 dL/dSH rows
+        for (int half = 0; half < 2; half++) {
+            const int rows = min(kGbShRows, nvalid - half * kGbShRows);
+            if (rows <= 0) break;  // wave-uniform
+            sh_stage_in<kGbShRows, 64, SH_MODE == kShLdsSplit>(sh_src, g0 + half * kGbShRows, rows, s_sh, kShStride,
+                                                              lane);
+            __syncthreads();
+            if ((lane >> 5) == half && idx < a.P) {
+                float* row = &s_sh[(lane & 31) * kShStride];
+                if (sh_late) {
+                    const float len = sqrtf(sh_v.x * sh_v.x + sh_v.y * sh_v.y + sh_v.z * sh_v.z);
+                    float ddx, ddy, ddz;
+                    sh_backward(ShLds{row}, a.D, M, sh_v.x / len, sh_v.y / len, sh_v.z / len, sh_g, ddx, ddy, ddz);
+                    const float3 v = sh_v;
+                    const float sum2 = v.x * v.x + v.y * v.y + v.z * v.z;
+                    const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
+                    float3 dm = dmean_late;
+                    dm.x += ((sum2 - v.x * v.x) * ddx - v.y * v.x * ddy - v.z * v.x * ddz) * invsum32;
+                    dm.y += (-v.x * v.y * ddx + (sum2 - v.y * v.y) * ddy - v.z * v.y * ddz) * invsum32;
+                    dm.z += (-v.x * v.z * ddx - v.y * v.z * ddy + (sum2 - v.z * v.z) * ddz) * invsum32;
+                    store3(a.dL_dmean3D, idx, dm.x, dm.y, dm.z);
+                } else {
+                    for (int k = 0; k < kShRowF; k += 4)
+                        *reinterpret_cast<float4*>(&row[k]) = make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+            }
+            __syncthreads();
+            if (a.dL_dsh || a.dL_ddc)
+                sh_stage_out<kGbShRows, 64, SH_MODE == kShLdsSplit>(sh_dst, g0 + half * kGbShRows, rows, s_sh,
+                                                                   kShStride, lane);
+            __syncthreads();
+        }
+    } else if constexpr (SH_MODE != kShGlobal) {
         // coalesced write-back of the wave's dL/dSH rows
         __syncthreads();
         sh_stage_out<64, 64, SH_MODE == kShLdsSplit>(sh_dst, g0, nvalid, s_sh, kShStride, lane);
