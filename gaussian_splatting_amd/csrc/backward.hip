@@ -112,25 +112,20 @@ __device__ __forceinline__ void reduce_records(int P, int g0, const uint32_t* __
         }
         // segmented inclusive scan, one DPP step per distance (gsr_common.h wave_sum_to_lane63)
         const int r = lane & 15, row = lane >> 4;
-        const bool t1 = lane - 1 >= cur.seg0 && r >= 1, t2 = lane - 2 >= cur.seg0 && r >= 2,
-                   t4 = lane - 4 >= cur.seg0 && r >= 4, t8 = lane - 8 >= cur.seg0 && r >= 8,
-                   tb15 = (row & 1) && row * 16 - 1 >= cur.seg0, tb31 = row >= 2 && 31 >= cur.seg0;
+        // the masks as 0/1 factors: v += shifted * m is one FMA (records are finite)
+        const float m1 = lane - 1 >= cur.seg0 && r >= 1 ? 1.f : 0.f, m2 = lane - 2 >= cur.seg0 && r >= 2 ? 1.f : 0.f,
+                    m4 = lane - 4 >= cur.seg0 && r >= 4 ? 1.f : 0.f, m8 = lane - 8 >= cur.seg0 && r >= 8 ? 1.f : 0.f,
+                    mb15 = (row & 1) && row * 16 - 1 >= cur.seg0 ? 1.f : 0.f,
+                    mb31 = row >= 2 && 31 >= cur.seg0 ? 1.f : 0.f;
         float v[10] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w, z.x, z.y};
 #pragma unroll
         for (int i = 0; i < 10; i++) {
-            float t;
-            t = dpp_f32<0x111, 0xf, true>(v[i]);
-            v[i] += t1 ? t : 0.f;
-            t = dpp_f32<0x112, 0xf, true>(v[i]);
-            v[i] += t2 ? t : 0.f;
-            t = dpp_f32<0x114, 0xf, true>(v[i]);
-            v[i] += t4 ? t : 0.f;
-            t = dpp_f32<0x118, 0xf, true>(v[i]);
-            v[i] += t8 ? t : 0.f;
-            t = dpp_f32<0x142, 0xa, false>(v[i]);
-            v[i] += tb15 ? t : 0.f;
-            t = dpp_f32<0x143, 0xc, false>(v[i]);
-            v[i] += tb31 ? t : 0.f;
+            v[i] = fmaf(dpp_f32<0x111, 0xf, true>(v[i]), m1, v[i]);
+            v[i] = fmaf(dpp_f32<0x112, 0xf, true>(v[i]), m2, v[i]);
+            v[i] = fmaf(dpp_f32<0x114, 0xf, true>(v[i]), m4, v[i]);
+            v[i] = fmaf(dpp_f32<0x118, 0xf, true>(v[i]), m8, v[i]);
+            v[i] = fmaf(dpp_f32<0x142, 0xa, false>(v[i]), mb15, v[i]);
+            v[i] = fmaf(dpp_f32<0x143, 0xc, false>(v[i]), mb31, v[i]);
         }
         // the last lane of each run hands the total to its owner
         const int next_owner = __shfl_down(cur.owner, 1);
