@@ -109,9 +109,60 @@ __device__ T block_exclusive_scan(T v, T* s_tmp, T* total) {
 // Gaussians (lane l: n tiles in rectangle r), each once; `owner` is the lane of the
 // instance's Gaussian, (tx, ty) the tile's column and row.  f may shuffle from `owner`
 // (all lanes are active).
+#ifndef GSR_FEI_DPP
+#define GSR_FEI_DPP 1
+#endif
+template <uint32_t CTRL, uint32_t ROW_MASK, bool BOUND_ZERO>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROW_MASK, 0xf, BOUND_ZERO);
+}
+// Inclusive prefix sum / max over the wave: row_shr 1, 2, 4, 8 inside each 16-lane row, then
+// row_bcast:15 and row_bcast:31 carry the row totals up (identity 0).  Six VALU steps, no LDS.
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
+    v += dpp_u32<0x111, 0xf, true>(v);
+    v += dpp_u32<0x112, 0xf, true>(v);
+    v += dpp_u32<0x114, 0xf, true>(v);
+    v += dpp_u32<0x118, 0xf, true>(v);
+    v += dpp_u32<0x142, 0xa, false>(v);
+    v += dpp_u32<0x143, 0xc, false>(v);
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
+    v = max(v, dpp_u32<0x111, 0xf, true>(v));
+    v = max(v, dpp_u32<0x112, 0xf, true>(v));
+    v = max(v, dpp_u32<0x114, 0xf, true>(v));
+    v = max(v, dpp_u32<0x118, 0xf, true>(v));
+    v = max(v, dpp_u32<0x142, 0xa, false>(v));
+    v = max(v, dpp_u32<0x143, 0xc, false>(v));
+    return v;
+}
+
 template <class F>
 __device__ __forceinline__ void for_each_instance(uint32_t n, uint2 r, uint32_t gx, F&& f) {
     const int lane = threadIdx.x & 63;
+#if GSR_FEI_DPP
+    // Owner of slot s: the largest lane whose run starts at or before s.  Each round, the lanes
+    // whose runs start inside it mark their start in the wave's LDS row (lane + 1), and an
+    // inclusive max-scan over the wave spreads the marks; the previous round's last owner
+    // fills the slots before the first mark.  (One wave's LDS accesses execute in order.)
+    __shared__ uint32_t s_mark[kBinThreads];
+    uint32_t* mark = s_mark + (threadIdx.x & ~63u);
+    const uint32_t incl = wave_incl_sum(n);
+    const uint32_t excl = incl - n;
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    const uint32_t w = (r.y & 0xffffu) - (r.x & 0xffffu);
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < total; base += 64) {
+        const uint32_t s = base + lane;
+        mark[lane] = 0u;
+        __builtin_amdgcn_wave_barrier();
+        if (n && excl >= base && excl < base + 64) mark[excl - base] = (uint32_t)lane + 1u;
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t m = max(wave_incl_max(mark[lane]), carry);
+        __builtin_amdgcn_wave_barrier();
+        carry = (uint32_t)__builtin_amdgcn_readlane((int)m, 63);
+        const int owner = (int)m - 1;
+#else
     uint32_t incl = n;
     for (int off = 1; off < 64; off <<= 1) {
         const uint32_t u = __shfl_up(incl, off);
@@ -129,6 +180,7 @@ __device__ __forceinline__ void for_each_instance(uint32_t n, uint2 r, uint32_t 
             const int cand = owner + step;
             if (__shfl(excl, cand) <= s) owner = cand;
         }
+#endif
         const uint32_t k = s - __shfl(excl, owner);
         const uint32_t ow = __shfl(w, owner), org = __shfl(r.x, owner);
         const bool valid = s < total;
