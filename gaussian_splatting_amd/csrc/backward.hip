@@ -75,15 +75,22 @@ __device__ __forceinline__ void reduce_records(int P, int g0, const uint32_t* __
         bool has;
         int owner, seg0;
     };
+    // The owner of record e: the largest lane whose range starts at or before e.  Called for
+    // consecutive chunks in order: lanes whose ranges start in the chunk mark the start (lane + 1)
+    // in LDS, a DPP max-scan spreads the marks, the previous chunk's last owner fills the rest
+    // (no dependent ds_bpermute chain; one wave's LDS accesses execute in order).
+    __shared__ uint32_t s_mark[64];
+    uint32_t carry = 0;
     auto probe2 = [&](uint32_t base) -> Slot {
         const uint32_t e = base + lane;
-        int owner = 0;
-#pragma unroll
-        for (int step = 32; step > 0; step >>= 1) {
-            const int cand = owner + step;
-            const uint32_t v = __shfl(my0, cand & 63);
-            if (cand < 64 && v <= e) owner = cand;
-        }
+        s_mark[lane] = 0u;
+        __builtin_amdgcn_wave_barrier();
+        if (n && my0 >= base && my0 < base + 64) s_mark[my0 - base] = (uint32_t)lane + 1u;
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t m = max(wave_incl_max(s_mark[lane]), carry);
+        __builtin_amdgcn_wave_barrier();
+        carry = (uint32_t)__builtin_amdgcn_readlane((int)m, 63);
+        const int owner = m ? (int)m - 1 : 0;
         const uint32_t o0 = __shfl(my0, owner), ow = __shfl(w, owner), ox = __shfl(x0, owner),
                        oy = __shfl(y0, owner);
         const unsigned long long okey = __shfl(key, owner);

@@ -289,6 +289,31 @@ __device__ __forceinline__ float dpp_f32(float v) {
                               __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROW_MASK, 0xf, BOUND_ZERO));
 }
 
+template <uint32_t CTRL, uint32_t ROW_MASK, bool BOUND_ZERO>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROW_MASK, 0xf, BOUND_ZERO);
+}
+// Inclusive prefix sum / max over the wave: row_shr 1, 2, 4, 8 inside each 16-lane row, then
+// row_bcast:15 and row_bcast:31 carry the row totals up (identity 0).  Six VALU steps, no LDS.
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
+    v += dpp_u32<0x111, 0xf, true>(v);
+    v += dpp_u32<0x112, 0xf, true>(v);
+    v += dpp_u32<0x114, 0xf, true>(v);
+    v += dpp_u32<0x118, 0xf, true>(v);
+    v += dpp_u32<0x142, 0xa, false>(v);
+    v += dpp_u32<0x143, 0xc, false>(v);
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
+    v = max(v, dpp_u32<0x111, 0xf, true>(v));
+    v = max(v, dpp_u32<0x112, 0xf, true>(v));
+    v = max(v, dpp_u32<0x114, 0xf, true>(v));
+    v = max(v, dpp_u32<0x118, 0xf, true>(v));
+    v = max(v, dpp_u32<0x142, 0xa, false>(v));
+    v = max(v, dpp_u32<0x143, 0xc, false>(v));
+    return v;
+}
+
 // Full wave64 sum, valid in lane 63: Hillis-Steele prefix inside each 16-lane row
 // (row_shr 1,2,4,8 with zero fill), then row_bcast:15 / row_bcast:31 carry the row
 // totals upward.  Six VALU ops, no LDS traffic.
