@@ -88,9 +88,13 @@ template <typename T>
 __device__ T block_exclusive_scan(T v, T* s_tmp, T* total) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
     T incl = v;
-    for (int off = 1; off < 64; off <<= 1) {
-        const T u = __shfl_up(incl, off);
-        if (lane >= off) incl += u;
+    if constexpr (sizeof(T) == 4) {
+        incl = (T)wave_incl_sum((uint32_t)v);  // DPP
+    } else {
+        for (int off = 1; off < 64; off <<= 1) {
+            const T u = __shfl_up(incl, off);
+            if (lane >= off) incl += u;
+        }
     }
     __syncthreads();
     if (lane == 63) s_tmp[w] = incl;

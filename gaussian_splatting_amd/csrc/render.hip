@@ -235,8 +235,7 @@ __global__ void __launch_bounds__(64) GSR_FWD_OCCUPANCY render_fwd_kernel(Render
     uint32_t lm = last[0];
 #pragma unroll
     for (int k = 1; k < NQ; k++) lm = max(lm, last[k]);
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) lm = max(lm, (uint32_t)__shfl_xor((int)lm, off));
+    lm = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_max(lm), 63);  // DPP max, no ds_bpermute chain
     if (NPART == 2) {
         unsigned long long old = 0;
         if (lane == 0)
@@ -362,10 +361,7 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
     int slim[4];
 #pragma unroll
     for (int q = 0; q < 4; q++) {
-        int v = nc[q];
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off));
-        slim[q] = (int)uniform_u32((uint32_t)v);
+        slim[q] = __builtin_amdgcn_readlane((int)wave_incl_max((uint32_t)nc[q]), 63);  // DPP max over the wave
     }
     const int limit = max(max(slim[0], slim[1]), max(slim[2], slim[3]));
     const int end = min(limit, start + a.seg_ck * kCkStride);
