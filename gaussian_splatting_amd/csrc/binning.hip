@@ -73,10 +73,13 @@ __device__ __forceinline__ uint32_t rect_tiles(uint2 r) {
 // Sum over the workgroup (a multiple of 64 threads); result valid in every thread.
 template <typename T>
 __device__ T block_sum(T v, T* s_tmp) {
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    if constexpr (sizeof(T) == 4)
+        v = (T)wave_incl_sum((uint32_t)v);  // DPP: the wave's sum lands in lane 63
+    else
+        v = (T)wave_incl_sum_u64((unsigned long long)v);
     const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
     __syncthreads();
-    if ((threadIdx.x & 63) == 0) s_tmp[w] = v;
+    if ((threadIdx.x & 63) == 63) s_tmp[w] = v;
     __syncthreads();
     T t = 0;
     for (int i = 0; i < nw; i++) t += s_tmp[i];
@@ -88,14 +91,10 @@ template <typename T>
 __device__ T block_exclusive_scan(T v, T* s_tmp, T* total) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
     T incl = v;
-    if constexpr (sizeof(T) == 4) {
-        incl = (T)wave_incl_sum((uint32_t)v);  // DPP
-    } else {
-        for (int off = 1; off < 64; off <<= 1) {
-            const T u = __shfl_up(incl, off);
-            if (lane >= off) incl += u;
-        }
-    }
+    if constexpr (sizeof(T) == 4)
+        incl = (T)wave_incl_sum((uint32_t)v);  // DPP, no ds_bpermute chain
+    else
+        incl = (T)wave_incl_sum_u64((unsigned long long)v);
     __syncthreads();
     if (lane == 63) s_tmp[w] = incl;
     __syncthreads();

@@ -304,6 +304,19 @@ __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
     v += dpp_u32<0x143, 0xc, false>(v);
     return v;
 }
+__device__ __forceinline__ unsigned long long wave_incl_sum_u64(unsigned long long v) {
+#define GSR_DPP64(CTRL, RM, BZ)                                                                      \
+    v += ((unsigned long long)dpp_u32<CTRL, RM, BZ>((uint32_t)(v >> 32)) << 32) |                     \
+         (unsigned long long)dpp_u32<CTRL, RM, BZ>((uint32_t)v)
+    GSR_DPP64(0x111, 0xf, true);
+    GSR_DPP64(0x112, 0xf, true);
+    GSR_DPP64(0x114, 0xf, true);
+    GSR_DPP64(0x118, 0xf, true);
+    GSR_DPP64(0x142, 0xa, false);
+    GSR_DPP64(0x143, 0xc, false);
+#undef GSR_DPP64
+    return v;
+}
 __device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
     v = max(v, dpp_u32<0x111, 0xf, true>(v));
     v = max(v, dpp_u32<0x112, 0xf, true>(v));
