@@ -188,9 +188,16 @@ gsr::BinningState carve_binning(char* base, size_t C, size_t* total) {
 void carve_recs(char* base, size_t R, size_t P, gsr::GradRecs* recs, gsr::GradRecs* sums, size_t* total) {
     using namespace gsr;
     Carver c{base, 0};
-    recs->a = c.take<float4>(R);
-    recs->b = c.take<float4>(R);
-    recs->c = c.take<float2>(R);
+    if (GSR_REC_AOS) {  // interleaved 48-byte records (gsr_common.h)
+        float4* r48 = c.take<float4>(3 * R);
+        recs->a = r48;
+        recs->b = r48 + 1;
+        recs->c = reinterpret_cast<float2*>(r48 + 2);
+    } else {
+        recs->a = c.take<float4>(R);
+        recs->b = c.take<float4>(R);
+        recs->c = c.take<float2>(R);
+    }
     sums->a = c.take<float4>(P);
     sums->b = c.take<float4>(P);
     sums->c = c.take<float2>(P);

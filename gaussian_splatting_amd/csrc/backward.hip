@@ -104,18 +104,18 @@ __device__ __forceinline__ void reduce_records(int P, int g0, const uint32_t* __
     float4 x = make_float4(0.f, 0.f, 0.f, 0.f), y = x;
     float2 z = make_float2(0.f, 0.f);
     if (cur.has) {
-        x = recs.a[E0 + lane];
-        y = recs.b[E0 + lane];
-        z = recs.c[E0 + lane];
+        x = recs.a[(size_t)kRecAB * (E0 + lane)];
+        y = recs.b[(size_t)kRecAB * (E0 + lane)];
+        z = recs.c[(size_t)kRecC * (E0 + lane)];
     }
     for (uint32_t base = E0; base < E1; base += 64) {
         const Slot nxt = base + 64 < E1 ? probe2(base + 64) : Slot{false, -1, lane};
         float4 nx = make_float4(0.f, 0.f, 0.f, 0.f), ny = nx;
         float2 nz = make_float2(0.f, 0.f);
         if (nxt.has) {
-            nx = recs.a[base + 64 + lane];
-            ny = recs.b[base + 64 + lane];
-            nz = recs.c[base + 64 + lane];
+            nx = recs.a[(size_t)kRecAB * (base + 64 + lane)];
+            ny = recs.b[(size_t)kRecAB * (base + 64 + lane)];
+            nz = recs.c[(size_t)kRecC * (base + 64 + lane)];
         }
         // segmented inclusive scan, one DPP step per distance (gsr_common.h wave_sum_to_lane63)
         const int r = lane & 15, row = lane >> 4;

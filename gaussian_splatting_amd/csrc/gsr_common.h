@@ -170,6 +170,14 @@ struct GradRecs {
     float4* b;  // (dmean2D.x, dmean2D.y, dopacity_eff, dconic.b)
     float2* c;  // (dconic.a, dconic.c)
 };
+// The render backward's per-instance records (not the per-Gaussian sums, which stay three
+// arrays): GSR_REC_AOS interleaves them as 48-byte records a, b, (c, pad), so one instance's
+// three stores land in one or two cache lines instead of three.  Index strides:
+#ifndef GSR_REC_AOS
+#define GSR_REC_AOS 1
+#endif
+constexpr int kRecAB = GSR_REC_AOS ? 3 : 1;  // float4 units between records (a, b)
+constexpr int kRecC = GSR_REC_AOS ? 6 : 1;   // float2 units between records (c)
 
 // ---------------------------------------------------------------------------
 // SH coefficient addressing.  Two layouts reach the kernels:

@@ -484,9 +484,12 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
                                  -0.5f * (float)a.H * o * (cc * B.y + cb * B.x), Cc.y, -0.5f * o * B.w);
                 rc = make_float2(-0.5f * o * B.z, -0.5f * o * Cc.x);
             }
-            a.recs.a[e] = ra;
-            a.recs.b[e] = rb;
-            a.recs.c[e] = rc;
+            a.recs.a[(size_t)kRecAB * e] = ra;
+            a.recs.b[(size_t)kRecAB * e] = rb;
+            if (GSR_REC_AOS)  // the whole 16-byte slot: full-width stores only
+                reinterpret_cast<float4*>(a.recs.c)[(size_t)kRecAB * e] = make_float4(rc.x, rc.y, 0.f, 0.f);
+            else
+                a.recs.c[e] = rc;
         }
         __syncthreads();
     }
