@@ -131,6 +131,11 @@ def main():
     ]
     for r in res:
         print(json.dumps({k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items()}))
+    # K2 (tile_scan, one workgroup) stamps its phases at workgroup slot 1000 of the count buffer
+    k2 = read(fb, 0, 1001)[1000, :5]
+    if k2[0] > 0:
+        print(json.dumps({"kernel": "tile_scan", "phase_clk": [int(x) for x in np.diff(k2)],
+                          "labels": ["tile scan", "chunk scan", "barrier", "class counts + zeroing"]}))
     # backward: one workgroup per (tile, segment) unit; per-tile sums of the unit durations
     sf, sb = read(fr, 0, tiles), read(fr, 1, units)
     okb = (sb[:, 0] > 0) & (sb[:, 1] >= sb[:, 0])
