@@ -311,6 +311,7 @@ __global__ void __launch_bounds__(kBinThreads) tile_scan_kernel(uint32_t tiles, 
                                                                 uint32_t* __restrict__ cls_count) {
     __shared__ u64 s_tmp[kBinWaves];
     __shared__ uint32_t s_cls[kSortClasses];
+    GSR_STAMP(g_st_count, 1000, 0);  // K2's phases at workgroup slot 1000 of K1's buffer (tools/stamps.py)
     if (threadIdx.x < kSortClasses) s_cls[threadIdx.x] = 0;  // published by the scan's barriers
     if (threadIdx.x < kUnitLists * kUnitShards) unit_cnt[threadIdx.x * kUnitCntStride] = 0u;  // render work lists
     const uint32_t T = blockDim.x;
@@ -343,6 +344,7 @@ __global__ void __launch_bounds__(kBinThreads) tile_scan_kernel(uint32_t tiles, 
         }
         carry += all;
     }
+    GSR_STAMP(g_st_count, 1000, 1);
     if (threadIdx.x == 0) {
         total[0] = carry;
         // the host's copy (coherent pinned memory, mapped): no copy launch behind this kernel
@@ -357,13 +359,16 @@ __global__ void __launch_bounds__(kBinThreads) tile_scan_kernel(uint32_t tiles, 
         if (c < (uint32_t)nchunks) chunk_base[c] = at;
         carry += all;
     }
+    GSR_STAMP(g_st_count, 1000, 2);
     __syncthreads();
+    GSR_STAMP(g_st_count, 1000, 3);
     if (threadIdx.x < kSortClasses) cls_count[threadIdx.x] = s_cls[threadIdx.x];
     // Leave the tile and cell counters zeroed (all reads of them are done): a rebuild of the
     // lists (capacity hint too small, api.hip) counts again without a memset.  preprocess
     // zeroes them for the first count of a call.
     for (uint32_t i = threadIdx.x; i < n_counters; i += T) cnt[i] = 0u;
     for (uint32_t i = threadIdx.x; i < tiles; i += T) tile_join[i] = 0ull;  // render_fwd's half-tile join
+    GSR_STAMP(g_st_count, 1000, 4);
 }
 
 // ---- K3 ---------------------------------------------------------------------
