@@ -149,7 +149,6 @@ gsr::GeomState carve_geom(char* base, int P, uint32_t gx, uint32_t gy, size_t* t
     g.cls_list = c.take<uint32_t>(2 * (size_t)tiles);
     g.cls_count = c.take<uint32_t>(2);
     g.chunk_total = c.take<unsigned long long>(chunks);
-    g.chunk_base = c.take<unsigned long long>(chunks);
     g.total = c.take<unsigned long long>(1);
     g.unit_cnt = c.take<uint32_t>((size_t)kUnitLists * kUnitShards * kUnitCntStride);
     g.unit_part = c.take<uint2>((size_t)(kUnitLists - 1) * kUnitShards * unit_part_cap(tiles));

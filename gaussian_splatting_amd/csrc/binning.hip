@@ -11,15 +11,16 @@
 //                    counters per word); the flush is one RETURNING atomic add
 //                    per (chunk, tile), whose result -- the chunk's offset inside
 //                    the tile's block -- is kept in chunk_off[chunk][tile];
-//   K2 tile_scan     one workgroup: exclusive scans of the tile counts (-> the
-//                    per-tile ranges, identifyTileRanges' output) and of the
-//                    chunk totals (-> each chunk's first record index); it also
+//   K2 tile_scan     one workgroup: exclusive scan of the tile counts (-> the
+//                    per-tile ranges, identifyTileRanges' output); it also
 //                    lists the tiles too long for one wave's sort (two classes);
 //   K3 tile_scatter  every chunk loads its cursors (tile start + chunk offset)
 //                    into LDS and scatters 64-bit keys (depth bits << 32 |
 //                    index << 4) with LDS atomics (the low 4 bits of a tile-list
 //                    entry, its quadrant mask, are filled in by the forward
-//                    render); it also writes each Gaussian's first record index;
+//                    render); it also writes each Gaussian's first record index
+//                    (the chunk's base summed from K0a's chunk totals, then an
+//                    in-order scan of tiles_touched);
 //   K4 tile_sort     per tile, a bitonic network held in registers (exchanges
 //                    inside a lane, across lanes by swizzle/permute, across
 //                    waves through LDS), writing the Gaussian ids -- the tile
@@ -304,9 +305,7 @@ __global__ void __launch_bounds__(kBinThreads) tile_scan_kernel(uint32_t tiles, 
                                                                 uint32_t n_counters, uint32_t* __restrict__ unit_cnt,
                                                                 unsigned long long* __restrict__ tile_join,
                                                                 uint2* __restrict__ ranges,
-                                                                uint32_t* __restrict__ tile_base, int nchunks,
-                                                                const u64* __restrict__ chunk_total,
-                                                                u64* __restrict__ chunk_base, u64* __restrict__ total,
+                                                                uint32_t* __restrict__ tile_base, u64* __restrict__ total,
                                                                 u64* host_total, u64 cap, uint32_t* __restrict__ cls_list,
                                                                 uint32_t* __restrict__ cls_count) {
     __shared__ u64 s_tmp[kBinWaves];
@@ -350,15 +349,6 @@ __global__ void __launch_bounds__(kBinThreads) tile_scan_kernel(uint32_t tiles, 
         // the host's copy (coherent pinned memory, mapped): no copy launch behind this kernel
         if (host_total) __hip_atomic_store(host_total, carry, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    carry = 0;
-    for (uint32_t base = 0; base < (uint32_t)nchunks; base += T) {
-        const uint32_t c = base + threadIdx.x;
-        const u64 v = c < (uint32_t)nchunks ? chunk_total[c] : 0ull;
-        u64 all = 0;
-        const u64 at = carry + block_exclusive_scan(v, s_tmp, &all);
-        if (c < (uint32_t)nchunks) chunk_base[c] = at;
-        carry += all;
-    }
     GSR_STAMP(g_st_count, 1000, 2);
     __syncthreads();
     GSR_STAMP(g_st_count, 1000, 3);
@@ -377,13 +367,17 @@ __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
     int P, int chunk, const uint2* __restrict__ rect, const uint32_t* __restrict__ tiles_touched,
     const uint32_t* __restrict__ depth_key, const uint4* __restrict__ order, const uint32_t* __restrict__ n_visible,
     uint32_t tiles, uint32_t gx, uint32_t* __restrict__ tile_base,
-    const uint32_t* __restrict__ chunk_off, const u64* __restrict__ chunk_base, u64* __restrict__ keys, u64 cap,
+    const uint32_t* __restrict__ chunk_off, const u64* __restrict__ chunk_total, u64* __restrict__ keys, u64 cap,
     uint32_t* __restrict__ rec_start, float4* __restrict__ rec) {
     extern __shared__ uint32_t s_cur[];  // tiles words
     __shared__ u64 s_tmp[kBinWaves];
     const int g0 = blockIdx.x * chunk, g1 = min(P, g0 + chunk);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     GSR_STAMP(g_st_scatter, blockIdx.x, 0);
+    // this chunk's first record index: the instance totals of the chunks before it (K0a), summed
+    // here (loads issued first, they land while the cursors load) instead of scanned in K2
+    u64 before = 0;
+    for (uint32_t c = threadIdx.x; c < blockIdx.x; c += blockDim.x) before += chunk_total[c];
     if (LDS) {
         // this chunk's cursors: tile start + the chunk's offset inside the tile (K1); entries of
         // tiles the chunk does not touch are garbage and never used
@@ -391,7 +385,7 @@ __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
         for (uint32_t i = threadIdx.x; i < tiles; i += blockDim.x) s_cur[i] = tile_base[i] + off[i];
     }
     // first record index of every Gaussian: chunk base + in-order scan of tiles_touched
-    u64 carry = chunk_base[blockIdx.x];
+    u64 carry = block_sum(before, s_tmp);
     for (int gb = g0; gb < g1; gb += kBinThreads) {
         const int g = gb + (int)threadIdx.x;
         const uint32_t n = g < g1 ? tiles_touched[g] : 0u;
@@ -662,8 +656,8 @@ size_t bin_cell_count(uint32_t gx, uint32_t gy) {
     return bin_cells(gx, gy, &cgx);
 }
 
-// K0 + K1 + K2: spatial order, tile counts, ranges, tile starts, chunk offsets, record
-// bases, the long-list class lists and the instance count (g.total).
+// K0 + K1 + K2: spatial order, chunk instance totals, tile counts, ranges, tile starts,
+// chunk offsets, the long-list class lists and the instance count (g.total).
 hipError_t launch_bin_count(int P, const GeomState& g, uint32_t gx, uint32_t gy, uint2* ranges, size_t cap,
                             unsigned long long* host_total, hipStream_t stream) {
     const uint32_t tiles = gx * gy;
@@ -688,8 +682,7 @@ hipError_t launch_bin_count(int P, const GeomState& g, uint32_t gx, uint32_t gy,
         hipLaunchKernelGGL(tile_count_kernel<false>, grid, block, 0, stream, P, chunk, g.rect, g.tiles_touched,
                            g.order, g.n_visible, tiles, gx, g.tile_cnt, g.chunk_off);
     hipLaunchKernelGGL(tile_scan_kernel, dim3(1), block, 0, stream, tiles, g.tile_cnt, tiles + cells, g.unit_cnt, g.tile_join,
-                       ranges, g.tile_base, nchunks,
-                       g.chunk_total, g.chunk_base, g.total, (u64*)host_total, (u64)cap, g.cls_list, g.cls_count);
+                       ranges, g.tile_base, g.total, (u64*)host_total, (u64)cap, g.cls_list, g.cls_count);
     return hipGetLastError();
 }
 
@@ -705,10 +698,10 @@ hipError_t launch_bin_scatter(int P, const GeomState& g, uint32_t gx, uint32_t g
     if (lds)
         hipLaunchKernelGGL(tile_scatter_kernel<true>, grid, block, cur_bytes, stream, P, chunk, g.rect,
                            g.tiles_touched, g.depth_key, g.order, g.n_visible, tiles, gx, g.tile_base, g.chunk_off,
-                           g.chunk_base, b.keys, (u64)cap, g.rec_start, g.rec);
+                           g.chunk_total, b.keys, (u64)cap, g.rec_start, g.rec);
     else
         hipLaunchKernelGGL(tile_scatter_kernel<false>, grid, block, 0, stream, P, chunk, g.rect, g.tiles_touched,
-                           g.depth_key, g.order, g.n_visible, tiles, gx, g.tile_base, g.chunk_off, g.chunk_base,
+                           g.depth_key, g.order, g.n_visible, tiles, gx, g.tile_base, g.chunk_off, g.chunk_total,
                            b.keys, (u64)cap, g.rec_start, g.rec);
     return hipGetLastError();
 }

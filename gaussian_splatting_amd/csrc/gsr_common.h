@@ -89,7 +89,6 @@ struct GeomState {
     uint32_t* cls_list;         // [2][tiles] tiles whose lists are too long for one wave's sort, by class
     uint32_t* cls_count;        // [2] entries of each class list
     unsigned long long* chunk_total;  // [chunks] tiles_touched per Gaussian chunk
-    unsigned long long* chunk_base;   // [chunks] its exclusive scan
     unsigned long long* total;        // [1] number of instances (num_rendered)
     // backward work list (render.hip, see kUnitLists): counters [list][shard] one per 128-B line,
     // zeroed by K2 before each forward render; the partial-segment lists, [4][shard][unit_part_cap]
