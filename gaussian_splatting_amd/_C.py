@@ -105,17 +105,19 @@ class _Resizer:
     """The reference's resizeFunctional (rasterize_points.cu:29-43) as a C callback."""
 
     def __init__(self, tensor: torch.Tensor):
-        self.tensor = tensor
-        self.cb = _lib.ALLOC_FN(self._resize)
+        # The callback closes over the tensor, not over self: a bound method would make a
+        # reference cycle (self -> cb -> method -> self), so the multi-GB buffers would live
+        # until Python's cyclic GC ran -- about twenty steps of them at 5M@4K (200 GB reserved).
+        def resize(_ctx, nbytes):
+            try:
+                tensor.resize_(int(nbytes))
+                if _poison():
+                    tensor.fill_(255)
+                return tensor.data_ptr()
+            except Exception:  # e.g. out of memory: the library reports GSR_ERR_ALLOC
+                return None
 
-    def _resize(self, _ctx, nbytes):
-        try:
-            self.tensor.resize_(int(nbytes))
-            if _poison():
-                self.tensor.fill_(255)
-            return self.tensor.data_ptr()
-        except Exception:  # e.g. out of memory: the library reports GSR_ERR_ALLOC
-            return None
+        self.cb = _lib.ALLOC_FN(resize)
 
 
 def _present(t) -> bool:

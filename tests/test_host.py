@@ -150,3 +150,26 @@ def test_grad_arena_layout():
         assert p1 == p0 + 4 * n0  # back to back, no gaps
     dc, rest = a.split_features()
     assert dc.shape == (5, 1, 3) and rest.shape == (5, 15, 3)
+
+
+def test_resizer_frees_without_cyclic_gc():
+    """The scratch-buffer callback must not form a reference cycle: the multi-GB geometry,
+    binning and backward buffers are freed by reference counting as soon as the caller drops
+    them, not at the next cyclic GC (which let ~20 steps of buffers pile up at 5M@4K)."""
+    import gc
+    import weakref
+
+    import torch
+
+    from gaussian_splatting_amd import _C
+
+    gc.disable()
+    try:
+        t = torch.empty(0, dtype=torch.uint8)
+        ref = weakref.ref(t)
+        rs = _C._Resizer(t)
+        assert rs.cb(None, 4096) == t.data_ptr() and t.numel() == 4096
+        del rs, t
+        assert ref() is None
+    finally:
+        gc.enable()
