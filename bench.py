@@ -132,7 +132,7 @@ def main():
     views = world > 1 and (args.exchange == "views" or (args.exchange == "auto" and world <= 4))
     ex = ViewExchange(P, dev) if views else None
 
-    def step():
+    def step(collective=True):
         fwd = _C.rasterize_gaussians(bg, scene.means3D, empty, scene.opacities, scene.scales, scene.rotations, 1.0,
                                      empty, cam.viewmatrix, cam.projmatrix, cam.tanfovx, cam.tanfovy, H, W, scene.shs,
                                      Kdeg, cam.campos, False, False, False)
@@ -140,23 +140,27 @@ def main():
         bwd = (bg, scene.means3D, radii, empty, scene.opacities, scene.scales, scene.rotations, 1.0, empty,
                cam.viewmatrix, cam.projmatrix, cam.tanfovx, cam.tanfovy, gc, gd, scene.shs, Kdeg, cam.campos, geom, nr,
                binning, img, False, False)
-        if views:  # N > 1: exchange the 44-B view blocks, every rank sums all views' gradients
+        if views and collective:  # N > 1: exchange the 44-B view blocks, every rank sums all views' gradients
             _C.rasterize_gaussians_backward_screen(*bwd, view_block=ex.local_block())
             ex.exchange()
             _C.gauss_backward_views(scene.means3D, None, scene.shs, Kdeg, scene.opacities, scene.scales,
                                     scene.rotations, 1.0, ex.gathered, out=arena.views())
         else:
             _C.rasterize_gaussians_backward(*bwd, out=arena.views())
-            if world > 1:
+            if world > 1 and collective:
                 arena.all_reduce()
         return nr
 
     # Untimed clock ramp: the GPU lowers its clock when idle and takes ~0.1 s of load to come back
     # (measured: 1.225 ms/step after 3 warm-up steps vs 1.200 after 300).  Then the W warm-up steps.
+    # The ramp runs a time-bounded number of steps, which differs between ranks, so it runs
+    # without collectives (a mismatched collective count would hang the job).
     t_ramp = time.perf_counter()
     while time.perf_counter() - t_ramp < args.ramp_seconds:
-        step()
+        step(collective=False)
         torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
     for _ in range(args.warmup):
         nr = step()
     torch.cuda.synchronize()
