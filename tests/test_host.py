@@ -173,3 +173,26 @@ def test_resizer_frees_without_cyclic_gc():
         assert ref() is None
     finally:
         gc.enable()
+
+
+def test_product_path_never_touches_the_oracle():
+    """The oracle is the checker only: no product module (the packages a user imports, and the
+    native sources behind them) may import, load or link anything under oracle/."""
+    import re
+
+    product = ["gaussian_splatting_amd", "diff_gaussian_rasterization", "simple_knn", "fused_ssim",
+               "plyfile", "fused_ssim_cuda.py"]
+    pat = re.compile(r"(^|\s)(import\s+oracle|from\s+oracle)\b|oracle/|gsr_oracle|liboracle")
+    offenders = []
+    for entry in product:
+        path = os.path.join(ROOT, entry)
+        files = [path] if os.path.isfile(path) else [
+            os.path.join(d, f) for d, _, fs in os.walk(path) for f in fs
+            if f.endswith((".py", ".hip", ".cpp", ".h"))]
+        for f in files:
+            with open(f, encoding="utf-8", errors="replace") as fh:
+                for n, line in enumerate(fh, 1):
+                    code = line.split("#")[0] if f.endswith(".py") else line.split("//")[0]
+                    if pat.search(code):
+                        offenders.append("%s:%d: %s" % (os.path.relpath(f, ROOT), n, line.strip()))
+    assert not offenders, "\n".join(offenders)
