@@ -22,29 +22,39 @@ from . import _lib
 
 __all__ = ["rasterize_gaussians", "rasterize_gaussians_backward", "rasterize_gaussians_backward_screen",
            "gauss_backward_views", "view_block_floats", "mark_visible", "adamUpdate", "fusedssim",
-           "fusedssim_backward"]
+           "fusedssim_backward", "forward_rebuilds", "debug_forward_state"]
 
 
 # Sync-free forward (gsr_rasterize_forward_ex): the binning buffer is sized from a capacity
-# hint -- a slowly decaying maximum of recent num_rendered for the same (device, P, W, H),
-# plus a margin -- so the forward never waits for the host mid-way.  A hint that turns
-# out too small only costs a redo of the binning stage inside the library.
+# hint -- a decaying maximum of recent num_rendered for the same (device, W, H) and point
+# count, plus a margin -- so the forward never waits for the host mid-way.  A hint that
+# turns out too small only costs a redo of the binning stage inside the library
+# (forward_rebuilds() counts them).  One entry per (device, W, H): a new point count (after
+# densification) replaces the old entry instead of piling up next to it.
 # GSR_SYNC_FORWARD=1 restores the reference's synchronising forward.
 _capacity: dict = {}
 _CAP_MARGIN = 1.05
-_CAP_DECAY = 0.98
+_CAP_DECAY = 0.9
 _INT_MAX = 2**31 - 1
 
 
-def _capacity_hint(key) -> int:
+def _capacity_hint(key, P: int) -> int:
     if os.environ.get("GSR_SYNC_FORWARD", "0") == "1":
         return 0
-    last = _capacity.get(key, 0)
+    p, last = _capacity.get(key, (P, 0))
+    if p != P:
+        return 0
     return min(_INT_MAX, int(last * _CAP_MARGIN) + 1024) if last > 0 else 0
 
 
-def _note_rendered(key, nr: int) -> None:
-    _capacity[key] = max(int(nr), int(_capacity.get(key, 0) * _CAP_DECAY))
+def _note_rendered(key, P: int, nr: int) -> None:
+    p, last = _capacity.get(key, (P, 0))
+    _capacity[key] = (P, max(int(nr), int(last * _CAP_DECAY)) if p == P else int(nr))
+
+
+def forward_rebuilds() -> int:
+    """Forwards (process-wide) whose capacity hint was too small, so the binning stage was redone."""
+    return int(_lib.load().gsr_forward_rebuilds())
 
 
 # GSR_POISON=1 (the GPU test suite sets it): every scratch buffer the library requests is
@@ -85,6 +95,17 @@ class _Inputs:
         if t is None or t.numel() == 0:
             return None
         return self.req(t, name, align16)
+
+    def radii(self, t: torch.Tensor) -> int:
+        """Device pointer of the int32 radii, kept alive (a contiguous copy if needed) for the call."""
+        _require_device(t, "radii")
+        if t.dtype != torch.int32:
+            raise RuntimeError(f"radii: expected an int32 tensor, got {t.dtype}")
+        if t.device != self.device:
+            raise RuntimeError(f"radii: tensor on {t.device}, expected {self.device}")
+        t = t.contiguous()
+        self.keep.append(t)
+        return t.data_ptr()
 
     def req(self, t: torch.Tensor, name: str, align16: bool = False, small: bool = False) -> int:
         if small and t.device.type != "cuda":
@@ -171,7 +192,7 @@ def rasterize_gaussians(*args) -> Tuple[int, torch.Tensor, torch.Tensor, torch.T
     rg, rb, ri = _Resizer(geom), _Resizer(binning), _Resizer(img)
     nr = ctypes.c_int(0)
     cap = ctypes.c_int(0)
-    key = (device.index, P, W, H)
+    key = (device.index, W, H)
     common_head = (rg.cb, None, rb.cb, None, ri.cb, None, P, int(degree), M,
                    ins.req(background, "bg", small=True), W, H, ins.req(means3D, "means3D"))
     sh_args = ((ins.req(dc, "dc"), ins.opt(sh, "sh", align16=True)) if split else (ins.opt(sh, "sh", align16=True),))
@@ -183,13 +204,14 @@ def rasterize_gaussians(*args) -> Tuple[int, torch.Tensor, torch.Tensor, torch.T
                 (campos.to(device) if campos is not None else None), "campos"),
         float(tan_fovx), float(tan_fovy), int(bool(prefiltered)), out_color.data_ptr(), out_invdepth.data_ptr(),
         int(bool(antialiasing)), radii.data_ptr(), int(bool(debug)), _stream_handle(device), ctypes.byref(nr),
-        _capacity_hint(key), ctypes.byref(cap))
+        _capacity_hint(key, P), ctypes.byref(cap))
     fn = lib.gsr_rasterize_forward_dc if split else lib.gsr_rasterize_forward_ex
     with torch.cuda.device(device):
         rc = fn(*common_head, *sh_args, *common_tail)
     _lib.check(rc, "rasterize_gaussians")
-    _note_rendered(key, nr.value)
-    binning._gsr_capacity = int(cap.value)  # the layout the backward must use (kept across save_for_backward)
+    _note_rendered(key, P, nr.value)
+    # The binning buffer's layout (its capacity) is recovered by the backward from the buffer's
+    # size (include/gsr.h gsr_rasterize_backward_ex), so nothing rides on the tensor object.
     return int(nr.value), out_color, radii, geom, binning, img, out_invdepth
 
 
@@ -271,7 +293,7 @@ def rasterize_gaussians_backward(*args, out=None):
            ins.req(viewmatrix, "viewmatrix", small=True), ins.req(projmatrix, "projmatrix", small=True),
            ins.opt(campos if campos is not None and campos.device.type == "cuda" else
                    (campos.to(device) if campos is not None else None), "campos"),
-           float(tan_fovx), float(tan_fovy), radii.contiguous().data_ptr(), geomBuffer.data_ptr(),
+           float(tan_fovx), float(tan_fovy), ins.radii(radii), geomBuffer.data_ptr(),
            binningBuffer.data_ptr() if binningBuffer.numel() else None, imageBuffer.data_ptr(),
            ins.req(dL_dout_color, "dL_dout_color"),
            ins.req(dL_dout_invdepth, "dL_dout_invdepth") if has_inv else None,
@@ -280,12 +302,38 @@ def rasterize_gaussians_backward(*args, out=None):
     sh_grads = ((dL_ddc.data_ptr(), dL_dsh.data_ptr() if M > 0 else None) if split else
                 (dL_dsh.data_ptr() if M > 0 else None,))
     tail = (dL_dscales.data_ptr(), dL_drotations.data_ptr(), int(bool(antialiasing)), int(bool(debug)), rs.cb, None,
-            _stream_handle(device), int(getattr(binningBuffer, "_gsr_capacity", 0)), int(binningBuffer.numel()))
+            _stream_handle(device), 0, int(binningBuffer.numel()))
     fn = lib.gsr_rasterize_backward_dc if split else lib.gsr_rasterize_backward_ex
     with torch.cuda.device(device):
         rc = fn(*head, *sh_args, *mid, *sh_grads, *tail)
     _lib.check(rc, "rasterize_gaussians_backward")
     return result
+
+
+def debug_forward_state(fwd, P: int) -> dict:
+    """The forward's private tile lists and per-pixel state (include/gsr.h gsr_debug_forward_state),
+    for parity tests: ``ranges`` [tiles, 2], ``point_list`` [R] (Gaussian indices, tile-major, each
+    tile in (depth, index) order), ``n_contrib`` [H, W], ``final_T`` [H, W]; int64 / float32 CPU
+    tensors.  ``fwd`` is the tuple ``rasterize_gaussians`` returned."""
+    num_rendered, color, _radii, geom, binning, img, _inv = fwd
+    H, W = int(color.size(1)), int(color.size(2))
+    device = color.device
+    tiles = ((W + 15) // 16) * ((H + 15) // 16)
+    i32 = dict(dtype=torch.int32, device=device)
+    ranges = torch.zeros((tiles, 2), **i32)
+    plist = torch.zeros((max(int(num_rendered), 1),), **i32)
+    n_contrib = torch.zeros((H, W), **i32)
+    final_T = torch.zeros((H, W), dtype=torch.float32, device=device)
+    lib = _lib.load()
+    with torch.cuda.device(device):
+        rc = lib.gsr_debug_forward_state(int(P), W, H, int(num_rendered), 0, int(binning.numel()), geom.data_ptr(),
+                                         binning.data_ptr() if binning.numel() else None, img.data_ptr(),
+                                         ranges.data_ptr(), plist.data_ptr(), n_contrib.data_ptr(),
+                                         final_T.data_ptr(), _stream_handle(device))
+    _lib.check(rc, "debug_forward_state")
+    u = lambda t: t.cpu().numpy().view("uint32").astype("int64")  # noqa: E731
+    return {"ranges": torch.from_numpy(u(ranges)), "point_list": torch.from_numpy(u(plist)[:int(num_rendered)] >> 4),
+            "n_contrib": torch.from_numpy(u(n_contrib)), "final_T": final_T.cpu()}
 
 
 def view_block_floats(P: int) -> int:
@@ -337,12 +385,12 @@ def rasterize_gaussians_backward_screen(*args, view_block: torch.Tensor) -> None
             ins.req(scales, "scales"), float(scale_modifier), ins.req(rotations, "rotations", align16=True),
             ins.req(viewmatrix, "viewmatrix", small=True), ins.req(projmatrix, "projmatrix", small=True),
             ins.req(campos if campos.device.type == "cuda" else campos.to(device), "campos"),
-            float(tan_fovx), float(tan_fovy), radii.contiguous().data_ptr(), geomBuffer.data_ptr(),
+            float(tan_fovx), float(tan_fovy), ins.radii(radii), geomBuffer.data_ptr(),
             binningBuffer.data_ptr() if binningBuffer.numel() else None, imageBuffer.data_ptr(),
             ins.req(dL_dout_color, "dL_dout_color"),
             ins.req(dL_dout_invdepth, "dL_dout_invdepth") if has_inv else None,
             int(bool(antialiasing)), int(bool(debug)), rs.cb, None, _stream_handle(device),
-            int(getattr(binningBuffer, "_gsr_capacity", 0)), int(binningBuffer.numel()), view_block.data_ptr())
+            0, int(binningBuffer.numel()), view_block.data_ptr())
     _lib.check(rc, "rasterize_gaussians_backward_screen")
 
 

@@ -74,6 +74,8 @@ SIGNATURES = {
                                            ctypes.c_size_t, _vp]),
     "gsr_gauss_backward_views": (_i, [_i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _f, _i, _vp, ctypes.c_longlong, _vp,
                                       _vp, _vp, _vp, _vp, _vp, _vp]),
+    "gsr_debug_forward_state": (_i, [_i, _i, _i, _i, _i, ctypes.c_size_t, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "gsr_forward_rebuilds": (ctypes.c_longlong, []),
     "gsr_last_error": (ctypes.c_char_p, []),
     "gsr_version": (ctypes.c_char_p, []),
     "gsr_profile_enable": (_i, [_i]),

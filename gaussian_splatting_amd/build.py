@@ -37,7 +37,12 @@ def _newest_input_mtime() -> float:
 # Per-file flags.  The SLP vectorizer packs adjacent fp32 ops into v_pk_*_f32 plus
 # v_mov shuffles; on gfx950 packed fp32 is not faster than two plain ops
 # (MI355X_MICROARCH.md, "price of one filler"), so the VALU-bound kernels opt out.
-FILE_FLAGS = {"render.hip": ["-fno-slp-vectorize"], "preprocess.hip": ["-fno-slp-vectorize"]}
+# preprocess.hip is compiled without FMA contraction: every integer it derives from floats
+# (radius, getRect's tile rectangle, tiles_touched, hence num_rendered and the tile lists) then
+# comes from the same individually rounded operations as the reference's and the oracle's
+# (oracle/Makefile builds with -ffp-contract=off), so those integers are identical, not close.
+FILE_FLAGS = {"render.hip": ["-fno-slp-vectorize"],
+              "preprocess.hip": ["-fno-slp-vectorize", "-ffp-contract=off"]}
 
 
 def _compile(src: str, objdir: str = OBJ, extra=()) -> str:

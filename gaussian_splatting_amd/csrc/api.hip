@@ -11,6 +11,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <atomic>
 #include <mutex>
 #include <vector>
 
@@ -183,6 +184,47 @@ gsr::BinningState carve_binning(char* base, size_t C, size_t* total) {
     return b;
 }
 
+// Binning capacities of the _ex / _dc forwards are multiples of kCapQuantum.  Over those the
+// buffer size is strictly increasing (the keys alone grow by 8 * kCapQuantum bytes a step) and
+// every sub-array's length depends on C / kCkStride at most, so the size of the binning buffer
+// identifies its layout: the backward recovers the capacity from the tensor's byte count, which
+// survives any transport of the saved tensor (saved-tensor hooks, save_on_cpu, clone).
+constexpr size_t kCapQuantum = 256;
+static_assert(kCapQuantum % gsr::kCkStride == 0, "capacity quantum is a whole number of checkpoint strides");
+
+size_t quantize_capacity(size_t c) { return (c + kCapQuantum - 1) / kCapQuantum * kCapQuantum; }
+
+size_t binning_bytes_for(size_t C) {
+    size_t b = 0;
+    carve_binning(nullptr, C, &b);
+    return b;
+}
+
+// Capacity the binning buffer of a forward was laid out for: the explicit value if given,
+// else the multiple of kCapQuantum whose layout has exactly `bytes` bytes, else R (the exact
+// layout of gsr_rasterize_forward).  Returns false if `bytes` matches no layout holding R.
+bool resolve_capacity(int R, int capacity, size_t bytes, size_t* C) {
+    if (capacity > 0) {
+        *C = (size_t)capacity;
+        return bytes == 0 || binning_bytes_for(*C) == bytes;
+    }
+    if (bytes == 0) {
+        *C = (size_t)R;
+        return true;
+    }
+    size_t lo = quantize_capacity((size_t)R) / kCapQuantum, hi = bytes / (8 * kCapQuantum) + 1;
+    while (lo < hi) {  // first k in [lo, hi] with bytes_for(k * quantum) >= bytes
+        const size_t mid = lo + (hi - lo) / 2;
+        if (binning_bytes_for(mid * kCapQuantum) < bytes) lo = mid + 1; else hi = mid;
+    }
+    if (binning_bytes_for(lo * kCapQuantum) == bytes) {
+        *C = lo * kCapQuantum;
+        return true;
+    }
+    *C = (size_t)R;
+    return binning_bytes_for((size_t)R) == bytes;
+}
+
 // Backward scratch: per-tile limit keys, R per-instance records, P per-Gaussian sums.
 void carve_recs(char* base, size_t R, size_t P, gsr::GradRecs* recs, gsr::GradRecs* sums, size_t* total) {
     using namespace gsr;
@@ -261,6 +303,9 @@ int total_readback(TotalReadback** out) {
     return GSR_OK;
 }
 
+// Forwards whose capacity hint was too small (the binning stage was redone), for gsr_forward_rebuilds().
+std::atomic<long long> g_rebuilds{0};
+
 void* call_alloc(gsr_alloc_fn fn, void* ctx, size_t bytes) {
     if (!fn) return nullptr;
     return fn(ctx, bytes ? bytes : 1);
@@ -272,7 +317,9 @@ extern "C" {
 
 const char* gsr_last_error(void) { return g_err; }
 
-const char* gsr_version(void) { return "gsr 0.1.0 gfx950"; }
+const char* gsr_version(void) { return "gsr 0.2.0 gfx950"; }
+
+long long gsr_forward_rebuilds(void) { return g_rebuilds.load(std::memory_order_relaxed); }
 
 int gsr_fused_ssim_forward(int B, int CH, int H, int W, float C1, float C2, const float* img1, const float* img2,
                            float* ssim_map, float* dm_dmu1, float* dm_dsigma1_sq, float* dm_dsigma12, void* stream) {
@@ -566,10 +613,16 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
                  const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix, const float* cam_pos,
                  float tan_fovx, float tan_fovy, int prefiltered, float* out_color, float* out_invdepth,
                  int antialiasing, int* radii, int debug, void* stream_, int* num_rendered, int capacity_hint,
-                 int* binning_capacity) {
+                 int* binning_capacity, bool quantized = true) {
     using namespace gsr;
     g_err[0] = 0;
     hipStream_t stream = (hipStream_t)stream_;
+    // _ex / _dc forwards lay the binning buffer out for a multiple of kCapQuantum (the backward
+    // recovers it from the buffer's size); gsr_rasterize_forward keeps the exact C = R layout
+    const auto capacity_for = [quantized](size_t c) {
+        const size_t q = quantize_capacity(c);
+        return quantized && q <= (size_t)INT_MAX ? q : c;
+    };
     if (num_rendered) *num_rendered = 0;
     if (binning_capacity) *binning_capacity = 0;
     if (P < 0 || width <= 0 || height <= 0)
@@ -710,15 +763,16 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
     if (int rc = queue_total()) return rc;
     if (capacity_hint <= 0) {
         if (int rc = wait_total(&total)) return rc;
-        C = (size_t)total;
+        C = capacity_for((size_t)total);
         if (int rc = bin_and_render(C)) return rc;
     } else {
         // everything is queued before the host waits, and it waits for the counts only
-        C = (size_t)capacity_hint;
+        C = capacity_for((size_t)capacity_hint);
         if (int rc = bin_and_render(C)) return rc;
         if (int rc = wait_total(&total)) return rc;
         if (total > C) {  // the hint was too small: recount (resets the cursors) and rebuild exactly
-            C = (size_t)total;
+            g_rebuilds.fetch_add(1, std::memory_order_relaxed);
+            C = capacity_for((size_t)total);
             HIP_TRY(launch_bin_count(P, geom, gx, gy, img.ranges, C, nullptr, stream), "bin_count");
             if (int rc = bin_and_render(C)) return rc;
         }
@@ -740,7 +794,7 @@ int gsr_rasterize_forward(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn 
     return forward_impl(geom_alloc, geom_ctx, binning_alloc, binning_ctx, image_alloc, image_ctx, P, D, M, background,
                         width, height, means3D, nullptr, shs, colors_precomp, opacities, scales, scale_modifier, rotations,
                         cov3D_precomp, viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, prefiltered, out_color,
-                        out_invdepth, antialiasing, radii, debug, stream, num_rendered, 0, nullptr);
+                        out_invdepth, antialiasing, radii, debug, stream, num_rendered, 0, nullptr, false);
 }
 
 int gsr_rasterize_forward_ex(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_alloc, void* binning_ctx,
@@ -797,21 +851,23 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
     }
     if (dc && M > 0 && !shs) return fail(GSR_ERR_ARGUMENT, "rasterize_backward: %d rest SH coefficients but no shs", M);
     if (dc) M += 1;  // as in the forward
+    if (!colors_precomp && (shs || dc) && (D < 0 || D > 3 || (D + 1) * (D + 1) > M))
+        return fail(GSR_ERR_ARGUMENT, "rasterize_backward: SH degree %d needs %d coefficients, got %d", D,
+                    (D + 1) * (D + 1), M);
 
     const float focal_y = height / (2.0f * tan_fovy);
     const float focal_x = width / (2.0f * tan_fovx);
     const uint32_t gx = (width + kTile - 1) / kTile, gy = (height + kTile - 1) / kTile;
     const uint32_t tiles = gx * gy;
-    // the binning buffer is laid out for the capacity the forward used (>= R)
-    const size_t C = binning_capacity > 0 ? (size_t)binning_capacity : (size_t)R;
+    // the binning buffer is laid out for the capacity the forward used (>= R): given, or
+    // recovered from the buffer's size (resolve_capacity)
+    size_t C = 0;
+    if (!resolve_capacity(R, binning_capacity, binning_bytes, &C))
+        return fail(GSR_ERR_ARGUMENT,
+                    "rasterize_backward: a binning buffer of %zu bytes matches no layout for R=%d (capacity %d)",
+                    binning_bytes, R, binning_capacity);
     if (C < (size_t)R) return fail(GSR_ERR_ARGUMENT, "rasterize_backward: binning capacity %zu < R=%d", C, R);
     size_t tmp = 0;
-    if (binning_bytes && C > 0) {  // (an empty forward still got a 1-byte buffer)
-        carve_binning(nullptr, C, &tmp);
-        if (tmp != binning_bytes)
-            return fail(GSR_ERR_ARGUMENT, "rasterize_backward: binning buffer of %zu bytes does not match capacity %zu",
-                        binning_bytes, C);
-    }
     GeomState geom = carve_geom((char*)geom_buffer, P, gx, gy, &tmp);
     ImageState img = carve_image((char*)image_buffer, width, height, tiles, &tmp);
     BinningState bin = carve_binning((char*)binning_buffer, C, &tmp);
@@ -975,6 +1031,42 @@ int gsr_rasterize_backward_screen(int P, int D, int M, int R, const float* backg
                          scratch_alloc, scratch_ctx, stream, binning_capacity, binning_bytes, view_block);
 }
 
+int gsr_debug_forward_state(int P, int width, int height, int R, int binning_capacity, size_t binning_bytes,
+                            const void* geom_buffer, const void* binning_buffer, const void* image_buffer,
+                            unsigned int* ranges, unsigned int* point_list, unsigned int* n_contrib, float* final_T,
+                            void* stream_) {
+    using namespace gsr;
+    g_err[0] = 0;
+    hipStream_t stream = (hipStream_t)stream_;
+    (void)geom_buffer;
+    if (P <= 0 || R < 0 || width <= 0 || height <= 0)
+        return fail(GSR_ERR_ARGUMENT, "debug_forward_state: invalid sizes P=%d R=%d W=%d H=%d", P, R, width, height);
+    if (!image_buffer || (R > 0 && !binning_buffer))
+        return fail(GSR_ERR_ARGUMENT, "debug_forward_state: missing forward buffers");
+    size_t C = 0, tmp = 0;
+    if (!resolve_capacity(R, binning_capacity, binning_bytes, &C) || C < (size_t)R)
+        return fail(GSR_ERR_ARGUMENT, "debug_forward_state: binning buffer of %zu bytes matches no layout for R=%d",
+                    binning_bytes, R);
+    const uint32_t gx = (width + kTile - 1) / kTile, gy = (height + kTile - 1) / kTile;
+    ImageState img = carve_image((char*)image_buffer, width, height, gx * gy, &tmp);
+    const size_t N = (size_t)width * height;
+    if (ranges) HIP_TRY(hipMemcpyAsync(ranges, img.ranges, sizeof(uint2) * gx * gy, hipMemcpyDeviceToDevice, stream),
+                        "debug_forward_state ranges");
+    if (n_contrib)
+        HIP_TRY(hipMemcpyAsync(n_contrib, img.n_contrib, sizeof(uint32_t) * N, hipMemcpyDeviceToDevice, stream),
+                "debug_forward_state n_contrib");
+    if (final_T)
+        HIP_TRY(hipMemcpyAsync(final_T, img.final_T, sizeof(float) * N, hipMemcpyDeviceToDevice, stream),
+                "debug_forward_state final_T");
+    if (point_list && R > 0) {
+        BinningState bin = carve_binning((char*)binning_buffer, C, &tmp);
+        HIP_TRY(hipMemcpyAsync(point_list, bin.gid_sorted, sizeof(uint32_t) * (size_t)R, hipMemcpyDeviceToDevice,
+                               stream),
+                "debug_forward_state point_list");
+    }
+    return GSR_OK;
+}
+
 int gsr_gauss_backward_views(int P, int D, int M, const float* means3D, const float* dc, const float* shs,
                              const float* opacities, const float* scales, const float* rotations, float scale_modifier,
                              int n_views, const float* blocks, long long block_floats, float* dL_dmean3D,
@@ -994,6 +1086,9 @@ int gsr_gauss_backward_views(int P, int D, int M, const float* means3D, const fl
     if (dc && M > 0 && !shs) return fail(GSR_ERR_ARGUMENT, "gauss_backward_views: rest SH without shs");
     if ((shs && !dL_dsh) || (dc && !dL_ddc)) return fail(GSR_ERR_ARGUMENT, "gauss_backward_views: missing SH outputs");
     if (!dc && !shs) return fail(GSR_ERR_ARGUMENT, "gauss_backward_views: needs SH (precomputed colours are per view)");
+    if ((D + 1) * (D + 1) > (dc ? M + 1 : M))  // as the forward (forward_impl): never read past a row
+        return fail(GSR_ERR_ARGUMENT, "gauss_backward_views: SH degree %d needs %d coefficients, got %d", D,
+                    (D + 1) * (D + 1), dc ? M + 1 : M);
     ViewsBwdArgs a{};
     a.P = P; a.D = D; a.M = dc ? M + 1 : M;
     a.means3D = means3D; a.shs = (dc && M == 0) ? nullptr : shs; a.dc = dc; a.opacities = opacities; a.scales = scales;

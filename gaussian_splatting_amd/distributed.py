@@ -82,7 +82,14 @@ class GradArena:
 def reduce_densification_stats(grad_norm_sum: torch.Tensor, denom: torch.Tensor, max_radii2D: torch.Tensor,
                                group: Optional[dist.ProcessGroup] = None) -> None:
     """Make densification statistics global (train.py:212-215, gaussian_model.py:643-654):
-    SUM of the screen-space gradient norms and their counts, MAX of the 2-D radii."""
+    SUM of the screen-space gradient norms and their counts, MAX of the 2-D radii.
+
+    Call it EXACTLY ONCE per densification interval, on the running accumulators
+    (``xyz_gradient_accum``, ``denom``, ``max_radii2D``), right before ``densify_and_prune``:
+    each rank accumulates its own views' statistics locally every iteration (the reference's
+    ``add_densification_stats``), and this one reduction makes every rank's accumulators the sum
+    over all ranks' views.  The SUM is in place, so a second call on the same accumulators would
+    add the other ranks' totals again (N-fold growth per call)."""
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
         return
     stats = torch.cat([grad_norm_sum.reshape(-1), denom.reshape(-1)])

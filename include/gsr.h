@@ -107,8 +107,12 @@ int gsr_rasterize_backward(int P, int D, int M, int R, const float* background, 
                            void* scratch_ctx, void* stream);
 
 /* Backward for a forward made by gsr_rasterize_forward_ex: binning_capacity is the
- * value it returned (0 = R); binning_bytes, if nonzero, is the binning buffer's size
- * and is checked against the layout (a mismatch is GSR_ERR_ARGUMENT). */
+ * value it returned, or 0.  With 0 and a nonzero binning_bytes (the binning buffer's
+ * size) the capacity is recovered from the size: gsr_rasterize_forward_ex lays the
+ * buffer out for a multiple of 256 instances, over which the size determines the layout
+ * (so the buffer can travel through any tensor copy, e.g. saved-tensor hooks).  With 0
+ * and 0 it is R (gsr_rasterize_forward's exact layout).  A size that matches no layout,
+ * or a given capacity whose layout has another size, is GSR_ERR_ARGUMENT. */
 int gsr_rasterize_backward_ex(int P, int D, int M, int R, const float* background, int width, int height,
                               const float* means3D, const float* shs, const float* colors_precomp,
                               const float* opacities, const float* scales, float scale_modifier,
@@ -195,6 +199,25 @@ int gsr_gauss_backward_views(int P, int D, int M, const float* means3D, const fl
  * `present` is P bytes (bool). */
 int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
                      unsigned char* present, void* stream);
+
+/* Inspection of a forward's private state, for parity tests (the reference keeps the same
+ * state in its binning / image buffers: BinningState::point_list and ImageState::ranges /
+ * n_contrib / accum_alpha, cuda_rasterizer/rasterizer_impl.h:39-72).  Copies, on `stream`,
+ * device to device, into caller-provided device arrays (any may be NULL to skip it):
+ *   ranges     [tiles][2]  each tile's [start, end) in point_list (identifyTileRanges);
+ *   point_list [R]         the tile lists, tile-major, each tile in (depth, index) order;
+ *                          entry = Gaussian index << 4 | the forward's 4-bit quadrant mask;
+ *   n_contrib  [H*W]       last contributor (1-based list position) per pixel;
+ *   final_T    [H*W]       transmittance after the last contributor.
+ * binning_capacity / binning_bytes as for gsr_rasterize_backward_ex. */
+int gsr_debug_forward_state(int P, int width, int height, int R, int binning_capacity, size_t binning_bytes,
+                            const void* geom_buffer, const void* binning_buffer, const void* image_buffer,
+                            unsigned int* ranges, unsigned int* point_list, unsigned int* n_contrib, float* final_T,
+                            void* stream);
+
+/* Number of forwards (process-wide) whose capacity hint was too small, so the binning stage
+ * was redone with the exact count (gsr_rasterize_forward_ex). */
+long long gsr_forward_rebuilds(void);
 
 /* Message of the last error on this thread ("" if none). */
 const char* gsr_last_error(void);

@@ -496,6 +496,115 @@ void SYM(get_image)(void* h, real* final_T, uint32_t* n_contrib) {
     if (n_contrib) memcpy(n_contrib, s->n_contrib, N * sizeof(uint32_t));
 }
 
+/* computeCov3D (CR/forward.cu:149-190) over P Gaussians, for pinning against the reference's
+ * Python covariance (scene/gaussian_model.py:32-42 via utils/general_utils.py:78-110). */
+void SYM(cov3d)(int P, const real* scales, real mod, const real* rotations, real* cov3D) {
+    for (int i = 0; i < P; i++) cov3d_fwd(scales + 3 * i, mod, rotations + 4 * i, cov3D + 6 * i);
+}
+
+/* Distance of every pixel's blend (CR/forward.cu:455-500, walked exactly as the forward above)
+ * to the reference's discrete thresholds, for explaining fp32 disagreements between two
+ * implementations: per pixel, over the entries the loop visits up to and including its
+ * termination, the minimum of |power| (the power > 0 skip), |alpha * 255 - 1| (the alpha < 1/255
+ * skip; alpha before that test) and |test_T * 1e4 - 1| (the T < 1e-4 termination). */
+void SYM(pixel_margins)(void* h, real* m_power, real* m_alpha, real* m_T, int nthreads) {
+    OracleState* s = (OracleState*)h;
+    set_threads(nthreads);
+    const int W = s->W, H = s->H;
+    const size_t tiles = (size_t)s->gx * s->gy;
+#pragma omp parallel for schedule(dynamic, 4)
+    for (long tile = 0; tile < (long)tiles; tile++) {
+        const unsigned tx = (unsigned)(tile % s->gx), ty = (unsigned)(tile / s->gx);
+        const uint32_t r0 = s->ranges[2 * tile], r1 = s->ranges[2 * tile + 1];
+        for (int ly = 0; ly < BLOCK_Y; ly++)
+            for (int lx = 0; lx < BLOCK_X; lx++) {
+                unsigned pxi = tx * BLOCK_X + lx, pyi = ty * BLOCK_Y + ly;
+                if (pxi >= (unsigned)W || pyi >= (unsigned)H) continue;
+                const size_t pix_id = (size_t)W * pyi + pxi;
+                const real pfx = (real)pxi, pfy = (real)pyi;
+                real T = R(1), mp = R(1e30), ma = R(1e30), mt = R(1e30);
+                for (uint32_t k = r0; k < r1; k++) {
+                    const uint32_t g = s->point_list[k];
+                    const real* xy = s->means2D + 2 * g;
+                    const real* co = s->conic_opacity + 4 * g;
+                    real dx = xy[0] - pfx, dy = xy[1] - pfy;
+                    real power = R(-0.5) * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+                    real ap = power < 0 ? -power : power;
+                    if (ap < mp) mp = ap;
+                    if (power > R(0)) continue;
+                    real alpha = FMINR(R(0.99), co[3] * EXP(power));
+                    real da = alpha * R(255) - R(1);
+                    da = da < 0 ? -da : da;
+                    if (da < ma) ma = da;
+                    if (alpha < R(1) / R(255)) continue;
+                    real test_T = T * (R(1) - alpha);
+                    real dt = test_T * R(10000) - R(1);
+                    dt = dt < 0 ? -dt : dt;
+                    if (dt < mt) mt = dt;
+                    if (test_T < R(0.0001)) break;
+                    T = test_T;
+                }
+                m_power[pix_id] = mp;
+                m_alpha[pix_id] = ma;
+                m_T[pix_id] = mt;
+            }
+    }
+}
+
+/* The Gaussians whose own blend, at some pixel, comes within the given margins of one of the
+ * reference's discrete thresholds (same walk and measures as pixel_margins): the power > 0 or
+ * alpha < 1/255 skip of that Gaussian at that pixel, or the pixel terminating at it (T < 1e-4).
+ * A different fp32 evaluation order may decide such an event the other way, which moves that
+ * pixel's whole term in or out of the Gaussian's gradient.  flags[g] = 1 for those. */
+void SYM(threshold_gaussians)(void* h, real mp, real ma, real mt, unsigned char* flags, int nthreads) {
+    OracleState* s = (OracleState*)h;
+    set_threads(nthreads);
+    const int W = s->W, H = s->H;
+    const size_t tiles = (size_t)s->gx * s->gy;
+    memset(flags, 0, (size_t)s->P);
+#pragma omp parallel for schedule(dynamic, 4)
+    for (long tile = 0; tile < (long)tiles; tile++) {
+        const unsigned tx = (unsigned)(tile % s->gx), ty = (unsigned)(tile / s->gx);
+        const uint32_t r0 = s->ranges[2 * tile], r1 = s->ranges[2 * tile + 1];
+        for (int ly = 0; ly < BLOCK_Y; ly++)
+            for (int lx = 0; lx < BLOCK_X; lx++) {
+                unsigned pxi = tx * BLOCK_X + lx, pyi = ty * BLOCK_Y + ly;
+                if (pxi >= (unsigned)W || pyi >= (unsigned)H) continue;
+                const real pfx = (real)pxi, pfy = (real)pyi;
+                real T = R(1);
+                for (uint32_t k = r0; k < r1; k++) {
+                    const uint32_t g = s->point_list[k];
+                    const real* xy = s->means2D + 2 * g;
+                    const real* co = s->conic_opacity + 4 * g;
+                    real dx = xy[0] - pfx, dy = xy[1] - pfy;
+                    real power = R(-0.5) * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+                    int near = (power < 0 ? -power : power) < mp;
+                    if (power <= R(0)) {
+                        real alpha = FMINR(R(0.99), co[3] * EXP(power));
+                        real da = alpha * R(255) - R(1);
+                        near |= (da < 0 ? -da : da) < ma;
+                        if (alpha >= R(1) / R(255)) {
+                            real test_T = T * (R(1) - alpha);
+                            real dt = test_T * R(10000) - R(1);
+                            near |= (dt < 0 ? -dt : dt) < mt;
+                            if (near) {
+#pragma omp atomic write
+                                flags[g] = 1;
+                            }
+                            if (test_T < R(0.0001)) break;
+                            T = test_T;
+                            continue;
+                        }
+                    }
+                    if (near) {
+#pragma omp atomic write
+                        flags[g] = 1;
+                    }
+                }
+            }
+    }
+}
+
 #if defined(_OPENMP)
 #define ATOMIC_ADD(p, v) _Pragma("omp atomic") (p) += (v)
 #else

@@ -55,6 +55,15 @@ def _lib(precision: str):
         f = getattr(lib, pre + name)
         f.restype = i
         f.argtypes = [vp]
+    pm = getattr(lib, pre + "pixel_margins")
+    pm.restype = None
+    pm.argtypes = [vp, vp, vp, vp, i]
+    tg = getattr(lib, pre + "threshold_gaussians")
+    tg.restype = None
+    tg.argtypes = [vp, r, r, r, vp, i]
+    c3 = getattr(lib, pre + "cov3d")
+    c3.restype = None
+    c3.argtypes = [i, vp, r, vp, vp]
     mv = getattr(lib, pre + "mark_visible")
     mv.restype = None
     mv.argtypes = [i, vp, vp, vp]
@@ -135,6 +144,24 @@ class OracleHandle:
         getattr(self._lib, self._pre + "get_image")(self.h, _ptr(fT), _ptr(nc))
         return dict(final_T=fT.reshape(self.H, self.W), n_contrib=nc.reshape(self.H, self.W))
 
+    def pixel_margins(self, nthreads: int = 1):
+        """Per pixel [H, W]: the blend's smallest distances to the reference's discrete thresholds
+        (|power| vs the power > 0 skip, |255 alpha - 1| vs the alpha skip, |1e4 test_T - 1| vs the
+        termination), over the entries the reference's loop visits (gsr_oracle.c pixel_margins)."""
+        N = self.W * self.H
+        out = [np.zeros(N, self.dtype) for _ in range(3)]
+        getattr(self._lib, self._pre + "pixel_margins")(self.h, *[_ptr(o) for o in out], int(nthreads))
+        return {k: o.reshape(self.H, self.W) for k, o in zip(("power", "alpha", "T"), out)}
+
+    def threshold_gaussians(self, m_power: float, m_alpha: float, m_T: float, nthreads: int = 1) -> np.ndarray:
+        """bool [P]: Gaussians whose own blend at some pixel lies within the margins of a discrete
+        threshold of the reference (power > 0 / alpha < 1/255 skips, T < 1e-4 termination at it)."""
+        _, _, rtype = _lib(self.precision)
+        flags = np.zeros(max(self.P, 1), np.uint8)
+        getattr(self._lib, self._pre + "threshold_gaussians")(self.h, rtype(m_power), rtype(m_alpha), rtype(m_T),
+                                                              _ptr(flags), int(nthreads))
+        return flags[:self.P].astype(bool)
+
     def prefilter_violation(self) -> bool:
         return bool(getattr(self._lib, self._pre + "prefilter_violation")(self.h))
 
@@ -206,6 +233,19 @@ def forward(
     )
     handle = OracleHandle(precision, h, P, M, W, H)
     return ForwardResult(color, invd, radii[:P], int(nr.value), handle)
+
+
+def cov3d(scales, rotations, scale_modifier: float = 1.0, precision: str = "f32") -> np.ndarray:
+    """computeCov3D (CR/forward.cu:149-190): upper triangle [P, 6] of (S R)^T (S R); rotations are used
+    as given (the reference's kernel does not normalise them)."""
+    lib, pre, rtype = _lib(precision)
+    dt = np.float32 if precision == "f32" else np.float64
+    s = _arr(scales, dt)
+    q = _arr(rotations, dt)
+    P = 0 if s is None else s.reshape(-1, 3).shape[0]
+    out = np.zeros((max(P, 1), 6), dt)
+    getattr(lib, pre + "cov3d")(P, _ptr(s), rtype(scale_modifier), _ptr(q), _ptr(out))
+    return out[:P]
 
 
 def mark_visible(means3D, viewmatrix, precision: str = "f32") -> np.ndarray:

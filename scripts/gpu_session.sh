@@ -14,13 +14,13 @@ ok() { local rc=$1; [ "$rc" -eq 0 ] || [ "$rc" -eq 1 ]; }
 for stage in "$@"; do
   case $stage in
     tests)
-      timeout -k 10 900 python -m pytest tests -m gpu -q -x -k "not fullsize" > "$OUT/pytest.log" 2>&1; rc=$?
+      timeout -k 10 900 python -u -m pytest tests -m gpu -v -x --timeout 300 --timeout-method thread -k "not fullsize" > "$OUT/pytest.log" 2>&1; rc=$?
       echo "tests rc=$rc"; tail -5 "$OUT/pytest.log"; ok $rc || exit $rc ;;
     smoke)
       timeout -k 10 600 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1; rc=$?
       echo "smoke rc=$rc"; tail -2 "$OUT/smoke.log"; [ $rc -eq 0 ] || exit $rc ;;
     full)
-      timeout -k 10 900 python -m pytest tests -m gpu -q -k "fullsize" > "$OUT/pytest_full.log" 2>&1; rc=$?
+      timeout -k 10 1000 python -u -m pytest tests -m gpu -v -s --timeout 600 --timeout-method thread -k "fullsize" > "$OUT/pytest_full.log" 2>&1; rc=$?
       echo "full rc=$rc"; tail -5 "$OUT/pytest_full.log"; ok $rc || exit $rc ;;
     bench)
       timeout -k 10 600 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"; rc=$?

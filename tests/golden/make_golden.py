@@ -14,6 +14,12 @@ Two kinds of vectors, both small .npz files of inputs and expected outputs:
                   convention of train.py:155)
      ssim.npz     utils/loss_utils.py ssim/_ssim (conv2d SSIM), mean and autograd gradient: pins
                   oracle/ssim.py, the oracle of the fused-SSIM kernels
+     cov3d.npz    scene/gaussian_model.py:32-42 build_covariance_from_scaling_rotation with
+                  utils/general_utils.py:65-110 (build_rotation, build_scaling_rotation,
+                  strip_symmetric) -- GaussianModel.get_covariance, the cov3D_precomp input of
+                  compute_cov3D_python (gaussian_renderer/__init__.py:86-87); compiled from the
+                  reference's source with "cuda" read as "cpu".  Pins the oracle's computeCov3D
+                  and the HIP cov3D_precomp path
    These pin the camera conventions, the SH polynomial and the loss-gradient convention of the
    oracle and the HIP path.  The reference's rasterizer itself cannot run here (CUDA source,
    no nvcc, and BACKWARD::render is missing from the source; SURVEY.md section 8c).
@@ -126,6 +132,60 @@ def make_ssim_vectors(loss_utils):
     np.savez_compressed(os.path.join(HERE, "ssim.npz"), **out)
 
 
+class _CudaToCpu(__import__("ast").NodeTransformer):
+    """Reads the device literal "cuda" as "cpu" -- the only change made to the reference's code."""
+
+    def visit_Constant(self, node):
+        if node.value == "cuda":
+            node.value = "cpu"
+        return node
+
+
+def _reference_covariance(reference):
+    """GaussianModel.get_covariance's function (scene/gaussian_model.py:32-42, built by setup_functions)
+    with build_scaling_rotation / build_rotation / strip_symmetric (utils/general_utils.py:65-110),
+    compiled from the reference's source with the device literal "cuda" read as "cpu" so it runs here.
+    (scene/ does not import in this container: cameras.py needs cv2.)"""
+    import ast
+
+    ns = {"torch": torch, "np": np}
+    gu = ast.parse(open(os.path.join(reference, "utils/general_utils.py")).read())
+    funcs = [n for n in gu.body if isinstance(n, ast.FunctionDef)]
+    exec(compile(_CudaToCpu().visit(ast.Module(body=funcs, type_ignores=[])), "general_utils", "exec"), ns)
+    gm = ast.parse(open(os.path.join(reference, "scene/gaussian_model.py")).read())
+    cls = next(n for n in gm.body if isinstance(n, ast.ClassDef) and n.name == "GaussianModel")
+    setup = next(n for n in cls.body if isinstance(n, ast.FunctionDef) and n.name == "setup_functions")
+    inner = next(n for n in setup.body if isinstance(n, ast.FunctionDef)
+                 and n.name == "build_covariance_from_scaling_rotation")
+    exec(compile(_CudaToCpu().visit(ast.Module(body=[inner], type_ignores=[])), "gaussian_model", "exec"), ns)
+    return ns["build_covariance_from_scaling_rotation"], ns["build_rotation"]
+
+
+def make_cov3d_vectors(reference):
+    """cov3d.npz: the reference's own covariance (GaussianModel.get_covariance =
+    build_covariance_from_scaling_rotation(get_scaling, modifier, _rotation), the cov3D_precomp input of
+    compute_cov3D_python, gaussian_renderer/__init__.py:86-87) on the scene of the cov3d_precomp case, with
+    un-normalised raw quaternions (get_covariance passes _rotation; build_rotation normalises), plus the
+    normalised quaternion get_rotation would give (the rasterizer's scales/rotations input)."""
+    from tests import common as C
+
+    cov_fn, build_rotation = _reference_covariance(reference)
+    case = next(c for c in C.SMALL_CASES if c.name == "cov3d_precomp")
+    inp = C.build(C.Case(case.name, P=case.P, W=case.W, H=case.H, seed=case.seed))  # scales/rotations form
+    g = torch.Generator().manual_seed(21)
+    raw_rot = inp["rotations"] * (0.5 + 2.0 * torch.rand(case.P, 1, generator=g))  # as stored in _rotation
+    out = {}
+    for tag, mod in (("", 1.0), ("_mod", 0.7)):
+        cov = cov_fn(inp["scales"], mod, raw_rot)
+        out["cov3D" + tag] = cov.numpy().astype(np.float32)
+        out["modifier" + tag] = np.array(mod)
+    out["scales"] = inp["scales"].numpy()
+    out["raw_rotations"] = raw_rot.numpy()
+    out["rotations"] = torch.nn.functional.normalize(raw_rot).numpy()  # get_rotation (rotation_activation)
+    out["R"] = build_rotation(raw_rot).numpy()
+    np.savez_compressed(os.path.join(HERE, "cov3d.npz"), **out)
+
+
 def make_raster_vectors():
     from tests import common as C
     from gaussian_splatting_amd import synthetic as syn
@@ -174,6 +234,7 @@ def main():
     make_l1_vectors(loss_utils)
     make_ssim_vectors(loss_utils)
     sys.path.remove(args.reference)
+    make_cov3d_vectors(args.reference)
     make_sh_vectors(sh_utils)
     make_raster_vectors()
     for f in sorted(os.listdir(HERE)):

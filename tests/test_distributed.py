@@ -94,6 +94,54 @@ def test_view_sharded_allreduce_equals_sum_of_views():
         np.testing.assert_array_equal(s[2 * P:], maxr)
 
 
+def _accumulator_worker(rank, port, outdir, steps):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        from gaussian_splatting_amd.distributed import reduce_densification_stats
+
+        accum, denom, maxr = _local_accumulators(rank, steps)
+        reduce_densification_stats(accum, denom, maxr)  # once, right before densify_and_prune
+        np.save(os.path.join(outdir, f"acc{rank}.npy"), torch.cat([accum.ravel(), denom.ravel(), maxr]).numpy())
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def _local_accumulators(rank, steps, P=64):
+    """train.py's running accumulators over `steps` iterations of this rank's views
+    (add_densification_stats, gaussian_model.py:643-654, and the max_radii2D update of train.py:212-213)."""
+    g = torch.Generator().manual_seed(100 + rank)
+    accum = torch.zeros(P, 1)
+    denom = torch.zeros(P, 1)
+    maxr = torch.zeros(P)
+    for _ in range(steps):
+        visible = torch.rand(P, generator=g) < 0.7
+        norm = torch.rand(P, 1, generator=g)
+        radii = torch.randint(0, 20, (P,), generator=g).float() * visible
+        accum[visible] += norm[visible]
+        denom[visible] += 1
+        maxr[visible] = torch.max(maxr[visible], radii[visible])
+    return accum, denom, maxr
+
+
+def test_densification_stats_reduced_once_per_interval():
+    """The way train.py would use it: each rank accumulates every iteration, then ONE reduction before
+    densify_and_prune gives every rank the statistics of all ranks' views over the whole interval."""
+    steps = 100
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_accumulator_worker, args=(_free_port(), d, steps), nprocs=WORLD, join=True,
+                           start_method="spawn")
+        got = [np.load(os.path.join(d, f"acc{r}.npy")) for r in range(WORLD)]
+    np.testing.assert_array_equal(got[0], got[1])
+    loc = [_local_accumulators(r, steps) for r in range(WORLD)]
+    P = 64
+    np.testing.assert_allclose(got[0][:P], sum(a.ravel() for a, _, _ in loc).numpy(), rtol=1e-6)
+    np.testing.assert_array_equal(got[0][P:2 * P], sum(b.ravel() for _, b, _ in loc).numpy())
+    np.testing.assert_array_equal(got[0][2 * P:], torch.max(loc[0][2], loc[1][2]).numpy())
+    assert got[0][P:2 * P].max() <= WORLD * steps  # counts stay bounded by the number of views seen
+
+
 def test_separate_sh_arena_is_gaussian_model_groups():
     """The separate-SH arena holds GaussianModel's six parameter groups back to back, in training_setup's order
     (gaussian_model.py:235-242), each one contiguous -- the 3DGS-accel backward writes them in place."""

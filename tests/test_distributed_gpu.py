@@ -1,0 +1,109 @@
+"""The multi-rank path on the GPU ("Parity check"): two ranks share cuda:0 with
+gloo collectives (the one-GPU rehearsal of bench.py's GSR_BENCH_SHARE_GPU mode; the 8-GPU RCCL run is
+the driver's).  Rank r renders view r (camera yawed 5 degrees per rank) through the HIP kernels and the
+two exchanges run for real:
+
+  * GradArena.all_reduce -- the backward writes the 59-float parameter gradients into the flat arena,
+    one all-reduce sums them;
+  * ViewExchange -- each rank writes its view block (gsr_rasterize_backward_screen), one all-gather,
+    and every rank runs gsr_gauss_backward_views over both blocks.
+
+Both must equal the oracle's sum of the per-view gradients (unit-scale upstream gradient, the small-case
+bar max |diff| / max |ref| <= 2e-4), and the replicas must be bitwise identical after each exchange.
+"""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from tests import common as C
+
+pytestmark = pytest.mark.gpu
+
+WORLD = 2
+CASE = C.Case("dist_gpu", P=3000, W=96, H=80, focal=90.0)
+KEYS = ("dL_dmeans3D", "dL_dsh", "dL_dopacity", "dL_dscales", "dL_drotations")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _inputs(rank):
+    inp = C.build(C.Case(CASE.name, P=CASE.P, W=CASE.W, H=CASE.H, focal=CASE.focal, yaw=5.0 * rank))
+    gc, gd = C.unit_grads(CASE.H, CASE.W, seed=1 + rank)
+    return inp, gc, gd
+
+
+def _worker(rank, port, outdir):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        from gaussian_splatting_amd import _C
+        from gaussian_splatting_amd.distributed import GradArena, ViewExchange
+
+        dev = torch.device("cuda", 0)
+        inp, gc, gd = _inputs(rank)
+        fwd = C.run_gpu_forward(inp, device=dev)
+        M = inp["shs"].shape[1]
+        # exchange 1: all-reduce of the parameter-gradient arena
+        arena = GradArena(CASE.P, M, dev)
+        C.run_gpu_backward(inp, fwd, gc, gd, device=dev, out=arena.views())
+        arena.all_reduce()
+        torch.cuda.synchronize()
+        np.save(os.path.join(outdir, f"allreduce{rank}.npy"), arena.flat.cpu().numpy())
+        # exchange 2: all-gather of the view blocks, then the per-Gaussian backward over both views
+        d = lambda k: inp[k].to(dev)  # noqa: E731
+        nr, color, radii, geom, binning, img, invd = fwd
+        bwd = (d("bg"), d("means3D"), radii, torch.Tensor([]), d("opacities"), d("scales"), d("rotations"), 1.0,
+               torch.Tensor([]), d("viewmatrix"), d("projmatrix"), inp["tanfovx"], inp["tanfovy"], gc.to(dev),
+               gd.to(dev), d("shs"), inp["sh_degree"], d("campos"), geom, nr, binning, img, False, False)
+        ex = ViewExchange(CASE.P, dev)
+        _C.rasterize_gaussians_backward_screen(*bwd, view_block=ex.local_block())
+        ex.exchange()
+        arena2 = GradArena(CASE.P, M, dev)
+        _C.gauss_backward_views(d("means3D"), None, d("shs"), inp["sh_degree"], d("opacities"), d("scales"),
+                                d("rotations"), 1.0, ex.gathered, out=arena2.views())
+        torch.cuda.synchronize()
+        np.save(os.path.join(outdir, f"views{rank}.npy"), arena2.flat.cpu().numpy())
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_two_ranks_on_gpu_equal_oracle_sum_of_views():
+    from gaussian_splatting_amd.distributed import GradArena
+
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_worker, args=(_free_port(), d), nprocs=WORLD, join=True, start_method="spawn")
+        got = {m: [np.load(os.path.join(d, f"{m}{r}.npy")) for r in range(WORLD)] for m in ("allreduce", "views")}
+    for m, (a, b) in got.items():
+        np.testing.assert_array_equal(a, b, err_msg=f"{m}: replicas differ")
+    ref = GradArena(CASE.P, 16, "cpu")
+    ref.flat.zero_()
+    per_view = []
+    for r in range(WORLD):
+        inp, gc, gd = _inputs(r)
+        g = C.run_oracle(inp).handle.backward(gc, gd)
+        per_view.append(g)
+        for k, t in ref.views().items():
+            t.add_(torch.from_numpy(g[k]).reshape(t.shape))
+    assert not np.allclose(per_view[0]["dL_dmeans3D"], per_view[1]["dL_dmeans3D"])  # two different views
+    for m, (a, _) in got.items():
+        arena = GradArena(CASE.P, 16, "cpu")
+        arena.flat.copy_(torch.from_numpy(a))
+        for k in KEYS:
+            err = C.rel_err(arena.views()[k].numpy(), ref.views()[k].numpy())
+            assert err <= 2e-4, (m, k, err)

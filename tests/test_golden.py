@@ -23,6 +23,30 @@ def _npz(name):
 
 
 # ---------------------------------------------------------------------------- reference vectors
+@pytest.mark.parametrize("tag", ["", "_mod"])
+def test_cov3d_matches_reference_get_covariance(tag):
+    """The oracle's computeCov3D (CR/forward.cu:149-190), fed the normalised quaternion the rasterizer gets
+    (get_rotation), equals the reference's own GaussianModel.get_covariance (build_scaling_rotation +
+    strip_symmetric on the raw quaternion) to float32 rounding; so does tests/common.py's restatement."""
+    from oracle import oracle
+
+    z = _npz("cov3d.npz")
+    mod = float(z["modifier" + tag])
+    exp = z["cov3D" + tag]
+    scale = np.abs(exp).max(1, keepdims=True)
+    got = oracle.cov3d(z["scales"], z["rotations"], mod)
+    assert float((np.abs(got - exp) / scale).max()) <= 1e-6
+    res = C.cov3d_reference(torch.tensor(z["scales"]) * mod, torch.tensor(z["raw_rotations"])).numpy()
+    assert float((np.abs(res - exp) / scale).max()) <= 1e-6
+    # the quaternion convention: build_rotation's matrix is the one the oracle's cov3D is made of
+    R = z["R"]
+    S = z["scales"] * mod
+    M = R * S[:, None, :]
+    full = M @ M.transpose(0, 2, 1)
+    tri = np.stack([full[:, 0, 0], full[:, 0, 1], full[:, 0, 2], full[:, 1, 1], full[:, 1, 2], full[:, 2, 2]], 1)
+    np.testing.assert_allclose(tri, exp, rtol=1e-5, atol=1e-9)
+
+
 def test_camera_matrices_match_reference():
     """syn.world2view / syn.projection / make_camera follow getWorld2View2 + getProjectionMatrix composed as
     scene/cameras.py:86-89 (transposed view, full projection = view @ proj^T, campos = inverse(view)[3,:3])."""

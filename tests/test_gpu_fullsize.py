@@ -1,14 +1,22 @@
-"""Full-size parity at the benchmark configuration (1M Gaussians, 1920x1080, SH degree 3) and at
-BASELINE.json's largest single-GPU configuration (5M Gaussians, 3840x2160, SH degree 3: ~115M
-tile instances, lists of ~3,500 entries per tile -- the long-list sort classes and the tile-list
-sizing).
+"""Full-size parity at BASELINE.json's single-GPU configurations: 500k and 1M Gaussians at
+1920x1080 SH3, and 5M Gaussians at 3840x2160 SH3 (~115M tile instances, lists of ~3,500
+entries per tile -- the long-list sort classes and the tile-list sizing).
 
-The oracle (OpenMP C restatement of the reference) runs the same frame on the host.
-At this size a handful of pixels sit exactly on a discrete threshold of the reference
-algorithm (alpha = 1/255, T = 1e-4, integer radius rounding), where an fp32
-rounding difference (FMA contraction, exp implementation) flips the decision; the
-test therefore checks the 1e-5 bar on >= 99.9% of pixels and bounds the rest, and
-checks size-independent properties exactly (determinism, tile-list invariants).
+The oracle (OpenMP C restatement of the reference, float32, -ffp-contract=off) runs the same
+frame on the host.  What is checked:
+  * integer / index work is identical, not close: num_rendered, radii, every tile's range and
+    its whole sorted list (the reference's identifyTileRanges / point_list);
+  * every pixel whose colour or inverse depth differs by more than 1e-5 is explained by a
+    discrete threshold of the reference's blend that fp32 rounding flips: its last contributor
+    differs, or the oracle's walk over that pixel comes within a small margin of power = 0,
+    alpha = 1/255 or T = 1e-4 (oracle pixel_margins).  Zero unexplained pixels; counts printed;
+  * gradients with a unit-scale (randn) upstream gradient, and with the reference's L1 one:
+    max |diff| / max |ref| <= 2e-4 per tensor over every Gaussian not at a threshold flip.  A
+    Gaussian is at a flip when its own blend at some pixel lies within the margins of a discrete
+    threshold (oracle threshold_gaussians), or it shares a tile with a pixel whose last contributor
+    differs: a flip moves that pixel's whole term in or out of its gradient.  Those are counted and
+    printed with their own error;
+  * bitwise determinism and the reference's colours-precomputed consistency switch.
 """
 import os
 
@@ -21,59 +29,145 @@ from gaussian_splatting_amd import synthetic as syn
 
 pytestmark = [pytest.mark.gpu, pytest.mark.slow]
 
+ATOL_PIX = 1e-5       # north_star: forward RGB within 1e-5 abs fp32
+RTOL_GRAD = 2e-4      # the small-case bar, unit upstream gradient
+# threshold margins (oracle pixel_margins): a pixel within these of a discrete decision of the
+# reference's blend can legitimately fall either way under a different fp32 evaluation order
+MARGIN_POWER = 1e-5   # |power| (absolute)
+MARGIN_ALPHA = 1e-4   # |255 alpha - 1|
+MARGIN_T = 1e-4       # |1e4 T - 1|
+THREADS = max(1, min(16, os.cpu_count() or 1))
+
 
 def _np(t):
     return t.detach().float().cpu().numpy()
 
 
-@pytest.fixture(scope="module", params=["1m_1080p_sh3", "5m_4k_sh3"])
+@pytest.fixture(scope="module", params=["500k_1080p_sh3", "1m_1080p_sh3", "5m_4k_sh3"])
 def fullsize(request):
+    from gaussian_splatting_amd import _C
+
     scene, cam = syn.config_scene(request.param, seed=0)
     inp = dict(bg=torch.zeros(3), means3D=scene.means3D, opacities=scene.opacities, shs=scene.shs,
                sh_degree=scene.sh_degree, scales=scene.scales, rotations=scene.rotations, colors_precomp=None,
                cov3D_precomp=None, viewmatrix=cam.viewmatrix, projmatrix=cam.projmatrix, campos=cam.campos,
                tanfovx=cam.tanfovx, tanfovy=cam.tanfovy, H=cam.height, W=cam.width, scale_modifier=1.0,
                antialiasing=False)
-    threads = min(32, os.cpu_count() or 1)
-    ref = C.run_oracle(inp, nthreads=threads)
-    gc, gd = syn.upstream_grads(cam.height, cam.width)
-    ref_g = ref.handle.backward(gc, gd, nthreads=threads)
+    ref = C.run_oracle(inp, nthreads=THREADS)
+    l1 = syn.upstream_grads(cam.height, cam.width)
+    unit = C.unit_grads(cam.height, cam.width, seed=11)
+    ref_l1 = ref.handle.backward(*l1, nthreads=THREADS)
+    ref_unit = ref.handle.backward(*unit, nthreads=THREADS)
     fwd = C.run_gpu_forward(inp)
-    out = C.run_gpu_backward(inp, fwd, gc, gd)
+    state = _C.debug_forward_state(fwd, scene.means3D.shape[0])
+    out_l1 = C.run_gpu_backward(inp, fwd, *l1)
+    out_unit = C.run_gpu_backward(inp, fwd, *unit)
     torch.cuda.synchronize()
-    return inp, ref, ref_g, fwd, out, (gc, gd)
+    return dict(name=request.param, inp=inp, ref=ref, ref_l1=ref_l1, ref_unit=ref_unit, fwd=fwd, state=state,
+                out_l1=out_l1, out_unit=out_unit, l1=l1, unit=unit)
 
 
-def test_fullsize_forward(fullsize):
-    inp, ref, _, fwd, _, _ = fullsize
-    nr, color, radii, *_, invd = fwd
-    assert abs(nr - ref.num_rendered) <= 1e-4 * ref.num_rendered
-    r = _np(radii).astype(np.int64)
-    same = (r == ref.radii).mean()
-    assert same >= 0.9999, same
-    assert np.abs(r - ref.radii).max() <= 1
-    for got, exp in ((_np(color), ref.color), (_np(invd), ref.invdepth)):
-        d = np.abs(got - exp)
-        assert (d <= 1e-5).mean() >= 0.999, (d <= 1e-5).mean()
-        assert d.mean() <= 1e-6, d.mean()
+def test_fullsize_integers_identical(fullsize):
+    """num_rendered, radii, tile ranges and the sorted tile lists equal the f32 oracle's exactly."""
+    ref, fwd, st = fullsize["ref"], fullsize["fwd"], fullsize["state"]
+    nr, _, radii, *_ = fwd
+    assert nr == ref.num_rendered, (nr, ref.num_rendered)
+    np.testing.assert_array_equal(_np(radii).astype(np.int64), ref.radii.astype(np.int64))
+    rb = ref.handle.binning()
+    gr = st["ranges"].numpy()
+    er = rb["ranges"].astype(np.int64)
+    glen, elen = gr[:, 1] - gr[:, 0], er[:, 1] - er[:, 0]
+    np.testing.assert_array_equal(glen, elen)  # tiles_touched summed per tile
+    nz = elen > 0
+    np.testing.assert_array_equal(gr[nz, 0], er[nz, 0])  # (empty tiles: the reference leaves [0, 0))
+    np.testing.assert_array_equal(st["point_list"].numpy(), rb["point_list"].astype(np.int64))
+    print(f"[{fullsize['name']}] num_rendered={nr} identical; {int(nz.sum())} non-empty tiles, lists identical")
 
 
-def test_fullsize_backward(fullsize):
-    _, _, ref_g, _, out, _ = fullsize
+def _flips(fullsize):
+    """Pixels over the 1e-5 bar, and which of them each threshold explains."""
+    ref, fwd, st = fullsize["ref"], fullsize["fwd"], fullsize["state"]
+    color, invd = _np(fwd[1]), _np(fwd[6])
+    d = np.maximum(np.abs(color - ref.color).max(0), np.abs(invd - ref.invdepth)[0])
+    over = d > ATOL_PIX
+    img = ref.handle.image()
+    nc_diff = st["n_contrib"].numpy() != img["n_contrib"].astype(np.int64)
+    m = ref.handle.pixel_margins(nthreads=THREADS)
+    near = (m["power"] < MARGIN_POWER) | (m["alpha"] < MARGIN_ALPHA) | (m["T"] < MARGIN_T)
+    return d, over, nc_diff, near, m
+
+
+def test_fullsize_forward_every_pixel_explained(fullsize):
+    d, over, nc_diff, near, m = _flips(fullsize)
+    explained = nc_diff | near
+    unexplained = over & ~explained
+    n = d.size
+    print(f"[{fullsize['name']}] pixels {n}: |diff|>1e-5: {int(over.sum())}; n_contrib differs: "
+          f"{int(nc_diff.sum())} ({int((over & nc_diff).sum())} over the bar); within a threshold margin: "
+          f"{int(near.sum())} (power {int((m['power'] < MARGIN_POWER).sum())}, alpha "
+          f"{int((m['alpha'] < MARGIN_ALPHA).sum())}, T {int((m['T'] < MARGIN_T).sum())}); unexplained: "
+          f"{int(unexplained.sum())}; max|diff| on unflipped pixels {float(d[~explained].max()):.2e}")
+    if unexplained.any():
+        ys, xs = np.nonzero(unexplained)
+        worst = np.argsort(-d[unexplained])[:10]
+        details = [(int(ys[i]), int(xs[i]), float(d[ys[i], xs[i]]), float(m["power"][ys[i], xs[i]]),
+                    float(m["alpha"][ys[i], xs[i]]), float(m["T"][ys[i], xs[i]])) for i in worst]
+        raise AssertionError(f"{int(unexplained.sum())} unexplained pixels (y, x, diff, margins): {details}")
+    assert float(d[~explained].max()) <= ATOL_PIX
+
+
+def _tainted(fullsize, flipped):
+    """Gaussians whose gradient a threshold flip can move by a whole pixel's term: those whose own blend
+    comes within the margins of a discrete threshold at some pixel (oracle threshold_gaussians), and every
+    Gaussian listed in a tile holding a pixel whose last contributor differs."""
+    mask = fullsize["ref"].handle.threshold_gaussians(MARGIN_POWER, MARGIN_ALPHA, MARGIN_T, nthreads=THREADS)
+    return mask | _tile_members(fullsize, flipped)
+
+
+def _tile_members(fullsize, flipped):
+    """Gaussians listed in a tile that holds a flipped pixel."""
+    st = fullsize["state"]
+    W = fullsize["inp"]["W"]
+    gx = (W + 15) // 16
+    ys, xs = np.nonzero(flipped)
+    tiles = np.unique((ys // 16) * gx + xs // 16)
+    r = st["ranges"].numpy()
+    pl = st["point_list"].numpy()
+    P = fullsize["inp"]["means3D"].shape[0]
+    mask = np.zeros(P, bool)
+    for t in tiles:
+        mask[pl[r[t, 0]:r[t, 1]]] = True
+    return mask
+
+
+@pytest.mark.parametrize("upstream", ["unit", "l1"])
+def test_fullsize_backward(fullsize, upstream):
+    d, over, nc_diff, near, _ = _flips(fullsize)
+    taint = _tainted(fullsize, nc_diff)
+    ref_g = fullsize["ref_unit" if upstream == "unit" else "ref_l1"]
+    out = fullsize["out_unit" if upstream == "unit" else "out_l1"]
+    rows = []
     for k, got in zip(C.GRAD_NAMES, out):
-        g, e = _np(got), ref_g[k]
+        g, e = _np(got).astype(np.float64), ref_g[k]
         assert g.shape == e.shape
-        d = np.abs(g.astype(np.float64) - e)
-        scale = np.abs(e).max()
-        # 99.9% of entries within 1e-4 of the tensor's scale; the 1e-5 absolute bar with the L1 loss
-        assert np.quantile(d, 0.999) <= 1e-4 * scale, (k, np.quantile(d, 0.999) / scale)
-        assert d.max() <= 1e-5, (k, d.max())
+        scale = max(float(np.abs(e).max()), 1e-30)
+        diff = np.abs(g - e).reshape(g.shape[0], -1).max(1)
+        clean = float(diff[~taint].max()) / scale if (~taint).any() else 0.0
+        dirty = float(diff[taint].max()) / scale if taint.any() else 0.0
+        rows.append((k, scale, clean, dirty))
+    print(f"[{fullsize['name']}/{upstream}] Gaussians at a threshold flip: {int(taint.sum())} "
+          f"of {taint.size}; per tensor (max|ref|, max rel elsewhere, max rel at flips): "
+          + "; ".join(f"{k} {s:.2e} {c:.2e} {t:.2e}" for k, s, c, t in rows))
+    for k, s, c, t in rows:
+        assert c <= RTOL_GRAD, (k, c)
+        assert np.isfinite(t)
+    assert taint.mean() <= 0.05, taint.mean()
 
 
 def test_fullsize_deterministic(fullsize):
-    inp, _, _, fwd, out, (gc, gd) = fullsize
+    inp, fwd, out = fullsize["inp"], fullsize["fwd"], fullsize["out_unit"]
     fwd2 = C.run_gpu_forward(inp)
-    out2 = C.run_gpu_backward(inp, fwd2, gc, gd)
+    out2 = C.run_gpu_backward(inp, fwd2, *fullsize["unit"])
     assert fwd2[0] == fwd[0]
     assert torch.equal(fwd2[1], fwd[1]) and torch.equal(fwd2[6], fwd[6])
     for a, b in zip(out, out2):
@@ -83,12 +177,13 @@ def test_fullsize_deterministic(fullsize):
 def test_fullsize_colors_precomp_matches_sh(fullsize):
     """The reference's own consistency switch (gaussian_renderer/__init__.py:86-104): colours computed from
     the SHs outside the rasterizer give the same image as in-kernel SH evaluation."""
-    inp, ref, _, fwd, _, _ = fullsize
+    inp, fwd = fullsize["inp"], fullsize["fwd"]
     means = inp["means3D"]
     dirs = torch.nn.functional.normalize(means - inp["campos"][None], dim=1)
     rgb = _sh_eval(inp["shs"], dirs, inp["sh_degree"])
     inp2 = dict(inp, colors_precomp=torch.clamp_min(rgb + 0.5, 0.0), shs=None)
     fwd2 = C.run_gpu_forward(inp2)
+    assert fwd2[0] == fwd[0]
     d = (fwd2[1] - fwd[1]).abs()
     assert (d <= 1e-5).float().mean() >= 0.999
     assert float(d.mean()) <= 1e-6
