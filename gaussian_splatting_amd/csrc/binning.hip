@@ -46,12 +46,13 @@ namespace gsr {
 constexpr int kBinThreads = 1024;
 constexpr int kBinWaves = kBinThreads / 64;
 constexpr uint32_t kLdsTilesMax = 36864;  // K3 keeps one u32 per tile in LDS (144 KiB)
-constexpr uint32_t kSortWaveMax = 1024;   // longest list tile_sort_kernel sorts (one wave, 16 keys per lane)
-// Longer lists go to two persistent kernels: class 0 (1024, 2048], 128 threads x 16 keys
-// in registers; class 1 (> 2048), 512 threads x 8 or 16 keys in registers up to 8192
-// keys, and a network in global memory beyond.
+constexpr uint32_t kSortWaveMax = 1024;   // longest list tile_sort_kernel sorts (one wave per tile)
+// Longer lists go to two persistent 256-thread kernels walking K2's class lists: class 0
+// (1024, 4096], class 1 (> 4096; bucket sort up to 8192 keys, a network in global memory
+// beyond).
 constexpr int kSortClasses = 2;
-constexpr uint32_t kBigRegMax = 8192;
+constexpr uint32_t kClass0Max = 4096;
+constexpr uint32_t kBucketMax = 8192;
 
 typedef unsigned long long u64;
 
@@ -335,7 +336,7 @@ __global__ void __launch_bounds__(kBinThreads) tile_scan_kernel(uint32_t tiles, 
                 ranges[b + i] = make_uint2((uint32_t)lo, (uint32_t)hi);
                 tile_base[b + i] = (uint32_t)at;
                 if (v[i] > kSortWaveMax) {  // long list: one of the class kernels (K4)
-                    const int c = v[i] <= 2048u ? 0 : 1;
+                    const int c = v[i] <= kClass0Max ? 0 : 1;
                     cls_list[(size_t)c * tiles + atomicAdd(&s_cls[c], 1u)] = b + i;
                 }
             }
@@ -534,11 +535,175 @@ __device__ __forceinline__ uint32_t tile_len(uint2 r, u64 cap) {
     return hi > r.x ? (uint32_t)(hi - r.x) : 0u;
 }
 
-// One wave per tile, lists up to kSortWaveMax (64 x 16 keys in registers, no LDS, no
-// barrier).  Longer lists were put on K2's class lists and go to the kernels below.
+// Bitonic network in global memory, for lists longer than any register/LDS sort here (any
+// length; slow -- real scenes rarely produce such tiles, and the bucket sort below takes every
+// list up to kBucketMax).  The "flip" form: every comparator is ascending; for block size k the
+// first step pairs i with i ^ (k - 1), the others with i ^ j, so keys past n behave as +infinity
+// and are never touched.
+__device__ void sort_list_global(u64* __restrict__ keys, uint32_t lo, uint32_t n, uint32_t* __restrict__ gid_sorted) {
+    u64* k = keys + lo;
+    uint32_t N2 = 1;
+    while (N2 < n) N2 <<= 1;
+    for (uint32_t kk = 2; kk <= N2; kk <<= 1) {
+        for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
+            for (uint32_t p = threadIdx.x; p < N2 / 2; p += blockDim.x) {
+                const uint32_t a = ((p & ~(j - 1)) << 1) | (p & (j - 1));  // p-th index with bit j clear
+                const uint32_t b = (j == (kk >> 1)) ? (a ^ (kk - 1)) : (a | j);
+                if (b < n) {
+                    const u64 x = k[a], y = k[b];
+                    if (y < x) {
+                        k[a] = y;
+                        k[b] = x;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) gid_sorted[lo + i] = (uint32_t)k[i];
+}
+
+// ---- bucket-rank sort ---------------------------------------------------------
+// A tile's keys are unique 64-bit values (depth bits << 32 | Gaussian << 4), so a key's
+// place in the sorted list is the number of smaller keys.  Two steps, all in LDS:
+//  1. bucket: the tile's key range [min, max] is cut into 2^lg equal bins (the key minus min,
+//     shifted right); each key takes a slot in its bin with a returning LDS atomic (the order
+//     inside a bin is arbitrary), a scan of the bin counts gives the bin starts, and the keys
+//     are scattered to their bins;
+//  2. rank: a key's position is its bin's start plus the number of smaller keys in its bin.
+//     Neighbouring lanes hold keys of the same or adjacent bins, so their LDS reads of a bin
+//     are mostly broadcasts.
+// The work is ~n plus the sum over bins of size^2, against ~78 compare-exchange stages per key
+// for a 4096-key bitonic network (the sort this replaces).  When the bins are badly skewed --
+// the tile's depths cluster in a sliver of their range, sum of squares above kSkew * n -- the
+// list goes to the bitonic network instead (the caller's fallback).  The result is the
+// reference's (depth, index) order exactly: keys are compared whole.
+#ifndef GSR_BIN_SHIFT
+#define GSR_BIN_SHIFT 1
+#endif
+#ifndef GSR_SKEW
+#define GSR_SKEW 48
+#endif
+constexpr int kBinShift = GSR_BIN_SHIFT;  // bins = pow2 >= n >> kBinShift (about two keys per bin)
+constexpr uint32_t kSkew = GSR_SKEW;      // fallback when sum(bin size^2) > kSkew * n
+
+template <int T, int NMAX, int NBMAX>
+struct BucketLds {
+    u64 buf[NMAX];
+    uint32_t start[NBMAX + 1];
+    u64 red[2 * (T / 64)];
+    uint32_t tmp[T / 64];
+};
+
+template <int T>
+__device__ __forceinline__ void block_minmax_u64(u64& mn, u64& mx, u64* red) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const u64 a = __shfl_xor(mn, o), b = __shfl_xor(mx, o);
+        mn = a < mn ? a : mn;
+        mx = b > mx ? b : mx;
+    }
+    if constexpr (T > 64) {
+        const int w = threadIdx.x >> 6;
+        __syncthreads();
+        if ((threadIdx.x & 63) == 0) {
+            red[2 * w] = mn;
+            red[2 * w + 1] = mx;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < T / 64; i++) {
+            mn = red[2 * i] < mn ? red[2 * i] : mn;
+            mx = red[2 * i + 1] > mx ? red[2 * i + 1] : mx;
+        }
+    }
+}
+
+// Sorts keys[lo, lo + n) (n <= T * E) into gid_sorted[lo, lo + n) (low key halves) and returns
+// true, or returns false (nothing written, uniformly over the workgroup) when the bins are too
+// skewed.  The keys are loaded once, striped over the workgroup (all E loads of a thread in
+// flight together), and stay in registers until they are scattered to their bins.  The caller
+// must barrier before reusing the LDS.
+template <int T, int E, int NMAX, int NBMAX>
+__device__ bool bucket_sort_list(const u64* __restrict__ keys, uint32_t lo, uint32_t n,
+                                 uint32_t* __restrict__ gid_sorted, BucketLds<T, NMAX, NBMAX>& s) {
+    static_assert(T * E <= NMAX, "LDS bucket buffer");
+    const uint32_t tid = threadIdx.x;
+    u64 k[E];
+    uint32_t o[E];
+    u64 mn = ~0ull, mx = 0ull;
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        const uint32_t i = (uint32_t)e * T + tid;
+        k[e] = i < n ? keys[lo + i] : 0ull;
+    }
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        if ((uint32_t)e * T + tid < n) {
+            mn = k[e] < mn ? k[e] : mn;
+            mx = k[e] > mx ? k[e] : mx;
+        }
+    }
+    block_minmax_u64<T>(mn, mx, s.red);
+    uint32_t lg = 0;
+    while ((1u << lg) < (n >> kBinShift) && (1u << lg) < (uint32_t)NBMAX) lg++;
+    const u64 range = mx - mn;
+    const uint32_t bits = range ? 64u - (uint32_t)__clzll((long long)range) : 0u;
+    const uint32_t sh = bits > lg ? bits - lg : 0u;
+    const uint32_t nb = (uint32_t)(range >> sh) + 1u;  // <= 2^lg bins
+    const uint32_t per = (nb + T - 1) / T;            // bins per thread in the scan
+    for (uint32_t i = tid; i < per * T + 1; i += T) s.start[i] = 0u;
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < E; e++)
+        if ((uint32_t)e * T + tid < n) o[e] = atomicAdd(&s.start[(uint32_t)((k[e] - mn) >> sh)], 1u);
+    __syncthreads();
+    // bin counts -> bin starts (in place), and the sum of squared bin sizes
+    uint32_t run = 0, sq = 0;
+    for (uint32_t c = 0; c < per; c++) {
+        const uint32_t v = s.start[tid * per + c];
+        run += v;
+        sq += v * v;
+    }
+    uint32_t all = 0;
+    uint32_t at = block_exclusive_scan(run, s.tmp, &all);
+    const uint32_t sumsq = block_sum(sq, s.tmp);  // (ends with a barrier: every count was read)
+    if (sumsq > kSkew * n) return false;  // uniform
+    for (uint32_t c = 0; c < per; c++) {
+        const uint32_t v = s.start[tid * per + c];
+        s.start[tid * per + c] = at;
+        at += v;
+    }
+    if (tid == 0) s.start[nb] = n;  // bins past nb are empty and never looked up
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < E; e++)
+        if ((uint32_t)e * T + tid < n) s.buf[s.start[(uint32_t)((k[e] - mn) >> sh)] + o[e]] = k[e];
+    __syncthreads();
+    for (uint32_t j = tid; j < n; j += T) {
+        const u64 kj = s.buf[j];
+        const uint32_t b = (uint32_t)((kj - mn) >> sh);
+        const uint32_t st = s.start[b], en = s.start[b + 1];
+        uint32_t c = 0;
+#pragma unroll 4
+        for (uint32_t q = st; q < en; q++) c += s.buf[q] < kj ? 1u : 0u;
+        gid_sorted[lo + st + c] = (uint32_t)kj;
+    }
+    return true;
+}
+
+// Lists of up to kSortWaveMax keys: one wave per tile.  Short lists (<= kBucketMinN) are
+// sorted by a bitonic network in registers (no LDS, no barrier); longer ones by the bucket
+// sort, with the register network as its skew fallback.
+#ifndef GSR_BUCKET_MIN_N
+#define GSR_BUCKET_MIN_N 128
+#endif
+constexpr uint32_t kBucketMinN = GSR_BUCKET_MIN_N;
+
 __global__ void __launch_bounds__(64) tile_sort_kernel(const uint2* __restrict__ ranges,
                                                        const u64* __restrict__ keys, u64 cap,
                                                        uint32_t* __restrict__ gid_sorted) {
+    __shared__ BucketLds<64, kSortWaveMax, kSortWaveMax / 2> s;
     const uint2 r = ranges[blockIdx.x];
     const uint32_t n = tile_len(r, cap);
     GSR_STAMP(g_st_sort, blockIdx.x, 0);
@@ -546,6 +711,16 @@ __global__ void __launch_bounds__(64) tile_sort_kernel(const uint2* __restrict__
     if (n <= 1) {
         if (n == 1 && threadIdx.x == 0) gid_sorted[r.x] = (uint32_t)keys[r.x];
         return;
+    }
+    if (n > kSortWaveMax) return;  // a class kernel's list (K2)
+    if (n > kBucketMinN) {  // uniform
+        const bool done = n <= 256   ? bucket_sort_list<64, 4>(keys, r.x, n, gid_sorted, s)
+                          : n <= 512 ? bucket_sort_list<64, 8>(keys, r.x, n, gid_sorted, s)
+                                     : bucket_sort_list<64, 16>(keys, r.x, n, gid_sorted, s);
+        if (done) {
+            GSR_STAMP(g_st_sort, blockIdx.x, 1);
+            return;
+        }
     }
     if (n <= 64)
         sort_list<64, 1>(keys, r.x, n, gid_sorted, nullptr);
@@ -560,69 +735,36 @@ __global__ void __launch_bounds__(64) tile_sort_kernel(const uint2* __restrict__
     GSR_STAMP(g_st_sort, blockIdx.x, 1);
 }
 
-// Persistent: T-thread workgroups walk one class list of long tiles (K2) and sort
-// each list of (lo_excl, T * 16] keys in registers.
-template <int T>
-__global__ void __launch_bounds__(T) tile_sort_class_kernel(const uint2* __restrict__ ranges,
-                                                            const u64* __restrict__ keys, u64 cap,
-                                                            uint32_t* __restrict__ gid_sorted,
-                                                            const uint32_t* __restrict__ list,
-                                                            const uint32_t* __restrict__ count) {
-    __shared__ u64 s_x[T * 16];
+// Persistent: 256-thread workgroups walk one class list of long tiles (K2).  Class 0
+// (kSortWaveMax, kClass0Max]: bucket sort, skew fallback a 256 x 16 register network (its
+// exchange buffer aliases the bucket buffer).  Class 1 (> kClass0Max): bucket sort up to
+// kBucketMax keys, the global-memory network beyond or on skew.
+constexpr int kClassThreads = 256;
+
+template <int CLASS>
+__global__ void __launch_bounds__(kClassThreads) tile_sort_class_kernel(const uint2* __restrict__ ranges,
+                                                                        u64* __restrict__ keys, u64 cap,
+                                                                        uint32_t* __restrict__ gid_sorted,
+                                                                        const uint32_t* __restrict__ list,
+                                                                        const uint32_t* __restrict__ count) {
+    constexpr int NMAX = CLASS == 0 ? (int)kClass0Max : (int)kBucketMax;
+    __shared__ BucketLds<kClassThreads, NMAX, NMAX / 2> s;
+    static_assert(sizeof(s.buf) >= kClassThreads * 16 * sizeof(u64), "the fallback network's buffer");
     const uint32_t nb = count[0];
     for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
         const uint2 r = ranges[list[b]];
         const uint32_t n = tile_len(r, cap);  // may be shorter than its class when truncated by cap
-        sort_list<T, 16>(keys, r.x, n, gid_sorted, s_x);
-        __syncthreads();  // s_x is reused by the next tile
-    }
-}
-
-// Class 1: lists beyond 2048 keys, 512-thread workgroups walking K2's list.  Up to 8192
-// keys the registers hold them (8 or 16 per thread); beyond, a network on the global keys
-// (any length; slow -- real scenes rarely produce such tiles).  The global network uses
-// the "flip" form: every comparator is ascending; for block size k the first step pairs
-// i with i ^ (k - 1), the others with i ^ j, so keys past n behave as +infinity and are
-// never touched.
-constexpr int kBigThreads = 512;
-
-__global__ void __launch_bounds__(kBigThreads) tile_sort_big_kernel(const uint2* __restrict__ ranges,
-                                                                    u64* __restrict__ keys, u64 cap,
-                                                                    uint32_t* __restrict__ gid_sorted,
-                                                                    const uint32_t* __restrict__ list,
-                                                                    const uint32_t* __restrict__ count) {
-    __shared__ u64 s_x[kBigThreads * 16];
-    const uint32_t nb = count[0];
-    for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
-        const uint2 r = ranges[list[b]];
-        const uint32_t n = tile_len(r, cap);  // may be shorter than its class when truncated by cap
-        if (n <= (uint32_t)kBigThreads * 8) {
-            sort_list<kBigThreads, 8>(keys, r.x, n, gid_sorted, s_x);
-        } else if (n <= kBigRegMax) {
-            sort_list<kBigThreads, 16>(keys, r.x, n, gid_sorted, s_x);
-        } else {
-            u64* k = keys + r.x;
-            uint32_t N2 = 1;
-            while (N2 < n) N2 <<= 1;
-            for (uint32_t kk = 2; kk <= N2; kk <<= 1) {
-                for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
-                    for (uint32_t p = threadIdx.x; p < N2 / 2; p += blockDim.x) {
-                        const uint32_t lo = ((p & ~(j - 1)) << 1) | (p & (j - 1));  // p-th index with bit j clear
-                        const uint32_t hi = (j == (kk >> 1)) ? (lo ^ (kk - 1)) : (lo | j);
-                        if (hi < n) {
-                            const u64 x = k[lo], y = k[hi];
-                            if (y < x) {
-                                k[lo] = y;
-                                k[hi] = x;
-                            }
-                        }
-                    }
-                    __syncthreads();
-                }
-            }
-            for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) gid_sorted[r.x + i] = (uint32_t)k[i];
+        if (n <= 1) {
+            if (n == 1 && threadIdx.x == 0) gid_sorted[r.x] = (uint32_t)keys[r.x];
+        } else if (n > (uint32_t)NMAX || !bucket_sort_list<kClassThreads, NMAX / kClassThreads>(keys, r.x, n,
+                                                                                               gid_sorted, s)) {
+            __syncthreads();
+            if (CLASS == 0 || n <= (uint32_t)kClassThreads * 16)
+                sort_list<kClassThreads, 16>(keys, r.x, n, gid_sorted, s.buf);
+            else
+                sort_list_global(keys, r.x, n, gid_sorted);
         }
-        __syncthreads();  // s_x is reused by the next tile
+        __syncthreads();  // the LDS is reused by the next tile
     }
 }
 
@@ -713,9 +855,9 @@ hipError_t launch_tile_sort(uint32_t tiles, const uint2* ranges, const GeomState
     hipLaunchKernelGGL(tile_sort_kernel, dim3(tiles), dim3(64), 0, stream, ranges, b.keys, c, b.gid_sorted);
     // persistent class kernels: grids sized to fill the chip when their lists are long
     const auto grid = [&](uint32_t want) { return dim3(tiles < want ? tiles : want); };
-    hipLaunchKernelGGL(tile_sort_class_kernel<128>, grid(2048), dim3(128), 0, stream, ranges, b.keys, c,
+    hipLaunchKernelGGL(tile_sort_class_kernel<0>, grid(2048), dim3(kClassThreads), 0, stream, ranges, b.keys, c,
                        b.gid_sorted, g.cls_list, g.cls_count);
-    hipLaunchKernelGGL(tile_sort_big_kernel, grid(512), dim3(kBigThreads), 0, stream, ranges, b.keys, c,
+    hipLaunchKernelGGL(tile_sort_class_kernel<1>, grid(512), dim3(kClassThreads), 0, stream, ranges, b.keys, c,
                        b.gid_sorted, g.cls_list + tiles, g.cls_count + 1);
     return hipGetLastError();
 }
