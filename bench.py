@@ -67,9 +67,36 @@ def step_algorithmic_bytes(P, I, W, H, K):
     return (304 + 36 * K) * P + 132 * I + 48 * W * H
 
 
-def cpu_baseline(cfg_name: str, P: int, W: int, H: int, threads: int, min_seconds: float = 10.0):
-    """Oracle (C restatement of the reference, oracle/) forward + backward on the host, on the same
-    frame as the GPU, repeated until at least ``min_seconds`` of CPU work (a bounded sample)."""
+def cpu_baseline(cfg_name: str, P: int, W: int, H: int, forward_only: bool = False):
+    """north_star's CPU baseline: the pure-PyTorch fallback rasterizer (oracle/torch_fallback.py, fp32)
+    on this host's cores, forward + autograd backward on the same frame as the GPU.  A bounded sample
+    (SURVEY.md 8d): preprocess, binning and the preprocess backward run in full; the render runs on a
+    stratified sample of the tiles and is scaled to the frame by list entries."""
+    from oracle import torch_fallback as tf
+
+    scene, cam = syn.config_scene(cfg_name, seed=0, P=P)
+    gc, gd = (None, None) if forward_only else syn.upstream_grads(H, W)
+    frac = 1.0 if P <= 100_000 else 0.25
+    reps = 5 if P <= 100_000 else 2
+    tf.splats_per_second(scene, cam, scene.sh_degree, gc, gd, tile_fraction=min(frac, 0.02))  # untimed warm-up
+    t0 = time.perf_counter()
+    value, t_frame, res = tf.splats_per_second(scene, cam, scene.sh_degree, gc, gd, tile_fraction=frac, reps=reps)
+    wall = time.perf_counter() - t0
+    threads = torch.get_num_threads()
+    what = "forward" if forward_only else "forward + autograd backward"
+    sample = (f"{reps} reps of the full frame" if frac >= 1.0 else
+              f"{reps} reps; render on every {round(1 / frac)}th tile of the length-sorted order "
+              f"({res['rendered_instances']} of {res['num_rendered']} list entries), scaled by entries")
+    return {"value": value, "unit": "Gaussian-splats/s", "cores": threads, "host_cpus": os.cpu_count(),
+            "kind": "port", "impl": "pure-PyTorch fallback rasterizer (oracle/torch_fallback.py, fp32)",
+            "sample": f"{cfg_name} ({P} Gaussians, {W}x{H}) {what}: {sample}; {t_frame:.2f} s per frame, "
+                      f"{wall:.1f} s timed, torch.get_num_threads() = {threads} (the box's OMP_NUM_THREADS share) "
+                      f"of os.cpu_count() = {os.cpu_count()}"}
+
+
+def cpu_baseline_c(cfg_name: str, P: int, W: int, H: int, threads: int, min_seconds: float = 8.0):
+    """Second CPU figure: the C restatement (oracle/gsr_oracle.c, OpenMP) forward + backward on the
+    same frame, repeated until at least ``min_seconds`` of CPU work."""
     from oracle import oracle
 
     scene, cam = syn.config_scene(cfg_name, seed=0, P=P)
@@ -85,8 +112,56 @@ def cpu_baseline(cfg_name: str, P: int, W: int, H: int, threads: int, min_second
         reps += 1
         del r
     return {"value": reps * P / total, "unit": "Gaussian-splats/s", "cores": threads, "kind": "port",
+            "impl": "C restatement (oracle/gsr_oracle.c, float32, OpenMP)",
             "sample": f"{reps} full {cfg_name} frames ({P} Gaussians, {W}x{H}), forward+backward, "
-                      f"{total:.1f} s on {threads} OpenMP threads (oracle/gsr_oracle.c, float32)"}
+                      f"{total:.1f} s on {threads} OpenMP threads"}
+
+
+def cpu_only(cfg_name: str) -> None:
+    """BASELINE.json configs[0] ("forward-only via PyTorch CPU fallback, plumbing, no GPU"): the
+    fallback alone, one JSON line, no HIP device touched."""
+    cfg = syn.CONFIGS[cfg_name]
+    base = cpu_baseline(cfg_name, cfg["P"], cfg["width"], cfg["height"], forward_only=True)
+    print(json.dumps({"metric": "Gaussian-splats/sec forward, CPU fallback", "value": base["value"],
+                      "unit": "Gaussian-splats/s", "n_gpus": 0, "higher_is_better": True, "dtype": "fp32",
+                      "data": "synthetic (frustum-uniform Gaussians, SURVEY.md 8d; seed 0)",
+                      "config": {"workload": cfg_name, "gaussians": cfg["P"], "width": cfg["width"],
+                                 "height": cfg["height"], "sh_degree": cfg["sh_degree"], "pass": "forward"},
+                      "cpu_baseline": base}), flush=True)
+
+
+def multi_rank_diagnostics(args, world, rank, views, ex, arena, per_rank, P, dev):
+    """N > 1: which exchange ran and why, its measured time alone (an untimed pass after the timed
+    region, every rank running the same collective count), the bytes each rank receives, and every
+    rank's own ms/step -- so a straggler or a wrong ``auto`` threshold shows in the record."""
+    reps = 5
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        if views:
+            ex.exchange()
+        else:
+            arena.all_reduce()
+    torch.cuda.synchronize()
+    ms = torch.tensor([(time.perf_counter() - t0) / reps * 1e3], dtype=torch.float64, device=dev)
+    dist.all_reduce(ms, op=dist.ReduceOp.MAX)
+    if views:
+        recv = (world - 1) * ex.block_floats * 4
+        why = (f"--exchange {args.exchange}: all-gather of 44-B/Gaussian view blocks"
+               + (" (auto picks it up to 4 ranks: fewer received bytes than the 2(N-1)/N x 236 B/Gaussian "
+                  "all-reduce; DESIGN.md section 7)" if args.exchange == "auto" else ""))
+    else:
+        recv = int(2 * (world - 1) / world * arena.flat.numel() * 4)
+        why = (f"--exchange {args.exchange}: RCCL all-reduce of the 59-float/Gaussian gradient arena"
+               + (" (auto picks it above 4 ranks, where the multi-view kernel's extra time would exceed the "
+                  "bytes saved at an assumed ~330 GB/s bus rate; DESIGN.md section 7)" if args.exchange == "auto"
+                  else ""))
+    return {"exchange": "views" if views else "allreduce", "why": why,
+            "exchange_ms": float(ms.item()), "received_bytes_per_rank": recv,
+            "exchange_GBs_per_rank": recv / (float(ms.item()) * 1e-3) / 1e9 if ms.item() > 0 else None,
+            "per_rank_ms_per_step": [round(e / args.steps * 1e3, 4) for e in per_rank],
+            "backend": dist.get_backend()}
 
 
 def main():
@@ -96,13 +171,20 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="1m_1080p_sh3", choices=sorted(syn.CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-census", action="store_true",
+                    help="skip the census pass (profiler runs: keeps its kernel instantiations out of the trace)")
     ap.add_argument("--exchange", choices=("auto", "views", "allreduce"), default="auto",
                     help="N > 1: all-gather the view blocks or all-reduce the parameter gradients; auto = views "
                          "up to 4 ranks, all-reduce beyond (DESIGN.md section 7)")
-    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="threads of the C-restatement figure (default 16)")
+    ap.add_argument("--cpu-only", action="store_true",
+                    help="no GPU: time the pure-PyTorch fallback forward on --config (BASELINE configs[0] plumbing)")
     ap.add_argument("--ramp-seconds", type=float, default=0.3,
                     help="untimed steps before the warmup, until the GPU clock has ramped up (DVFS)")
     args = ap.parse_args()
+    if args.cpu_only:
+        cpu_only(args.config)
+        return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -176,6 +258,9 @@ def main():
     stages = _lib.profile_collect()
     per_stage = {k: (v[0] / v[1] if v[1] else 0.0) for k, v in stages.items()}
     dom = max(per_stage, key=per_stage.get)
+    # Work census (untimed, census kernel instantiations): how many (pixel, splat) pairs the render
+    # kernels blend -- their cost follows these pairs, not the per-instance bytes of the roofline.
+    census = None if args.no_census else _lib.census(lambda: step(collective=False), dev)
 
     _lib.profile_reset()
     _lib.profile_enable(True, stages=[dom])
@@ -192,23 +277,39 @@ def main():
     _lib.profile_enable(False)
     dom_total, dom_calls = _lib.profile_collect()[dom]
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    per_rank = [elapsed]
     if world > 1:
+        gathered = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(gathered, t)
+        per_rank = [float(g.item()) for g in gathered]
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
+    multi = multi_rank_diagnostics(args, world, rank, views, ex, arena, per_rank, P, dev) if world > 1 else None
 
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
         value = world * P * args.steps / elapsed
         dom_ms = dom_total / dom_calls if dom_calls else 0.0  # HIP events on the launch stream, timed region
         alg = algorithmic_bytes(dom, P, nr, W, H, K)
-        traffic, traffic_src = None, None
+        traffic, traffic_src, kk = None, None, {}
         if args.config == "1m_1080p_sh3" and os.path.exists(PMC_PROFILE):
             prof = json.load(open(PMC_PROFILE))
-            kk = prof.get("kernels", {}).get(dom)
+            kk = prof.get("kernels", {}).get(dom) or {}
             if kk:
                 traffic = kk["hbm_read_bytes"] + kk["hbm_write_bytes"]
                 traffic_src = prof.get("source")
         achieved = alg / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
+        valu_frac = None
+        if traffic is not None and kk.get("valu_insts"):
+            # wave64 VALU issues in 2 cycles on a 32-wide SIMD; 1024 SIMDs at 2.4 GHz (MI355X_MICROARCH.md)
+            valu_frac = kk["valu_insts"] * 2.0 / (dom_ms * 1e-3 * 2.4e9 * 1024)
+        work = dict(census or {})
+        for k, stage in (("fwd", "render_fwd"), ("bwd", "render_bwd")) if census else ():
+            t_ms = per_stage.get(stage, 0.0)
+            pairs = census["fwd_pairs_blended" if k == "fwd" else "bwd_pairs_grad"]
+            work[f"{stage}_pairs_per_s"] = pairs / (t_ms * 1e-3) if t_ms > 0 else None
+        if census:
+            work["pairs_per_instance"] = census["fwd_pairs_blended"] / nr if nr else None
         line = {
             "metric": "Gaussian-splats/sec fwd+bwd @1080p, 1M Gaussians",
             "value": value,
@@ -229,13 +330,21 @@ def main():
                            "" if world == 1 else " + RCCL all-gather of view blocks" if views else " + RCCL all-reduce")},
             "roofline": {"kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                         "algorithmic_bytes_per_launch": alg, "mean_launch_ms": dom_ms},
+                         "algorithmic_bytes_per_launch": alg, "mean_launch_ms": dom_ms,
+                         # what actually limits the render kernels: "hbm" above is the
+                         # contract's roofline axis, not the limiter
+                         "limiter": ("VALU issue + latency (per (pixel, splat) pair work)"
+                                     if dom.startswith("render") else "hbm"),
+                         "valu_issue_frac": valu_frac},
+            "work": work,
             "stage_ms": {k: round(v, 4) for k, v in per_stage.items()},  # untimed breakdown pass
             "step_algorithmic_GBs": step_algorithmic_bytes(P, nr, W, H, K) / (ms_per_step * 1e-3) / 1e9,
         }
+        if multi is not None:
+            line["multi_gpu"] = multi
         if world == 1 and not args.no_cpu_baseline:
-            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-            line["cpu_baseline"] = cpu_baseline(args.config, P, W, H, threads)
+            line["cpu_baseline"] = cpu_baseline(args.config, P, W, H)
+            line["cpu_baseline_c"] = cpu_baseline_c(args.config, P, W, H, args.cpu_threads or min(16, os.cpu_count() or 1))
         else:
             line["cpu_baseline"] = None
         print(json.dumps(line), flush=True)

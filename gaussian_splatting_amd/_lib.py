@@ -81,6 +81,7 @@ SIGNATURES = {
     "gsr_profile_enable": (_i, [_i]),
     "gsr_profile_collect": (_i, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong), _i]),
     "gsr_profile_reset": (None, []),
+    "gsr_census_set": (_i, [ctypes.c_void_p]),
     "gsr_profile_stage_name": (ctypes.c_char_p, [_i]),
     "gsr_knn_mean_dist2": (_i, [_i, _vp, _vp, ALLOC_FN, _vp, _vp]),
     "gsr_fused_ssim_forward": (_i, [_i, _i, _i, _i, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
@@ -192,3 +193,25 @@ def profile_collect() -> dict:
     calls = (ctypes.c_longlong * n)()
     k = lib.gsr_profile_collect(ms, calls, n)
     return {lib.gsr_profile_stage_name(i).decode(): (ms[i], calls[i]) for i in range(k)}
+
+
+# ---- census (include/gsr.h "Census"): work counts of the render kernels ----------------------
+CENSUS_NAMES = ("fwd_entries_staged", "fwd_quadrant_evals", "fwd_pairs_alpha", "fwd_pairs_blended",
+                "bwd_entries_staged", "bwd_quadrant_evals", "bwd_pairs_grad", "bwd_entry_reductions")
+
+
+def census(fn, device=None) -> dict:
+    """Run ``fn()`` (forward / backward calls) with the census render kernels and return the counts
+    it added.  Diagnostic only: the census kernels are slower than the production ones."""
+    import torch
+
+    buf = torch.zeros(len(CENSUS_NAMES), dtype=torch.int64, device=device or "cuda")
+    lib = load()
+    torch.cuda.synchronize()
+    lib.gsr_census_set(ctypes.c_void_p(buf.data_ptr()))
+    try:
+        fn()
+        torch.cuda.synchronize()
+    finally:
+        lib.gsr_census_set(None)
+    return dict(zip(CENSUS_NAMES, (int(v) for v in buf.cpu().tolist())))

@@ -94,6 +94,7 @@ struct Profiler {
     }
 };
 Profiler g_prof;
+unsigned long long* g_census = nullptr;  // gsr_census_set: device counters of the census render kernels
 
 struct StageScope {
     int stage;
@@ -550,6 +551,11 @@ int gsr_densify_apply(int P, const void* scratch, const gsr_densify_group* group
     return GSR_OK;
 }
 
+int gsr_census_set(void* device_counters) {
+    g_census = reinterpret_cast<unsigned long long*>(device_counters);
+    return GSR_OK;
+}
+
 int gsr_profile_enable(int stage_mask) {
     std::lock_guard<std::mutex> lk(g_prof.mu);
     g_prof.mask = (unsigned)stage_mask;
@@ -753,6 +759,7 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
             ra.full_cap = (uint32_t)unit_full_cap(C);
             ra.tile_join = geom.tile_join;
             ra.seg_ck = bwd_segment_checkpoints();
+            ra.census = g_census;
             HIP_TRY(launch_render_fwd(ra, stream), "render_fwd");
         }
         return check_debug(debug, stream, "render_fwd");
@@ -897,6 +904,7 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
         ra.ckpt = bin.ckpt; ra.depth_key = geom.depth_key; ra.seg_ck = seg_ck;
         ra.unit_cnt = geom.unit_cnt; ra.unit_part = geom.unit_part; ra.unit_full = bin.unit_full;
         ra.full_cap = (uint32_t)unit_full_cap(C);
+        ra.census = g_census;
         HIP_TRY(launch_render_bwd(ra, max_units, stream), "render_bwd");
     }
     if (int rc = check_debug(debug, stream, "render_bwd")) return rc;

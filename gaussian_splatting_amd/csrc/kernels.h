@@ -47,6 +47,7 @@ struct RenderFwdArgs {
     uint32_t full_cap;     // unit_full_cap(binning capacity): stride of unit_full's shards
     unsigned long long* tile_join;  // GeomState::tile_join
     int seg_ck;
+    unsigned long long* census;     // diagnostic pair counts (gsr_census_set) or null
 };
 
 struct RenderBwdArgs {
@@ -68,6 +69,7 @@ struct RenderBwdArgs {
     const uint2* unit_full;
     uint32_t full_cap;
     int seg_ck;                         // checkpoints per backward segment (segment = seg_ck * kCkStride)
+    unsigned long long* census;         // diagnostic pair counts (gsr_census_set) or null
 };
 
 struct GaussBwdArgs {

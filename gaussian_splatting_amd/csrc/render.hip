@@ -93,7 +93,9 @@ __device__ __forceinline__ float splat_alpha(float p2, float opacity, float& G) 
 // that both halves stage the same entries.  Grid: groups of 8 consecutive tiles x NPART parts,
 // block b -> tile 8 (b / (8 NPART)) + b % 8, part (b / 8) % NPART: the parts of a tile sit on
 // the same XCD (blocks are dealt round-robin over the 8 XCDs) and share its L2.
-template <int NQ>
+// CENSUS (diagnostic instantiation, gsr_census_set): counts the work the blend does -- see
+// include/gsr.h "Census" for the counters -- with wave-uniform scalar counters, one atomic per wave.
+template <int NQ, bool CENSUS>
 __global__ void __launch_bounds__(64) GSR_FWD_OCCUPANCY render_fwd_kernel(RenderFwdArgs a) {
   {
     constexpr int NPART = 4 / NQ;
@@ -131,7 +133,9 @@ __global__ void __launch_bounds__(64) GSR_FWD_OCCUPANCY render_fwd_kernel(Render
 
     const uint2 range = a.ranges[tile];
     const int n = (int)(range.y - range.x);
+    unsigned long long c_staged = 0, c_eval = 0, c_alpha = 0, c_blend = 0;  // CENSUS only
     for (int b0 = 0; b0 < n && alive; b0 += kBatch) {
+        if (CENSUS) c_staged += (unsigned long long)min(kBatch, n - b0);
         uint32_t qm = 0;
         if (b0 + lane < n) {
             uint32_t* ent = a.gid_sorted + range.x + b0 + lane;  // Gaussian << 4 | quadrant mask
@@ -180,6 +184,11 @@ __global__ void __launch_bounds__(64) GSR_FWD_OCCUPANCY render_fwd_kernel(Render
                 float G;
                 const float alpha = splat_alpha(p2, xy.z, G);
                 const float w0 = alpha * Tl[k];  // > 0 iff this pixel blends the splat
+                if (CENSUS) {
+                    c_eval++;
+                    c_alpha += (unsigned long long)__popcll(__ballot(w0 > 0.f));
+                    c_blend += (unsigned long long)__popcll(__ballot(w0 > 0.f && Tl[k] * (1.f - alpha) >= 0.0001f));
+                }
                 if (!__any(w0 > 0.f)) continue;  // uniform
                 const float test_T = Tl[k] * (1.f - alpha);
                 const bool term = test_T < 0.0001f;  // live pixel: ends it, splat not added
@@ -200,6 +209,12 @@ __global__ void __launch_bounds__(64) GSR_FWD_OCCUPANCY render_fwd_kernel(Render
 #ifdef GSR_STAMPS
         if (threadIdx.x == 0 && part == 0) g_st_rfwd[(size_t)tile * kStampSlots + 3] = (unsigned long long)(b0 + kBatch);
 #endif
+    }
+    if (CENSUS && lane == 0) {
+        atomicAdd(&a.census[0], c_staged);
+        atomicAdd(&a.census[1], c_eval);
+        atomicAdd(&a.census[2], c_alpha);
+        atomicAdd(&a.census[3], c_blend);
     }
     if (part == 0) {
         GSR_STAMP(g_st_rfwd, tile, 1);
@@ -279,14 +294,17 @@ hipError_t launch_render_fwd(const RenderFwdArgs& a, hipStream_t stream) {
     const uint32_t tiles = a.gx * a.gy;
     if (tiles == 0) return hipSuccess;
     const uint32_t groups = (tiles + 7) / 8;
-    if (fwd_quads_per_wave() == 4)
-        hipLaunchKernelGGL(render_fwd_kernel<4>, dim3(groups * 8), dim3(kWave), 0, stream, a);
+    if (a.census)
+        hipLaunchKernelGGL((render_fwd_kernel<2, true>), dim3(groups * 16), dim3(kWave), 0, stream, a);
+    else if (fwd_quads_per_wave() == 4)
+        hipLaunchKernelGGL((render_fwd_kernel<4, false>), dim3(groups * 8), dim3(kWave), 0, stream, a);
     else
-        hipLaunchKernelGGL(render_fwd_kernel<2>, dim3(groups * 16), dim3(kWave), 0, stream, a);
+        hipLaunchKernelGGL((render_fwd_kernel<2, false>), dim3(groups * 16), dim3(kWave), 0, stream, a);
     return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
+template <bool CENSUS>
 __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(RenderBwdArgs a) {
   {
     // One wave per unit = (tile, segment): the entries [start, end) of the tile's list, start a
@@ -384,8 +402,10 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
         a.img.lim_key[tile] = ((unsigned long long)a.depth_key[gl] << 32) | gl;
     }
     const uint32_t ttx = tile % a.gx, tty = tile / a.gx;
+    unsigned long long c_staged = 0, c_eval = 0, c_alpha = 0, c_red = 0;  // CENSUS only
     for (int b0 = start; b0 < end; b0 += kBatch) {
         const bool has = b0 + lane < end;
+        if (CENSUS) c_staged += (unsigned long long)min(kBatch, end - b0);
         uint32_t qm = 0, e = 0;
         float ca = 0.f, cb = 0.f, cc = 0.f, o = 0.f;  // this lane's entry: raw conic and opacity, for the flush
         if (has) {
@@ -432,6 +452,10 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
                 float G;
                 float alpha = splat_alpha(p2, xy.z, G);
                 alpha = pos < nc[q] ? alpha : 0.f;  // the forward stopped this pixel before `pos`
+                if (CENSUS) {
+                    c_eval++;
+                    c_alpha += (unsigned long long)__popcll(__ballot(alpha > 0.f));
+                }
                 if (!__any(alpha > 0.f)) continue;  // uniform
                 contrib = true;
                 const float w = alpha * T[q];
@@ -469,6 +493,7 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
                     if (slot_k < 2) acc[8 + slot_k] = w2;
                 }
                 written |= 1ull << j;
+                if (CENSUS) c_red++;
             }
         }
         __syncthreads();
@@ -493,6 +518,12 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
         }
         __syncthreads();
     }
+    if (CENSUS && lane == 0) {
+        atomicAdd(&a.census[4], c_staged);
+        atomicAdd(&a.census[5], c_eval);
+        atomicAdd(&a.census[6], c_alpha);
+        atomicAdd(&a.census[7], c_red);
+    }
     GSR_STAMP(g_st_rbwd, blockIdx.x, 1);
     GSR_STAMP_RT(g_st_rbwd, blockIdx.x, 5);
     GSR_STAMP_VAL(g_st_rbwd, blockIdx.x, 2, tile);
@@ -504,7 +535,10 @@ size_t bwd_max_units(size_t R, uint32_t tiles, int seg_ck) { return R / ((size_t
 
 hipError_t launch_render_bwd(const RenderBwdArgs& a, size_t max_units, hipStream_t stream) {
     if (max_units == 0) return hipSuccess;
-    hipLaunchKernelGGL(render_bwd_kernel, dim3((uint32_t)max_units), dim3(kWave), 0, stream, a);
+    if (a.census)
+        hipLaunchKernelGGL(render_bwd_kernel<true>, dim3((uint32_t)max_units), dim3(kWave), 0, stream, a);
+    else
+        hipLaunchKernelGGL(render_bwd_kernel<false>, dim3((uint32_t)max_units), dim3(kWave), 0, stream, a);
     return hipGetLastError();
 }
 

@@ -238,6 +238,20 @@ int gsr_profile_collect(double* total_ms, long long* calls, int max_stages);
 void gsr_profile_reset(void);
 const char* gsr_profile_stage_name(int stage);
 
+/* Census (diagnostic; no reference counterpart): with a device buffer of 8 zeroed uint64
+ * counters set, the render kernels of later forward / backward calls run their census
+ * instantiations (slower: a few extra wave-uniform ops per evaluation) and add, per call:
+ *   [0] forward list entries staged (per half-tile wave; each tile's two halves both stage)
+ *   [1] forward (entry, 8x8 quadrant) evaluations  (64 pixel evaluations each)
+ *   [2] forward (pixel, entry) pairs with alpha > 0 reaching a live pixel
+ *   [3] forward (pixel, entry) pairs blended (alpha > 0 and the pixel does not end there)
+ *   [4] backward list entries staged
+ *   [5] backward (entry, quadrant) evaluations
+ *   [6] backward (pixel, entry) pairs with a gradient term (alpha > 0, before n_contrib)
+ *   [7] backward per-entry wave reductions (gradient records with content)
+ * NULL turns the census off.  Not thread-safe against concurrent calls. */
+int gsr_census_set(void* device_counters);
+
 #ifdef __cplusplus
 }
 #endif

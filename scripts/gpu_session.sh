@@ -36,14 +36,32 @@ for stage in "$@"; do
         GSR_LIBRARY=$ROOT/$lib timeout -k 10 300 python bench.py --no-cpu-baseline --steps 30 > "$OUT/bench_$v.json" 2> "$OUT/bench_$v.err"; rc=$?
         echo "variant $v rc=$rc"; python -c "import json,sys; d=json.load(open('$OUT/bench_$v.json')); print(' ', d['ms_per_step'], d['stage_ms'])"; [ $rc -eq 0 ] || exit $rc
       done ;;
+    cfg:*)  # bench + kernel stats of one config: cfg:<config>
+      c=${stage#cfg:}
+      timeout -k 10 600 python bench.py --config $c --no-cpu-baseline > "$OUT/bench_$c.json" 2> "$OUT/bench_$c.err"; rc=$?
+      echo "bench $c rc=$rc"; cat "$OUT/bench_$c.json"; [ $rc -eq 0 ] || exit $rc
+      (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$c" -o run -- \
+        python3 "$ROOT/bench.py" --config $c --steps 5 --warmup 2 --no-cpu-baseline --no-census > "$OUT/prof_$c.log" 2>&1); rc=$?
+      echo "prof $c rc=$rc"; [ $rc -eq 0 ] || exit $rc ;;
+    pmccfg:*)  # PMC passes of one config: pmccfg:<config>
+      c=${stage#pmccfg:}
+      bash scripts/pmc_session.sh "$TAG/pmc_$c" scripts/pmc_all.txt $c; rc=$?
+      echo "pmc $c rc=$rc"; [ $rc -eq 0 ] || exit $rc ;;
+    rehearse2)  # N=2 on one GPU (gloo collectives): the multi-rank bench path, both exchanges
+      for ex in views allreduce; do
+        GSR_BENCH_SHARE_GPU=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+          --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 2 --exchange $ex \
+          > "$OUT/rehearse2_$ex.json" 2> "$OUT/rehearse2_$ex.err"; rc=$?
+        echo "rehearse2 $ex rc=$rc"; cat "$OUT/rehearse2_$ex.json"; [ $rc -eq 0 ] || exit $rc
+      done ;;
     prof)
       (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
-        python3 "$ROOT/bench.py" --steps 10 --warmup 2 --no-cpu-baseline > "$OUT/prof.log" 2>&1); rc=$?
+        python3 "$ROOT/bench.py" --steps 10 --warmup 2 --no-cpu-baseline --no-census > "$OUT/prof.log" 2>&1); rc=$?
       echo "prof rc=$rc"; tail -3 "$OUT/prof.log"; [ $rc -eq 0 ] || exit $rc ;;
     pmc)
       for ctr in "FETCH_SIZE" "WRITE_SIZE"; do
         (cd /tmp && timeout -k 10 600 rocprofv3 --pmc $ctr --output-format csv -d "$OUT/pmc_$ctr" -o run -- \
-          python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/pmc_$ctr.log" 2>&1); rc=$?
+          python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-census > "$OUT/pmc_$ctr.log" 2>&1); rc=$?
         echo "pmc $ctr rc=$rc"; tail -2 "$OUT/pmc_$ctr.log"; [ $rc -eq 0 ] || exit $rc
       done ;;
   esac

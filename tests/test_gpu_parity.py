@@ -316,3 +316,39 @@ def test_capacity_forward_matches_sync_forward(hint, monkeypatch):
     assert got[0] == ref[0]
     for a, b in zip(got[1:], ref[1:]):
         np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("name", ["sh3_scalerot", "dense_opaque", "lists_1k_2k"])
+def test_census_counts_pairs(name):
+    """The census render kernels (include/gsr.h "Census") count the (pixel, entry) pairs the blend
+    performs: blended pairs in the forward equal the pure-PyTorch fallback's count of kept pairs,
+    and the backward's pairs with a gradient term are exactly those pairs; the census kernels'
+    outputs are bitwise those of the production kernels."""
+    from gaussian_splatting_amd import _lib
+    from oracle import torch_fallback as tf
+
+    case = next(c for c in C.SMALL_CASES if c.name == name)
+    inp = C.build(case)
+    gc, gd = C.unit_grads(case.H, case.W)
+    fwd = C.run_gpu_forward(inp)
+    out = C.run_gpu_backward(inp, fwd, gc, gd)
+    box = {}
+
+    def run():
+        box["fwd"] = C.run_gpu_forward(inp)
+        box["out"] = C.run_gpu_backward(inp, box["fwd"], gc, gd)
+    cz = _lib.census(run)
+    fb = tf.rasterize(inp["means3D"], inp["opacities"], inp["viewmatrix"], inp["projmatrix"], inp["campos"],
+                      inp["tanfovx"], inp["tanfovy"], inp["H"], inp["W"], bg=inp["bg"], shs=inp["shs"],
+                      sh_degree=inp["sh_degree"], colors_precomp=inp["colors_precomp"], scales=inp["scales"],
+                      rotations=inp["rotations"], cov3D_precomp=inp["cov3D_precomp"],
+                      scale_modifier=inp["scale_modifier"], antialiasing=inp["antialiasing"])
+    assert cz["fwd_pairs_blended"] > 0
+    assert cz["fwd_pairs_blended"] == fb["pairs_blended"], (cz, fb["pairs_blended"])
+    assert cz["bwd_pairs_grad"] == cz["fwd_pairs_blended"], cz
+    assert cz["fwd_pairs_alpha"] >= cz["fwd_pairs_blended"]
+    assert cz["fwd_quadrant_evals"] * 64 >= cz["fwd_pairs_alpha"]
+    assert cz["bwd_entry_reductions"] <= cz["bwd_entries_staged"] <= fwd[0]
+    assert torch.equal(box["fwd"][1], fwd[1])
+    for a, b in zip(box["out"], out):
+        assert torch.equal(a, b)
