@@ -42,6 +42,11 @@ namespace gsr {
 
 constexpr int kBatch = 64;  // list entries staged per round (one per lane)
 
+// A/B switch: skip a backward quadrant whose pixels all have alpha = 0.
+#ifndef GSR_BWD_ANYSKIP
+#define GSR_BWD_ANYSKIP 1
+#endif
+
 GSR_STAMP_BUFFER(g_st_rfwd);
 GSR_STAMP_BUFFER(g_st_rbwd);
 
@@ -312,19 +317,23 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
     // dispatcher deals equal-sized pieces of work round-robin over the SIMDs and the short ones
     // fill the slots that free up last -- no tile's full list ever sits on one SIMD.
     uint2 unit;
-    {  // full segments first, then the partial ones, longest quarter first; shards in order
-        uint32_t i = blockIdx.x;
-        int l = 0;
-        for (; l < kUnitLists * kUnitShards; l++) {
-            const uint32_t c = uniform_u32(a.unit_cnt[l * kUnitCntStride]);
-            if (i < c) break;
-            i -= c;
-        }
-        if (l == kUnitLists * kUnitShards) return;  // past the list (the grid is sized for the worst case)
+    {  // full segments first, then the partial ones, longest quarter first; shards in order.
+        // All 40 list counters in one vector load, an inclusive DPP scan, and a ballot find the
+        // list holding this block's unit (a chain of dependent scalar loads before, r2).
+        static_assert(kUnitLists * kUnitShards <= kWave, "one lane per list counter");
+        constexpr int nl = kUnitLists * kUnitShards;
+        const int lane = threadIdx.x;
+        const uint32_t c = lane < nl ? a.unit_cnt[lane * kUnitCntStride] : 0u;
+        const uint32_t incl = wave_incl_sum(c);
+        const uint32_t i = blockIdx.x;
+        const int l = __popcll(__ballot(lane < nl && incl <= i));  // lists wholly before unit i
+        if (l >= nl) return;  // past the lists (the grid is sized for the worst case)
+        const uint32_t before = l ? (uint32_t)__builtin_amdgcn_readlane((int)incl, l - 1) : 0u;
+        const uint32_t k = i - before;
         if (l < kUnitShards)
-            unit = a.unit_full[(size_t)l * a.full_cap + i];
+            unit = a.unit_full[(size_t)l * a.full_cap + k];
         else
-            unit = a.unit_part[(size_t)(l - kUnitShards) * unit_part_cap(a.gx * a.gy) + i];
+            unit = a.unit_part[(size_t)(l - kUnitShards) * unit_part_cap(a.gx * a.gy) + k];
     }
     const uint32_t tile = unit.x;
     const int start = (int)unit.y * kCkStride;
@@ -346,33 +355,47 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
                                 : nullptr;
     float T[4], gB[4], g0[4], g1[4], g2[4], gi[4];
     int nc[4];
+    // Every slot's pixel state is loaded with no branch in between (an outside pixel reads a
+    // clamped, valid address and is zeroed afterwards), so all the loads are in flight at once.
+    float c0[4], c1[4], c2[4], cd[4], fT[4], k0[4], k1[4], k2[4], k3[4], k4[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int px = min(tile_x0 + (q & 1) * 8 + lx, a.W - 1), py = min(tile_y0 + (q >> 1) * 8 + ly, a.H - 1);
+        const size_t pix = (size_t)py * a.W + px;
+        nc[q] = (int)a.img.n_contrib[pix];
+        g0[q] = a.dL_dpix[pix];
+        g1[q] = a.dL_dpix[N + pix];
+        g2[q] = a.dL_dpix[2 * N + pix];
+        gi[q] = a.dL_dinvdepth ? a.dL_dinvdepth[pix] : 0.f;
+        c0[q] = a.img.accum[pix];
+        c1[q] = a.img.accum[N + pix];
+        c2[q] = a.img.accum[2 * N + pix];
+        cd[q] = a.img.accum[3 * N + pix];
+        fT[q] = a.img.final_T[pix];
+        // blend state at `start`: the forward's checkpoint (gsr_common.h), or the empty state
+        const float* ck = a.ckpt + (size_t)((range.x + (uint32_t)start) / kCkStride) * kCkFloats + lane;
+        const bool has_ck = start > 0;
+        k0[q] = has_ck ? ck[(0 * 4 + q) * 64] : 1.f;
+        k1[q] = has_ck ? ck[(1 * 4 + q) * 64] : 0.f;
+        k2[q] = has_ck ? ck[(2 * 4 + q) * 64] : 0.f;
+        k3[q] = has_ck ? ck[(3 * 4 + q) * 64] : 0.f;
+        k4[q] = has_ck ? ck[(4 * 4 + q) * 64] : 0.f;
+    }
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         const int px = tile_x0 + (q & 1) * 8 + lx, py = tile_y0 + (q >> 1) * 8 + ly;
-        T[q] = 1.f;
-        nc[q] = 0;
-        gB[q] = g0[q] = g1[q] = g2[q] = gi[q] = 0.f;
-        if (px < a.W && py < a.H) {
-            const size_t pix = (size_t)py * a.W + px;
-            nc[q] = (int)a.img.n_contrib[pix];
-            g0[q] = a.dL_dpix[pix];
-            g1[q] = a.dL_dpix[N + pix];
-            g2[q] = a.dL_dpix[2 * N + pix];
-            if (a.dL_dinvdepth) gi[q] = a.dL_dinvdepth[pix];
-            // dL/dpix . (what the forward accumulated from `start` on) + the background term of
-            // dL/dalpha (CR/backward.cu:587-590); shrinks to "behind this entry" as the walk proceeds
-            float c0 = a.img.accum[pix], c1 = a.img.accum[N + pix], c2 = a.img.accum[2 * N + pix],
-                  cd = a.img.accum[3 * N + pix];
-            if (ck) {
-                T[q] = ck[(0 * 4 + q) * 64];
-                c0 -= ck[(1 * 4 + q) * 64];
-                c1 -= ck[(2 * 4 + q) * 64];
-                c2 -= ck[(3 * 4 + q) * 64];
-                cd -= ck[(4 * 4 + q) * 64];
-            }
-            gB[q] = g0[q] * c0 + g1[q] * c1 + g2[q] * c2 + gi[q] * cd +
-                    a.img.final_T[pix] * (a.bg[0] * g0[q] + a.bg[1] * g1[q] + a.bg[2] * g2[q]);
-        }
+        const bool in = px < a.W && py < a.H;
+        nc[q] = in ? nc[q] : 0;
+        g0[q] = in ? g0[q] : 0.f;
+        g1[q] = in ? g1[q] : 0.f;
+        g2[q] = in ? g2[q] : 0.f;
+        gi[q] = in ? gi[q] : 0.f;
+        T[q] = k0[q];
+        // dL/dpix . (what the forward accumulated from `start` on) + the background term of
+        // dL/dalpha (CR/backward.cu:587-590); shrinks to "behind this entry" as the walk proceeds
+        gB[q] = in ? g0[q] * (c0[q] - k1[q]) + g1[q] * (c1[q] - k2[q]) + g2[q] * (c2[q] - k3[q]) +
+                         gi[q] * (cd[q] - k4[q]) + fT[q] * (a.bg[0] * g0[q] + a.bg[1] * g1[q] + a.bg[2] * g2[q])
+                   : 0.f;
     }
     // Per-slot limits: entries at positions >= slim[q] reach no pixel of slot q (the forward
     // stopped all of them earlier), so the slot is skipped from there on.
@@ -456,7 +479,9 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
                     c_eval++;
                     c_alpha += (unsigned long long)__popcll(__ballot(alpha > 0.f));
                 }
+#if GSR_BWD_ANYSKIP
                 if (!__any(alpha > 0.f)) continue;  // uniform
+#endif
                 contrib = true;
                 const float w = alpha * T[q];
                 const float sdot = g0[q] * col.x + g1[q] * col.y + g2[q] * col.z + gi[q] * xy.w;
