@@ -370,4 +370,25 @@ __device__ __forceinline__ float row_fold(float x, float y) {
     return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
+// eight_fold(x, y, hi8) with hi8 = (lane & 8): on every 16-lane row, lanes 0-7 get x[l] + x[l+8]
+// and lanes 8-15 get y[l-8] + y[l] (DPP row_ror:8; gfx950 has no 8-lane swap instruction).
+__device__ __forceinline__ float eight_fold(float x, float y, bool hi8) {
+    const float a = hi8 ? y : x, b = hi8 ? x : y;
+    return a + dpp_f32<0x128, 0xf, true>(b);
+}
+// Sum over each 8-lane half row, in every lane of it: quad_perm [1,0,3,2], [2,3,0,1], then
+// row_half_mirror (no lane shifted out, so every step folds into one v_add_f32_dpp).
+__device__ __forceinline__ float half_row_allsum(float v) {
+    v += dpp_f32<0xB1, 0xf, true>(v);
+    v += dpp_f32<0x4E, 0xf, true>(v);
+    v += dpp_f32<0x141, 0xf, true>(v);
+    return v;
+}
+// Sum over each 16-lane row, in every lane of it (half_row_allsum, then row_mirror).
+__device__ __forceinline__ float row_allsum(float v) {
+    v = half_row_allsum(v);
+    v += dpp_f32<0x140, 0xf, true>(v);
+    return v;
+}
+
 }  // namespace gsr

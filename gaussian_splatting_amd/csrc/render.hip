@@ -46,6 +46,11 @@ constexpr int kBatch = 64;  // list entries staged per round (one per lane)
 #ifndef GSR_BWD_ANYSKIP
 #define GSR_BWD_ANYSKIP 1
 #endif
+// A/B switch: the backward's ten per-entry sums carried across entries (zeroed after each
+// reduction) instead of declared per entry.
+#ifndef GSR_BWD_CARRY_R
+#define GSR_BWD_CARRY_R 0
+#endif
 
 GSR_STAMP_BUFFER(g_st_rfwd);
 GSR_STAMP_BUFFER(g_st_rbwd);
@@ -74,9 +79,9 @@ __device__ __forceinline__ float4 stage_conic(float4 v0, float4 v1, uint32_t qm)
 // one value: the exponent is forced to -inf when positive so alpha becomes 0, and alpha below
 // 1/255 is zeroed.  Returns alpha for a contributing pixel, 0 otherwise; G = exp(power).
 __device__ __forceinline__ float splat_alpha(float p2, float opacity, float& G) {
-    G = __builtin_amdgcn_exp2f(p2 > 0.f ? -INFINITY : p2);  // raw v_exp_f32: tiny results are zeroed below
+    G = __builtin_amdgcn_exp2f(p2);  // raw v_exp_f32 (+inf for a large positive p2: masked below)
     const float alpha = fminf(0.99f, opacity * G);
-    return alpha >= 1.0f / 255.0f ? alpha : 0.f;
+    return (p2 <= 0.f) & (alpha >= 1.0f / 255.0f) ? alpha : 0.f;  // one mask, one select
 }
 
 // ---------------------------------------------------------------------------
@@ -206,8 +211,9 @@ __global__ void __launch_bounds__(64) GSR_FWD_OCCUPANCY render_fwd_kernel(Render
                 D[k] += xy.w * w;
                 last[k] = blended ? pos1 : last[k];
                 Tc[k] = blended ? test_T : Tc[k];  // T after the last contributor = final_T
-                // a slot can only die where one of its pixels terminated just now (mask logic, SALU)
-                if (__any(term && w0 > 0.f) && !__any(Tl[k] > 0.f)) alive &= ~(1u << k);
+                // the slot dies when its last live pixel terminated just now (one compare; guarding
+                // it with "some pixel terminated here" cost two VALU to materialise the guard)
+                if (!__any(Tl[k] > 0.f)) alive &= ~(1u << k);
             }
         }
         __syncthreads();
@@ -343,7 +349,7 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
     const float pxf0 = (float)(tile_x0 + lx), pyf0 = (float)(tile_y0 + ly);  // this lane's pixel in quadrant 0
 
     __shared__ float4 s_xy[kBatch], s_cq[kBatch], s_col[kBatch];  // as in the forward
-    __shared__ float4 s_acc[kBatch][3];                           // per entry: the 10 reduced sums (+2 pad)
+    __shared__ float4 s_acc[kBatch][3];                           // per entry: the 10 reduced sums (r8, r9 in 2 parts)
     GSR_STAMP(g_st_rbwd, blockIdx.x, 0);
     GSR_STAMP_HWID(g_st_rbwd, blockIdx.x);
     GSR_STAMP_RT(g_st_rbwd, blockIdx.x, 4);
@@ -414,8 +420,11 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
             live |= 1u << q;
             next_lim = min(next_lim, slim[q]);
         }
-    // where this lane's row of the reduce-scatter lands in s_acc (see below)
-    const int row = lane >> 4, slot_k = ((row & 1) << 1) | (row >> 1);
+    // where this lane's part of the reduce-scatter lands in s_acc (see below): in each 16-lane
+    // row, lane 0 holds a sum of w0, lane 8 one of w1, lane 15 a row partial of r8 / r9
+    const int row = lane >> 4, slot_k = ((row & 1) << 1) | (row >> 1), li = lane & 15;
+    const bool hi8 = (lane & 8) != 0, acc_wr = li == 0 || li == 8 || li == 15, acc_h4 = li == 15;
+    const int acc_off = li == 0 ? slot_k : li == 8 ? 4 + slot_k : 8 + row;
 
     if (start == 0 && lane == 0) {
         // the key of the entry at limit - 1 (tiles with limit 0 get 0 from bwd_units_kernel): entries
@@ -426,6 +435,11 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
     }
     const uint32_t ttx = tile % a.gx, tty = tile / a.gx;
     unsigned long long c_staged = 0, c_eval = 0, c_alpha = 0, c_red = 0;  // CENSUS only
+    // The ten per-entry sums stay zero between entries (reset after each reduction), so an entry
+    // whose first quadrants are inactive does not materialise zeros (10 VALU) before accumulating.
+#if GSR_BWD_CARRY_R
+    float r0 = 0.f, r1 = 0.f, r2 = 0.f, r3 = 0.f, r4 = 0.f, r5 = 0.f, r6 = 0.f, r7 = 0.f, r8 = 0.f, r9 = 0.f;
+#endif
     for (int b0 = start; b0 < end; b0 += kBatch) {
         const bool has = b0 + lane < end;
         if (CENSUS) c_staged += (unsigned long long)min(kBatch, end - b0);
@@ -465,22 +479,27 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
             }
             const uint32_t m = uniform_u32(__float_as_uint(cq.w)) & live;
             if (m == 0) continue;
+#if !GSR_BWD_CARRY_R
             float r0 = 0.f, r1 = 0.f, r2 = 0.f, r3 = 0.f, r4 = 0.f, r5 = 0.f, r6 = 0.f, r7 = 0.f, r8 = 0.f, r9 = 0.f;
+#endif
             bool contrib = false;
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 if (!(m & (1u << q))) continue;  // uniform
                 const float dx = xy.x - (pxf0 + (float)((q & 1) * 8)), dy = xy.y - (pyf0 + (float)((q >> 1) * 8));
                 const float p2 = dx * (cq.x * dx + cq.y * dy) + cq.z * dy * dy;
-                float G;
-                float alpha = splat_alpha(p2, xy.z, G);
-                alpha = pos < nc[q] ? alpha : 0.f;  // the forward stopped this pixel before `pos`
+                // the skip tests and "the forward stopped this pixel before `pos`" as ONE mask,
+                // shared by alpha and u below (no separate alpha > 0 test)
+                const float G = __builtin_amdgcn_exp2f(p2);
+                const float ac = fminf(0.99f, xy.z * G);
+                const bool on = (p2 <= 0.f) & (ac >= 1.0f / 255.0f) & (pos < nc[q]);
+                const float alpha = on ? ac : 0.f;
                 if (CENSUS) {
                     c_eval++;
                     c_alpha += (unsigned long long)__popcll(__ballot(alpha > 0.f));
                 }
 #if GSR_BWD_ANYSKIP
-                if (!__any(alpha > 0.f)) continue;  // uniform
+                if (!__any(on)) continue;  // uniform
 #endif
                 contrib = true;
                 const float w = alpha * T[q];
@@ -488,7 +507,7 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
                 gB[q] -= w * sdot;  // now dL/dpix . (colour strictly behind this entry) + background term
                 const float one_m_a = 1.f - alpha;
                 const float dLda = T[q] * sdot - gB[q] * __builtin_amdgcn_rcpf(one_m_a);
-                const float u = alpha > 0.f ? dLda * G : 0.f;
+                const float u = on ? dLda * G : 0.f;
                 r0 += w * g0[q];
                 r1 += w * g1[q];
                 r2 += w * g2[q];
@@ -504,19 +523,18 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
             }
             if (contrib) {  // uniform
                 // Reduce-scatter over the wave: two lane-swap halvings take the ten sums from
-                // 64 lanes to 16 (packing four sums per register), then one 16-lane row sum.
+                // 64 lanes to 16 (four sums per register), a DPP 8-lane fold packs w0 and w1 into
+                // one register, and three DPP steps finish each 8-lane half (24 VALU; r8 / r9
+                // leave as two row partials each, added by the flush).
                 const float h0 = half_fold(r0, r1), h1 = half_fold(r2, r3), h2 = half_fold(r4, r5),
                             h3 = half_fold(r6, r7), h4 = half_fold(r8, r9);
-                // rows of w0: r0 r2 r1 r3; w1: r4 r6 r5 r7; w2: r8 r8 r9 r9
-                const float w0 = row_sum_to_lane15(row_fold(h0, h1));
-                const float w1 = row_sum_to_lane15(row_fold(h2, h3));
-                const float w2 = row_sum_to_lane15(row_fold(h4, h4));
-                if ((lane & 15) == 15) {
-                    float* acc = reinterpret_cast<float*>(&s_acc[j][0]);
-                    acc[slot_k] = w0;
-                    acc[4 + slot_k] = w1;
-                    if (slot_k < 2) acc[8 + slot_k] = w2;
-                }
+                // rows of w0: r0 r2 r1 r3; w1: r4 r6 r5 r7; h4: r8 r8 r9 r9
+                const float f = half_row_allsum(eight_fold(row_fold(h0, h1), row_fold(h2, h3), hi8));
+                const float g4 = row_allsum(h4);
+                if (acc_wr) reinterpret_cast<float*>(&s_acc[j][0])[acc_off] = acc_h4 ? g4 : f;
+#if GSR_BWD_CARRY_R
+                r0 = r1 = r2 = r3 = r4 = r5 = r6 = r7 = r8 = r9 = 0.f;
+#endif
                 written |= 1ull << j;
                 if (CENSUS) c_red++;
             }
@@ -528,11 +546,13 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
             if ((written >> lane) & 1ull) {
                 const float4 A = s_acc[lane][0], B = s_acc[lane][1], Cc = s_acc[lane][2];
                 // dL/dmean2D in NDC units (x 0.5 W, 0.5 H, CR/backward.cu:509-510,600-601);
-                // dL/dconic with the reference's -0.5 factors (CR/backward.cu:604-606)
+                // dL/dconic with the reference's -0.5 factors (CR/backward.cu:604-606).  (Applying
+                // these linear maps per Gaussian in gauss_reduce instead measured +10 us in all, r2o.)
                 ra = A;
+                const float s8 = Cc.x + Cc.y, s9 = Cc.z + Cc.w;  // r8, r9 from their row partials
                 rb = make_float4(-0.5f * (float)a.W * o * (ca * B.x + cb * B.y),
-                                 -0.5f * (float)a.H * o * (cc * B.y + cb * B.x), Cc.y, -0.5f * o * B.w);
-                rc = make_float2(-0.5f * o * B.z, -0.5f * o * Cc.x);
+                                 -0.5f * (float)a.H * o * (cc * B.y + cb * B.x), s9, -0.5f * o * B.w);
+                rc = make_float2(-0.5f * o * B.z, -0.5f * o * s8);
             }
             a.recs.a[(size_t)kRecAB * e] = ra;
             a.recs.b[(size_t)kRecAB * e] = rb;
