@@ -507,8 +507,15 @@ __device__ __forceinline__ void view_backward(const ViewCam& c, const GaussIn& g
 // With GSR_GB_HALVES the SH rows go through LDS 32 at a time at the end of the kernel
 // (lanes 0-31, then 32-63): 6.6 KiB of LDS per wave instead of 13, twice the waves per CU.
 constexpr int kGbShRows = GSR_GB_HALVES ? 32 : 64;
+// Occupancy target (A/B: GSR_GB_WAVES).  Unconstrained, the body takes 134 VGPRs: 3 waves per
+// SIMD, too few loads in flight for an HBM-bound kernel.
+#ifdef GSR_GB_WAVES
+#define GSR_GB_OCCUPANCY __attribute__((amdgpu_waves_per_eu(GSR_GB_WAVES, GSR_GB_WAVES)))
+#else
+#define GSR_GB_OCCUPANCY
+#endif
 template <int SH_MODE>
-__global__ void __launch_bounds__(64) gauss_bwd_kernel(GaussBwdArgs a) {
+__global__ void __launch_bounds__(64) GSR_GB_OCCUPANCY gauss_bwd_kernel(GaussBwdArgs a) {
     __shared__ __attribute__((aligned(16))) float s_sh[SH_MODE != kShGlobal ? kGbShRows * kShStride : 4];
     const int lane = threadIdx.x;
     const int g0 = blockIdx.x * 64;
@@ -529,7 +536,22 @@ __global__ void __launch_bounds__(64) gauss_bwd_kernel(GaussBwdArgs a) {
     float3 sh_v = make_float3(0.f, 0.f, 0.f), sh_g = sh_v, dmean_late = sh_v;
 
     const bool valid = idx < a.P;
-    const bool visible = valid && a.radii[idx] > 0;
+    // The summed render gradients decide everything below: a Gaussian whose ten sums are all
+    // zero -- culled, or visible but behind saturated pixels everywhere (about 86% of a 1M@1080p
+    // frame) -- has all-zero parameter gradients, so it only writes zeros: none of its geometry
+    // and none of its 192-byte SH row is read.
+    float4 sa = make_float4(0.f, 0.f, 0.f, 0.f), sb = sa;
+    float2 sc = make_float2(0.f, 0.f);
+    int rad = 0;
+    if (valid) {
+        rad = a.radii[idx];
+        sa = a.sums.a[idx];
+        sb = a.sums.b[idx];
+        sc = a.sums.c[idx];
+    }
+    const bool any_grad = (sa.x != 0.f) | (sa.y != 0.f) | (sa.z != 0.f) | (sa.w != 0.f) | (sb.x != 0.f) |
+                          (sb.y != 0.f) | (sb.z != 0.f) | (sb.w != 0.f) | (sc.x != 0.f) | (sc.y != 0.f);
+    const bool visible = valid && rad > 0 && any_grad;
     if (valid && !visible) {
         store3(a.dL_dmean2D, idx, 0.f, 0.f, 0.f);
         if (a.dL_dconic) reinterpret_cast<float4*>(a.dL_dconic)[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -553,10 +575,7 @@ __global__ void __launch_bounds__(64) gauss_bwd_kernel(GaussBwdArgs a) {
         }
     }
     if (visible) {
-        // ---- summed render gradients of this Gaussian
-        const uint32_t r = (uint32_t)idx;  // sums are per Gaussian
-        const float4 sa = a.sums.a[r], sb = a.sums.b[r];
-        const float2 sc = a.sums.c[r];
+        // ---- summed render gradients of this Gaussian (loaded above)
         const float3 dcol = make_float3(sa.x, sa.y, sa.z);
         const float dinvd = sa.w;
         const float m2x = sb.x, m2y = sb.y;
@@ -769,11 +788,12 @@ __global__ void __launch_bounds__(64) gauss_bwd_kernel(GaussBwdArgs a) {
     if constexpr (kShLate) {
         // SH backward, half a wave at a time through LDS: coalesced stage-in of 32 rows,
         // their lanes evaluate it in place, coalesced write-back of the 32 dL/dSH rows
+        const unsigned long long need = __ballot(sh_late);  // rows whose SH is read at all
         for (int half = 0; half < 2; half++) {
             const int rows = min(kGbShRows, nvalid - half * kGbShRows);
             if (rows <= 0) break;  // wave-uniform
             sh_stage_in<kGbShRows, 64, SH_MODE == kShLdsSplit>(sh_src, g0 + half * kGbShRows, rows, s_sh, kShStride,
-                                                              lane);
+                                                              lane, need >> (half * kGbShRows));
             __syncthreads();
             if ((lane >> 5) == half && idx < a.P) {
                 float* row = &s_sh[(lane & 31) * kShStride];

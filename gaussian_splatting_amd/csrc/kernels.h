@@ -115,17 +115,18 @@ constexpr int kShRowF = 48;     // floats per staged SH row (M = 16)
 constexpr int kShRestF = 45;    // floats per rest row in the split layout
 
 template <int ROWS, int THREADS, bool SPLIT>
-__device__ __forceinline__ void sh_stage_in(const ShAddr& sa, int r0, int rows, float* lds, int stride, int tid) {
+// rowmask: bit r set = stage row r (rows left out are not read; their LDS contents are undefined).
+__device__ __forceinline__ void sh_stage_in(const ShAddr& sa, int r0, int rows, float* lds, int stride, int tid,
+                                            unsigned long long rowmask = ~0ull) {
     if constexpr (!SPLIT) {
         const float4* src = reinterpret_cast<const float4*>(sa.shs + (size_t)r0 * kShRowF);
         const int n4 = rows * (kShRowF / 4);
 #pragma unroll
         for (int k = 0; k < ROWS * kShRowF / 4 / THREADS; k++) {
             const int i4 = k * THREADS + tid;
-            if (i4 < n4) {
-                const int d = i4 * 4, row = d / kShRowF, col = d - row * kShRowF;
+            const int d = i4 * 4, row = d / kShRowF, col = d - row * kShRowF;
+            if (i4 < n4 && ((rowmask >> row) & 1ull))
                 *reinterpret_cast<float4*>(&lds[row * stride + col]) = src[i4];
-            }
         }
         return;
     } else {
@@ -134,7 +135,9 @@ __device__ __forceinline__ void sh_stage_in(const ShAddr& sa, int r0, int rows, 
 #pragma unroll
     for (int k = 0; k < (ROWS * kShRestF / 4 + THREADS - 1) / THREADS; k++) {
         const int i4 = k * THREADS + tid;
-        if (i4 < n4) {
+        // a 16-byte piece may straddle two rows (45-float rows): read it when either is wanted
+        const int ra = (i4 * 4) / kShRestF, rb = (i4 * 4 + 3) / kShRestF;
+        if (i4 < n4 && (((rowmask >> ra) | (rowmask >> rb)) & 1ull)) {
             const float4 v = reinterpret_cast<const float4*>(rest)[i4];
             const float f[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -149,7 +152,8 @@ __device__ __forceinline__ void sh_stage_in(const ShAddr& sa, int r0, int rows, 
         lds[row * stride + 3 + d - row * kShRestF] = rest[d];
     }
     const float* dc = sa.dc + (size_t)r0 * 3;
-    for (int i = tid; i < rows * 3; i += THREADS) lds[(i / 3) * stride + i % 3] = dc[i];
+    for (int i = tid; i < rows * 3; i += THREADS)
+        if ((rowmask >> (i / 3)) & 1ull) lds[(i / 3) * stride + i % 3] = dc[i];
     }
 }
 
