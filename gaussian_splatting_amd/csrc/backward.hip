@@ -553,22 +553,26 @@ __global__ void __launch_bounds__(64) GSR_GB_OCCUPANCY gauss_bwd_kernel(GaussBwd
                           (sb.y != 0.f) | (sb.z != 0.f) | (sb.w != 0.f) | (sc.x != 0.f) | (sc.y != 0.f);
     const bool visible = valid && rad > 0 && any_grad;
     if (valid && !visible) {
-        store3(a.dL_dmean2D, idx, 0.f, 0.f, 0.f);
-        if (a.dL_dconic) reinterpret_cast<float4*>(a.dL_dconic)[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
-        a.dL_dopacity[idx] = 0.f;
-        store3(a.dL_dcolor, idx, 0.f, 0.f, 0.f);
-        if (a.dL_dinvdepth) a.dL_dinvdepth[idx] = 0.f;
-        store3(a.dL_dmean3D, idx, 0.f, 0.f, 0.f);
-        for (int k = 0; k < 6; k++) a.dL_dcov3D[6 * idx + k] = 0.f;
-        if (a.dL_dscale) store3(a.dL_dscale, idx, 0.f, 0.f, 0.f);
-        if (a.dL_drot) reinterpret_cast<float4*>(a.dL_drot)[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (!a.sparse) {  // (sparse: the outputs were zero-filled beforehand)
+            store3(a.dL_dmean2D, idx, 0.f, 0.f, 0.f);
+            if (a.dL_dconic) reinterpret_cast<float4*>(a.dL_dconic)[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
+            a.dL_dopacity[idx] = 0.f;
+            store3(a.dL_dcolor, idx, 0.f, 0.f, 0.f);
+            if (a.dL_dinvdepth) a.dL_dinvdepth[idx] = 0.f;
+            store3(a.dL_dmean3D, idx, 0.f, 0.f, 0.f);
+            for (int k = 0; k < 6; k++) a.dL_dcov3D[6 * idx + k] = 0.f;
+            if (a.dL_dscale) store3(a.dL_dscale, idx, 0.f, 0.f, 0.f);
+            if (a.dL_drot) reinterpret_cast<float4*>(a.dL_drot)[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
         if (a.dL_dsh || a.dL_ddc) {
             if constexpr (kShLate) {
                 // rows zeroed in the SH pass below
             } else if constexpr (SH_MODE != kShGlobal) {
+                // the LDS row is zeroed even when sparse: a split-layout piece straddling into a
+                // wanted row writes this row's floats too (sh_stage_out)
                 for (int k = 0; k < kShRowF; k += 4)
                     *reinterpret_cast<float4*>(&s_sh[lane * kShStride + k]) = make_float4(0.f, 0.f, 0.f, 0.f);
-            } else {
+            } else if (!a.sparse) {
                 const ShGlobal acc{sh_src, sh_dst, idx};
                 for (int k = 0; k < M; k++) acc.store(k, make_float3(0.f, 0.f, 0.f));
             }
@@ -809,7 +813,7 @@ __global__ void __launch_bounds__(64) GSR_GB_OCCUPANCY gauss_bwd_kernel(GaussBwd
                     dm.y += (-v.x * v.y * ddx + (sum2 - v.y * v.y) * ddy - v.z * v.y * ddz) * invsum32;
                     dm.z += (-v.x * v.z * ddx - v.y * v.z * ddy + (sum2 - v.z * v.z) * ddz) * invsum32;
                     store3(a.dL_dmean3D, idx, dm.x, dm.y, dm.z);
-                } else {
+                } else if (!a.sparse || SH_MODE == kShLdsSplit) {  // split: see sh_stage_out
                     for (int k = 0; k < kShRowF; k += 4)
                         *reinterpret_cast<float4*>(&row[k]) = make_float4(0.f, 0.f, 0.f, 0.f);
                 }
@@ -817,13 +821,15 @@ __global__ void __launch_bounds__(64) GSR_GB_OCCUPANCY gauss_bwd_kernel(GaussBwd
             __syncthreads();
             if (a.dL_dsh || a.dL_ddc)
                 sh_stage_out<kGbShRows, 64, SH_MODE == kShLdsSplit>(sh_dst, g0 + half * kGbShRows, rows, s_sh,
-                                                                   kShStride, lane);
+                                                                   kShStride, lane,
+                                                                   a.sparse ? need >> (half * kGbShRows) : ~0ull);
             __syncthreads();
         }
     } else if constexpr (SH_MODE != kShGlobal) {
         // coalesced write-back of the wave's dL/dSH rows
+        const unsigned long long rows_out = a.sparse ? __ballot(visible) : ~0ull;
         __syncthreads();
-        sh_stage_out<64, 64, SH_MODE == kShLdsSplit>(sh_dst, g0, nvalid, s_sh, kShStride, lane);
+        sh_stage_out<64, 64, SH_MODE == kShLdsSplit>(sh_dst, g0, nvalid, s_sh, kShStride, lane, rows_out);
     }
 }
 
@@ -1030,6 +1036,35 @@ hipError_t launch_view_header(float* blk, const float* view, const float* proj, 
                               hipStream_t stream) {
     hipLaunchKernelGGL(view_header_kernel, dim3(1), dim3(64), 0, stream, blk, view, proj, campos, tan_fovx, tan_fovy,
                        focal_x, focal_y, antialiasing, have_invdepth);
+    return hipGetLastError();
+}
+
+// 16-byte stores (1 KiB per wave-instruction) over each range's aligned body, dwords for its
+// unaligned head and tail.  A small grid (GSR_FILL_BLOCKS workgroups of 256): beside render_bwd
+// it should take few wave slots and only the HBM bandwidth render_bwd leaves idle.
+#ifndef GSR_FILL_BLOCKS
+#define GSR_FILL_BLOCKS 128
+#endif
+__global__ void __launch_bounds__(256) zero_fill_kernel(FillArgs f) {
+    const unsigned long long tid = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
+    for (int s = 0; s < f.count; s++) {
+        float* p = f.ptr[s];
+        const unsigned long long n = f.n[s];
+        const unsigned long long head = ((16 - (reinterpret_cast<uintptr_t>(p) & 15)) & 15) / 4;
+        const unsigned long long h = head < n ? head : n;
+        const unsigned long long n4 = (n - h) / 4;
+        float4* body = reinterpret_cast<float4*>(p + h);
+        for (unsigned long long i = tid; i < n4; i += stride) body[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (tid < h) p[tid] = 0.f;
+        const unsigned long long t0 = h + 4 * n4;
+        if (tid < n - t0) p[t0 + tid] = 0.f;
+    }
+}
+
+hipError_t launch_zero_fill(const FillArgs& f, hipStream_t stream) {
+    if (f.count == 0) return hipSuccess;
+    hipLaunchKernelGGL(zero_fill_kernel, dim3(GSR_FILL_BLOCKS), dim3(256), 0, stream, f);
     return hipGetLastError();
 }
 

@@ -102,7 +102,18 @@ struct GaussBwdArgs {
     float* dL_ddc;        // [P,1,3] when the forward took dc, else null
     float* dL_dscale;     // [P,3] or null
     float* dL_drot;       // [P,4] or null
+    int sparse;           // outputs already zero (zero_fill on the side stream): write only non-zero rows
 };
+
+// Zero-fill of up to kFillSegs float ranges (the backward's dense outputs), run on a side
+// stream while render_bwd (VALU-bound) leaves HBM bandwidth idle.
+constexpr int kFillSegs = 12;
+struct FillArgs {
+    float* ptr[kFillSegs];
+    unsigned long long n[kFillSegs];  // floats
+    int count;
+};
+hipError_t launch_zero_fill(const FillArgs& f, hipStream_t stream);
 
 // ---- SH rows through LDS (preprocess and gauss_bwd, M = 16) -----------------------
 // LDS row r holds the 48 floats [coefficient 0..15][3] of Gaussian r0 + r at
@@ -158,18 +169,18 @@ __device__ __forceinline__ void sh_stage_in(const ShAddr& sa, int r0, int rows, 
 }
 
 template <int ROWS, int THREADS, bool SPLIT>
+// rowmask: bit r set = write row r (rows left out are not written).
 __device__ __forceinline__ void sh_stage_out(const ShGradAddr& ga, int r0, int rows, const float* lds, int stride,
-                                             int tid) {
+                                             int tid, unsigned long long rowmask = ~0ull) {
     if constexpr (!SPLIT) {
         float4* dst = reinterpret_cast<float4*>(ga.dsh + (size_t)r0 * kShRowF);
         const int n4 = rows * (kShRowF / 4);
 #pragma unroll
         for (int k = 0; k < ROWS * kShRowF / 4 / THREADS; k++) {
             const int i4 = k * THREADS + tid;
-            if (i4 < n4) {
-                const int d = i4 * 4, row = d / kShRowF, col = d - row * kShRowF;
+            const int d = i4 * 4, row = d / kShRowF, col = d - row * kShRowF;
+            if (i4 < n4 && ((rowmask >> row) & 1ull))
                 dst[i4] = *reinterpret_cast<const float4*>(&lds[row * stride + col]);
-            }
         }
         return;
     } else {
@@ -178,7 +189,10 @@ __device__ __forceinline__ void sh_stage_out(const ShGradAddr& ga, int r0, int r
 #pragma unroll
     for (int k = 0; k < (ROWS * kShRestF / 4 + THREADS - 1) / THREADS; k++) {
         const int i4 = k * THREADS + tid;
-        if (i4 < n4) {
+        // a piece straddling two rows is written when either is wanted: the caller keeps the LDS
+        // rows it does not want zero, which is what they hold in the output already
+        const int ra = (i4 * 4) / kShRestF, rb = (i4 * 4 + 3) / kShRestF;
+        if (i4 < n4 && (((rowmask >> ra) | (rowmask >> rb)) & 1ull)) {
             float f[4];
 #pragma unroll
             for (int c = 0; c < 4; c++) {
@@ -190,10 +204,11 @@ __device__ __forceinline__ void sh_stage_out(const ShGradAddr& ga, int r0, int r
     }
     if (tid < (nf & 3)) {
         const int d = n4 * 4 + tid, row = d / kShRestF;
-        rest[d] = lds[row * stride + 3 + d - row * kShRestF];
+        if ((rowmask >> row) & 1ull) rest[d] = lds[row * stride + 3 + d - row * kShRestF];
     }
     float* dc = ga.ddc + (size_t)r0 * 3;
-    for (int i = tid; i < rows * 3; i += THREADS) dc[i] = lds[(i / 3) * stride + i % 3];
+    for (int i = tid; i < rows * 3; i += THREADS)
+        if ((rowmask >> (i / 3)) & 1ull) dc[i] = lds[(i / 3) * stride + i % 3];
     }
 }
 // SH path of preprocess / gauss_bwd: per-lane global loads, or LDS staging of either layout
