@@ -147,10 +147,12 @@ def multi_rank_diagnostics(args, world, rank, views, ex, arena, per_rank, P, dev
     ms = torch.tensor([(time.perf_counter() - t0) / reps * 1e3], dtype=torch.float64, device=dev)
     dist.all_reduce(ms, op=dist.ReduceOp.MAX)
     if views:
-        recv = (world - 1) * ex.block_floats * 4
-        why = (f"--exchange {args.exchange}: all-gather of 44-B/Gaussian view blocks"
-               + (" (auto picks it up to 4 ranks: fewer received bytes than the 2(N-1)/N x 236 B/Gaussian "
-                  "all-reduce; DESIGN.md section 7)" if args.exchange == "auto" else ""))
+        recv = ex.received_bytes()
+        why = (f"--exchange {args.exchange}: all-gather of "
+               + ("sparse view blocks (48 B per Gaussian with a non-zero render gradient; "
+                  f"{ex.last_entries} entries in the largest block)" if ex.sparse else "dense 44-B/Gaussian view blocks")
+               + (" -- auto picks it at every N: fewer received bytes than the 2(N-1)/N x 236 B/Gaussian all-reduce "
+                  "(DESIGN.md section 7)" if args.exchange == "auto" else ""))
     else:
         recv = int(2 * (world - 1) / world * arena.flat.numel() * 4)
         why = (f"--exchange {args.exchange}: RCCL all-reduce of the 59-float/Gaussian gradient arena"
@@ -173,9 +175,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-census", action="store_true",
                     help="skip the census pass (profiler runs: keeps its kernel instantiations out of the trace)")
-    ap.add_argument("--exchange", choices=("auto", "views", "allreduce"), default="auto",
-                    help="N > 1: all-gather the view blocks or all-reduce the parameter gradients; auto = views "
-                         "up to 4 ranks, all-reduce beyond (DESIGN.md section 7)")
+    ap.add_argument("--exchange", choices=("auto", "views", "dense", "allreduce"), default="auto",
+                    help="N > 1: all-gather the sparse view blocks (views; auto picks it at every N), the dense "
+                         "view blocks (dense), or all-reduce the parameter gradients (DESIGN.md section 7)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="threads of the C-restatement figure (default 16)")
     ap.add_argument("--cpu-only", action="store_true",
                     help="no GPU: time the pure-PyTorch fallback forward on --config (BASELINE configs[0] plumbing)")
@@ -211,8 +213,8 @@ def main():
     bg = torch.zeros(3, device=dev)
     empty = torch.empty(0, device=dev)
     arena = GradArena(P, scene.shs.shape[1], dev)
-    views = world > 1 and (args.exchange == "views" or (args.exchange == "auto" and world <= 4))
-    ex = ViewExchange(P, dev) if views else None
+    views = world > 1 and args.exchange in ("auto", "views", "dense")
+    ex = ViewExchange(P, dev, sparse=args.exchange != "dense") if views else None
 
     def step(collective=True):
         fwd = _C.rasterize_gaussians(bg, scene.means3D, empty, scene.opacities, scene.scales, scene.rotations, 1.0,
@@ -327,7 +329,8 @@ def main():
             "config": {"workload": args.config, "gaussians": P, "width": W, "height": H, "sh_degree": Kdeg,
                        "num_rendered": nr, "views": "one per GPU, yaw 5 deg x rank",
                        "parallelism": f"view-sharded x{world}" + (
-                           "" if world == 1 else " + RCCL all-gather of view blocks" if views else " + RCCL all-reduce")},
+                           "" if world == 1 else (" + RCCL all-gather of " + ("sparse " if ex.sparse else "")
+                                                  + "view blocks") if views else " + RCCL all-reduce")},
             "roofline": {"kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "algorithmic_bytes_per_launch": alg, "mean_launch_ms": dom_ms,

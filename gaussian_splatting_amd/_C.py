@@ -21,7 +21,8 @@ import torch
 from . import _lib
 
 __all__ = ["rasterize_gaussians", "rasterize_gaussians_backward", "rasterize_gaussians_backward_screen",
-           "gauss_backward_views", "view_block_floats", "mark_visible", "adamUpdate", "fusedssim",
+           "gauss_backward_views", "view_block_floats", "view_pack_floats", "view_block_pack", "view_block_unpack",
+           "mark_visible", "adamUpdate", "fusedssim",
            "fusedssim_backward", "forward_rebuilds", "debug_forward_state"]
 
 
@@ -339,6 +340,50 @@ def debug_forward_state(fwd, P: int) -> dict:
 def view_block_floats(P: int) -> int:
     """Floats in one view block (include/gsr.h, multi-GPU view exchange)."""
     return int(_lib.load().gsr_view_block_floats(int(P)))
+
+
+def view_pack_floats(entries: int) -> int:
+    """Floats of a packed (sparse) view block holding ``entries`` entries (include/gsr.h)."""
+    return int(_lib.load().gsr_view_pack_floats(int(entries)))
+
+
+def view_block_pack(view_block: torch.Tensor, packed: torch.Tensor, scratch: torch.Tensor, count: torch.Tensor,
+                    P: int) -> None:
+    """Pack a dense view block into ``packed`` (capacity from its size); the entry count lands in
+    ``count`` (an int32 device tensor of one element) and in the packed header (include/gsr.h
+    gsr_view_block_pack).  Only Gaussians with a non-zero render gradient are kept."""
+    _require_device(view_block, "view_block")
+    nb = view_block_floats(P)
+    if view_block.numel() != nb or view_block.dtype != torch.float32 or not view_block.is_contiguous():
+        raise RuntimeError(f"view_block must be a contiguous float32 tensor of {nb} values")
+    cap = (packed.numel() - 64) // 12
+    if packed.dtype != torch.float32 or not packed.is_contiguous() or cap < 0:
+        raise RuntimeError("packed must be a contiguous float32 tensor of at least 64 values")
+    need = int(_lib.load().gsr_view_pack_scratch_bytes(int(P)))
+    if scratch.numel() * scratch.element_size() < need or count.numel() != 1 or count.dtype != torch.int32:
+        raise RuntimeError("view_block_pack: scratch too small or count not an int32 scalar tensor")
+    lib = _lib.load()
+    with torch.cuda.device(view_block.device):
+        rc = lib.gsr_view_block_pack(int(P), view_block.data_ptr(), packed.data_ptr(), int(cap), scratch.data_ptr(),
+                                     count.data_ptr(), _stream_handle(view_block.device))
+    _lib.check(rc, "view_block_pack")
+
+
+def view_block_unpack(packed: torch.Tensor, blocks: torch.Tensor, P: int) -> None:
+    """Unpack ``packed`` ([n_views, packed_floats]) into dense view blocks ``blocks``
+    ([n_views, view_block_floats(P)]; include/gsr.h gsr_view_block_unpack)."""
+    _require_device(packed, "packed")
+    nb = view_block_floats(P)
+    if packed.dim() != 2 or blocks.dim() != 2 or blocks.size(1) != nb or packed.size(0) != blocks.size(0):
+        raise RuntimeError(f"packed [n_views, k] and blocks [n_views, {nb}] expected")
+    if not (packed.is_contiguous() and blocks.is_contiguous()):
+        raise RuntimeError("packed and blocks must be contiguous")
+    cap = (packed.size(1) - 64) // 12
+    lib = _lib.load()
+    with torch.cuda.device(packed.device):
+        rc = lib.gsr_view_block_unpack(int(P), int(packed.size(0)), packed.data_ptr(), int(packed.size(1)),
+                                       blocks.data_ptr(), int(cap), _stream_handle(packed.device))
+    _lib.check(rc, "view_block_unpack")
 
 
 def rasterize_gaussians_backward_screen(*args, view_block: torch.Tensor) -> None:

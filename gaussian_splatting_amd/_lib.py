@@ -69,6 +69,10 @@ SIGNATURES = {
                                        _vp, _vp, _vp, _vp, _vp, _i, _i, ALLOC_FN, _vp, _vp, _i, ctypes.c_size_t]),
     "gsr_mark_visible": (_i, [_i, _vp, _vp, _vp, _vp, _vp]),
     "gsr_view_block_floats": (ctypes.c_ulonglong, [_i]),
+    "gsr_view_pack_floats": (ctypes.c_ulonglong, [ctypes.c_longlong]),
+    "gsr_view_pack_scratch_bytes": (ctypes.c_ulonglong, [_i]),
+    "gsr_view_block_pack": (_i, [_i, _vp, _vp, ctypes.c_longlong, _vp, _vp, _vp]),
+    "gsr_view_block_unpack": (_i, [_i, _i, _vp, ctypes.c_longlong, _vp, ctypes.c_longlong, _vp]),
     "gsr_rasterize_backward_screen": (_i, [_i, _i, _i, _i, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp,
                                            _vp, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, ALLOC_FN, _vp, _vp, _i,
                                            ctypes.c_size_t, _vp]),

@@ -1097,6 +1097,43 @@ int gsr_rasterize_backward_dc(int P, int D, int M, int R, const float* backgroun
 // ---- multi-GPU view exchange (include/gsr.h) -----------------------------------------
 unsigned long long gsr_view_block_floats(int P) { return P > 0 ? gsr::view_block_floats((size_t)P) : 0ull; }
 
+unsigned long long gsr_view_pack_floats(long long entries) {
+    return gsr::view_pack_floats(entries > 0 ? (size_t)entries : 0);
+}
+
+unsigned long long gsr_view_pack_scratch_bytes(int P) { return P > 0 ? 4ull * ((P + 255) / 256) : 4ull; }
+
+int gsr_view_block_pack(int P, const float* view_block, float* packed, long long cap, void* scratch,
+                        unsigned int* count, void* stream) {
+    g_err[0] = 0;
+    if (P <= 0 || cap < 0) return fail(GSR_ERR_ARGUMENT, "view_block_pack: P=%d cap=%lld", P, cap);
+    if (!view_block || !packed || !scratch) return fail(GSR_ERR_ARGUMENT, "view_block_pack: null pointer");
+    if ((reinterpret_cast<uintptr_t>(view_block) & 15) || (reinterpret_cast<uintptr_t>(packed) & 15))
+        return fail(GSR_ERR_ARGUMENT, "view_block_pack: blocks must be 16-byte aligned");
+    HIP_TRY(gsr::launch_view_pack((uint32_t)P, view_block, packed, (unsigned long long)cap,
+                                  reinterpret_cast<uint32_t*>(scratch), count, (hipStream_t)stream),
+            "view_block_pack");
+    return GSR_OK;
+}
+
+int gsr_view_block_unpack(int P, int n_views, const float* packed, long long packed_floats, float* blocks,
+                          long long cap, void* stream) {
+    g_err[0] = 0;
+    if (P <= 0 || n_views < 0 || cap < 0 || packed_floats < (long long)gsr::view_pack_floats(0))
+        return fail(GSR_ERR_ARGUMENT, "view_block_unpack: P=%d views=%d packed_floats=%lld cap=%lld", P, n_views,
+                    packed_floats, cap);
+    if ((size_t)packed_floats < gsr::view_pack_floats((size_t)cap))
+        return fail(GSR_ERR_ARGUMENT, "view_block_unpack: %lld floats per packed block cannot hold %lld entries",
+                    packed_floats, cap);
+    if (n_views > 0 && (!packed || !blocks)) return fail(GSR_ERR_ARGUMENT, "view_block_unpack: null pointer");
+    if ((reinterpret_cast<uintptr_t>(packed) & 15) || (reinterpret_cast<uintptr_t>(blocks) & 15) || (packed_floats & 3))
+        return fail(GSR_ERR_ARGUMENT, "view_block_unpack: blocks must be 16-byte aligned");
+    HIP_TRY(gsr::launch_view_unpack((uint32_t)P, n_views, packed, (unsigned long long)packed_floats, blocks,
+                                    (unsigned long long)cap, (hipStream_t)stream),
+            "view_block_unpack");
+    return GSR_OK;
+}
+
 int gsr_rasterize_backward_screen(int P, int D, int M, int R, const float* background, int width, int height,
                                   const float* means3D, const float* dc, const float* shs, const float* opacities,
                                   const float* scales, float scale_modifier, const float* rotations,

@@ -1031,6 +1031,149 @@ __global__ void view_header_kernel(float* blk, const float* view, const float* p
     }
 }
 
+// ---- sparse view blocks (multi-GPU exchange) ------------------------------------------
+// Only the Gaussians with a non-zero render gradient need to travel: behind saturated pixels
+// most have none (about 14% of a 1M@1080p view do).  A packed block is the view block's header
+// (64 floats, the entry count in float kViewPackCount) followed by count entries of 12 floats:
+// Gaussian index (bits), sums.a (4), sums.b (4), sums.c (2), flag word (bits), in Gaussian
+// order (a deterministic compaction: per-workgroup counts, one scan, an in-order scatter).
+constexpr int kPackThreads = 256;
+
+__device__ __forceinline__ bool view_entry_live(const float* body, uint32_t P, uint32_t g) {
+    const float4 a = reinterpret_cast<const float4*>(body)[g];
+    const float4 b = reinterpret_cast<const float4*>(body + 4 * (size_t)P)[g];
+    const float2 c = reinterpret_cast<const float2*>(body + 8 * (size_t)P)[g];
+    const uint32_t f = __float_as_uint(body[10 * (size_t)P + g]);
+    return (f & 1u) && ((a.x != 0.f) | (a.y != 0.f) | (a.z != 0.f) | (a.w != 0.f) | (b.x != 0.f) | (b.y != 0.f) |
+                        (b.z != 0.f) | (b.w != 0.f) | (c.x != 0.f) | (c.y != 0.f));
+}
+
+// rank of this thread among the live threads of its workgroup, and the workgroup's total
+__device__ __forceinline__ uint32_t block_live_rank(bool live, uint32_t* s_w, uint32_t* total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const unsigned long long m = __ballot(live);
+    const uint32_t in_wave = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) s_w[w] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t before = 0, all = 0;
+    for (int k = 0; k < kPackThreads / 64; k++) {
+        before += k < w ? s_w[k] : 0u;
+        all += s_w[k];
+    }
+    *total = all;
+    return before + in_wave;
+}
+
+__global__ void __launch_bounds__(kPackThreads) view_pack_count_kernel(uint32_t P, const float* __restrict__ block,
+                                                                       uint32_t* __restrict__ wg_cnt) {
+    __shared__ uint32_t s_w[kPackThreads / 64];
+    const uint32_t g = blockIdx.x * kPackThreads + threadIdx.x;
+    const bool live = g < P && view_entry_live(block + kViewBlockHeader, P, g);
+    uint32_t total = 0;
+    block_live_rank(live, s_w, &total);
+    if (threadIdx.x == 0) wg_cnt[blockIdx.x] = total;
+}
+
+// one workgroup: exclusive scan of the per-workgroup counts (in place), total into the packed header
+__global__ void __launch_bounds__(1024) view_pack_scan_kernel(uint32_t nb, uint32_t* __restrict__ wg_cnt,
+                                                              float* __restrict__ packed, uint32_t* __restrict__ count) {
+    __shared__ uint32_t s_tot[1024 / 64];
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < nb; base += blockDim.x) {
+        const uint32_t i = base + threadIdx.x;
+        const uint32_t v = i < nb ? wg_cnt[i] : 0u;
+        const uint32_t incl = wave_incl_sum(v);
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+        if (lane == 63) s_tot[w] = incl;
+        __syncthreads();
+        uint32_t before = 0, all = 0;
+        for (int k = 0; k < (int)(blockDim.x / 64); k++) {
+            before += k < w ? s_tot[k] : 0u;
+            all += s_tot[k];
+        }
+        if (i < nb) wg_cnt[i] = carry + before + incl - v;
+        carry += all;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        packed[kViewPackCount] = __uint_as_float(carry);
+        if (count) count[0] = carry;
+    }
+}
+
+__global__ void __launch_bounds__(kPackThreads) view_pack_scatter_kernel(uint32_t P, const float* __restrict__ block,
+                                                                         const uint32_t* __restrict__ wg_off,
+                                                                         float* __restrict__ packed,
+                                                                         unsigned long long cap) {
+    __shared__ uint32_t s_w[kPackThreads / 64];
+    if (blockIdx.x == 0 && threadIdx.x < kViewBlockHeader && threadIdx.x != kViewPackCount)
+        packed[threadIdx.x] = block[threadIdx.x];
+    const float* body = block + kViewBlockHeader;
+    const uint32_t g = blockIdx.x * kPackThreads + threadIdx.x;
+    const bool live = g < P && view_entry_live(body, P, g);
+    uint32_t total = 0;
+    const uint32_t pos = wg_off[blockIdx.x] + block_live_rank(live, s_w, &total);
+    if (live && pos < cap) {
+        const float4 a = reinterpret_cast<const float4*>(body)[g];
+        const float4 b = reinterpret_cast<const float4*>(body + 4 * (size_t)P)[g];
+        const float2 c = reinterpret_cast<const float2*>(body + 8 * (size_t)P)[g];
+        const float f = body[10 * (size_t)P + g];
+        float4* e = reinterpret_cast<float4*>(packed + kViewBlockHeader + (size_t)kViewPackEntry * pos);
+        e[0] = make_float4(__uint_as_float(g), a.x, a.y, a.z);
+        e[1] = make_float4(a.w, b.x, b.y, b.z);
+        e[2] = make_float4(b.w, c.x, c.y, f);
+    }
+}
+
+hipError_t launch_view_pack(uint32_t P, const float* block, float* packed, unsigned long long cap, uint32_t* scratch,
+                            uint32_t* count, hipStream_t stream) {
+    const uint32_t nb = (P + kPackThreads - 1) / kPackThreads;
+    hipLaunchKernelGGL(view_pack_count_kernel, dim3(nb), dim3(kPackThreads), 0, stream, P, block, scratch);
+    hipLaunchKernelGGL(view_pack_scan_kernel, dim3(1), dim3(1024), 0, stream, nb, scratch, packed, count);
+    hipLaunchKernelGGL(view_pack_scatter_kernel, dim3(nb), dim3(kPackThreads), 0, stream, P, block, scratch, packed,
+                       cap);
+    return hipGetLastError();
+}
+
+// packed [n_views][packed_floats] -> dense view blocks [n_views][view_block_floats(P)], whose
+// bodies the caller zeroed: header copy and one entry per thread.
+__global__ void __launch_bounds__(kPackThreads) view_unpack_kernel(uint32_t P, const float* __restrict__ packed,
+                                                                   unsigned long long packed_floats,
+                                                                   float* __restrict__ blocks,
+                                                                   unsigned long long block_floats,
+                                                                   unsigned long long cap) {
+    const uint32_t v = blockIdx.y;
+    const float* pk = packed + v * packed_floats;
+    float* blk = blocks + v * block_floats;
+    if (blockIdx.x == 0 && threadIdx.x < kViewBlockHeader) blk[threadIdx.x] = threadIdx.x == kViewPackCount ? 0.f
+                                                                                                       : pk[threadIdx.x];
+    uint32_t n = __float_as_uint(pk[kViewPackCount]);
+    n = n < cap ? n : (uint32_t)cap;
+    float* body = blk + kViewBlockHeader;
+    for (uint32_t i = blockIdx.x * kPackThreads + threadIdx.x; i < n; i += gridDim.x * kPackThreads) {
+        const float4* e = reinterpret_cast<const float4*>(pk + kViewBlockHeader + (size_t)kViewPackEntry * i);
+        const float4 e0 = e[0], e1 = e[1], e2 = e[2];
+        const uint32_t g = __float_as_uint(e0.x);
+        if (g >= P) continue;  // never for a block packed by view_pack_scatter_kernel
+        reinterpret_cast<float4*>(body)[g] = make_float4(e0.y, e0.z, e0.w, e1.x);
+        reinterpret_cast<float4*>(body + 4 * (size_t)P)[g] = make_float4(e1.y, e1.z, e1.w, e2.x);
+        reinterpret_cast<float2*>(body + 8 * (size_t)P)[g] = make_float2(e2.y, e2.z);
+        body[10 * (size_t)P + g] = e2.w;
+    }
+}
+
+hipError_t launch_view_unpack(uint32_t P, int n_views, const float* packed, unsigned long long packed_floats,
+                              float* blocks, unsigned long long cap, hipStream_t stream) {
+    if (n_views <= 0) return hipSuccess;
+    const size_t bf = view_block_floats(P);
+    const hipError_t e = hipMemsetAsync(blocks, 0, (size_t)n_views * bf * sizeof(float), stream);
+    if (e != hipSuccess) return e;
+    const uint32_t gx = (uint32_t)((cap + kPackThreads - 1) / kPackThreads);
+    hipLaunchKernelGGL(view_unpack_kernel, dim3(gx < 1024 ? (gx ? gx : 1) : 1024, n_views), dim3(kPackThreads), 0,
+                       stream, P, packed, packed_floats, blocks, (unsigned long long)bf, cap);
+    return hipGetLastError();
+}
+
 hipError_t launch_view_header(float* blk, const float* view, const float* proj, const float* campos, float tan_fovx,
                               float tan_fovy, float focal_x, float focal_y, int antialiasing, int have_invdepth,
                               hipStream_t stream) {

@@ -162,6 +162,12 @@ constexpr int kViewCamView = 0, kViewCamProj = 16, kViewCamPos = 32, kViewCamTan
 __host__ __device__ inline size_t view_block_floats(size_t P) {
     return (kViewBlockHeader + 11 * P + 63) / 64 * 64;
 }
+// Packed (sparse) view block: the header, the entry count in header float kViewPackCount, then
+// kViewPackEntry floats per Gaussian with a non-zero render gradient (backward.hip view_pack).
+constexpr int kViewPackCount = 63, kViewPackEntry = 12;
+__host__ __device__ inline size_t view_pack_floats(size_t entries) {
+    return (kViewBlockHeader + kViewPackEntry * entries + 63) / 64 * 64;
+}
 
 // Per-instance gradient records (backward scratch), SoA so stores are aligned.
 struct GradRecs {

@@ -335,6 +335,10 @@ struct ViewsBwdArgs {
     float* dL_drot;
 };
 hipError_t launch_gauss_bwd_views(const ViewsBwdArgs& a, hipStream_t stream);
+hipError_t launch_view_pack(uint32_t P, const float* block, float* packed, unsigned long long cap, uint32_t* scratch,
+                            uint32_t* count, hipStream_t stream);
+hipError_t launch_view_unpack(uint32_t P, int n_views, const float* packed, unsigned long long packed_floats,
+                              float* blocks, unsigned long long cap, hipStream_t stream);
 hipError_t launch_view_header(float* blk, const float* view, const float* proj, const float* campos, float tan_fovx,
                               float tan_fovy, float focal_x, float focal_y, int antialiasing, int have_invdepth,
                               hipStream_t stream);

@@ -195,6 +195,26 @@ int gsr_gauss_backward_views(int P, int D, int M, const float* means3D, const fl
                              float* dL_ddc, float* dL_dsh, float* dL_dopacity, float* dL_dscale, float* dL_drot,
                              void* stream);
 
+/* Sparse view blocks.  Behind saturated pixels most Gaussians get no render gradient (about
+ * 14% of a 1M@1080p view have one), so a view block travels packed: its header (64 floats,
+ * the entry count as uint32 bits in float 63) and, per Gaussian that is visible with a non-zero
+ * sum, 12 floats (index bits, the 10 sums, the flag word), in Gaussian order.
+ * gsr_view_pack_floats(n): floats of a packed block holding n entries (padded to 256 B).
+ * gsr_view_pack_scratch_bytes(P): device scratch gsr_view_block_pack needs.
+ * gsr_view_block_pack: view_block (gsr_view_block_floats(P) floats) -> packed
+ *   (gsr_view_pack_floats(cap) floats); *count (device uint32, may be NULL) receives the entry
+ *   count, which may exceed cap (then only the first cap entries are written).
+ * gsr_view_block_unpack: n_views packed blocks (packed_floats apart) -> n_views dense view
+ *   blocks (gsr_view_block_floats(P) apart; bodies zeroed first), entries beyond cap ignored.
+ *   Unpacked blocks give gsr_gauss_backward_views the dense blocks' result (a Gaussian left out
+ *   had all-zero sums, which add nothing). */
+unsigned long long gsr_view_pack_floats(long long entries);
+unsigned long long gsr_view_pack_scratch_bytes(int P);
+int gsr_view_block_pack(int P, const float* view_block, float* packed, long long cap, void* scratch,
+                        unsigned int* count, void* stream);
+int gsr_view_block_unpack(int P, int n_views, const float* packed, long long packed_floats, float* blocks,
+                          long long cap, void* stream);
+
 /* Frustum test, view-space z > 0.2 (CudaRasterizer::Rasterizer::markVisible).
  * `present` is P bytes (bool). */
 int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,

@@ -5,8 +5,9 @@ two exchanges run for real:
 
   * GradArena.all_reduce -- the backward writes the 59-float parameter gradients into the flat arena,
     one all-reduce sums them;
-  * ViewExchange -- each rank writes its view block (gsr_rasterize_backward_screen), one all-gather,
-    and every rank runs gsr_gauss_backward_views over both blocks.
+  * ViewExchange -- each rank writes its view block (gsr_rasterize_backward_screen), one all-gather of the
+    packed (sparse) blocks -- and of the dense ones -- and every rank runs gsr_gauss_backward_views over
+    both views.
 
 Both must equal the oracle's sum of the per-view gradients (unit-scale upstream gradient, the small-case
 bar max |diff| / max |ref| <= 2e-4), and the replicas must be bitwise identical after each exchange.
@@ -69,14 +70,17 @@ def _worker(rank, port, outdir):
         bwd = (d("bg"), d("means3D"), radii, torch.Tensor([]), d("opacities"), d("scales"), d("rotations"), 1.0,
                torch.Tensor([]), d("viewmatrix"), d("projmatrix"), inp["tanfovx"], inp["tanfovy"], gc.to(dev),
                gd.to(dev), d("shs"), inp["sh_degree"], d("campos"), geom, nr, binning, img, False, False)
-        ex = ViewExchange(CASE.P, dev)
-        _C.rasterize_gaussians_backward_screen(*bwd, view_block=ex.local_block())
-        ex.exchange()
-        arena2 = GradArena(CASE.P, M, dev)
-        _C.gauss_backward_views(d("means3D"), None, d("shs"), inp["sh_degree"], d("opacities"), d("scales"),
-                                d("rotations"), 1.0, ex.gathered, out=arena2.views())
-        torch.cuda.synchronize()
-        np.save(os.path.join(outdir, f"views{rank}.npy"), arena2.flat.cpu().numpy())
+        for mode, sparse in (("views", True), ("dense", False)):  # sparse (default) and dense view blocks
+            ex = ViewExchange(CASE.P, dev, sparse=sparse)
+            _C.rasterize_gaussians_backward_screen(*bwd, view_block=ex.local_block())
+            ex.exchange()
+            arena2 = GradArena(CASE.P, M, dev)
+            _C.gauss_backward_views(d("means3D"), None, d("shs"), inp["sh_degree"], d("opacities"), d("scales"),
+                                    d("rotations"), 1.0, ex.gathered, out=arena2.views())
+            torch.cuda.synchronize()
+            np.save(os.path.join(outdir, f"{mode}{rank}.npy"), arena2.flat.cpu().numpy())
+            if sparse:
+                assert ex.last_entries is None or 0 < ex.last_entries <= CASE.P
         dist.barrier()
     finally:
         dist.destroy_process_group()
@@ -88,7 +92,10 @@ def test_two_ranks_on_gpu_equal_oracle_sum_of_views():
 
     with tempfile.TemporaryDirectory() as d:
         mp.start_processes(_worker, args=(_free_port(), d), nprocs=WORLD, join=True, start_method="spawn")
-        got = {m: [np.load(os.path.join(d, f"{m}{r}.npy")) for r in range(WORLD)] for m in ("allreduce", "views")}
+        got = {m: [np.load(os.path.join(d, f"{m}{r}.npy")) for r in range(WORLD)]
+               for m in ("allreduce", "views", "dense")}
+    # the sparse exchange gives the dense one's gradients
+    np.testing.assert_array_equal(got["views"][0], got["dense"][0])
     for m, (a, b) in got.items():
         np.testing.assert_array_equal(a, b, err_msg=f"{m}: replicas differ")
     ref = GradArena(CASE.P, 16, "cpu")

@@ -121,6 +121,69 @@ def test_views_sum_equals_sum_of_single_views(split):
         assert err <= 2e-6 * max(scale, 1e-3) + 1e-9, (k, err, scale)
 
 
+def _live(block, P):
+    """Gaussians a packed block keeps: visible (flag bit 0) with a non-zero sum."""
+    body = block[64:64 + 11 * P]
+    sums = torch.cat([body[:4 * P].view(P, 4), body[4 * P:8 * P].view(P, 4), body[8 * P:10 * P].view(P, 2)], 1)
+    flags = body[10 * P:11 * P].view(torch.int32)
+    return ((flags & 1) != 0) & (sums != 0).any(1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("split", [False, True])
+def test_sparse_blocks_pack_unpack(split):
+    """Packed (sparse) view blocks: the entry count is the number of visible Gaussians with a non-zero
+    sum, unpacking restores exactly those rows (the rest zero), and the multi-view backward over the
+    unpacked blocks equals the one over the dense blocks."""
+    from gaussian_splatting_amd import _C
+
+    dev = torch.device("cuda", 0)
+    blocks, t = [], None
+    for yaw in (0.0, 9.0, -15.0):
+        inp, case = _view_inputs(dict(P=3000, W=96, H=80, opacity_std=3.0), yaw, dev)
+        _, block, t = _single_and_block(inp, case, dev, split)
+        blocks.append(block)
+    P = t["means3D"].shape[0]
+    dense = torch.stack(blocks)
+    packed = torch.zeros(len(blocks), _C.view_pack_floats(P), device=dev)
+    scratch = torch.empty(4 * P, dtype=torch.uint8, device=dev)
+    count = torch.zeros(1, dtype=torch.int32, device=dev)
+    counts = []
+    for v, b in enumerate(blocks):
+        _C.view_block_pack(b, packed[v], scratch, count, P)
+        live = _live(b, P)
+        counts.append(int(count.item()))
+        assert counts[-1] == int(live.sum()) and 0 < counts[-1] < P, (counts[-1], int(live.sum()))
+        assert int(packed[v, 63].view(torch.int32).item()) == counts[-1]
+        idx = packed[v, 64:64 + 12 * counts[-1]].view(-1, 12)[:, 0].view(torch.int32).long()
+        assert torch.equal(idx, torch.nonzero(live).view(-1))  # Gaussian order
+    # a packed size that holds the largest count, as the exchange sizes it
+    size = _C.view_pack_floats(max(counts))
+    recv = packed[:, :size].contiguous()
+    unpacked = torch.full_like(dense, float("nan"))
+    _C.view_block_unpack(recv, unpacked, P)
+    for v, b in enumerate(blocks):
+        live = _live(b, P)
+        body_d, body_u = b[64:64 + 11 * P], unpacked[v, 64:64 + 11 * P]
+        assert torch.equal(unpacked[v, :41], b[:41])  # the camera header (floats 41-62 are unused)
+        cols = [(0, 4), (4, 8), (8, 10)]
+        for lo, hi in cols:
+            w = hi - lo
+            d = body_d[lo * P:hi * P].view(P, w)
+            u = body_u[lo * P:hi * P].view(P, w)
+            assert torch.equal(u[live], d[live])
+            assert bool((u[~live] == 0).all())
+        assert torch.equal(body_u[10 * P:].view(torch.int32)[live], body_d[10 * P:].view(torch.int32)[live])
+    got = _views_backward(t, unpacked, split, dev)
+    ref = _views_backward(t, dense, split, dev)
+    for k in ref:
+        assert torch.equal(got[k], ref[k]), k
+    # a packed block smaller than the count: the count is reported whole, cap entries are written
+    small = torch.zeros(_C.view_pack_floats(5), device=dev)
+    _C.view_block_pack(blocks[0], small, scratch, count, P)
+    assert int(count.item()) == counts[0]
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
