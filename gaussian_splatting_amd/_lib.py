@@ -201,7 +201,8 @@ def profile_collect() -> dict:
 
 # ---- census (include/gsr.h "Census"): work counts of the render kernels ----------------------
 CENSUS_NAMES = ("fwd_entries_staged", "fwd_quadrant_evals", "fwd_pairs_alpha", "fwd_pairs_blended",
-                "bwd_entries_staged", "bwd_quadrant_evals", "bwd_pairs_grad", "bwd_entry_reductions")
+                "bwd_entries_staged", "bwd_quadrant_evals", "bwd_pairs_grad", "bwd_entry_reductions",
+                "bwd_evals_idle", "fwd_evals_idle")
 
 
 def census(fn, device=None) -> dict:

@@ -143,7 +143,7 @@ __global__ void __launch_bounds__(64) GSR_FWD_OCCUPANCY render_fwd_kernel(Render
 
     const uint2 range = a.ranges[tile];
     const int n = (int)(range.y - range.x);
-    unsigned long long c_staged = 0, c_eval = 0, c_alpha = 0, c_blend = 0;  // CENSUS only
+    unsigned long long c_staged = 0, c_eval = 0, c_alpha = 0, c_blend = 0, c_idle = 0;  // CENSUS only
     for (int b0 = 0; b0 < n && alive; b0 += kBatch) {
         if (CENSUS) c_staged += (unsigned long long)min(kBatch, n - b0);
         uint32_t qm = 0;
@@ -197,7 +197,9 @@ __global__ void __launch_bounds__(64) GSR_FWD_OCCUPANCY render_fwd_kernel(Render
                 if (CENSUS) {
                     c_eval++;
                     c_alpha += (unsigned long long)__popcll(__ballot(w0 > 0.f));
-                    c_blend += (unsigned long long)__popcll(__ballot(w0 > 0.f && Tl[k] * (1.f - alpha) >= 0.0001f));
+                    const unsigned long long bl = __ballot(w0 > 0.f && Tl[k] * (1.f - alpha) >= 0.0001f);
+                    c_blend += (unsigned long long)__popcll(bl);
+                    c_idle += bl ? 0ull : 1ull;
                 }
                 if (!__any(w0 > 0.f)) continue;  // uniform
                 const float test_T = Tl[k] * (1.f - alpha);
@@ -226,6 +228,7 @@ __global__ void __launch_bounds__(64) GSR_FWD_OCCUPANCY render_fwd_kernel(Render
         atomicAdd(&a.census[1], c_eval);
         atomicAdd(&a.census[2], c_alpha);
         atomicAdd(&a.census[3], c_blend);
+        atomicAdd(&a.census[9], c_idle);
     }
     if (part == 0) {
         GSR_STAMP(g_st_rfwd, tile, 1);
@@ -356,9 +359,6 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
 
     const uint2 range = a.ranges[tile];
     const size_t N = (size_t)a.W * a.H;
-    // blend state at `start`: the forward's checkpoint (gsr_common.h), or the empty state
-    const float* ck = start > 0 ? a.ckpt + (size_t)((range.x + (uint32_t)start) / kCkStride) * kCkFloats + lane
-                                : nullptr;
     float T[4], gB[4], g0[4], g1[4], g2[4], gi[4];
     int nc[4];
     // Every slot's pixel state is loaded with no branch in between (an outside pixel reads a
@@ -434,7 +434,7 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
         a.img.lim_key[tile] = ((unsigned long long)a.depth_key[gl] << 32) | gl;
     }
     const uint32_t ttx = tile % a.gx, tty = tile / a.gx;
-    unsigned long long c_staged = 0, c_eval = 0, c_alpha = 0, c_red = 0;  // CENSUS only
+    unsigned long long c_staged = 0, c_eval = 0, c_alpha = 0, c_red = 0, c_idle = 0;  // CENSUS only
     // The ten per-entry sums stay zero between entries (reset after each reduction), so an entry
     // whose first quadrants are inactive does not materialise zeros (10 VALU) before accumulating.
 #if GSR_BWD_CARRY_R
@@ -497,6 +497,7 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
                 if (CENSUS) {
                     c_eval++;
                     c_alpha += (unsigned long long)__popcll(__ballot(alpha > 0.f));
+                    c_idle += __any(on) ? 0ull : 1ull;
                 }
 #if GSR_BWD_ANYSKIP
                 if (!__any(on)) continue;  // uniform
@@ -568,6 +569,7 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
         atomicAdd(&a.census[5], c_eval);
         atomicAdd(&a.census[6], c_alpha);
         atomicAdd(&a.census[7], c_red);
+        atomicAdd(&a.census[8], c_idle);
     }
     GSR_STAMP(g_st_rbwd, blockIdx.x, 1);
     GSR_STAMP_RT(g_st_rbwd, blockIdx.x, 5);

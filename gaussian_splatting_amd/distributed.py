@@ -207,7 +207,14 @@ class ViewExchange:
         return (self.world - 1) * _C.view_pack_floats(self.last_entries) * 4
 
     def means2D_grad(self, rank: Optional[int] = None) -> torch.Tensor:
-        """dL/dmeans2D (x, y) of a rank's view, [P, 2] (a strided view of its block): the
-        densification statistics' input (train.py:215)."""
-        b = self.gathered[self.rank if rank is None else rank]
-        return b[64 + 4 * self.P: 64 + 8 * self.P].view(self.P, 4)[:, :2]
+        """dL/dmeans2D (x, y) of a rank's view, [P, 2]: the densification statistics' input
+        (train.py:215).  This rank's own view (and every view of a dense exchange) is a strided
+        view of its block; another rank's view after a sparse exchange is a copy with zeros for
+        the Gaussians its packed block left out (the unpack clears only their flag words)."""
+        r = self.rank if rank is None else rank
+        b = self._local if (self.sparse and r == self.rank) else self.gathered[r]
+        g = b[64 + 4 * self.P: 64 + 8 * self.P].view(self.P, 4)[:, :2]
+        if not self.sparse or r == self.rank or self.last_entries is None:
+            return g
+        flags = b[64 + 10 * self.P: 64 + 11 * self.P].view(torch.int32)
+        return torch.where((flags & 1).bool()[:, None], g, torch.zeros((), dtype=g.dtype, device=g.device))

@@ -205,9 +205,10 @@ int gsr_gauss_backward_views(int P, int D, int M, const float* means3D, const fl
  *   (gsr_view_pack_floats(cap) floats); *count (device uint32, may be NULL) receives the entry
  *   count, which may exceed cap (then only the first cap entries are written).
  * gsr_view_block_unpack: n_views packed blocks (packed_floats apart) -> n_views dense view
- *   blocks (gsr_view_block_floats(P) apart; bodies zeroed first), entries beyond cap ignored.
- *   Unpacked blocks give gsr_gauss_backward_views the dense blocks' result (a Gaussian left out
- *   had all-zero sums, which add nothing). */
+ *   blocks (gsr_view_block_floats(P) apart), entries beyond cap ignored.  Only the flag words
+ *   are cleared first: a Gaussian left out has flag 0 and its sums are left as they were
+ *   (gsr_gauss_backward_views never reads them).  Unpacked blocks give gsr_gauss_backward_views
+ *   the dense blocks' result (a Gaussian left out had all-zero sums, which add nothing). */
 unsigned long long gsr_view_pack_floats(long long entries);
 unsigned long long gsr_view_pack_scratch_bytes(int P);
 int gsr_view_block_pack(int P, const float* view_block, float* packed, long long cap, void* scratch,
@@ -258,7 +259,7 @@ int gsr_profile_collect(double* total_ms, long long* calls, int max_stages);
 void gsr_profile_reset(void);
 const char* gsr_profile_stage_name(int stage);
 
-/* Census (diagnostic; no reference counterpart): with a device buffer of 8 zeroed uint64
+/* Census (diagnostic; no reference counterpart): with a device buffer of 10 zeroed uint64
  * counters set, the render kernels of later forward / backward calls run their census
  * instantiations (slower: a few extra wave-uniform ops per evaluation) and add, per call:
  *   [0] forward list entries staged (per half-tile wave; each tile's two halves both stage)
@@ -269,6 +270,8 @@ const char* gsr_profile_stage_name(int stage);
  *   [5] backward (entry, quadrant) evaluations
  *   [6] backward (pixel, entry) pairs with a gradient term (alpha > 0, before n_contrib)
  *   [7] backward per-entry wave reductions (gradient records with content)
+ *   [8] backward evaluations in which no pixel has a gradient term (idle)
+ *   [9] forward evaluations in which no pixel blends (idle)
  * NULL turns the census off.  Not thread-safe against concurrent calls. */
 int gsr_census_set(void* device_counters);
 

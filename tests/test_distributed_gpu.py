@@ -79,6 +79,8 @@ def _worker(rank, port, outdir):
                                     d("rotations"), 1.0, ex.gathered, out=arena2.views())
             torch.cuda.synchronize()
             np.save(os.path.join(outdir, f"{mode}{rank}.npy"), arena2.flat.cpu().numpy())
+            m2d = np.stack([ex.means2D_grad(r).cpu().numpy() for r in range(WORLD)])  # densification input
+            np.save(os.path.join(outdir, f"m2d_{mode}{rank}.npy"), m2d)
             if sparse:
                 assert ex.last_entries is None or 0 < ex.last_entries <= CASE.P
         dist.barrier()
@@ -94,6 +96,11 @@ def test_two_ranks_on_gpu_equal_oracle_sum_of_views():
         mp.start_processes(_worker, args=(_free_port(), d), nprocs=WORLD, join=True, start_method="spawn")
         got = {m: [np.load(os.path.join(d, f"{m}{r}.npy")) for r in range(WORLD)]
                for m in ("allreduce", "views", "dense")}
+        m2d = {m: [np.load(os.path.join(d, f"m2d_{m}{r}.npy")) for r in range(WORLD)] for m in ("views", "dense")}
+    # every rank sees every view's dL/dmeans2D, the same through either exchange
+    for r in range(WORLD):
+        np.testing.assert_array_equal(m2d["views"][r], m2d["dense"][r])
+        np.testing.assert_array_equal(m2d["dense"][r], m2d["dense"][0])
     # the sparse exchange gives the dense one's gradients
     np.testing.assert_array_equal(got["views"][0], got["dense"][0])
     for m, (a, b) in got.items():

@@ -133,8 +133,9 @@ def _live(block, P):
 @pytest.mark.parametrize("split", [False, True])
 def test_sparse_blocks_pack_unpack(split):
     """Packed (sparse) view blocks: the entry count is the number of visible Gaussians with a non-zero
-    sum, unpacking restores exactly those rows (the rest zero), and the multi-view backward over the
-    unpacked blocks equals the one over the dense blocks."""
+    sum, unpacking restores exactly those rows and clears the others' flag words (their sums are left
+    as they were, here NaN, and never read), and the multi-view backward over the unpacked blocks
+    equals the one over the dense blocks."""
     from gaussian_splatting_amd import _C
 
     dev = torch.device("cuda", 0)
@@ -172,8 +173,11 @@ def test_sparse_blocks_pack_unpack(split):
             d = body_d[lo * P:hi * P].view(P, w)
             u = body_u[lo * P:hi * P].view(P, w)
             assert torch.equal(u[live], d[live])
-            assert bool((u[~live] == 0).all())
-        assert torch.equal(body_u[10 * P:].view(torch.int32)[live], body_d[10 * P:].view(torch.int32)[live])
+            assert bool(u[~live].isnan().all())  # left as they were: never read (flag 0)
+        flags_u = body_u[10 * P:].view(torch.int32)
+        assert torch.equal(flags_u[live], body_d[10 * P:].view(torch.int32)[live])
+        assert bool((flags_u[~live] == 0).all())
+    # the NaN sums of the left-out Gaussians must not reach the gradients
     got = _views_backward(t, unpacked, split, dev)
     ref = _views_backward(t, dense, split, dev)
     for k in ref:

@@ -5,8 +5,10 @@
 
 Renders one view, copies its view block N times (N = 1, 2, 4, 8: the gathered buffer an
 N-rank job holds after the all-gather) and times gauss_backward_views over it, next to the
-single-view backward's gauss_bwd stage.  Also prints the exchange volumes per rank:
-all-gather of view blocks vs all-reduce of the 59-float parameter gradients.
+single-view backward's gauss_bwd stage; then the same for the sparse form (pack once, the
+packed block repeated N times, unpack, gauss_backward_views over the unpacked blocks).  Also
+prints the exchange volumes per rank: all-gather of dense / sparse view blocks vs all-reduce
+of the 59-float parameter gradients.
 """
 from __future__ import annotations
 
@@ -70,12 +72,27 @@ def main():
     _lib.profile_enable(False)
     t, n = _lib.profile_collect()["gauss_bwd"]
     res = {"config": a.config, "P": P, "gauss_bwd_single_ms": t / n, "views_ms": {}, "exchange_MB_per_rank": {}}
+    # the sparse form: pack once (timed), the packed block repeated N times, unpack (timed)
+    packed = torch.empty(_C.view_pack_floats(P), device=dev)
+    scratch = torch.empty(4 * ((P + 255) // 256), dtype=torch.uint8, device=dev)
+    count = torch.zeros(1, dtype=torch.int32, device=dev)
+    res["pack_ms"] = timed(lambda: _C.view_block_pack(block, packed, scratch, count, P))
+    n_live = int(count.item())
+    size = _C.view_pack_floats(n_live)
+    res["live_entries"], res["live_fraction"] = n_live, n_live / P
+    res["views_sparse_ms"], res["unpack_ms"] = {}, {}
     for N in (1, 2, 4, 8):
         blocks = block.unsqueeze(0).repeat(N, 1).contiguous()
         res["views_ms"][N] = timed(lambda: _C.gauss_backward_views(scene.means3D, None, scene.shs, D, scene.opacities,
                                                                   scene.scales, scene.rotations, 1.0, blocks,
                                                                   arena.views()))
+        recv = packed[:size].unsqueeze(0).repeat(N, 1).contiguous()
+        res["unpack_ms"][N] = timed(lambda: _C.view_block_unpack(recv, blocks, P))
+        res["views_sparse_ms"][N] = timed(lambda: _C.gauss_backward_views(scene.means3D, None, scene.shs, D,
+                                                                         scene.opacities, scene.scales,
+                                                                         scene.rotations, 1.0, blocks, arena.views()))
         res["exchange_MB_per_rank"][N] = {"allgather_view_blocks": (N - 1) * nb * 4 / 1e6,
+                                          "allgather_sparse_blocks": (N - 1) * size * 4 / 1e6,
                                           "allreduce_param_grads": 2 * (N - 1) / N * arena.flat.numel() * 4 / 1e6}
     print(json.dumps(res))
 
