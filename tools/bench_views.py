@@ -3,10 +3,10 @@
 
     python tools/bench_views.py [--config 1m_1080p_sh3]
 
-Renders one view, copies its view block N times (N = 1, 2, 4, 8: the gathered buffer an
-N-rank job holds after the all-gather) and times gauss_backward_views over it, next to the
-single-view backward's gauss_bwd stage; then the same for the sparse form (pack once, the
-packed block repeated N times, unpack, gauss_backward_views over the unpacked blocks).  Also
+Renders N = 1, 2, 4, 8 distinct views (yaw 5 deg apart, as bench.py's ranks) and times
+gauss_backward_views over their view blocks (the gathered buffer an N-rank job holds after the
+all-gather), next to the single-view backward's gauss_bwd stage; then the same for the sparse
+form (pack, unpack at the largest count, gauss_backward_views over the unpacked blocks).  Also
 prints the exchange volumes per rank: all-gather of dense / sparse view blocks vs all-reduce
 of the 59-float parameter gradients.
 """
@@ -72,27 +72,44 @@ def main():
     _lib.profile_enable(False)
     t, n = _lib.profile_collect()["gauss_bwd"]
     res = {"config": a.config, "P": P, "gauss_bwd_single_ms": t / n, "views_ms": {}, "exchange_MB_per_rank": {}}
-    # the sparse form: pack once (timed), the packed block repeated N times, unpack (timed)
-    packed = torch.empty(_C.view_pack_floats(P), device=dev)
+    # N distinct views, as an N-rank job has them (bench.py: yaw 5 deg x rank): their dense blocks
+    # and their packed forms (pack timed on view 0), all packed at the largest count
+    view_blocks = [block]
+    for v in range(1, 8):
+        _, cam_v = syn.config_scene(a.config, seed=0, yaw_deg=5.0 * v)
+        cam_v = cam_v.to(dev)
+        fv = _C.rasterize_gaussians(bg, scene.means3D, empty, scene.opacities, scene.scales, scene.rotations, 1.0,
+                                    empty, cam_v.viewmatrix, cam_v.projmatrix, cam_v.tanfovx, cam_v.tanfovy, H, W,
+                                    scene.shs, D, cam_v.campos, False, False, False)
+        bv = torch.empty(nb, device=dev)
+        _C.rasterize_gaussians_backward_screen(bg, scene.means3D, fv[2], empty, scene.opacities, scene.scales,
+                                               scene.rotations, 1.0, empty, cam_v.viewmatrix, cam_v.projmatrix,
+                                               cam_v.tanfovx, cam_v.tanfovy, gc, gd, scene.shs, D, cam_v.campos,
+                                               fv[3], fv[0], fv[4], fv[5], False, False, view_block=bv)
+        view_blocks.append(bv)
+    packed = torch.empty(8, _C.view_pack_floats(P), device=dev)
     scratch = torch.empty(4 * ((P + 255) // 256), dtype=torch.uint8, device=dev)
     count = torch.zeros(1, dtype=torch.int32, device=dev)
-    res["pack_ms"] = timed(lambda: _C.view_block_pack(block, packed, scratch, count, P))
-    n_live = int(count.item())
-    size = _C.view_pack_floats(n_live)
-    res["live_entries"], res["live_fraction"] = n_live, n_live / P
+    res["pack_ms"] = timed(lambda: _C.view_block_pack(block, packed[0], scratch, count, P))
+    counts = []
+    for v, bv in enumerate(view_blocks):
+        _C.view_block_pack(bv, packed[v], scratch, count, P)
+        counts.append(int(count.item()))
+    res["live_entries"], res["live_fraction"] = counts, [c / P for c in counts]
     res["views_sparse_ms"], res["unpack_ms"] = {}, {}
     for N in (1, 2, 4, 8):
-        blocks = block.unsqueeze(0).repeat(N, 1).contiguous()
+        blocks = torch.stack(view_blocks[:N])
         res["views_ms"][N] = timed(lambda: _C.gauss_backward_views(scene.means3D, None, scene.shs, D, scene.opacities,
                                                                   scene.scales, scene.rotations, 1.0, blocks,
                                                                   arena.views()))
-        recv = packed[:size].unsqueeze(0).repeat(N, 1).contiguous()
+        size = _C.view_pack_floats(max(counts[:N]))
+        recv = packed[:N, :size].contiguous()
         res["unpack_ms"][N] = timed(lambda: _C.view_block_unpack(recv, blocks, P))
         res["views_sparse_ms"][N] = timed(lambda: _C.gauss_backward_views(scene.means3D, None, scene.shs, D,
                                                                          scene.opacities, scene.scales,
                                                                          scene.rotations, 1.0, blocks, arena.views()))
         res["exchange_MB_per_rank"][N] = {"allgather_view_blocks": (N - 1) * nb * 4 / 1e6,
-                                          "allgather_sparse_blocks": (N - 1) * size * 4 / 1e6,
+                                          "allgather_sparse_blocks": (N - 1) * _C.view_pack_floats(max(counts[:N])) * 4 / 1e6,
                                           "allreduce_param_grads": 2 * (N - 1) / N * arena.flat.numel() * 4 / 1e6}
     print(json.dumps(res))
 
