@@ -240,9 +240,11 @@ void carve_recs(char* base, size_t R, size_t P, gsr::GradRecs* recs, gsr::GradRe
         recs->b = c.take<float4>(R);
         recs->c = c.take<float2>(R);
     }
+    recs->flag = GSR_REC_FLAG ? c.take<uint8_t>(R) : nullptr;
     sums->a = c.take<float4>(P);
     sums->b = c.take<float4>(P);
     sums->c = c.take<float2>(P);
+    sums->flag = nullptr;
     *total = align_up(c.off);
 }
 

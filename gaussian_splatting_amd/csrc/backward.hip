@@ -31,7 +31,8 @@ namespace gsr {
 // for entries before each tile's last contributor; instance (g, tile t) has one iff
 // key(g) = depth bits << 32 | g <= lim_key[t] (tile lists are sorted by key), and
 // the others are read as zeros without touching memory (render.hip, "Entries at
-// positions >= limit").
+// positions >= limit").  Of those, only entries with a gradient term have a record with
+// content; the rest wrote a zero content byte (GSR_REC_FLAG) and are skipped too.
 constexpr int kRecStride = 12;  // floats per Gaussian in the LDS hand-off of chunk totals (10 used), 48 B
 
 // Sums of the records of the wave's 64 consecutive Gaussians [g0, g0 + 64), one
@@ -103,7 +104,10 @@ __device__ __forceinline__ void reduce_records(int P, int g0, const uint32_t* __
         ty = ty * ow > k ? ty - 1 : ty;
         ty = (ty + 1) * ow <= k ? ty + 1 : ty;
         const uint32_t tile = (oy + ty) * gx + ox + (k - ty * ow);
-        return Slot{okey <= lim_key[tile], owner, seg0};
+        // GSR_REC_FLAG: a staged entry without a gradient term wrote its content byte only (the
+        // byte load does not wait for the limit key's)
+        const bool content = !GSR_REC_FLAG || recs.flag[e] != 0;
+        return Slot{okey <= lim_key[tile] && content, owner, seg0};
     };
     float4* part = reinterpret_cast<float4*>(s_rec);  // [64][3] float4: a Gaussian's chunk total
     Slot cur = E0 < E1 ? probe2(E0) : Slot{false, -1, lane};

@@ -174,7 +174,15 @@ struct GradRecs {
     float4* a;  // (dcolor.r, dcolor.g, dcolor.b, dinvdepth)
     float4* b;  // (dmean2D.x, dmean2D.y, dopacity_eff, dconic.b)
     float2* c;  // (dconic.a, dconic.c)
+    uint8_t* flag;  // per-instance records only (GSR_REC_FLAG): 1 = the record has content
 };
+// A/B switch: the render backward writes a record only for an entry with a gradient term (~half
+// of the staged entries at 1M@1080p) and one content byte for every staged entry; the reduction
+// reads the byte and skips the record of an entry without content, instead of every staged
+// entry's 48-byte record, zeros included.
+#ifndef GSR_REC_FLAG
+#define GSR_REC_FLAG 1
+#endif
 // The render backward's per-instance records (not the per-Gaussian sums, which stay three
 // arrays): GSR_REC_AOS interleaves them as 48-byte records a, b, (c, pad), so one instance's
 // three stores land in one or two cache lines instead of three.  Index strides:

@@ -541,10 +541,12 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
             }
         }
         __syncthreads();
-        if (has) {
+        const bool content = (written >> lane) & 1ull;
+        if (GSR_REC_FLAG && has) a.recs.flag[e] = content ? 1 : 0;
+        if (has && (content || !GSR_REC_FLAG)) {
             float4 ra = make_float4(0.f, 0.f, 0.f, 0.f), rb = ra;
             float2 rc = make_float2(0.f, 0.f);
-            if ((written >> lane) & 1ull) {
+            if (content) {
                 const float4 A = s_acc[lane][0], B = s_acc[lane][1], Cc = s_acc[lane][2];
                 // dL/dmean2D in NDC units (x 0.5 W, 0.5 H, CR/backward.cu:509-510,600-601);
                 // dL/dconic with the reference's -0.5 factors (CR/backward.cu:604-606).  (Applying
