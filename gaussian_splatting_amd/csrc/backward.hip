@@ -177,7 +177,9 @@ __global__ void __launch_bounds__(64) gauss_reduce_kernel(int P, const uint32_t*
                                                           const unsigned long long* __restrict__ lim_key,
                                                           GradRecs recs, GradRecs sums, uint32_t* __restrict__ flags,
                                                           const int* __restrict__ radii,
-                                                          const uint8_t* __restrict__ clamped) {
+                                                          const uint8_t* __restrict__ clamped,
+                                                          uint32_t* __restrict__ live,
+                                                          uint32_t* __restrict__ live_count, uint32_t live_cap) {
     __shared__ __attribute__((aligned(16))) float s_rec[64 * kRecStride];
     const int g = blockIdx.x * 64 + (int)threadIdx.x;
     float4 sa, sb;
@@ -191,14 +193,31 @@ __global__ void __launch_bounds__(64) gauss_reduce_kernel(int P, const uint32_t*
         // view-block flag word (gauss_bwd_views_kernel): bit 0 visible, bits 1-3 the SH clamp mask
         if (flags) flags[g] = (radii[g] > 0 ? 1u : 0u) | ((uint32_t)(clamped[g] & 7u) << 1);
     }
+    if (live) {
+        // append the Gaussians with a gradient (gauss_bwd's condition) to the live list: one
+        // atomic per wave; the list order varies from run to run, each entry's result does not
+        const bool lv = g < P && radii[g] > 0 &&
+                        ((sa.x != 0.f) | (sa.y != 0.f) | (sa.z != 0.f) | (sa.w != 0.f) | (sb.x != 0.f) |
+                         (sb.y != 0.f) | (sb.z != 0.f) | (sb.w != 0.f) | (sc.x != 0.f) | (sc.y != 0.f));
+        const unsigned long long m = __ballot(lv);
+        if (m) {  // uniform
+            const int lane = threadIdx.x;
+            const uint32_t shard = blockIdx.x % kLiveShards;
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(&live_count[shard * kLiveCntStride], (uint32_t)__popcll(m));
+            base = (uint32_t)__shfl((int)base, 0);
+            if (lv) live[(size_t)shard * live_cap + base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)g;
+        }
+    }
 }
 
 hipError_t launch_gauss_reduce(int P, const GeomState& g, uint32_t gx, const unsigned long long* lim_key,
                                const GradRecs& recs, const GradRecs& sums, uint32_t* flags, const int* radii,
-                               hipStream_t stream) {
+                               uint32_t* live, uint32_t* live_count, hipStream_t stream) {
     if (P == 0) return hipSuccess;
     hipLaunchKernelGGL(gauss_reduce_kernel, dim3((P + 63) / 64), dim3(64), 0, stream, P, g.rec_start, g.tiles_touched,
-                       g.rect, g.depth_key, gx, lim_key, recs, sums, flags, radii, g.clamped);
+                       g.rect, g.depth_key, gx, lim_key, recs, sums, flags, radii, g.clamped, live, live_count,
+                       live_list_cap((uint32_t)P));
     return hipGetLastError();
 }
 
@@ -518,18 +537,28 @@ constexpr int kGbShRows = GSR_GB_HALVES ? 32 : 64;
 #else
 #define GSR_GB_OCCUPANCY
 #endif
-template <int SH_MODE>
+// LIST: lane i of the grid takes entry i of the live list (the Gaussians with a gradient,
+// gauss_reduce), with per-lane SH access (kShGlobal); the outputs were zero-filled, so no other
+// row is touched.  At 1M@1080p that is ~2000 waves instead of 15625.
+template <int SH_MODE, bool LIST = false>
 __global__ void __launch_bounds__(64) GSR_GB_OCCUPANCY gauss_bwd_kernel(GaussBwdArgs a) {
     __shared__ __attribute__((aligned(16))) float s_sh[SH_MODE != kShGlobal ? kGbShRows * kShStride : 4];
     const int lane = threadIdx.x;
     const int g0 = blockIdx.x * 64;
-    const int idx = g0 + lane;
+    int idx = g0 + lane;
+    if constexpr (LIST) {  // block b: entries [64 (b / shards), +64) of shard b % shards
+        const uint32_t shard = blockIdx.x % kLiveShards, k0 = (blockIdx.x / kLiveShards) * 64;
+        const uint32_t n = a.live_count[shard * kLiveCntStride];
+        if (k0 >= n) return;  // uniform: past the shard's list (the grid is sized for the worst case)
+        idx = k0 + lane < n ? (int)a.live[(size_t)shard * a.live_cap + k0 + lane] : a.P;
+    }
     const int nvalid = min(64, a.P - g0);
     const int M = a.M;
 
     const ShAddr sh_src{a.shs, a.dc, M};
     const ShGradAddr sh_dst{a.dL_dsh, a.dL_ddc, M};
     constexpr bool kShLate = SH_MODE != kShGlobal && GSR_GB_HALVES;
+    static_assert(!LIST || kShLate || SH_MODE == kShGlobal, "the live list stages SH rows late (halves)");
     if constexpr (SH_MODE != kShGlobal && !kShLate) {
         // coalesced stage-in of the wave's SH rows (64 x 48 floats, either layout)
         sh_stage_in<64, 64, SH_MODE == kShLdsSplit>(sh_src, g0, nvalid, s_sh, kShStride, lane);
@@ -798,10 +827,14 @@ __global__ void __launch_bounds__(64) GSR_GB_OCCUPANCY gauss_bwd_kernel(GaussBwd
         // their lanes evaluate it in place, coalesced write-back of the 32 dL/dSH rows
         const unsigned long long need = __ballot(sh_late);  // rows whose SH is read at all
         for (int half = 0; half < 2; half++) {
-            const int rows = min(kGbShRows, nvalid - half * kGbShRows);
+            const int rows = LIST ? kGbShRows : min(kGbShRows, nvalid - half * kGbShRows);
             if (rows <= 0) break;  // wave-uniform
-            sh_stage_in<kGbShRows, 64, SH_MODE == kShLdsSplit>(sh_src, g0 + half * kGbShRows, rows, s_sh, kShStride,
-                                                              lane, need >> (half * kGbShRows));
+            if constexpr (LIST)  // the lanes' rows, wherever they are
+                sh_gather_in<kGbShRows, 64, SH_MODE == kShLdsSplit>(sh_src, sh_late ? idx : -1, half * kGbShRows, s_sh,
+                                                                   kShStride, lane);
+            else
+                sh_stage_in<kGbShRows, 64, SH_MODE == kShLdsSplit>(sh_src, g0 + half * kGbShRows, rows, s_sh,
+                                                                  kShStride, lane, need >> (half * kGbShRows));
             __syncthreads();
             if ((lane >> 5) == half && idx < a.P) {
                 float* row = &s_sh[(lane & 31) * kShStride];
@@ -823,10 +856,15 @@ __global__ void __launch_bounds__(64) GSR_GB_OCCUPANCY gauss_bwd_kernel(GaussBwd
                 }
             }
             __syncthreads();
-            if (a.dL_dsh || a.dL_ddc)
+            if constexpr (LIST) {
+                if (a.dL_dsh || a.dL_ddc)
+                    sh_gather_out<kGbShRows, 64, SH_MODE == kShLdsSplit>(sh_dst, sh_late ? idx : -1, half * kGbShRows,
+                                                                        s_sh, kShStride, lane);
+            } else if (a.dL_dsh || a.dL_ddc) {
                 sh_stage_out<kGbShRows, 64, SH_MODE == kShLdsSplit>(sh_dst, g0 + half * kGbShRows, rows, s_sh,
                                                                    kShStride, lane,
                                                                    a.sparse ? need >> (half * kGbShRows) : ~0ull);
+            }
             __syncthreads();
         }
     } else if constexpr (SH_MODE != kShGlobal) {
@@ -1229,6 +1267,19 @@ hipError_t launch_zero_fill(const FillArgs& f, hipStream_t stream) {
 hipError_t launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t stream) {
     if (a.P == 0) return hipSuccess;
     const dim3 grid((a.P + 63) / 64), block(64);
+    const bool lds_ok = a.shs && a.dL_dsh && a.M == 16 && (!a.dc || a.dL_ddc) &&
+                        ((reinterpret_cast<uintptr_t>(a.shs) & 15) == 0) &&
+                        ((reinterpret_cast<uintptr_t>(a.dL_dsh) & 15) == 0);
+    if (a.live && a.sparse) {  // the live list: kLiveShards x live_cap entries at most
+        const dim3 lgrid(kLiveShards * ((a.live_cap + 63) / 64));
+        if (lds_ok && a.dc)
+            hipLaunchKernelGGL((gauss_bwd_kernel<kShLdsSplit, true>), lgrid, block, 0, stream, a);
+        else if (lds_ok)
+            hipLaunchKernelGGL((gauss_bwd_kernel<kShLdsCombined, true>), lgrid, block, 0, stream, a);
+        else
+            hipLaunchKernelGGL((gauss_bwd_kernel<kShGlobal, true>), lgrid, block, 0, stream, a);
+        return hipGetLastError();
+    }
     const bool lds = a.shs && a.dL_dsh && a.M == 16 && (!a.dc || a.dL_ddc) &&
                      ((reinterpret_cast<uintptr_t>(a.shs) & 15) == 0) &&
                      ((reinterpret_cast<uintptr_t>(a.dL_dsh) & 15) == 0);

@@ -183,6 +183,16 @@ struct GradRecs {
 #ifndef GSR_REC_FLAG
 #define GSR_REC_FLAG 1
 #endif
+
+// The live list (backward scratch): the Gaussians with a gradient, appended by gauss_reduce for
+// the sparse gauss_bwd.  Sharded by reduction workgroup (one counter per 128-byte line): a single
+// counter took 15625 returning atomics in a row at 1M Gaussians (gauss_reduce 62 -> 201 us).
+constexpr int kLiveShards = 64;
+constexpr int kLiveCntStride = 32;  // uint32 per counter line
+__host__ __device__ inline uint32_t live_list_cap(uint32_t P) {  // entries per shard
+    const uint32_t waves = (P + 63) / 64;
+    return (waves + kLiveShards - 1) / kLiveShards * 64;
+}
 // The render backward's per-instance records (not the per-Gaussian sums, which stay three
 // arrays): GSR_REC_AOS interleaves them as 48-byte records a, b, (c, pad), so one instance's
 // three stores land in one or two cache lines instead of three.  Index strides:

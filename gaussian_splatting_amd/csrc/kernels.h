@@ -70,6 +70,7 @@ struct RenderBwdArgs {
     uint32_t full_cap;
     int seg_ck;                         // checkpoints per backward segment (segment = seg_ck * kCkStride)
     unsigned long long* census;         // diagnostic pair counts (gsr_census_set) or null
+    uint32_t* live_count;               // the live list's shard counters, zeroed here, or null
 };
 
 struct GaussBwdArgs {
@@ -103,6 +104,9 @@ struct GaussBwdArgs {
     float* dL_dscale;     // [P,3] or null
     float* dL_drot;       // [P,4] or null
     int sparse;           // outputs already zero (zero_fill on the side stream): write only non-zero rows
+    const uint32_t* live;        // sparse: the Gaussians with a gradient (gauss_reduce), or null
+    const uint32_t* live_count;  // per shard: its length (device), kLiveCntStride apart
+    uint32_t live_cap;           // entries per shard (live_list_cap)
 };
 
 // Zero-fill of up to kFillSegs float ranges (the backward's dense outputs), run on a side
@@ -211,6 +215,62 @@ __device__ __forceinline__ void sh_stage_out(const ShGradAddr& ga, int r0, int r
         if ((rowmask >> (i / 3)) & 1ull) dc[i] = lds[(i / 3) * stride + i % 3];
     }
 }
+
+// Gathered forms of sh_stage_in / sh_stage_out: row r of the staged block belongs to the Gaussian
+// held by lane row0 + r of the wave in `g` (negative: row not read / not written), in any order --
+// the live-list backward's rows.  Combined layout: 16-byte pieces (12 per row, rows are 16-byte
+// aligned); split layout: dwords (45-float rest rows are only 4-byte aligned) plus the dc triple.
+// All lanes must call them (the row owners' indices travel by shuffle).
+template <int ROWS, int THREADS, bool SPLIT>
+__device__ __forceinline__ void sh_gather_in(const ShAddr& sa, int g, int row0, float* lds, int stride, int tid) {
+    if constexpr (!SPLIT) {
+#pragma unroll
+        for (int k = 0; k < ROWS * (kShRowF / 4) / THREADS; k++) {
+            const int i4 = k * THREADS + tid, row = i4 / (kShRowF / 4), c4 = i4 - row * (kShRowF / 4);
+            const int gr = __shfl(g, row0 + row);
+            if (gr >= 0)
+                *reinterpret_cast<float4*>(&lds[row * stride + 4 * c4]) =
+                    reinterpret_cast<const float4*>(sa.shs + (size_t)gr * kShRowF)[c4];
+        }
+    } else {
+        for (int k = 0; k < (ROWS * kShRestF + THREADS - 1) / THREADS; k++) {
+            const int d = k * THREADS + tid, row = min(d / kShRestF, ROWS - 1), c = d - row * kShRestF;
+            const int gr = __shfl(g, row0 + row);
+            if (d < ROWS * kShRestF && gr >= 0) lds[row * stride + 3 + c] = sa.shs[(size_t)gr * kShRestF + c];
+        }
+        for (int k = 0; k < (ROWS * 3 + THREADS - 1) / THREADS; k++) {
+            const int d = k * THREADS + tid, row = min(d / 3, ROWS - 1), c = d - row * 3;
+            const int gr = __shfl(g, row0 + row);
+            if (d < ROWS * 3 && gr >= 0) lds[row * stride + c] = sa.dc[(size_t)gr * 3 + c];
+        }
+    }
+}
+
+template <int ROWS, int THREADS, bool SPLIT>
+__device__ __forceinline__ void sh_gather_out(const ShGradAddr& ga, int g, int row0, const float* lds, int stride,
+                                              int tid) {
+    if constexpr (!SPLIT) {
+#pragma unroll
+        for (int k = 0; k < ROWS * (kShRowF / 4) / THREADS; k++) {
+            const int i4 = k * THREADS + tid, row = i4 / (kShRowF / 4), c4 = i4 - row * (kShRowF / 4);
+            const int gr = __shfl(g, row0 + row);
+            if (gr >= 0)
+                reinterpret_cast<float4*>(ga.dsh + (size_t)gr * kShRowF)[c4] =
+                    *reinterpret_cast<const float4*>(&lds[row * stride + 4 * c4]);
+        }
+    } else {
+        for (int k = 0; k < (ROWS * kShRestF + THREADS - 1) / THREADS; k++) {
+            const int d = k * THREADS + tid, row = min(d / kShRestF, ROWS - 1), c = d - row * kShRestF;
+            const int gr = __shfl(g, row0 + row);
+            if (d < ROWS * kShRestF && gr >= 0) ga.dsh[(size_t)gr * kShRestF + c] = lds[row * stride + 3 + c];
+        }
+        for (int k = 0; k < (ROWS * 3 + THREADS - 1) / THREADS; k++) {
+            const int d = k * THREADS + tid, row = min(d / 3, ROWS - 1), c = d - row * 3;
+            const int gr = __shfl(g, row0 + row);
+            if (d < ROWS * 3 && gr >= 0) ga.ddc[(size_t)gr * 3 + c] = lds[row * stride + c];
+        }
+    }
+}
 // SH path of preprocess / gauss_bwd: per-lane global loads, or LDS staging of either layout
 enum ShMode { kShGlobal = 0, kShLdsCombined = 1, kShLdsSplit = 2 };
 
@@ -313,7 +373,7 @@ hipError_t launch_ssim_bwd(int planes, int H, int W, const float* img1, const fl
 // backward.hip
 hipError_t launch_gauss_reduce(int P, const GeomState& g, uint32_t gx, const unsigned long long* lim_key,
                                const GradRecs& recs, const GradRecs& sums, uint32_t* flags, const int* radii,
-                               hipStream_t stream);
+                               uint32_t* live, uint32_t* live_count, hipStream_t stream);
 // multi-view backward over gathered view blocks (backward.hip section 4)
 struct ViewsBwdArgs {
     int P, D, M;

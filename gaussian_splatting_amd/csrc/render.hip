@@ -325,6 +325,8 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
     // multiple of the checkpoint stride.  Units come longest first (bwd_units_kernel), so the
     // dispatcher deals equal-sized pieces of work round-robin over the SIMDs and the short ones
     // fill the slots that free up last -- no tile's full list ever sits on one SIMD.
+    if (blockIdx.x == 0 && threadIdx.x < kLiveShards && a.live_count)  // gauss_reduce appends
+        a.live_count[threadIdx.x * kLiveCntStride] = 0u;
     uint2 unit;
     {  // full segments first, then the partial ones, longest quarter first; shards in order.
         // All 40 list counters in one vector load, an inclusive DPP scan, and a ballot find the
