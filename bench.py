@@ -312,8 +312,11 @@ def main():
             work[f"{stage}_pairs_per_s"] = pairs / (t_ms * 1e-3) if t_ms > 0 else None
         if census:
             work["pairs_per_instance"] = census["fwd_pairs_blended"] / nr if nr else None
+        # BASELINE.json's metric names the headline workload; another --config says its own
+        metric = ("Gaussian-splats/sec fwd+bwd @1080p, 1M Gaussians" if args.config == "1m_1080p_sh3" else
+                  f"Gaussian-splats/sec fwd+bwd @{W}x{H}, {P} Gaussians ({args.config}; not the headline metric)")
         line = {
-            "metric": "Gaussian-splats/sec fwd+bwd @1080p, 1M Gaussians",
+            "metric": metric,
             "value": value,
             "unit": "Gaussian-splats/s",
             "n_gpus": world,
