@@ -263,6 +263,18 @@ int bwd_segment_checkpoints() {
     return v;
 }
 
+// K2 folded into K3 in capacity mode (GSR_FUSED_BIN, default 1).
+#ifndef GSR_FUSED_BIN_DEFAULT
+#define GSR_FUSED_BIN_DEFAULT 1
+#endif
+bool fused_binning_mode() {
+    static const bool v = [] {
+        const char* e = getenv("GSR_FUSED_BIN");
+        return e ? atoi(e) != 0 : GSR_FUSED_BIN_DEFAULT != 0;
+    }();
+    return v;
+}
+
 // Per (host thread, device): a pinned 8-byte slot that num_rendered is copied into and the
 // event recorded behind that copy.  The host waits on the event -- i.e. for the binning
 // counts -- and not for the whole stream, so the render kernels queued behind the copy keep
@@ -704,10 +716,14 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
     const size_t kNoCap = ~(size_t)0;
     TotalReadback* rb = nullptr;
     if (int rc = total_readback(&rb)) return rc;
+    // capacity mode: the binning buffer's capacity, known up front (the ranges are clamped to it)
+    const size_t C_hint = capacity_hint > 0 ? capacity_for((size_t)capacity_hint) : 0;
+    // capacity mode with LDS cursors: K2 folded into K3 (binning.hip FusedScan)
+    const bool fused = capacity_hint > 0 && bin_fused_ok(tiles) && fused_binning_mode();
     {
         StageScope sc(ST_BIN_COUNT, stream);
-        HIP_TRY(launch_bin_count(P, geom, gx, gy, img.ranges, capacity_hint > 0 ? (size_t)capacity_hint : kNoCap,
-                                 rb->dev, stream),
+        HIP_TRY(launch_bin_count(P, geom, gx, gy, img.ranges, capacity_hint > 0 ? C_hint : kNoCap,
+                                 fused ? nullptr : rb->dev, stream, fused),
                 "bin_count");
     }
     if (int rc = check_debug(debug, stream, "bin_count")) return rc;
@@ -734,7 +750,7 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
             return fail(GSR_ERR_OVERFLOW, "rasterize_forward: %llu tile instances exceed INT_MAX", *total);
         return GSR_OK;
     };
-    auto bin_and_render = [&](size_t C) -> int {
+    auto bin_and_render = [&](size_t C, bool fused_now) -> int {
         size_t bin_bytes = 0;
         carve_binning(nullptr, C, &bin_bytes);
         char* bbase = (char*)call_alloc(binning_alloc, binning_ctx, bin_bytes);
@@ -743,15 +759,21 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
         {
             // always launched: besides the keys (none when C == 0) it writes every Gaussian's
             // first record index, which the backward's reduction reads even when nothing
-            // was rendered
+            // was rendered (fused: also the ranges, classes and the count)
             StageScope sc(ST_BIN_SCATTER, stream);
-            HIP_TRY(launch_bin_scatter(P, geom, gx, gy, bin, C, stream), "bin_scatter");
+            HIP_TRY(launch_bin_scatter(P, geom, gx, gy, bin, C, stream, img.ranges, fused_now ? rb->dev : nullptr,
+                                       fused_now),
+                    "bin_scatter");
         }
+        if (fused_now)
+            if (int rc = queue_total()) return rc;
         if (int rc = check_debug(debug, stream, "bin_scatter")) return rc;
         if (C > 0) {
             {
                 StageScope sc(ST_TILE_SORT, stream);
-                HIP_TRY(launch_tile_sort(tiles, img.ranges, geom, bin, C, stream), "tile_sort");
+                HIP_TRY(launch_tile_sort(tiles, img.ranges, geom, bin, C, stream, fused_now,
+                                         (uint32_t)bin_cell_count(gx, gy)),
+                        "tile_sort");
             }
             if (int rc = check_debug(debug, stream, "tile_sort")) return rc;
         }
@@ -773,21 +795,25 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
 
     unsigned long long total = 0;
     size_t C = 0;
-    if (int rc = queue_total()) return rc;
+    if (!fused)
+        if (int rc = queue_total()) return rc;
     if (capacity_hint <= 0) {
         if (int rc = wait_total(&total)) return rc;
         C = capacity_for((size_t)total);
-        if (int rc = bin_and_render(C)) return rc;
+        if (int rc = bin_and_render(C, false)) return rc;
     } else {
         // everything is queued before the host waits, and it waits for the counts only
-        C = capacity_for((size_t)capacity_hint);
-        if (int rc = bin_and_render(C)) return rc;
+        C = C_hint;
+        if (int rc = bin_and_render(C, fused)) return rc;
         if (int rc = wait_total(&total)) return rc;
         if (total > C) {  // the hint was too small: recount (resets the cursors) and rebuild exactly
             g_rebuilds.fetch_add(1, std::memory_order_relaxed);
             C = capacity_for((size_t)total);
+            if (fused)  // (the fused sort re-zeroes the counters only when it ran: C > 0)
+                HIP_TRY(hipMemsetAsync(geom.tile_cnt, 0, sizeof(uint32_t) * (tiles + bin_cell_count(gx, gy)), stream),
+                        "bin counters");
             HIP_TRY(launch_bin_count(P, geom, gx, gy, img.ranges, C, nullptr, stream), "bin_count");
-            if (int rc = bin_and_render(C)) return rc;
+            if (int rc = bin_and_render(C, false)) return rc;
         }
     }
     if (num_rendered) *num_rendered = (int)total;

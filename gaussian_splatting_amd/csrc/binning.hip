@@ -252,14 +252,29 @@ __global__ void __launch_bounds__(kBinThreads) cell_scatter_kernel(int P, int ch
 }
 
 // ---- K1 ---------------------------------------------------------------------
+// FusedZero (K2 folded into K3, capacity mode): what K2 used to clear before the render, cleared
+// here instead (nothing reads them between K1 and K3's end): the render work-list counters, the
+// half-tile join words and the long-list class counters.
+struct FusedZero {
+    uint32_t* unit_cnt;            // null: not fused
+    unsigned long long* tile_join;
+    uint32_t* cls_count;
+};
+
 template <bool LDS>
 __global__ void __launch_bounds__(kBinThreads) tile_count_kernel(int P, int chunk, const uint2* __restrict__ rect,
                                                                  const uint32_t* __restrict__ tiles_touched,
                                                                  const uint4* __restrict__ order,
                                                                  const uint32_t* __restrict__ n_visible,
                                                                  uint32_t tiles, uint32_t gx, uint32_t* __restrict__ cnt,
-                                                                 uint32_t* __restrict__ chunk_off) {
+                                                                 uint32_t* __restrict__ chunk_off, FusedZero fz) {
     extern __shared__ uint32_t s_hist[];  // (tiles + 1) / 2 words: 16-bit counters (a chunk has < 65536 Gaussians)
+    if (fz.unit_cnt) {
+        if (blockIdx.x == 0 && threadIdx.x < kUnitLists * kUnitShards) fz.unit_cnt[threadIdx.x * kUnitCntStride] = 0u;
+        if (blockIdx.x == 0 && threadIdx.x < kSortClasses) fz.cls_count[threadIdx.x] = 0u;
+        for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < tiles; i += gridDim.x * blockDim.x)
+            fz.tile_join[i] = 0ull;
+    }
     const int V = (int)n_visible[0];
     const int g0 = blockIdx.x * chunk, g1 = min(V, g0 + chunk);  // positions in order[]
     const uint32_t words = (tiles + 1) / 2;
@@ -363,13 +378,26 @@ __global__ void __launch_bounds__(kBinThreads) tile_scan_kernel(uint32_t tiles, 
 }
 
 // ---- K3 ---------------------------------------------------------------------
+// Fused (capacity mode, LDS cursors): K2's scan folded in.  Every workgroup scans the tile counts
+// itself (8160 words at 1080p, read from L2) for its cursors; workgroup b also publishes the
+// ranges and long-list classes of every gridDim-th group of 8 tiles, workgroup 0 the instance
+// count.  A kernel boundary and K2's single-workgroup pass (13 us at 1M@1080p) disappear.
+struct FusedScan {
+    const uint32_t* cnt;          // null: not fused (tile_base holds K2's tile starts)
+    uint2* ranges;
+    u64* total;
+    u64* host_total;
+    uint32_t* cls_list;
+    uint32_t* cls_count;
+};
+
 template <bool LDS>
 __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
     int P, int chunk, const uint2* __restrict__ rect, const uint32_t* __restrict__ tiles_touched,
     const uint32_t* __restrict__ depth_key, const uint4* __restrict__ order, const uint32_t* __restrict__ n_visible,
     uint32_t tiles, uint32_t gx, uint32_t* __restrict__ tile_base,
     const uint32_t* __restrict__ chunk_off, const u64* __restrict__ chunk_total, u64* __restrict__ keys, u64 cap,
-    uint32_t* __restrict__ rec_start, float4* __restrict__ rec) {
+    uint32_t* __restrict__ rec_start, float4* __restrict__ rec, FusedScan fs) {
     extern __shared__ uint32_t s_cur[];  // tiles words
     __shared__ u64 s_tmp[kBinWaves];
     const int g0 = blockIdx.x * chunk, g1 = min(P, g0 + chunk);
@@ -379,7 +407,44 @@ __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
     // here (loads issued first, they land while the cursors load) instead of scanned in K2
     u64 before = 0;
     for (uint32_t c = threadIdx.x; c < blockIdx.x; c += blockDim.x) before += chunk_total[c];
-    if (LDS) {
+    if (LDS && fs.cnt) {
+        // the tile starts (K2's scan, redone by every workgroup), then this chunk's cursors
+        const uint32_t* off = chunk_off + (size_t)blockIdx.x * tiles;
+        u64 carry_t = 0;
+        for (uint32_t base = 0; base < tiles; base += kBinThreads * kScanV) {
+            const uint32_t b = base + threadIdx.x * kScanV;
+            uint32_t v[kScanV];
+            u64 run = 0;
+#pragma unroll
+            for (int i = 0; i < kScanV; i++) {
+                v[i] = b + i < tiles ? fs.cnt[b + i] : 0u;
+                run += v[i];
+            }
+            u64 all = 0;
+            u64 at = carry_t + block_exclusive_scan(run, s_tmp, &all);
+            const bool publish = (b / kScanV) % gridDim.x == blockIdx.x;  // this group's ranges and classes
+#pragma unroll
+            for (int i = 0; i < kScanV; i++) {
+                if (b + i < tiles) {
+                    s_cur[b + i] = (uint32_t)at + off[b + i];  // garbage where the chunk has no instance: unused
+                    if (publish) {
+                        const u64 lo = at < cap ? at : cap, hi = at + v[i] < cap ? at + v[i] : cap;
+                        fs.ranges[b + i] = make_uint2((uint32_t)lo, (uint32_t)hi);
+                        if (v[i] > kSortWaveMax) {
+                            const int c = v[i] <= kClass0Max ? 0 : 1;
+                            fs.cls_list[(size_t)c * tiles + atomicAdd(&fs.cls_count[c], 1u)] = b + i;
+                        }
+                    }
+                }
+                at += v[i];
+            }
+            carry_t += all;
+        }
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            fs.total[0] = carry_t;
+            if (fs.host_total) __hip_atomic_store(fs.host_total, carry_t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    } else if (LDS) {
         // this chunk's cursors: tile start + the chunk's offset inside the tile (K1); entries of
         // tiles the chunk does not touch are garbage and never used
         const uint32_t* off = chunk_off + (size_t)blockIdx.x * tiles;
@@ -702,8 +767,13 @@ constexpr uint32_t kBucketMinN = GSR_BUCKET_MIN_N;
 
 __global__ void __launch_bounds__(64) tile_sort_kernel(const uint2* __restrict__ ranges,
                                                        const u64* __restrict__ keys, u64 cap,
-                                                       uint32_t* __restrict__ gid_sorted) {
+                                                       uint32_t* __restrict__ gid_sorted,
+                                                       uint32_t* __restrict__ zero_cnt, uint32_t n_cells) {
     __shared__ BucketLds<64, kSortWaveMax, kSortWaveMax / 2> s;
+    if (zero_cnt && threadIdx.x == 0) {  // fused binning: K2's re-zeroing of the tile / cell counters
+        zero_cnt[blockIdx.x] = 0u;
+        if (blockIdx.x < n_cells) zero_cnt[gridDim.x + blockIdx.x] = 0u;
+    }
     const uint2 r = ranges[blockIdx.x];
     const uint32_t n = tile_len(r, cap);
     GSR_STAMP(g_st_sort, blockIdx.x, 0);
@@ -793,6 +863,8 @@ uint32_t bin_cells(uint32_t gx, uint32_t gy, uint32_t* cgx) {
     return *cgx * ((gy + kCell - 1) / kCell);
 }
 
+bool bin_fused_ok(uint32_t tiles) { return tiles <= kLdsTilesMax; }
+
 size_t bin_cell_count(uint32_t gx, uint32_t gy) {
     uint32_t cgx = 0;
     return bin_cells(gx, gy, &cgx);
@@ -801,7 +873,7 @@ size_t bin_cell_count(uint32_t gx, uint32_t gy) {
 // K0 + K1 + K2: spatial order, chunk instance totals, tile counts, ranges, tile starts,
 // chunk offsets, the long-list class lists and the instance count (g.total).
 hipError_t launch_bin_count(int P, const GeomState& g, uint32_t gx, uint32_t gy, uint2* ranges, size_t cap,
-                            unsigned long long* host_total, hipStream_t stream) {
+                            unsigned long long* host_total, hipStream_t stream, bool fused) {
     const uint32_t tiles = gx * gy;
     int chunk = 0;
     const int nchunks = bin_chunks(P, &chunk);
@@ -817,42 +889,50 @@ hipError_t launch_bin_count(int P, const GeomState& g, uint32_t gx, uint32_t gy,
     hipLaunchKernelGGL(cell_scatter_kernel, grid, block, cell_bytes, stream, P, chunk, g.rect, g.tiles_touched,
                        cells, cgx, g.cell_cnt, g.cell_off, g.depth_key, g.order, g.n_visible);
     const size_t hist_bytes = lds ? ((tiles + 1) / 2) * sizeof(uint32_t) : 0;
+    if (fused && !lds) return hipErrorInvalidValue;  // the fused scan needs the LDS cursors
+    const FusedZero fz = fused ? FusedZero{g.unit_cnt, g.tile_join, g.cls_count} : FusedZero{nullptr, nullptr, nullptr};
     if (lds)
         hipLaunchKernelGGL(tile_count_kernel<true>, grid, block, hist_bytes, stream, P, chunk, g.rect, g.tiles_touched,
-                           g.order, g.n_visible, tiles, gx, g.tile_cnt, g.chunk_off);
+                           g.order, g.n_visible, tiles, gx, g.tile_cnt, g.chunk_off, fz);
     else
         hipLaunchKernelGGL(tile_count_kernel<false>, grid, block, 0, stream, P, chunk, g.rect, g.tiles_touched,
-                           g.order, g.n_visible, tiles, gx, g.tile_cnt, g.chunk_off);
-    hipLaunchKernelGGL(tile_scan_kernel, dim3(1), block, 0, stream, tiles, g.tile_cnt, tiles + cells, g.unit_cnt, g.tile_join,
-                       ranges, g.tile_base, g.total, (u64*)host_total, (u64)cap, g.cls_list, g.cls_count);
+                           g.order, g.n_visible, tiles, gx, g.tile_cnt, g.chunk_off, fz);
+    if (!fused)  // (fused: K3 scans the counts itself)
+        hipLaunchKernelGGL(tile_scan_kernel, dim3(1), block, 0, stream, tiles, g.tile_cnt, tiles + cells, g.unit_cnt,
+                           g.tile_join, ranges, g.tile_base, g.total, (u64*)host_total, (u64)cap, g.cls_list,
+                           g.cls_count);
     return hipGetLastError();
 }
 
 // K3: scatter the keys into a binning buffer of capacity `cap` (after launch_bin_count).
 hipError_t launch_bin_scatter(int P, const GeomState& g, uint32_t gx, uint32_t gy, const BinningState& b, size_t cap,
-                              hipStream_t stream) {
+                              hipStream_t stream, uint2* ranges, unsigned long long* host_total, bool fused) {
     const uint32_t tiles = gx * gy;
     int chunk = 0;
     const int nchunks = bin_chunks(P, &chunk);
     const bool lds = tiles <= kLdsTilesMax;
     const dim3 grid(nchunks), block(kBinThreads);
     const size_t cur_bytes = lds ? tiles * sizeof(uint32_t) : 0;
+    if (fused && !lds) return hipErrorInvalidValue;
+    const FusedScan fs = fused ? FusedScan{g.tile_cnt, ranges, g.total, (u64*)host_total, g.cls_list, g.cls_count}
+                               : FusedScan{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     if (lds)
         hipLaunchKernelGGL(tile_scatter_kernel<true>, grid, block, cur_bytes, stream, P, chunk, g.rect,
                            g.tiles_touched, g.depth_key, g.order, g.n_visible, tiles, gx, g.tile_base, g.chunk_off,
-                           g.chunk_total, b.keys, (u64)cap, g.rec_start, g.rec);
+                           g.chunk_total, b.keys, (u64)cap, g.rec_start, g.rec, fs);
     else
         hipLaunchKernelGGL(tile_scatter_kernel<false>, grid, block, 0, stream, P, chunk, g.rect, g.tiles_touched,
                            g.depth_key, g.order, g.n_visible, tiles, gx, g.tile_base, g.chunk_off, g.chunk_total,
-                           b.keys, (u64)cap, g.rec_start, g.rec);
+                           b.keys, (u64)cap, g.rec_start, g.rec, fs);
     return hipGetLastError();
 }
 
 hipError_t launch_tile_sort(uint32_t tiles, const uint2* ranges, const GeomState& g, const BinningState& b,
-                            size_t cap, hipStream_t stream) {
+                            size_t cap, hipStream_t stream, bool zero_counts, uint32_t cells) {
     if (tiles == 0 || cap == 0) return hipSuccess;
     const u64 c = cap;
-    hipLaunchKernelGGL(tile_sort_kernel, dim3(tiles), dim3(64), 0, stream, ranges, b.keys, c, b.gid_sorted);
+    hipLaunchKernelGGL(tile_sort_kernel, dim3(tiles), dim3(64), 0, stream, ranges, b.keys, c, b.gid_sorted,
+                       zero_counts ? g.tile_cnt : nullptr, cells);
     // persistent class kernels: grids sized to fill the chip when their lists are long
     const auto grid = [&](uint32_t want) { return dim3(tiles < want ? tiles : want); };
     hipLaunchKernelGGL(tile_sort_class_kernel<0>, grid(2048), dim3(kClassThreads), 0, stream, ranges, b.keys, c,

@@ -348,13 +348,18 @@ hipError_t launch_mark_visible(int P, const float* means3D, const float* view, b
 // binning.hip
 size_t bin_chunk_count(int P);
 size_t bin_cell_count(uint32_t gx, uint32_t gy);
-// host_total: mapped coherent host memory K2 also writes the instance count to, or null
+// host_total: mapped coherent host memory K2 (or the fused K3) also writes the instance count to, or
+// null.  fused (capacity mode, LDS cursors): K2 is folded into K3 -- launch_bin_count runs K0 + K1
+// only, launch_bin_scatter scans the counts and publishes ranges / classes / the count, and
+// launch_tile_sort re-zeroes the tile and cell counters.
 hipError_t launch_bin_count(int P, const GeomState& g, uint32_t gx, uint32_t gy, uint2* ranges, size_t cap,
-                            unsigned long long* host_total, hipStream_t stream);
+                            unsigned long long* host_total, hipStream_t stream, bool fused = false);
 hipError_t launch_bin_scatter(int P, const GeomState& g, uint32_t gx, uint32_t gy, const BinningState& b, size_t cap,
-                              hipStream_t stream);
+                              hipStream_t stream, uint2* ranges = nullptr, unsigned long long* host_total = nullptr,
+                              bool fused = false);
 hipError_t launch_tile_sort(uint32_t tiles, const uint2* ranges, const GeomState& g, const BinningState& b,
-                            size_t cap, hipStream_t stream);
+                            size_t cap, hipStream_t stream, bool zero_counts = false, uint32_t cells = 0);
+bool bin_fused_ok(uint32_t tiles);  // the fused form applies (LDS cursors)
 // render.hip
 hipError_t launch_render_fwd(const RenderFwdArgs& a, hipStream_t stream);
 hipError_t launch_render_bwd(const RenderBwdArgs& a, size_t max_units, hipStream_t stream);
