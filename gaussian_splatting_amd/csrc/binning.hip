@@ -430,10 +430,6 @@ __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
                     if (publish) {
                         const u64 lo = at < cap ? at : cap, hi = at + v[i] < cap ? at + v[i] : cap;
                         fs.ranges[b + i] = make_uint2((uint32_t)lo, (uint32_t)hi);
-                        if (v[i] > kSortWaveMax) {
-                            const int c = v[i] <= kClass0Max ? 0 : 1;
-                            fs.cls_list[(size_t)c * tiles + atomicAdd(&fs.cls_count[c], 1u)] = b + i;
-                        }
                     }
                 }
                 at += v[i];
@@ -443,6 +439,34 @@ __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             fs.total[0] = carry_t;
             if (fs.host_total) __hip_atomic_store(fs.host_total, carry_t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        // this workgroup's long-list tiles into the class lists: counted in LDS, one global atomic
+        // per class reserves the workgroup's run (one global atomic per tile serialised ~30000
+        // returning atomics on one counter at 4K: +340 us), then each tile takes its slot
+        __shared__ uint32_t s_cls[kSortClasses], s_cbase[kSortClasses];
+        const uint32_t groups = (tiles + kScanV - 1) / kScanV;
+        const uint32_t my_groups = groups > blockIdx.x ? (groups - blockIdx.x + gridDim.x - 1) / gridDim.x : 0u;
+        if (threadIdx.x < kSortClasses) s_cls[threadIdx.x] = 0u;
+        __syncthreads();
+        for (uint32_t j = threadIdx.x; j < my_groups * kScanV; j += blockDim.x) {
+            const uint32_t t = (blockIdx.x + (j / kScanV) * gridDim.x) * kScanV + j % kScanV;
+            const uint32_t v = t < tiles ? fs.cnt[t] : 0u;
+            if (v > kSortWaveMax) atomicAdd(&s_cls[v <= kClass0Max ? 0 : 1], 1u);
+        }
+        __syncthreads();
+        if (threadIdx.x < kSortClasses) {
+            const uint32_t k = s_cls[threadIdx.x];
+            s_cbase[threadIdx.x] = k ? atomicAdd(&fs.cls_count[threadIdx.x], k) : 0u;
+            s_cls[threadIdx.x] = 0u;
+        }
+        __syncthreads();
+        for (uint32_t j = threadIdx.x; j < my_groups * kScanV; j += blockDim.x) {
+            const uint32_t t = (blockIdx.x + (j / kScanV) * gridDim.x) * kScanV + j % kScanV;
+            const uint32_t v = t < tiles ? fs.cnt[t] : 0u;
+            if (v > kSortWaveMax) {
+                const int c = v <= kClass0Max ? 0 : 1;
+                fs.cls_list[(size_t)c * tiles + s_cbase[c] + atomicAdd(&s_cls[c], 1u)] = t;
+            }
         }
     } else if (LDS) {
         // this chunk's cursors: tile start + the chunk's offset inside the tile (K1); entries of
