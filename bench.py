@@ -227,8 +227,8 @@ def main():
         if views and collective:  # N > 1: exchange the 44-B view blocks, every rank sums all views' gradients
             _C.rasterize_gaussians_backward_screen(*bwd, view_block=ex.local_block())
             ex.exchange()
-            _C.gauss_backward_views(scene.means3D, None, scene.shs, Kdeg, scene.opacities, scene.scales,
-                                    scene.rotations, 1.0, ex.gathered, out=arena.views())
+            ex.views_backward(scene.means3D, None, scene.shs, Kdeg, scene.opacities, scene.scales, scene.rotations,
+                              1.0, out=arena.views())
         else:
             _C.rasterize_gaussians_backward(*bwd, out=arena.views())
             if world > 1 and collective:

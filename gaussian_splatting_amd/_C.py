@@ -21,7 +21,7 @@ import torch
 from . import _lib
 
 __all__ = ["rasterize_gaussians", "rasterize_gaussians_backward", "rasterize_gaussians_backward_screen",
-           "gauss_backward_views", "view_block_floats", "view_pack_floats", "view_block_pack", "view_block_unpack",
+           "gauss_backward_views", "view_block_floats", "view_pack_floats", "view_block_pack", "view_block_unpack", "view_block_index",
            "mark_visible", "adamUpdate", "fusedssim",
            "fusedssim_backward", "forward_rebuilds", "debug_forward_state"]
 
@@ -386,6 +386,23 @@ def view_block_unpack(packed: torch.Tensor, blocks: torch.Tensor, P: int) -> Non
     _lib.check(rc, "view_block_unpack")
 
 
+def view_block_index(packed: torch.Tensor, flags: torch.Tensor, P: int) -> None:
+    """Index ``packed`` ([n_views, packed_floats]) for ``gauss_backward_views(..., flags=flags)``:
+    ``flags`` ([n_views, P] int32) is cleared and, for each packed entry i of view v, flags[v, g] =
+    i << 4 | its flag bits (include/gsr.h gsr_view_block_index)."""
+    _require_device(packed, "packed")
+    if packed.dim() != 2 or flags.dim() != 2 or tuple(flags.shape) != (packed.size(0), P):
+        raise RuntimeError(f"packed [n_views, k] and flags [n_views, {P}] expected")
+    if flags.dtype != torch.int32 or not (packed.is_contiguous() and flags.is_contiguous()):
+        raise RuntimeError("packed (float32) and flags (int32) must be contiguous")
+    cap = (packed.size(1) - 64) // 12
+    lib = _lib.load()
+    with torch.cuda.device(packed.device):
+        rc = lib.gsr_view_block_index(int(P), int(packed.size(0)), packed.data_ptr(), int(packed.size(1)),
+                                      flags.data_ptr(), int(cap), _stream_handle(packed.device))
+    _lib.check(rc, "view_block_index")
+
+
 def rasterize_gaussians_backward_screen(*args, view_block: torch.Tensor) -> None:
     """The backward of ``rasterize_gaussians_backward`` up to the per-Gaussian render-gradient
     sums, written with the camera into ``view_block`` (a float32 tensor of
@@ -439,17 +456,22 @@ def rasterize_gaussians_backward_screen(*args, view_block: torch.Tensor) -> None
     _lib.check(rc, "rasterize_gaussians_backward_screen")
 
 
-def gauss_backward_views(means3D, dc, sh, degree, opacities, scales, rotations, scale_modifier, blocks, out) -> None:
+def gauss_backward_views(means3D, dc, sh, degree, opacities, scales, rotations, scale_modifier, blocks, out,
+                         flags=None) -> None:
     """The per-Gaussian backward summed over ``blocks`` ([n_views, view_block_floats(P)] float32,
     e.g. an all-gathered exchange buffer), written into ``out`` (names as the ``out=`` of
     ``rasterize_gaussians_backward``: dL_dmeans3D, dL_ddc (when dc is given), dL_dsh,
-    dL_dopacity, dL_dscales, dL_drotations; contiguous float32)."""
+    dL_dopacity, dL_dscales, dL_drotations; contiguous float32).  With ``flags`` (from
+    ``view_block_index``), ``blocks`` are packed blocks ([n_views, packed_floats]) read in place."""
     _require_device(means3D, "means3D")
     device = means3D.device
     P = means3D.size(0)
-    nb = view_block_floats(P)
+    nb = view_block_floats(P) if flags is None else int(blocks.size(1)) if blocks.dim() == 2 else -1
     if blocks.dim() != 2 or blocks.size(1) != nb or blocks.dtype != torch.float32 or not blocks.is_contiguous():
         raise RuntimeError(f"blocks must be a contiguous float32 [n_views, {nb}] tensor")
+    if flags is not None and (tuple(flags.shape) != (blocks.size(0), P) or flags.dtype != torch.int32 or
+                              not flags.is_contiguous()):
+        raise RuntimeError(f"flags must be a contiguous int32 [{blocks.size(0)}, {P}] tensor")
     M = sh.size(1) if _present(sh) else 0
     need = {"dL_dmeans3D": (P, 3), "dL_dsh": (P, M, 3), "dL_dopacity": (P, 1), "dL_dscales": (P, 3),
             "dL_drotations": (P, 4)}
@@ -463,15 +485,18 @@ def gauss_backward_views(means3D, dc, sh, degree, opacities, scales, rotations, 
         return
     lib = _lib.load()
     ins = _Inputs(device)
+    geo = (P, int(degree), M, ins.req(means3D, "means3D"), ins.opt(dc, "dc") if _present(dc) else None,
+           ins.opt(sh, "sh"), ins.req(opacities, "opacities"), ins.req(scales, "scales"),
+           ins.req(rotations, "rotations", align16=True), float(scale_modifier), int(blocks.size(0)),
+           blocks.data_ptr(), nb)
+    outs = (out["dL_dmeans3D"].data_ptr(), out["dL_ddc"].data_ptr() if _present(dc) else None,
+            out["dL_dsh"].data_ptr() if M > 0 else None, out["dL_dopacity"].data_ptr(), out["dL_dscales"].data_ptr(),
+            out["dL_drotations"].data_ptr(), _stream_handle(device))
     with torch.cuda.device(device):
-        rc = lib.gsr_gauss_backward_views(
-            P, int(degree), M, ins.req(means3D, "means3D"), ins.opt(dc, "dc") if _present(dc) else None,
-            ins.opt(sh, "sh"), ins.req(opacities, "opacities"), ins.req(scales, "scales"),
-            ins.req(rotations, "rotations", align16=True), float(scale_modifier), int(blocks.size(0)),
-            blocks.data_ptr(), nb, out["dL_dmeans3D"].data_ptr(),
-            out["dL_ddc"].data_ptr() if _present(dc) else None, out["dL_dsh"].data_ptr() if M > 0 else None,
-            out["dL_dopacity"].data_ptr(), out["dL_dscales"].data_ptr(), out["dL_drotations"].data_ptr(),
-            _stream_handle(device))
+        if flags is None:
+            rc = lib.gsr_gauss_backward_views(*geo, *outs)
+        else:
+            rc = lib.gsr_gauss_backward_views_packed(*geo, flags.data_ptr(), *outs)
     _lib.check(rc, "gauss_backward_views")
 
 

@@ -1191,6 +1191,25 @@ int gsr_view_block_unpack(int P, int n_views, const float* packed, long long pac
     return GSR_OK;
 }
 
+int gsr_view_block_index(int P, int n_views, const float* packed, long long packed_floats, unsigned int* flags,
+                         long long cap, void* stream) {
+    g_err[0] = 0;
+    if (P <= 0 || n_views < 0 || cap < 0 || packed_floats < (long long)gsr::view_pack_floats(0))
+        return fail(GSR_ERR_ARGUMENT, "view_block_index: P=%d views=%d packed_floats=%lld cap=%lld", P, n_views,
+                    packed_floats, cap);
+    if ((size_t)packed_floats < gsr::view_pack_floats((size_t)cap))
+        return fail(GSR_ERR_ARGUMENT, "view_block_index: %lld floats per packed block cannot hold %lld entries",
+                    packed_floats, cap);
+    if (cap >= (1ll << 28)) return fail(GSR_ERR_ARGUMENT, "view_block_index: %lld entries exceed 2^28", cap);
+    if (n_views > 0 && (!packed || !flags)) return fail(GSR_ERR_ARGUMENT, "view_block_index: null pointer");
+    if ((reinterpret_cast<uintptr_t>(packed) & 15) || (packed_floats & 3))
+        return fail(GSR_ERR_ARGUMENT, "view_block_index: packed blocks must be 16-byte aligned");
+    HIP_TRY(gsr::launch_view_index((uint32_t)P, n_views, packed, (unsigned long long)packed_floats, flags,
+                                   (unsigned long long)cap, (hipStream_t)stream),
+            "view_block_index");
+    return GSR_OK;
+}
+
 int gsr_rasterize_backward_screen(int P, int D, int M, int R, const float* background, int width, int height,
                                   const float* means3D, const float* dc, const float* shs, const float* opacities,
                                   const float* scales, float scale_modifier, const float* rotations,
@@ -1246,18 +1265,23 @@ int gsr_debug_forward_state(int P, int width, int height, int R, int binning_cap
     return GSR_OK;
 }
 
-int gsr_gauss_backward_views(int P, int D, int M, const float* means3D, const float* dc, const float* shs,
-                             const float* opacities, const float* scales, const float* rotations, float scale_modifier,
-                             int n_views, const float* blocks, long long block_floats, float* dL_dmean3D,
-                             float* dL_ddc, float* dL_dsh, float* dL_dopacity, float* dL_dscale, float* dL_drot,
-                             void* stream) {
+namespace {
+int backward_views_impl(int P, int D, int M, const float* means3D, const float* dc, const float* shs,
+                        const float* opacities, const float* scales, const float* rotations, float scale_modifier,
+                        int n_views, const float* blocks, long long block_floats, const unsigned int* flags,
+                        float* dL_dmean3D, float* dL_ddc, float* dL_dsh, float* dL_dopacity, float* dL_dscale,
+                        float* dL_drot, void* stream) {
     using namespace gsr;
     g_err[0] = 0;
     if (P < 0 || n_views < 0) return fail(GSR_ERR_ARGUMENT, "gauss_backward_views: P=%d views=%d", P, n_views);
     if (P == 0) return GSR_OK;
-    if ((size_t)block_floats != view_block_floats((size_t)P))
+    if (!flags && (size_t)block_floats != view_block_floats((size_t)P))
         return fail(GSR_ERR_ARGUMENT, "gauss_backward_views: block of %lld floats, expected %zu", block_floats,
                     view_block_floats((size_t)P));
+    if (flags && (block_floats < (long long)view_pack_floats(0) || (block_floats & 3) ||
+                  (reinterpret_cast<uintptr_t>(blocks) & 15)))
+        return fail(GSR_ERR_ARGUMENT, "gauss_backward_views: packed blocks of %lld floats (16-byte aligned)",
+                    block_floats);
     if (!means3D || !opacities || !scales || !rotations || (n_views > 0 && !blocks) || !dL_dmean3D || !dL_dopacity ||
         !dL_dscale || !dL_drot)
         return fail(GSR_ERR_ARGUMENT, "gauss_backward_views: null pointer");
@@ -1273,6 +1297,7 @@ int gsr_gauss_backward_views(int P, int D, int M, const float* means3D, const fl
     a.means3D = means3D; a.shs = (dc && M == 0) ? nullptr : shs; a.dc = dc; a.opacities = opacities; a.scales = scales;
     a.rotations = rotations; a.scale_modifier = scale_modifier; a.n_views = n_views; a.blocks = blocks;
     a.block_floats = (size_t)block_floats;
+    a.flags = flags;
     a.dL_dmean3D = dL_dmean3D; a.dL_dsh = a.shs ? dL_dsh : nullptr; a.dL_ddc = dc ? dL_ddc : nullptr;
     a.dL_dopacity = dL_dopacity; a.dL_dscale = dL_dscale; a.dL_drot = dL_drot;
     {
@@ -1280,4 +1305,26 @@ int gsr_gauss_backward_views(int P, int D, int M, const float* means3D, const fl
         HIP_TRY(launch_gauss_bwd_views(a, (hipStream_t)stream), "gauss_backward_views");
     }
     return GSR_OK;
+}
+}  // namespace
+
+int gsr_gauss_backward_views(int P, int D, int M, const float* means3D, const float* dc, const float* shs,
+                             const float* opacities, const float* scales, const float* rotations, float scale_modifier,
+                             int n_views, const float* blocks, long long block_floats, float* dL_dmean3D,
+                             float* dL_ddc, float* dL_dsh, float* dL_dopacity, float* dL_dscale, float* dL_drot,
+                             void* stream) {
+    return backward_views_impl(P, D, M, means3D, dc, shs, opacities, scales, rotations, scale_modifier, n_views,
+                               blocks, block_floats, nullptr, dL_dmean3D, dL_ddc, dL_dsh, dL_dopacity, dL_dscale,
+                               dL_drot, stream);
+}
+
+int gsr_gauss_backward_views_packed(int P, int D, int M, const float* means3D, const float* dc, const float* shs,
+                                    const float* opacities, const float* scales, const float* rotations,
+                                    float scale_modifier, int n_views, const float* packed, long long packed_floats,
+                                    const unsigned int* flags, float* dL_dmean3D, float* dL_ddc, float* dL_dsh,
+                                    float* dL_dopacity, float* dL_dscale, float* dL_drot, void* stream) {
+    if (n_views > 0 && !flags) return fail(GSR_ERR_ARGUMENT, "gauss_backward_views_packed: null flags");
+    return backward_views_impl(P, D, M, means3D, dc, shs, opacities, scales, rotations, scale_modifier, n_views,
+                               packed, packed_floats, flags, dL_dmean3D, dL_ddc, dL_dsh, dL_dopacity, dL_dscale,
+                               dL_drot, stream);
 }

@@ -900,6 +900,40 @@ struct ShReadOnly {
     }
     __device__ __forceinline__ void store(int, float3) const {}
 };
+// A view's flag word and summed render gradients for Gaussian idx: from a dense view block, or
+// (packed mode, a.flags set) the flag array and the packed entry it indexes (entry layout:
+// index bits, a.xyz | a.w, b.xyz | b.w, c.xy, flag bits -- view_pack_scatter_kernel).
+template <bool PACKED>
+__device__ __forceinline__ uint32_t view_flag(const ViewsBwdArgs& a, const float* blk, int v, int idx) {
+    if constexpr (PACKED) return a.flags[(size_t)v * a.P + idx];
+    return reinterpret_cast<const uint32_t*>(blk + kViewBlockHeader + 10 * (size_t)a.P)[idx];
+}
+template <bool PACKED>
+__device__ __forceinline__ void view_sums(const ViewsBwdArgs& a, const float* blk, uint32_t flags, int idx,
+                                          float4& sa, float4& sb, float2& sc) {
+    if constexpr (PACKED) {
+        const float4* e = reinterpret_cast<const float4*>(blk + kViewBlockHeader + (size_t)kViewPackEntry * (flags >> 4));
+        const float4 e0 = e[0], e1 = e[1], e2 = e[2];
+        sa = make_float4(e0.y, e0.z, e0.w, e1.x);
+        sb = make_float4(e1.y, e1.z, e1.w, e2.x);
+        sc = make_float2(e2.y, e2.z);
+    } else {
+        const float* sums = blk + kViewBlockHeader;
+        sa = reinterpret_cast<const float4*>(sums)[idx];
+        sb = reinterpret_cast<const float4*>(sums + 4 * (size_t)a.P)[idx];
+        sc = reinterpret_cast<const float2*>(sums + 8 * (size_t)a.P)[idx];
+    }
+}
+template <bool PACKED>
+__device__ __forceinline__ float4 view_sums_a(const ViewsBwdArgs& a, const float* blk, uint32_t flags, int idx) {
+    if constexpr (PACKED) {
+        const float4* e = reinterpret_cast<const float4*>(blk + kViewBlockHeader + (size_t)kViewPackEntry * (flags >> 4));
+        const float4 e0 = e[0], e1 = e[1];
+        return make_float4(e0.y, e0.z, e0.w, e1.x);
+    }
+    return reinterpret_cast<const float4*>(blk + kViewBlockHeader)[idx];
+}
+
 template <int K0, int K1>
 struct ShBand {  // accumulates B_k g for K0 <= k < K1; SH values are not needed (read as 0)
     float* acc;
@@ -915,7 +949,7 @@ struct ShBand {  // accumulates B_k g for K0 <= k < K1; SH values are not needed
 
 // dL/dSH of band [K0, K1) for lane idx, summed over the views it is visible in; written to
 // the lane's LDS row (LDS variants) or straight to global memory
-template <int K0, int K1, int SH_MODE>
+template <int K0, int K1, int SH_MODE, bool PACKED>
 __device__ __forceinline__ void views_sh_band(const ViewsBwdArgs& a, int idx, float3 mean, float* row,
                                               const ShGradAddr& dst) {
     float acc[3 * (K1 - K0)];
@@ -924,12 +958,12 @@ __device__ __forceinline__ void views_sh_band(const ViewsBwdArgs& a, int idx, fl
 #pragma unroll 1
     for (int v = 0; v < a.n_views; v++) {
         const float* blk = a.blocks + (size_t)v * a.block_floats;
-        const uint32_t flags = reinterpret_cast<const uint32_t*>(blk + kViewBlockHeader + 10 * (size_t)a.P)[idx];
+        const uint32_t flags = view_flag<PACKED>(a, blk, v, idx);
         if (!(flags & 1u)) continue;
         const float* cp = blk + kViewCamPos;
         const float3 d = make_float3(mean.x - cp[0], mean.y - cp[1], mean.z - cp[2]);
         const float len = sqrtf(d.x * d.x + d.y * d.y + d.z * d.z);
-        const float4 sa = reinterpret_cast<const float4*>(blk + kViewBlockHeader)[idx];
+        const float4 sa = view_sums_a<PACKED>(a, blk, flags, idx);
         const float3 g = make_float3((flags & 2u) ? 0.f : sa.x, (flags & 4u) ? 0.f : sa.y, (flags & 8u) ? 0.f : sa.z);
         float ddx, ddy, ddz;
         sh_backward(ShBand<K0, K1>{acc}, a.D, a.M, d.x / len, d.y / len, d.z / len, g, ddx, ddy, ddz);
@@ -950,7 +984,7 @@ __device__ __forceinline__ void views_sh_band(const ViewsBwdArgs& a, int idx, fl
     }
 }
 
-template <int SH_MODE>
+template <int SH_MODE, bool PACKED>
 // 3 waves per SIMD (the LDS limit of the SH staging): the register allocator then spills a
 // few values but the per-view latency chains overlap better (8 views: 0.50 -> 0.44 ms, r1af)
 #ifndef GSR_VIEWS_WAVES
@@ -995,15 +1029,14 @@ __global__ void __launch_bounds__(64) GSR_VIEWS_OCCUPANCY gauss_bwd_views_kernel
 #pragma unroll 1
         for (int v = 0; v < a.n_views; v++) {
             const float* blk = a.blocks + (size_t)v * a.block_floats;
-            const uint32_t flags = reinterpret_cast<const uint32_t*>(blk + kViewBlockHeader + 10 * (size_t)a.P)[idx];
+            const uint32_t flags = view_flag<PACKED>(a, blk, v, idx);
             if (!(flags & 1u)) continue;  // not visible in view v: no gradient from it
             const ViewCam cam{blk + kViewCamView, blk + kViewCamProj, blk + kViewCamPos, blk[kViewCamTanX],
                               blk[kViewCamTanY],  blk[kViewCamFocalX], blk[kViewCamFocalY],
                               (int)__float_as_uint(blk[kViewCamAA]), (int)__float_as_uint(blk[kViewCamInvDepth])};
-            const float* sums = blk + kViewBlockHeader;
-            const float4 sa = reinterpret_cast<const float4*>(sums)[idx];
-            const float4 sb = reinterpret_cast<const float4*>(sums + 4 * (size_t)a.P)[idx];
-            const float2 sc = reinterpret_cast<const float2*>(sums + 8 * (size_t)a.P)[idx];
+            float4 sa, sb;
+            float2 sc;
+            view_sums<PACKED>(a, blk, flags, idx, sa, sb, sc);
             ViewOut o;
             view_backward(cam, gi, sa, sb, sc, (uint8_t)((flags >> 1) & 7u), true, a.D, M, shr, o);
             dmean.x += o.dmean.x; dmean.y += o.dmean.y; dmean.z += o.dmean.z;
@@ -1020,10 +1053,10 @@ __global__ void __launch_bounds__(64) GSR_VIEWS_OCCUPANCY gauss_bwd_views_kernel
     if constexpr (SH_MODE != kShGlobal) __syncthreads();  // the staged SH rows are read for the last time
     float* row = SH_MODE != kShGlobal ? &s_sh[lane * kShStride] : nullptr;
     if (valid) {
-        views_sh_band<0, 1, SH_MODE>(a, idx, mean, row, sh_dst);
-        if (a.D > 0) views_sh_band<1, 4, SH_MODE>(a, idx, mean, row, sh_dst);
-        if (a.D > 1) views_sh_band<4, 9, SH_MODE>(a, idx, mean, row, sh_dst);
-        if (a.D > 2) views_sh_band<9, 16, SH_MODE>(a, idx, mean, row, sh_dst);
+        views_sh_band<0, 1, SH_MODE, PACKED>(a, idx, mean, row, sh_dst);
+        if (a.D > 0) views_sh_band<1, 4, SH_MODE, PACKED>(a, idx, mean, row, sh_dst);
+        if (a.D > 1) views_sh_band<4, 9, SH_MODE, PACKED>(a, idx, mean, row, sh_dst);
+        if (a.D > 2) views_sh_band<9, 16, SH_MODE, PACKED>(a, idx, mean, row, sh_dst);
         const int K = (a.D + 1) * (a.D + 1);
         if constexpr (SH_MODE != kShGlobal) {
             for (int k = K; k < 16; k++) row[3 * k] = row[3 * k + 1] = row[3 * k + 2] = 0.f;
@@ -1046,12 +1079,20 @@ hipError_t launch_gauss_bwd_views(const ViewsBwdArgs& a, hipStream_t stream) {
     const bool lds = a.shs && a.dL_dsh && a.M == 16 && (!a.dc || a.dL_ddc) &&
                      ((reinterpret_cast<uintptr_t>(a.shs) & 15) == 0) &&
                      ((reinterpret_cast<uintptr_t>(a.dL_dsh) & 15) == 0);
-    if (lds && a.dc)
-        hipLaunchKernelGGL(gauss_bwd_views_kernel<kShLdsSplit>, grid, block, 0, stream, a);
-    else if (lds)
-        hipLaunchKernelGGL(gauss_bwd_views_kernel<kShLdsCombined>, grid, block, 0, stream, a);
-    else
-        hipLaunchKernelGGL(gauss_bwd_views_kernel<kShGlobal>, grid, block, 0, stream, a);
+    if (a.flags) {  // packed blocks (gsr_view_block_index)
+        if (lds && a.dc)
+            hipLaunchKernelGGL((gauss_bwd_views_kernel<kShLdsSplit, true>), grid, block, 0, stream, a);
+        else if (lds)
+            hipLaunchKernelGGL((gauss_bwd_views_kernel<kShLdsCombined, true>), grid, block, 0, stream, a);
+        else
+            hipLaunchKernelGGL((gauss_bwd_views_kernel<kShGlobal, true>), grid, block, 0, stream, a);
+    } else if (lds && a.dc) {
+        hipLaunchKernelGGL((gauss_bwd_views_kernel<kShLdsSplit, false>), grid, block, 0, stream, a);
+    } else if (lds) {
+        hipLaunchKernelGGL((gauss_bwd_views_kernel<kShLdsCombined, false>), grid, block, 0, stream, a);
+    } else {
+        hipLaunchKernelGGL((gauss_bwd_views_kernel<kShGlobal, false>), grid, block, 0, stream, a);
+    }
     return hipGetLastError();
 }
 
@@ -1224,6 +1265,42 @@ hipError_t launch_view_unpack(uint32_t P, int n_views, const float* packed, unsi
     const uint32_t gx = (uint32_t)((cap + kPackThreads - 1) / kPackThreads);
     hipLaunchKernelGGL(view_unpack_kernel, dim3(gx < 1024 ? (gx ? gx : 1) : 1024, n_views), dim3(kPackThreads), 0,
                        stream, P, packed, packed_floats, blocks, (unsigned long long)bf, cap);
+    return hipGetLastError();
+}
+
+// Packed mode of the multi-view backward: instead of rebuilding dense view blocks, each view's
+// flag array [P] is cleared and, for every packed entry i, set to i << 4 | its flag bits -- one
+// 4-byte store per entry instead of four scattered stores of 44 bytes.
+__global__ void __launch_bounds__(kPackThreads) view_index_kernel(uint32_t P, const float* __restrict__ packed,
+                                                                  unsigned long long packed_floats,
+                                                                  uint32_t* __restrict__ flags,
+                                                                  unsigned long long cap) {
+    const uint32_t v = blockIdx.y;
+    const float* pk = packed + v * packed_floats;
+    uint32_t n = __float_as_uint(pk[kViewPackCount]);
+    n = n < cap ? n : (uint32_t)cap;
+    uint32_t* f = flags + (size_t)v * P;
+    for (uint32_t i = blockIdx.x * kPackThreads + threadIdx.x; i < n; i += gridDim.x * kPackThreads) {
+        const float* e = pk + kViewBlockHeader + (size_t)kViewPackEntry * i;
+        const uint32_t g = __float_as_uint(e[0]);
+        if (g < P) f[g] = (i << 4) | (__float_as_uint(e[11]) & 15u);
+    }
+}
+
+__global__ void __launch_bounds__(kPackThreads) flags_zero_kernel(uint32_t P, uint32_t* __restrict__ flags) {
+    uint32_t* f = flags + (size_t)blockIdx.y * P;
+    for (uint32_t g = blockIdx.x * kPackThreads + threadIdx.x; g < P; g += gridDim.x * kPackThreads) f[g] = 0u;
+}
+
+hipError_t launch_view_index(uint32_t P, int n_views, const float* packed, unsigned long long packed_floats,
+                             uint32_t* flags, unsigned long long cap, hipStream_t stream) {
+    if (n_views <= 0) return hipSuccess;
+    const uint32_t gz = (P + kPackThreads - 1) / kPackThreads;
+    hipLaunchKernelGGL(flags_zero_kernel, dim3(gz < 1024 ? (gz ? gz : 1) : 1024, n_views), dim3(kPackThreads), 0,
+                       stream, P, flags);
+    const uint32_t gx = (uint32_t)((cap + kPackThreads - 1) / kPackThreads);
+    hipLaunchKernelGGL(view_index_kernel, dim3(gx < 1024 ? (gx ? gx : 1) : 1024, n_views), dim3(kPackThreads), 0,
+                       stream, P, packed, packed_floats, flags, cap);
     return hipGetLastError();
 }
 

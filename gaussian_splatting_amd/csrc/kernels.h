@@ -390,8 +390,12 @@ struct ViewsBwdArgs {
     const float* rotations;
     float scale_modifier;
     int n_views;
-    const float* blocks;  // [n_views][block_floats]
+    const float* blocks;  // [n_views][block_floats]: view blocks, or packed blocks when `flags` is set
     size_t block_floats;
+    // Packed mode (gsr_view_block_index): the flag word of Gaussian g in view v is flags[v * P + g],
+    // its entry index in view v's packed block << 4 | the block's flag bits; the sums are read from
+    // that packed entry, the camera from the packed block's header.  Null: dense view blocks.
+    const uint32_t* flags;
     float* dL_dmean3D;
     float* dL_dsh;
     float* dL_ddc;
@@ -402,6 +406,8 @@ struct ViewsBwdArgs {
 hipError_t launch_gauss_bwd_views(const ViewsBwdArgs& a, hipStream_t stream);
 hipError_t launch_view_pack(uint32_t P, const float* block, float* packed, unsigned long long cap, uint32_t* scratch,
                             uint32_t* count, hipStream_t stream);
+hipError_t launch_view_index(uint32_t P, int n_views, const float* packed, unsigned long long packed_floats,
+                             uint32_t* flags, unsigned long long cap, hipStream_t stream);
 hipError_t launch_view_unpack(uint32_t P, int n_views, const float* packed, unsigned long long packed_floats,
                               float* blocks, unsigned long long cap, hipStream_t stream);
 hipError_t launch_view_header(float* blk, const float* view, const float* proj, const float* campos, float tan_fovx,

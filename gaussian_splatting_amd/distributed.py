@@ -120,15 +120,16 @@ class ViewExchange:
     ``sparse=True`` (the default) sends the blocks packed (include/gsr.h, "Sparse view blocks"):
     only Gaussians with a non-zero render-gradient sum, 48 B each (~14% of a 1M@1080p frame's
     Gaussians), all-gathered at the largest count over the ranks (one scalar all-reduce read by
-    the host) and unpacked into ``gathered``.  Left-out Gaussians had all-zero sums, so the
-    result equals the dense exchange's bit for bit; when a packed block would not be smaller
-    than a dense one, the dense blocks are sent (``last_entries`` is then None).
+    the host); each rank then indexes the gathered packed blocks (one flag word per Gaussian and
+    view, ``_C.view_block_index``) and the multi-view backward reads the packed entries in place.
+    Left-out Gaussians had all-zero sums, so the result equals the dense exchange's bit for bit;
+    when a packed block would not be smaller than a dense one, the dense blocks are sent
+    (``last_entries`` is then None).
 
         ex = ViewExchange(P, device)
         _C.rasterize_gaussians_backward_screen(*backward_args, view_block=ex.local_block())
         ex.exchange()
-        _C.gauss_backward_views(means3D, dc, sh, degree, opacities, scales, rotations, 1.0,
-                                ex.gathered, out=arena.views())
+        ex.views_backward(means3D, dc, sh, degree, opacities, scales, rotations, 1.0, out=arena.views())
     """
 
     def __init__(self, P: int, device, group: Optional[dist.ProcessGroup] = None, sparse: bool = True):
@@ -149,6 +150,8 @@ class ViewExchange:
             nbytes = int(_lib_scratch_bytes(P))
             self._scratch = torch.empty(nbytes, dtype=torch.uint8, device=device)
             self._count = torch.zeros(1, dtype=torch.int32, device=device)
+            self._flags = torch.empty(self.world, P, dtype=torch.int32, device=device)  # view_block_index
+        self._view_blocks, self._view_flags = self.gathered, None  # what views_backward reads
 
     def local_block(self) -> torch.Tensor:
         """Where this rank's backward writes its view block."""
@@ -162,11 +165,13 @@ class ViewExchange:
         (``_C.view_block_pack``, 48 B each, ~14% of a 1M@1080p view), the ranks agree on the
         largest entry count (one scalar all-reduce, read by the host: the one synchronisation of
         the exchange), ONE ``all_gather_into_tensor`` moves the packed blocks at that size, and
-        ``_C.view_block_unpack`` rebuilds the dense blocks on every rank -- the same gathered
-        bytes, the same kernel, so the replicas stay bitwise equal, and ``gauss_backward_views``
-        gives the dense exchange's result (a Gaussian left out had all-zero sums)."""
+        ``_C.view_block_index`` indexes the gathered packed blocks on every rank -- the same
+        gathered bytes, the same kernel, so the replicas stay bitwise equal, and
+        ``views_backward`` gives the dense exchange's result (a Gaussian left out had all-zero
+        sums)."""
         from . import _C
 
+        self._view_blocks, self._view_flags = self.gathered, None
         if not self.sparse:
             if self.world > 1:
                 dist.all_gather_into_tensor(self.gathered.view(-1), self.local_block(), group=self.group)
@@ -194,7 +199,16 @@ class ViewExchange:
             dist.all_gather_into_tensor(recv.view(-1), self._packed[:size], group=self.group)
         else:
             recv[0].copy_(self._packed[:size])
-        _C.view_block_unpack(recv, self.gathered, self.P)
+        _C.view_block_index(recv, self._flags, self.P)
+        self._view_blocks, self._view_flags = recv, self._flags
+
+    def views_backward(self, means3D, dc, sh, degree, opacities, scales, rotations, scale_modifier, out) -> None:
+        """The per-Gaussian backward summed over all ranks' views (``_C.gauss_backward_views`` over
+        what the last ``exchange`` gathered: dense view blocks, or packed blocks and their index)."""
+        from . import _C
+
+        _C.gauss_backward_views(means3D, dc, sh, degree, opacities, scales, rotations, scale_modifier,
+                                self._view_blocks, out, flags=self._view_flags)
 
     def received_bytes(self) -> int:
         """Bytes this rank received from the others in the last exchange."""
@@ -209,12 +223,16 @@ class ViewExchange:
     def means2D_grad(self, rank: Optional[int] = None) -> torch.Tensor:
         """dL/dmeans2D (x, y) of a rank's view, [P, 2]: the densification statistics' input
         (train.py:215).  This rank's own view (and every view of a dense exchange) is a strided
-        view of its block; another rank's view after a sparse exchange is a copy with zeros for
-        the Gaussians its packed block left out (the unpack clears only their flag words)."""
+        view of its block; another rank's view after a sparse exchange is built from its packed
+        entries, zeros for the Gaussians the packed block left out."""
         r = self.rank if rank is None else rank
-        b = self._local if (self.sparse and r == self.rank) else self.gathered[r]
-        g = b[64 + 4 * self.P: 64 + 8 * self.P].view(self.P, 4)[:, :2]
-        if not self.sparse or r == self.rank or self.last_entries is None:
-            return g
-        flags = b[64 + 10 * self.P: 64 + 11 * self.P].view(torch.int32)
-        return torch.where((flags & 1).bool()[:, None], g, torch.zeros((), dtype=g.dtype, device=g.device))
+        if self.sparse and r == self.rank:
+            return self._local[64 + 4 * self.P: 64 + 8 * self.P].view(self.P, 4)[:, :2]
+        if self._view_flags is None:  # dense blocks
+            return self.gathered[r][64 + 4 * self.P: 64 + 8 * self.P].view(self.P, 4)[:, :2]
+        pk = self._view_blocks[r]  # packed: scatter its entries' (b.x, b.y) -- entry layout, include/gsr.h
+        n = int(pk[63].view(torch.int32).item())
+        ent = pk[64: 64 + 12 * n].view(n, 12)
+        g = torch.zeros(self.P, 2, dtype=pk.dtype, device=pk.device)
+        g[ent[:, 0].view(torch.int32).long()] = ent[:, 5:7]
+        return g

@@ -216,6 +216,21 @@ int gsr_view_block_pack(int P, const float* view_block, float* packed, long long
 int gsr_view_block_unpack(int P, int n_views, const float* packed, long long packed_floats, float* blocks,
                           long long cap, void* stream);
 
+/* Packed mode of the multi-view backward (what ViewExchange uses): no dense blocks are rebuilt.
+ * gsr_view_block_index: flags ([n_views][P] uint32) cleared, then for entry i of packed block v,
+ *   flags[v * P + g] = i << 4 | the entry's flag bits (cap < 2^28 entries).  One 4-byte store per
+ *   entry instead of the unpack's 44 bytes scattered over four arrays.
+ * gsr_gauss_backward_views_packed: gsr_gauss_backward_views over the packed blocks themselves
+ *   (camera from each packed header, sums from the entry its flag word indexes); the same result
+ *   as over the unpacked blocks. */
+int gsr_view_block_index(int P, int n_views, const float* packed, long long packed_floats, unsigned int* flags,
+                         long long cap, void* stream);
+int gsr_gauss_backward_views_packed(int P, int D, int M, const float* means3D, const float* dc, const float* shs,
+                                    const float* opacities, const float* scales, const float* rotations,
+                                    float scale_modifier, int n_views, const float* packed, long long packed_floats,
+                                    const unsigned int* flags, float* dL_dmean3D, float* dL_ddc, float* dL_dsh,
+                                    float* dL_dopacity, float* dL_dscale, float* dL_drot, void* stream);
+
 /* Frustum test, view-space z > 0.2 (CudaRasterizer::Rasterizer::markVisible).
  * `present` is P bytes (bool). */
 int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,

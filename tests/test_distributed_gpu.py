@@ -75,8 +75,8 @@ def _worker(rank, port, outdir):
             _C.rasterize_gaussians_backward_screen(*bwd, view_block=ex.local_block())
             ex.exchange()
             arena2 = GradArena(CASE.P, M, dev)
-            _C.gauss_backward_views(d("means3D"), None, d("shs"), inp["sh_degree"], d("opacities"), d("scales"),
-                                    d("rotations"), 1.0, ex.gathered, out=arena2.views())
+            ex.views_backward(d("means3D"), None, d("shs"), inp["sh_degree"], d("opacities"), d("scales"),
+                              d("rotations"), 1.0, out=arena2.views())
             torch.cuda.synchronize()
             np.save(os.path.join(outdir, f"{mode}{rank}.npy"), arena2.flat.cpu().numpy())
             m2d = np.stack([ex.means2D_grad(r).cpu().numpy() for r in range(WORLD)])  # densification input

@@ -63,7 +63,7 @@ def _single_and_block(inp, case, dev, split):
     return dict(zip(names, out)), block, t
 
 
-def _views_backward(t, blocks, split, dev):
+def _views_backward(t, blocks, split, dev, flags=None):
     from gaussian_splatting_amd import _C
 
     P = t["means3D"].shape[0]
@@ -76,11 +76,11 @@ def _views_backward(t, blocks, split, dev):
         out["dL_ddc"] = torch.empty(P, 1, 3, device=dev)
         out["dL_dsh"] = torch.empty(P, M - 1, 3, device=dev)
         _C.gauss_backward_views(t["means3D"], dc, rest, t["sh_degree"], t["opacities"], t["scales"], t["rotations"],
-                                t["scale_modifier"], blocks, out)
+                                t["scale_modifier"], blocks, out, flags=flags)
     else:
         out["dL_dsh"] = torch.empty(P, M, 3, device=dev)
         _C.gauss_backward_views(t["means3D"], None, sh, t["sh_degree"], t["opacities"], t["scales"], t["rotations"],
-                                t["scale_modifier"], blocks, out)
+                                t["scale_modifier"], blocks, out, flags=flags)
     return out
 
 
@@ -180,6 +180,19 @@ def test_sparse_blocks_pack_unpack(split):
     # the NaN sums of the left-out Gaussians must not reach the gradients
     got = _views_backward(t, unpacked, split, dev)
     ref = _views_backward(t, dense, split, dev)
+    for k in ref:
+        assert torch.equal(got[k], ref[k]), k
+    # packed mode: the index (one flag word per Gaussian and view) and the backward over the packed
+    # blocks in place give the same result
+    flags = torch.full((len(blocks), P), -1, dtype=torch.int32, device=dev)
+    _C.view_block_index(recv, flags, P)
+    for v, b in enumerate(blocks):
+        live = _live(b, P)
+        f = flags[v]
+        assert bool((f[~live] == 0).all())
+        assert torch.equal(f[live] & 15, b[64 + 10 * P: 64 + 11 * P].view(torch.int32)[live] & 15)
+        assert torch.equal(f[live] >> 4, torch.arange(int(live.sum()), dtype=torch.int32, device=dev))
+    got = _views_backward(t, recv, split, dev, flags=flags)
     for k in ref:
         assert torch.equal(got[k], ref[k]), k
     # a packed block smaller than the count: the count is reported whole, cap entries are written

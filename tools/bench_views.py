@@ -105,6 +105,11 @@ def main():
         size = _C.view_pack_floats(max(counts[:N]))
         recv = packed[:N, :size].contiguous()
         res["unpack_ms"][N] = timed(lambda: _C.view_block_unpack(recv, blocks, P))
+        flags = torch.empty(N, P, dtype=torch.int32, device=dev)
+        res.setdefault("index_ms", {})[N] = timed(lambda: _C.view_block_index(recv, flags, P))
+        res.setdefault("views_packed_ms", {})[N] = timed(lambda: _C.gauss_backward_views(
+            scene.means3D, None, scene.shs, D, scene.opacities, scene.scales, scene.rotations, 1.0, recv,
+            arena.views(), flags=flags))
         res["views_sparse_ms"][N] = timed(lambda: _C.gauss_backward_views(scene.means3D, None, scene.shs, D,
                                                                          scene.opacities, scene.scales,
                                                                          scene.rotations, 1.0, blocks, arena.views()))
