@@ -226,7 +226,7 @@ def main():
                binning, img, False, False)
         if views and collective:  # N > 1: exchange the 44-B view blocks, every rank sums all views' gradients
             _C.rasterize_gaussians_backward_screen(*bwd, view_block=ex.local_block())
-            ex.exchange()
+            ex.exchange(zero=arena.flat)  # the outputs zeroed beside the exchange; a live-list backward
             ex.views_backward(scene.means3D, None, scene.shs, Kdeg, scene.opacities, scene.scales, scene.rotations,
                               1.0, out=arena.views())
         else:

@@ -22,6 +22,7 @@ from . import _lib
 
 __all__ = ["rasterize_gaussians", "rasterize_gaussians_backward", "rasterize_gaussians_backward_screen",
            "gauss_backward_views", "view_block_floats", "view_pack_floats", "view_block_pack", "view_block_unpack", "view_block_index",
+           "views_live_floats", "views_live_list",
            "mark_visible", "adamUpdate", "fusedssim",
            "fusedssim_backward", "forward_rebuilds", "debug_forward_state"]
 
@@ -403,6 +404,26 @@ def view_block_index(packed: torch.Tensor, flags: torch.Tensor, P: int) -> None:
     _lib.check(rc, "view_block_index")
 
 
+def views_live_floats(P: int) -> int:
+    """int32 words of a live-list buffer for ``views_live_list`` (include/gsr.h)."""
+    return int(_lib.load().gsr_views_live_floats(int(P)))
+
+
+def views_live_list(flags: torch.Tensor, live: torch.Tensor, P: int) -> None:
+    """The Gaussians some view flags (``flags`` from ``view_block_index``) into ``live``
+    (int32, ``views_live_floats(P)`` words), for ``gauss_backward_views(..., live=live)``."""
+    _require_device(flags, "flags")
+    if flags.dim() != 2 or flags.size(1) != P or flags.dtype != torch.int32 or not flags.is_contiguous():
+        raise RuntimeError(f"flags must be a contiguous int32 [n_views, {P}] tensor")
+    if live.dtype != torch.int32 or live.numel() < views_live_floats(P) or not live.is_contiguous():
+        raise RuntimeError(f"live must be a contiguous int32 tensor of {views_live_floats(P)} words")
+    lib = _lib.load()
+    with torch.cuda.device(flags.device):
+        rc = lib.gsr_views_live_list(int(P), int(flags.size(0)), flags.data_ptr(), live.data_ptr(),
+                                     _stream_handle(flags.device))
+    _lib.check(rc, "views_live_list")
+
+
 def rasterize_gaussians_backward_screen(*args, view_block: torch.Tensor) -> None:
     """The backward of ``rasterize_gaussians_backward`` up to the per-Gaussian render-gradient
     sums, written with the camera into ``view_block`` (a float32 tensor of
@@ -457,12 +478,14 @@ def rasterize_gaussians_backward_screen(*args, view_block: torch.Tensor) -> None
 
 
 def gauss_backward_views(means3D, dc, sh, degree, opacities, scales, rotations, scale_modifier, blocks, out,
-                         flags=None) -> None:
+                         flags=None, live=None) -> None:
     """The per-Gaussian backward summed over ``blocks`` ([n_views, view_block_floats(P)] float32,
     e.g. an all-gathered exchange buffer), written into ``out`` (names as the ``out=`` of
     ``rasterize_gaussians_backward``: dL_dmeans3D, dL_ddc (when dc is given), dL_dsh,
     dL_dopacity, dL_dscales, dL_drotations; contiguous float32).  With ``flags`` (from
-    ``view_block_index``), ``blocks`` are packed blocks ([n_views, packed_floats]) read in place."""
+    ``view_block_index``), ``blocks`` are packed blocks ([n_views, packed_floats]) read in place;
+    with ``live`` too (``views_live_list``) only the listed Gaussians' rows are written -- the
+    caller zeroes ``out`` beforehand."""
     _require_device(means3D, "means3D")
     device = means3D.device
     P = means3D.size(0)
@@ -495,8 +518,10 @@ def gauss_backward_views(means3D, dc, sh, degree, opacities, scales, rotations, 
     with torch.cuda.device(device):
         if flags is None:
             rc = lib.gsr_gauss_backward_views(*geo, *outs)
-        else:
+        elif live is None:
             rc = lib.gsr_gauss_backward_views_packed(*geo, flags.data_ptr(), *outs)
+        else:
+            rc = lib.gsr_gauss_backward_views_live(*geo, flags.data_ptr(), live.data_ptr(), *outs)
     _lib.check(rc, "gauss_backward_views")
 
 

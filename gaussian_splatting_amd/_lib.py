@@ -74,6 +74,8 @@ SIGNATURES = {
     "gsr_view_block_pack": (_i, [_i, _vp, _vp, ctypes.c_longlong, _vp, _vp, _vp]),
     "gsr_view_block_unpack": (_i, [_i, _i, _vp, ctypes.c_longlong, _vp, ctypes.c_longlong, _vp]),
     "gsr_view_block_index": (_i, [_i, _i, _vp, ctypes.c_longlong, _vp, ctypes.c_longlong, _vp]),
+    "gsr_views_live_floats": (ctypes.c_ulonglong, [_i]),
+    "gsr_views_live_list": (_i, [_i, _i, _vp, _vp, _vp]),
     "gsr_rasterize_backward_screen": (_i, [_i, _i, _i, _i, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp,
                                            _vp, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, ALLOC_FN, _vp, _vp, _i,
                                            ctypes.c_size_t, _vp]),
@@ -81,6 +83,8 @@ SIGNATURES = {
                                       _vp, _vp, _vp, _vp, _vp, _vp]),
     "gsr_gauss_backward_views_packed": (_i, [_i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _f, _i, _vp, ctypes.c_longlong,
                                              _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "gsr_gauss_backward_views_live": (_i, [_i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _f, _i, _vp, ctypes.c_longlong,
+                                           _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gsr_debug_forward_state": (_i, [_i, _i, _i, _i, _i, ctypes.c_size_t, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gsr_forward_rebuilds": (ctypes.c_longlong, []),
     "gsr_last_error": (ctypes.c_char_p, []),

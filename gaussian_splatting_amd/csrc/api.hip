@@ -1269,8 +1269,8 @@ namespace {
 int backward_views_impl(int P, int D, int M, const float* means3D, const float* dc, const float* shs,
                         const float* opacities, const float* scales, const float* rotations, float scale_modifier,
                         int n_views, const float* blocks, long long block_floats, const unsigned int* flags,
-                        float* dL_dmean3D, float* dL_ddc, float* dL_dsh, float* dL_dopacity, float* dL_dscale,
-                        float* dL_drot, void* stream) {
+                        const unsigned int* live, const unsigned int* live_count, float* dL_dmean3D, float* dL_ddc,
+                        float* dL_dsh, float* dL_dopacity, float* dL_dscale, float* dL_drot, void* stream) {
     using namespace gsr;
     g_err[0] = 0;
     if (P < 0 || n_views < 0) return fail(GSR_ERR_ARGUMENT, "gauss_backward_views: P=%d views=%d", P, n_views);
@@ -1298,6 +1298,9 @@ int backward_views_impl(int P, int D, int M, const float* means3D, const float* 
     a.rotations = rotations; a.scale_modifier = scale_modifier; a.n_views = n_views; a.blocks = blocks;
     a.block_floats = (size_t)block_floats;
     a.flags = flags;
+    a.live = live;
+    a.live_count = live_count;
+    a.live_cap = live_list_cap((uint32_t)P);
     a.dL_dmean3D = dL_dmean3D; a.dL_dsh = a.shs ? dL_dsh : nullptr; a.dL_ddc = dc ? dL_ddc : nullptr;
     a.dL_dopacity = dL_dopacity; a.dL_dscale = dL_dscale; a.dL_drot = dL_drot;
     {
@@ -1314,8 +1317,8 @@ int gsr_gauss_backward_views(int P, int D, int M, const float* means3D, const fl
                              float* dL_ddc, float* dL_dsh, float* dL_dopacity, float* dL_dscale, float* dL_drot,
                              void* stream) {
     return backward_views_impl(P, D, M, means3D, dc, shs, opacities, scales, rotations, scale_modifier, n_views,
-                               blocks, block_floats, nullptr, dL_dmean3D, dL_ddc, dL_dsh, dL_dopacity, dL_dscale,
-                               dL_drot, stream);
+                               blocks, block_floats, nullptr, nullptr, nullptr, dL_dmean3D, dL_ddc, dL_dsh, dL_dopacity,
+                               dL_dscale, dL_drot, stream);
 }
 
 int gsr_gauss_backward_views_packed(int P, int D, int M, const float* means3D, const float* dc, const float* shs,
@@ -1325,6 +1328,36 @@ int gsr_gauss_backward_views_packed(int P, int D, int M, const float* means3D, c
                                     float* dL_dopacity, float* dL_dscale, float* dL_drot, void* stream) {
     if (n_views > 0 && !flags) return fail(GSR_ERR_ARGUMENT, "gauss_backward_views_packed: null flags");
     return backward_views_impl(P, D, M, means3D, dc, shs, opacities, scales, rotations, scale_modifier, n_views,
-                               packed, packed_floats, flags, dL_dmean3D, dL_ddc, dL_dsh, dL_dopacity, dL_dscale,
-                               dL_drot, stream);
+                               packed, packed_floats, flags, nullptr, nullptr, dL_dmean3D, dL_ddc, dL_dsh, dL_dopacity,
+                               dL_dscale, dL_drot, stream);
+}
+
+unsigned long long gsr_views_live_floats(int P) {
+    return P > 0 ? (unsigned long long)gsr::kLiveShards * gsr::live_list_cap((uint32_t)P) +
+                       (unsigned long long)gsr::kLiveShards * gsr::kLiveCntStride
+                 : 0ull;
+}
+
+int gsr_views_live_list(int P, int n_views, const unsigned int* flags, unsigned int* live, void* stream) {
+    g_err[0] = 0;
+    if (P < 0 || n_views < 0) return fail(GSR_ERR_ARGUMENT, "views_live_list: P=%d views=%d", P, n_views);
+    if (P == 0) return GSR_OK;
+    if (!live || (n_views > 0 && !flags)) return fail(GSR_ERR_ARGUMENT, "views_live_list: null pointer");
+    unsigned int* count = live + (size_t)gsr::kLiveShards * gsr::live_list_cap((uint32_t)P);
+    HIP_TRY(gsr::launch_views_live((uint32_t)P, n_views, flags, live, count, (hipStream_t)stream), "views_live_list");
+    return GSR_OK;
+}
+
+int gsr_gauss_backward_views_live(int P, int D, int M, const float* means3D, const float* dc, const float* shs,
+                                  const float* opacities, const float* scales, const float* rotations,
+                                  float scale_modifier, int n_views, const float* packed, long long packed_floats,
+                                  const unsigned int* flags, const unsigned int* live, float* dL_dmean3D,
+                                  float* dL_ddc, float* dL_dsh, float* dL_dopacity, float* dL_dscale, float* dL_drot,
+                                  void* stream) {
+    if (n_views > 0 && (!flags || !live)) return fail(GSR_ERR_ARGUMENT, "gauss_backward_views_live: null list");
+    const unsigned int* count = live ? live + (size_t)gsr::kLiveShards * gsr::live_list_cap((uint32_t)(P > 0 ? P : 0))
+                                     : nullptr;
+    return backward_views_impl(P, D, M, means3D, dc, shs, opacities, scales, rotations, scale_modifier, n_views,
+                               packed, packed_floats, flags, live, count, dL_dmean3D, dL_ddc, dL_dsh, dL_dopacity,
+                               dL_dscale, dL_drot, stream);
 }

@@ -984,7 +984,7 @@ __device__ __forceinline__ void views_sh_band(const ViewsBwdArgs& a, int idx, fl
     }
 }
 
-template <int SH_MODE, bool PACKED>
+template <int SH_MODE, bool PACKED, bool LIST = false>
 // 3 waves per SIMD (the LDS limit of the SH staging): the register allocator then spills a
 // few values but the per-view latency chains overlap better (8 views: 0.50 -> 0.44 ms, r1af)
 #ifndef GSR_VIEWS_WAVES
@@ -999,13 +999,22 @@ __global__ void __launch_bounds__(64) GSR_VIEWS_OCCUPANCY gauss_bwd_views_kernel
     __shared__ __attribute__((aligned(16))) float s_sh[SH_MODE != kShGlobal ? 64 * kShStride : 4];
     const int lane = threadIdx.x;
     const int g0 = blockIdx.x * 64;
-    const int idx = g0 + lane;
+    int idx = g0 + lane;
+    if constexpr (LIST) {  // a lane per Gaussian some view flags (the outputs were zeroed beforehand)
+        const uint32_t shard = blockIdx.x % kLiveShards, k0 = (blockIdx.x / kLiveShards) * 64;
+        const uint32_t n = a.live_count[shard * kLiveCntStride];
+        if (k0 >= n) return;  // uniform: past the shard's list
+        idx = k0 + lane < n ? (int)a.live[(size_t)shard * a.live_cap + k0 + lane] : a.P;
+    }
     const int nvalid = min(64, a.P - g0);
     const int M = a.M;
     const ShAddr sh_src{a.shs, a.dc, M};
     const ShGradAddr sh_dst{a.dL_dsh, a.dL_ddc, M};
     if constexpr (SH_MODE != kShGlobal) {
-        sh_stage_in<64, 64, SH_MODE == kShLdsSplit>(sh_src, g0, nvalid, s_sh, kShStride, lane);
+        if constexpr (LIST)
+            sh_gather_in<64, 64, SH_MODE == kShLdsSplit>(sh_src, idx < a.P ? idx : -1, 0, s_sh, kShStride, lane);
+        else
+            sh_stage_in<64, 64, SH_MODE == kShLdsSplit>(sh_src, g0, nvalid, s_sh, kShStride, lane);
         __syncthreads();
     }
     const bool valid = idx < a.P;
@@ -1069,7 +1078,10 @@ __global__ void __launch_bounds__(64) GSR_VIEWS_OCCUPANCY gauss_bwd_views_kernel
     }
     if constexpr (SH_MODE != kShGlobal) {
         __syncthreads();
-        sh_stage_out<64, 64, SH_MODE == kShLdsSplit>(sh_dst, g0, nvalid, s_sh, kShStride, lane);
+        if constexpr (LIST)
+            sh_gather_out<64, 64, SH_MODE == kShLdsSplit>(sh_dst, idx < a.P ? idx : -1, 0, s_sh, kShStride, lane);
+        else
+            sh_stage_out<64, 64, SH_MODE == kShLdsSplit>(sh_dst, g0, nvalid, s_sh, kShStride, lane);
     }
 }
 
@@ -1079,7 +1091,15 @@ hipError_t launch_gauss_bwd_views(const ViewsBwdArgs& a, hipStream_t stream) {
     const bool lds = a.shs && a.dL_dsh && a.M == 16 && (!a.dc || a.dL_ddc) &&
                      ((reinterpret_cast<uintptr_t>(a.shs) & 15) == 0) &&
                      ((reinterpret_cast<uintptr_t>(a.dL_dsh) & 15) == 0);
-    if (a.flags) {  // packed blocks (gsr_view_block_index)
+    if (a.flags && a.live) {  // packed blocks, a lane per Gaussian some view flags (outputs pre-zeroed)
+        const dim3 lgrid(kLiveShards * ((a.live_cap + 63) / 64));
+        if (lds && a.dc)
+            hipLaunchKernelGGL((gauss_bwd_views_kernel<kShLdsSplit, true, true>), lgrid, block, 0, stream, a);
+        else if (lds)
+            hipLaunchKernelGGL((gauss_bwd_views_kernel<kShLdsCombined, true, true>), lgrid, block, 0, stream, a);
+        else
+            hipLaunchKernelGGL((gauss_bwd_views_kernel<kShGlobal, true, true>), lgrid, block, 0, stream, a);
+    } else if (a.flags) {  // packed blocks (gsr_view_block_index)
         if (lds && a.dc)
             hipLaunchKernelGGL((gauss_bwd_views_kernel<kShLdsSplit, true>), grid, block, 0, stream, a);
         else if (lds)
@@ -1301,6 +1321,33 @@ hipError_t launch_view_index(uint32_t P, int n_views, const float* packed, unsig
     const uint32_t gx = (uint32_t)((cap + kPackThreads - 1) / kPackThreads);
     hipLaunchKernelGGL(view_index_kernel, dim3(gx < 1024 ? (gx ? gx : 1) : 1024, n_views), dim3(kPackThreads), 0,
                        stream, P, packed, packed_floats, flags, cap);
+    return hipGetLastError();
+}
+
+// The Gaussians some view flags (visible with a gradient in a packed block), appended to the
+// sharded live list (one atomic per wave, kLiveShards counters the caller zeroed).
+__global__ void __launch_bounds__(64) views_live_kernel(uint32_t P, int n_views, const uint32_t* __restrict__ flags,
+                                                        uint32_t* __restrict__ live, uint32_t* __restrict__ live_count,
+                                                        uint32_t live_cap) {
+    const uint32_t g = blockIdx.x * 64 + threadIdx.x;
+    bool lv = false;
+    if (g < P)
+        for (int v = 0; v < n_views; v++) lv |= (flags[(size_t)v * P + g] & 1u) != 0;
+    const unsigned long long m = __ballot(lv);
+    if (!m) return;
+    const uint32_t shard = blockIdx.x % kLiveShards;
+    uint32_t base = 0;
+    if (threadIdx.x == 0) base = atomicAdd(&live_count[shard * kLiveCntStride], (uint32_t)__popcll(m));
+    base = (uint32_t)__shfl((int)base, 0);
+    if (lv) live[(size_t)shard * live_cap + base + (uint32_t)__popcll(m & ((1ull << threadIdx.x) - 1ull))] = g;
+}
+
+hipError_t launch_views_live(uint32_t P, int n_views, const uint32_t* flags, uint32_t* live, uint32_t* live_count,
+                             hipStream_t stream) {
+    const hipError_t e = hipMemsetAsync(live_count, 0, sizeof(uint32_t) * kLiveShards * kLiveCntStride, stream);
+    if (e != hipSuccess || P == 0) return e;
+    hipLaunchKernelGGL(views_live_kernel, dim3((P + 63) / 64), dim3(64), 0, stream, P, n_views, flags, live,
+                       live_count, live_list_cap(P));
     return hipGetLastError();
 }
 

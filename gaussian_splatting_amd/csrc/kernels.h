@@ -396,6 +396,11 @@ struct ViewsBwdArgs {
     // its entry index in view v's packed block << 4 | the block's flag bits; the sums are read from
     // that packed entry, the camera from the packed block's header.  Null: dense view blocks.
     const uint32_t* flags;
+    // with flags: the live list of Gaussians some view flags (launch_views_live), or null; with it
+    // the kernel runs a lane per listed Gaussian and the outputs must be zero beforehand
+    const uint32_t* live;
+    const uint32_t* live_count;
+    uint32_t live_cap;
     float* dL_dmean3D;
     float* dL_dsh;
     float* dL_ddc;
@@ -406,6 +411,8 @@ struct ViewsBwdArgs {
 hipError_t launch_gauss_bwd_views(const ViewsBwdArgs& a, hipStream_t stream);
 hipError_t launch_view_pack(uint32_t P, const float* block, float* packed, unsigned long long cap, uint32_t* scratch,
                             uint32_t* count, hipStream_t stream);
+hipError_t launch_views_live(uint32_t P, int n_views, const uint32_t* flags, uint32_t* live, uint32_t* live_count,
+                             hipStream_t stream);
 hipError_t launch_view_index(uint32_t P, int n_views, const float* packed, unsigned long long packed_floats,
                              uint32_t* flags, unsigned long long cap, hipStream_t stream);
 hipError_t launch_view_unpack(uint32_t P, int n_views, const float* packed, unsigned long long packed_floats,

@@ -151,13 +151,16 @@ class ViewExchange:
             self._scratch = torch.empty(nbytes, dtype=torch.uint8, device=device)
             self._count = torch.zeros(1, dtype=torch.int32, device=device)
             self._flags = torch.empty(self.world, P, dtype=torch.int32, device=device)  # view_block_index
-        self._view_blocks, self._view_flags = self.gathered, None  # what views_backward reads
+            self._live = torch.empty(_C.views_live_floats(P), dtype=torch.int32, device=device)
+        self._view_blocks, self._view_flags, self._view_live = self.gathered, None, None  # views_backward reads
+        self._side = None      # the stream zeroing the outputs during the exchange
+        self._zeroed = None    # the flat output buffer it zeroes
 
     def local_block(self) -> torch.Tensor:
         """Where this rank's backward writes its view block."""
         return self._local if self.sparse else self.gathered[self.rank]
 
-    def exchange(self) -> None:
+    def exchange(self, zero: Optional[torch.Tensor] = None) -> None:
         """Give every rank all N view blocks in ``gathered``.
 
         Dense: one in-place ``all_gather_into_tensor`` of the blocks (44 B per Gaussian).
@@ -168,10 +171,25 @@ class ViewExchange:
         ``_C.view_block_index`` indexes the gathered packed blocks on every rank -- the same
         gathered bytes, the same kernel, so the replicas stay bitwise equal, and
         ``views_backward`` gives the dense exchange's result (a Gaussian left out had all-zero
-        sums)."""
+        sums).
+
+        ``zero`` (optional): the flat buffer behind the ``out`` views later given to
+        ``views_backward`` (e.g. ``GradArena.flat``).  It is zeroed on a second stream while the
+        exchange runs, and the multi-view backward then writes only the rows of Gaussians some
+        view has a gradient for (a live list, ``_C.views_live_list``)."""
         from . import _C
 
-        self._view_blocks, self._view_flags = self.gathered, None
+        self._view_blocks, self._view_flags, self._view_live = self.gathered, None, None
+        self._zeroed = None
+        if zero is not None and self.sparse:
+            cur = torch.cuda.current_stream(zero.device)
+            if self._side is None:
+                self._side = torch.cuda.Stream(device=zero.device)
+            self._side.wait_stream(cur)
+            with torch.cuda.stream(self._side):
+                zero.zero_()
+            zero.record_stream(self._side)
+            self._zeroed = zero
         if not self.sparse:
             if self.world > 1:
                 dist.all_gather_into_tensor(self.gathered.view(-1), self.local_block(), group=self.group)
@@ -201,14 +219,19 @@ class ViewExchange:
             recv[0].copy_(self._packed[:size])
         _C.view_block_index(recv, self._flags, self.P)
         self._view_blocks, self._view_flags = recv, self._flags
+        if self._zeroed is not None:
+            _C.views_live_list(self._flags, self._live, self.P)
+            self._view_live = self._live
 
     def views_backward(self, means3D, dc, sh, degree, opacities, scales, rotations, scale_modifier, out) -> None:
         """The per-Gaussian backward summed over all ranks' views (``_C.gauss_backward_views`` over
         what the last ``exchange`` gathered: dense view blocks, or packed blocks and their index)."""
         from . import _C
 
+        if self._zeroed is not None:  # the outputs' zero fill (exchange(zero=...)) must be done
+            torch.cuda.current_stream(self._zeroed.device).wait_stream(self._side)
         _C.gauss_backward_views(means3D, dc, sh, degree, opacities, scales, rotations, scale_modifier,
-                                self._view_blocks, out, flags=self._view_flags)
+                                self._view_blocks, out, flags=self._view_flags, live=self._view_live)
 
     def received_bytes(self) -> int:
         """Bytes this rank received from the others in the last exchange."""

@@ -231,6 +231,21 @@ int gsr_gauss_backward_views_packed(int P, int D, int M, const float* means3D, c
                                     const unsigned int* flags, float* dL_dmean3D, float* dL_ddc, float* dL_dsh,
                                     float* dL_dopacity, float* dL_dscale, float* dL_drot, void* stream);
 
+/* Live-list form (sparse outputs): only the Gaussians some view flags are visited.
+ * gsr_views_live_floats(P): uint32 words of the list buffer (entries + shard counters).
+ * gsr_views_live_list: builds it from the flags of gsr_view_block_index.
+ * gsr_gauss_backward_views_live: gsr_gauss_backward_views_packed over the listed Gaussians only,
+ *   one lane each; every output row of the others is left untouched, so the caller zeroes the
+ *   outputs beforehand (ViewExchange does it on a second stream while the all-gather runs). */
+unsigned long long gsr_views_live_floats(int P);
+int gsr_views_live_list(int P, int n_views, const unsigned int* flags, unsigned int* live, void* stream);
+int gsr_gauss_backward_views_live(int P, int D, int M, const float* means3D, const float* dc, const float* shs,
+                                  const float* opacities, const float* scales, const float* rotations,
+                                  float scale_modifier, int n_views, const float* packed, long long packed_floats,
+                                  const unsigned int* flags, const unsigned int* live, float* dL_dmean3D,
+                                  float* dL_ddc, float* dL_dsh, float* dL_dopacity, float* dL_dscale, float* dL_drot,
+                                  void* stream);
+
 /* Frustum test, view-space z > 0.2 (CudaRasterizer::Rasterizer::markVisible).
  * `present` is P bytes (bool). */
 int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,

@@ -73,8 +73,9 @@ def _worker(rank, port, outdir):
         for mode, sparse in (("views", True), ("dense", False)):  # sparse (default) and dense view blocks
             ex = ViewExchange(CASE.P, dev, sparse=sparse)
             _C.rasterize_gaussians_backward_screen(*bwd, view_block=ex.local_block())
-            ex.exchange()
             arena2 = GradArena(CASE.P, M, dev)
+            arena2.flat.fill_(float("nan"))  # the sparse exchange's zero fill must cover every row
+            ex.exchange(zero=arena2.flat if sparse else None)
             ex.views_backward(d("means3D"), None, d("shs"), inp["sh_degree"], d("opacities"), d("scales"),
                               d("rotations"), 1.0, out=arena2.views())
             torch.cuda.synchronize()

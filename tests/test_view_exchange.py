@@ -63,24 +63,25 @@ def _single_and_block(inp, case, dev, split):
     return dict(zip(names, out)), block, t
 
 
-def _views_backward(t, blocks, split, dev, flags=None):
+def _views_backward(t, blocks, split, dev, flags=None, live=None):
     from gaussian_splatting_amd import _C
 
     P = t["means3D"].shape[0]
     sh = t["shs"]
     M = sh.shape[1]
-    out = {"dL_dmeans3D": torch.empty(P, 3, device=dev), "dL_dopacity": torch.empty(P, 1, device=dev),
-           "dL_dscales": torch.empty(P, 3, device=dev), "dL_drotations": torch.empty(P, 4, device=dev)}
+    new = torch.zeros if live is not None else torch.empty  # the live-list form leaves unlisted rows as they are
+    out = {"dL_dmeans3D": new(P, 3, device=dev), "dL_dopacity": new(P, 1, device=dev),
+           "dL_dscales": new(P, 3, device=dev), "dL_drotations": new(P, 4, device=dev)}
     if split:
         dc, rest = sh[:, :1].contiguous(), sh[:, 1:].contiguous()
-        out["dL_ddc"] = torch.empty(P, 1, 3, device=dev)
-        out["dL_dsh"] = torch.empty(P, M - 1, 3, device=dev)
+        out["dL_ddc"] = new(P, 1, 3, device=dev)
+        out["dL_dsh"] = new(P, M - 1, 3, device=dev)
         _C.gauss_backward_views(t["means3D"], dc, rest, t["sh_degree"], t["opacities"], t["scales"], t["rotations"],
-                                t["scale_modifier"], blocks, out, flags=flags)
+                                t["scale_modifier"], blocks, out, flags=flags, live=live)
     else:
-        out["dL_dsh"] = torch.empty(P, M, 3, device=dev)
+        out["dL_dsh"] = new(P, M, 3, device=dev)
         _C.gauss_backward_views(t["means3D"], None, sh, t["sh_degree"], t["opacities"], t["scales"], t["rotations"],
-                                t["scale_modifier"], blocks, out, flags=flags)
+                                t["scale_modifier"], blocks, out, flags=flags, live=live)
     return out
 
 
@@ -193,6 +194,17 @@ def test_sparse_blocks_pack_unpack(split):
         assert torch.equal(f[live] & 15, b[64 + 10 * P: 64 + 11 * P].view(torch.int32)[live] & 15)
         assert torch.equal(f[live] >> 4, torch.arange(int(live.sum()), dtype=torch.int32, device=dev))
     got = _views_backward(t, recv, split, dev, flags=flags)
+    for k in ref:
+        assert torch.equal(got[k], ref[k]), k
+    # live-list form: only Gaussians some view flags are visited (zeroed outputs), the same result
+    live = torch.empty(_C.views_live_floats(P), dtype=torch.int32, device=dev)
+    _C.views_live_list(flags, live, P)
+    any_live = torch.stack([_live(b, P) for b in blocks]).any(0)
+    cap = (live.numel() - 64 * 32) // 64
+    shard_n = live[64 * cap:].view(64, 32)[:, 0]
+    listed = torch.cat([live[s * cap: s * cap + int(shard_n[s])] for s in range(64)]).long()
+    assert torch.equal(torch.sort(listed).values, torch.nonzero(any_live).view(-1))
+    got = _views_backward(t, recv, split, dev, flags=flags, live=live)
     for k in ref:
         assert torch.equal(got[k], ref[k]), k
     # a packed block smaller than the count: the count is reported whole, cap entries are written

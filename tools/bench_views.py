@@ -110,6 +110,12 @@ def main():
         res.setdefault("views_packed_ms", {})[N] = timed(lambda: _C.gauss_backward_views(
             scene.means3D, None, scene.shs, D, scene.opacities, scene.scales, scene.rotations, 1.0, recv,
             arena.views(), flags=flags))
+        live = torch.empty(_C.views_live_floats(P), dtype=torch.int32, device=dev)
+        res.setdefault("live_list_ms", {})[N] = timed(lambda: _C.views_live_list(flags, live, P))
+        res.setdefault("zero_ms", {})[N] = timed(lambda: arena.flat.zero_())
+        res.setdefault("views_live_ms", {})[N] = timed(lambda: _C.gauss_backward_views(
+            scene.means3D, None, scene.shs, D, scene.opacities, scene.scales, scene.rotations, 1.0, recv,
+            arena.views(), flags=flags, live=live))
         res["views_sparse_ms"][N] = timed(lambda: _C.gauss_backward_views(scene.means3D, None, scene.shs, D,
                                                                          scene.opacities, scene.scales,
                                                                          scene.rotations, 1.0, blocks, arena.views()))
