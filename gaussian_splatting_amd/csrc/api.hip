@@ -164,9 +164,11 @@ gsr::ImageState carve_image(char* base, int W, int H, uint32_t tiles, size_t* to
     Carver c{base, 0};
     ImageState im{};
     const size_t N = (size_t)W * H;
-    im.final_T = c.take<float>(N);
-    im.n_contrib = c.take<uint32_t>(N);
-    im.accum = c.take<float>(4 * N);
+    const size_t NT = (size_t)tiles * 256;  // tile-major pixel planes (gsr_common.h tile_px)
+    (void)N;
+    im.final_T = c.take<float>(NT);
+    im.n_contrib = c.take<uint32_t>(NT);
+    im.accum = c.take<float>(4 * NT);
     im.ranges = c.take<uint2>(tiles);
     im.lim_key = c.take<unsigned long long>(tiles);
     *total = align_up(c.off);
@@ -1250,11 +1252,12 @@ int gsr_debug_forward_state(int P, int width, int height, int R, int binning_cap
     const size_t N = (size_t)width * height;
     if (ranges) HIP_TRY(hipMemcpyAsync(ranges, img.ranges, sizeof(uint2) * gx * gy, hipMemcpyDeviceToDevice, stream),
                         "debug_forward_state ranges");
+    (void)N;
     if (n_contrib)
-        HIP_TRY(hipMemcpyAsync(n_contrib, img.n_contrib, sizeof(uint32_t) * N, hipMemcpyDeviceToDevice, stream),
-                "debug_forward_state n_contrib");
+        HIP_TRY(launch_untile(img.n_contrib, n_contrib, width, height, gx, stream), "debug_forward_state n_contrib");
     if (final_T)
-        HIP_TRY(hipMemcpyAsync(final_T, img.final_T, sizeof(float) * N, hipMemcpyDeviceToDevice, stream),
+        HIP_TRY(launch_untile(reinterpret_cast<const uint32_t*>(img.final_T), reinterpret_cast<uint32_t*>(final_T),
+                              width, height, gx, stream),
                 "debug_forward_state final_T");
     if (point_list && R > 0) {
         BinningState bin = carve_binning((char*)binning_buffer, C, &tmp);

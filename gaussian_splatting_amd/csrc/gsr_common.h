@@ -97,11 +97,18 @@ struct GeomState {
     unsigned long long* tile_join;  // [tiles] the forward's half-tile waves combine their limits here (K2 zeroes)
 };
 
-// Image state: per pixel (N) and per tile.
+// Image state: per pixel and per tile.  The per-pixel planes are tile-major: pixel (x, y) of
+// tile t, in 8x8 quadrant q at lane l = (y & 7) * 8 + (x & 7), is element t * 256 + q * 64 + l
+// (tile_px), so a wave's 64 lanes of one quadrant read / write 256 contiguous bytes per plane.
+// (Image-major, each 8-pixel row was 32 B of a 128-B line whose other parts belong to other
+// quadrants and tiles: render_bwd fetched 312 MB for 75 MB of pixel state, r2zp.)
+__host__ __device__ inline size_t tile_px(uint32_t tile, int q, int lane) {
+    return (size_t)tile * 256 + (size_t)q * 64 + (size_t)lane;
+}
 struct ImageState {
-    float* final_T;       // [N]
-    uint32_t* n_contrib;  // [N]
-    float* accum;         // [4][N]: colour r,g,b and inverse depth, without background
+    float* final_T;       // [tiles * 256], tile-major (tile_px)
+    uint32_t* n_contrib;  // [tiles * 256]
+    float* accum;         // [4][tiles * 256]: colour r,g,b and inverse depth, without background
     uint2* ranges;        // [tiles]
     unsigned long long* lim_key;  // [tiles] key (depth bits << 32 | index) of the entry at limit - 1, 0 if
                                   // none: entries past it have no gradient record (backward.hip)

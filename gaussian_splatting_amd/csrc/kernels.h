@@ -362,6 +362,8 @@ hipError_t launch_tile_sort(uint32_t tiles, const uint2* ranges, const GeomState
 bool bin_fused_ok(uint32_t tiles);  // the fused form applies (LDS cursors)
 // render.hip
 hipError_t launch_render_fwd(const RenderFwdArgs& a, hipStream_t stream);
+// a tile-major pixel plane (tile_px) -> image order [H][W], 4-byte elements (inspection only)
+hipError_t launch_untile(const uint32_t* src, uint32_t* dst, int W, int H, uint32_t gx, hipStream_t stream);
 hipError_t launch_render_bwd(const RenderBwdArgs& a, size_t max_units, hipStream_t stream);
 // backward work list: one unit per (tile, segment of seg_ck * kCkStride entries below the tile's limit),
 // written by the forward render; at most R / (seg_ck kCkStride) + tiles of them

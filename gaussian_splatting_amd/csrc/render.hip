@@ -52,6 +52,13 @@ constexpr int kBatch = 64;  // list entries staged per round (one per lane)
 #define GSR_BWD_CARRY_R 0
 #endif
 
+// Traffic attribution builds only (results are wrong in them): GSR_ATTR bit 0
+// drops the backward's record / content-byte stores, bit 1 its checkpoint loads, bit 2 its
+// per-pixel state loads other than n_contrib.  The control flow is unchanged in all three.
+#ifndef GSR_ATTR
+#define GSR_ATTR 0
+#endif
+
 GSR_STAMP_BUFFER(g_st_rfwd);
 GSR_STAMP_BUFFER(g_st_rbwd);
 
@@ -235,22 +242,22 @@ __global__ void __launch_bounds__(64) GSR_FWD_OCCUPANCY render_fwd_kernel(Render
         GSR_STAMP_RT(g_st_rfwd, tile, 5);
         GSR_STAMP_VAL(g_st_rfwd, tile, 2, n);
     }
-    const size_t N = (size_t)a.W * a.H;
+    const size_t N = (size_t)a.W * a.H, NT = (size_t)tiles * 256;
 #pragma unroll
     for (int k = 0; k < NQ; k++) {
         const int q = qbase + k;
         const int px = tile_x0 + (q & 1) * 8 + lx, py = tile_y0 + (q >> 1) * 8 + ly;
         if (px < a.W && py < a.H) {
-            const size_t pix = (size_t)py * a.W + px;
+            const size_t pix = (size_t)py * a.W + px, t = tile_px(tile, q, lane);
             // the reference's final_T is T after the pixel's last contributor: entries after it
             // either do not blend (T unchanged) or end the pixel without blending
             const float T = Tc[k];
-            a.img.final_T[pix] = T;
-            a.img.n_contrib[pix] = last[k];
-            a.img.accum[pix] = C0[k];
-            a.img.accum[N + pix] = C1[k];
-            a.img.accum[2 * N + pix] = C2[k];
-            a.img.accum[3 * N + pix] = D[k];
+            a.img.final_T[t] = T;
+            a.img.n_contrib[t] = last[k];
+            a.img.accum[t] = C0[k];
+            a.img.accum[NT + t] = C1[k];
+            a.img.accum[2 * NT + t] = C2[k];
+            a.img.accum[3 * NT + t] = D[k];
             a.out_color[pix] = C0[k] + T * a.bg[0];
             a.out_color[N + pix] = C1[k] + T * a.bg[1];
             a.out_color[2 * N + pix] = C2[k] + T * a.bg[2];
@@ -293,6 +300,21 @@ __global__ void __launch_bounds__(64) GSR_FWD_OCCUPANCY render_fwd_kernel(Render
         a.unit_part[((size_t)b * kUnitShards + shard) * unit_part_cap(tiles) + base] =
             make_uint2(tile, nf * (uint32_t)a.seg_ck);
   }
+}
+
+__global__ void untile_kernel(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, int W, int H, uint32_t gx) {
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (x >= W || y >= H) return;
+    const uint32_t tile = blockIdx.y * gx + blockIdx.x;
+    const int q = ((y & 15) >> 3) * 2 + ((x & 15) >> 3), lane = (y & 7) * 8 + (x & 7);
+    dst[(size_t)y * W + x] = src[tile_px(tile, q, lane)];
+}
+
+hipError_t launch_untile(const uint32_t* src, uint32_t* dst, int W, int H, uint32_t gx, hipStream_t stream) {
+    const uint32_t gy = (H + kTile - 1) / kTile;
+    if (gx == 0 || gy == 0) return hipSuccess;
+    hipLaunchKernelGGL(untile_kernel, dim3(gx, gy), dim3(256), 0, stream, src, dst, W, H, gx);
+    return hipGetLastError();
 }
 
 // Quadrants per forward wave: 2 (half tiles) unless GSR_FWD_QUADS=4 (whole tiles, for A/B runs).
@@ -369,20 +391,24 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         const int px = min(tile_x0 + (q & 1) * 8 + lx, a.W - 1), py = min(tile_y0 + (q >> 1) * 8 + ly, a.H - 1);
-        const size_t pix = (size_t)py * a.W + px;
-        nc[q] = (int)a.img.n_contrib[pix];
-        g0[q] = a.dL_dpix[pix];
-        g1[q] = a.dL_dpix[N + pix];
-        g2[q] = a.dL_dpix[2 * N + pix];
-        gi[q] = a.dL_dinvdepth ? a.dL_dinvdepth[pix] : 0.f;
-        c0[q] = a.img.accum[pix];
-        c1[q] = a.img.accum[N + pix];
-        c2[q] = a.img.accum[2 * N + pix];
-        cd[q] = a.img.accum[3 * N + pix];
-        fT[q] = a.img.final_T[pix];
+        const size_t pix = (size_t)py * a.W + px, t = tile_px(tile, q, lane), NT = (size_t)a.gx * a.gy * 256;
+        nc[q] = (int)a.img.n_contrib[t];
+        if (GSR_ATTR & 4) {
+            g0[q] = g1[q] = g2[q] = gi[q] = c0[q] = c1[q] = c2[q] = cd[q] = fT[q] = 0.5f;
+        } else {
+            g0[q] = a.dL_dpix[pix];
+            g1[q] = a.dL_dpix[N + pix];
+            g2[q] = a.dL_dpix[2 * N + pix];
+            gi[q] = a.dL_dinvdepth ? a.dL_dinvdepth[pix] : 0.f;
+            c0[q] = a.img.accum[t];
+            c1[q] = a.img.accum[NT + t];
+            c2[q] = a.img.accum[2 * NT + t];
+            cd[q] = a.img.accum[3 * NT + t];
+            fT[q] = a.img.final_T[t];
+        }
         // blend state at `start`: the forward's checkpoint (gsr_common.h), or the empty state
         const float* ck = a.ckpt + (size_t)((range.x + (uint32_t)start) / kCkStride) * kCkFloats + lane;
-        const bool has_ck = start > 0;
+        const bool has_ck = start > 0 && !(GSR_ATTR & 2);
         k0[q] = has_ck ? ck[(0 * 4 + q) * 64] : 1.f;
         k1[q] = has_ck ? ck[(1 * 4 + q) * 64] : 0.f;
         k2[q] = has_ck ? ck[(2 * 4 + q) * 64] : 0.f;
@@ -544,8 +570,8 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
         }
         __syncthreads();
         const bool content = (written >> lane) & 1ull;
-        if (GSR_REC_FLAG && has) a.recs.flag[e] = content ? 1 : 0;
-        if (has && (content || !GSR_REC_FLAG)) {
+        if (GSR_REC_FLAG && has && !(GSR_ATTR & 1)) a.recs.flag[e] = content ? 1 : 0;
+        if (has && (content || !GSR_REC_FLAG) && !(GSR_ATTR & 1)) {
             float4 ra = make_float4(0.f, 0.f, 0.f, 0.f), rb = ra;
             float2 rc = make_float2(0.f, 0.f);
             if (content) {
