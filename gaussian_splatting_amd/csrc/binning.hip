@@ -117,6 +117,9 @@ __device__ T block_exclusive_scan(T v, T* s_tmp, T* total) {
 #ifndef GSR_FEI_DPP
 #define GSR_FEI_DPP 1
 #endif
+#ifndef GSR_FEI_FDIV
+#define GSR_FEI_FDIV 1
+#endif
 template <class F>
 __device__ __forceinline__ void for_each_instance(uint32_t n, uint2 r, uint32_t gx, F&& f) {
     const int lane = threadIdx.x & 63;
@@ -164,6 +167,15 @@ __device__ __forceinline__ void for_each_instance(uint32_t n, uint2 r, uint32_t 
         const uint32_t k = s - __shfl(excl, owner);
         const uint32_t ow = __shfl(w, owner), org = __shfl(r.x, owner);
         const bool valid = s < total;
+#if GSR_FEI_FDIV
+        // k / ow in fp32, branch-free (so the caller's shuffles from `owner` issue with these):
+        // (k + 1/2) / ow is at least 1/(2 ow) from an integer, and rcp + mul err by < 2^-22
+        // relative, so the floor is exact while k < 2^21 (a Gaussian touches < 2^21 tiles:
+        // launch_bin_count rejects grids of more than kLdsTilesMax cells, 589824 tiles).  Invalid lanes compute garbage that f ignores.
+        const uint32_t dy = (uint32_t)(((float)k + 0.5f) * __builtin_amdgcn_rcpf((float)max(ow, 1u)));
+        const uint32_t tx = (org & 0xffffu) + (k - dy * ow), ty = (org >> 16) + dy;
+        const uint32_t tile = ty * gx + tx;
+#else
         uint32_t tile = 0, tx = 0, ty = 0;
         if (valid) {
             const uint32_t dy = k / ow;
@@ -171,6 +183,7 @@ __device__ __forceinline__ void for_each_instance(uint32_t n, uint2 r, uint32_t 
             ty = (org >> 16) + dy;
             tile = ty * gx + tx;
         }
+#endif
         f(valid, owner, tile, tx, ty);
     }
 }
