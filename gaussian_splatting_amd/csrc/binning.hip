@@ -120,6 +120,9 @@ __device__ T block_exclusive_scan(T v, T* s_tmp, T* total) {
 #ifndef GSR_FEI_FDIV
 #define GSR_FEI_FDIV 1
 #endif
+#ifndef GSR_FEI_U24
+#define GSR_FEI_U24 1
+#endif
 template <class F>
 __device__ __forceinline__ void for_each_instance(uint32_t n, uint2 r, uint32_t gx, F&& f) {
     const int lane = threadIdx.x & 63;
@@ -173,8 +176,15 @@ __device__ __forceinline__ void for_each_instance(uint32_t n, uint2 r, uint32_t 
         // relative, so the floor is exact while k < 2^21 (a Gaussian touches < 2^21 tiles:
         // launch_bin_count rejects grids of more than kLdsTilesMax cells, 589824 tiles).  Invalid lanes compute garbage that f ignores.
         const uint32_t dy = (uint32_t)(((float)k + 0.5f) * __builtin_amdgcn_rcpf((float)max(ow, 1u)));
+        // 24-bit multiplies (full rate; v_mul_lo_u32 / v_mad_u64_u32 are quarter rate): every
+        // operand is < 2^16 (tile coordinates and widths, gx)
+#if GSR_FEI_U24
+        const uint32_t tx = (org & 0xffffu) + (k - __umul24(dy, ow)), ty = (org >> 16) + dy;
+        const uint32_t tile = __umul24(ty, gx) + tx;
+#else
         const uint32_t tx = (org & 0xffffu) + (k - dy * ow), ty = (org >> 16) + dy;
         const uint32_t tile = ty * gx + tx;
+#endif
 #else
         uint32_t tile = 0, tx = 0, ty = 0;
         if (valid) {
@@ -847,27 +857,36 @@ __global__ void __launch_bounds__(64) tile_sort_kernel(const uint2* __restrict__
 // exchange buffer aliases the bucket buffer).  Class 1 (> kClass0Max): bucket sort up to
 // kBucketMax keys, the global-memory network beyond or on skew.
 constexpr int kClassThreads = 256;
+// Class 0's workgroup size (A/B: its tiles hold 1-4k keys; more threads per tile shorten each
+// tile's barrier-separated phases at the same LDS per workgroup).
+#ifndef GSR_CLASS0_THREADS
+#define GSR_CLASS0_THREADS 256
+#endif
+template <int CLASS>
+constexpr int class_threads() { return CLASS == 0 ? GSR_CLASS0_THREADS : kClassThreads; }
 
 template <int CLASS>
-__global__ void __launch_bounds__(kClassThreads) tile_sort_class_kernel(const uint2* __restrict__ ranges,
+__global__ void __launch_bounds__(class_threads<CLASS>()) tile_sort_class_kernel(const uint2* __restrict__ ranges,
                                                                         u64* __restrict__ keys, u64 cap,
                                                                         uint32_t* __restrict__ gid_sorted,
                                                                         const uint32_t* __restrict__ list,
                                                                         const uint32_t* __restrict__ count) {
+    constexpr int T = class_threads<CLASS>();
     constexpr int NMAX = CLASS == 0 ? (int)kClass0Max : (int)kBucketMax;
-    __shared__ BucketLds<kClassThreads, NMAX, NMAX / 2> s;
-    static_assert(sizeof(s.buf) >= kClassThreads * 16 * sizeof(u64), "the fallback network's buffer");
+    constexpr int EF = CLASS == 0 ? NMAX / T : 16;  // the fallback network's keys per thread
+    __shared__ BucketLds<T, NMAX, NMAX / 2> s;
+    static_assert(sizeof(s.buf) >= T * EF * sizeof(u64), "the fallback network's buffer");
+    static_assert(CLASS != 0 || T * EF == NMAX, "class 0's fallback network covers the class");
     const uint32_t nb = count[0];
     for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
         const uint2 r = ranges[list[b]];
         const uint32_t n = tile_len(r, cap);  // may be shorter than its class when truncated by cap
         if (n <= 1) {
             if (n == 1 && threadIdx.x == 0) gid_sorted[r.x] = (uint32_t)keys[r.x];
-        } else if (n > (uint32_t)NMAX || !bucket_sort_list<kClassThreads, NMAX / kClassThreads>(keys, r.x, n,
-                                                                                               gid_sorted, s)) {
+        } else if (n > (uint32_t)NMAX || !bucket_sort_list<T, NMAX / T>(keys, r.x, n, gid_sorted, s)) {
             __syncthreads();
-            if (CLASS == 0 || n <= (uint32_t)kClassThreads * 16)
-                sort_list<kClassThreads, 16>(keys, r.x, n, gid_sorted, s.buf);
+            if (CLASS == 0 || n <= (uint32_t)T * EF)
+                sort_list<T, EF>(keys, r.x, n, gid_sorted, s.buf);
             else
                 sort_list_global(keys, r.x, n, gid_sorted);
         }
@@ -972,9 +991,9 @@ hipError_t launch_tile_sort(uint32_t tiles, const uint2* ranges, const GeomState
                        zero_counts ? g.tile_cnt : nullptr, cells);
     // persistent class kernels: grids sized to fill the chip when their lists are long
     const auto grid = [&](uint32_t want) { return dim3(tiles < want ? tiles : want); };
-    hipLaunchKernelGGL(tile_sort_class_kernel<0>, grid(2048), dim3(kClassThreads), 0, stream, ranges, b.keys, c,
+    hipLaunchKernelGGL(tile_sort_class_kernel<0>, grid(2048), dim3(class_threads<0>()), 0, stream, ranges, b.keys, c,
                        b.gid_sorted, g.cls_list, g.cls_count);
-    hipLaunchKernelGGL(tile_sort_class_kernel<1>, grid(512), dim3(kClassThreads), 0, stream, ranges, b.keys, c,
+    hipLaunchKernelGGL(tile_sort_class_kernel<1>, grid(512), dim3(class_threads<1>()), 0, stream, ranges, b.keys, c,
                        b.gid_sorted, g.cls_list + tiles, g.cls_count + 1);
     return hipGetLastError();
 }
