@@ -1361,9 +1361,16 @@ hipError_t launch_view_header(float* blk, const float* view, const float* proj, 
 
 // 16-byte stores (1 KiB per wave-instruction) over each range's aligned body, dwords for its
 // unaligned head and tail.  A small grid (GSR_FILL_BLOCKS workgroups of 256): beside render_bwd
-// it should take few wave slots and only the HBM bandwidth render_bwd leaves idle.
+// it should take few wave slots and only the HBM bandwidth render_bwd leaves idle.  The body
+// stores are non-temporal (`nt`): 236 MB of zeros written through the caches evicted the
+// records and pixel state render_bwd and gauss_reduce re-read (r2zv: render_bwd 298 -> 290 us,
+// gauss_reduce 67 -> 63, preprocess 75.6 -> 72, step -19 us; 32 / 64 / 96 / 128 workgroups
+// within noise once the stores stream, r2zw).
 #ifndef GSR_FILL_BLOCKS
-#define GSR_FILL_BLOCKS 128
+#define GSR_FILL_BLOCKS 64
+#endif
+#ifndef GSR_FILL_NT
+#define GSR_FILL_NT 1
 #endif
 __global__ void __launch_bounds__(256) zero_fill_kernel(FillArgs f) {
     const unsigned long long tid = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1375,7 +1382,14 @@ __global__ void __launch_bounds__(256) zero_fill_kernel(FillArgs f) {
         const unsigned long long h = head < n ? head : n;
         const unsigned long long n4 = (n - h) / 4;
         float4* body = reinterpret_cast<float4*>(p + h);
-        for (unsigned long long i = tid; i < n4; i += stride) body[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (unsigned long long i = tid; i < n4; i += stride) {
+#if GSR_FILL_NT  // streaming stores: the zeros do not displace render_bwd's lines from L2 / MALL
+            typedef float v4f __attribute__((ext_vector_type(4)));
+            __builtin_nontemporal_store((v4f){0.f, 0.f, 0.f, 0.f}, reinterpret_cast<v4f*>(body + i));
+#else
+            body[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+#endif
+        }
         if (tid < h) p[tid] = 0.f;
         const unsigned long long t0 = h + 4 * n4;
         if (tid < n - t0) p[t0 + tid] = 0.f;
