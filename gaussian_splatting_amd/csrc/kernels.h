@@ -129,6 +129,13 @@ hipError_t launch_zero_fill(const FillArgs& f, hipStream_t stream);
 constexpr int kShRowF = 48;     // floats per staged SH row (M = 16)
 constexpr int kShRestF = 45;    // floats per rest row in the split layout
 
+// SH rows are read once per pass (preprocess: 192 MB at 1M): non-temporal loads keep them from
+// displacing the lines the next kernels re-read (r2zx: preprocess 69.5 -> 62.7 us, bin_count
+// 45.6 -> 43.3, step -8 us).  Streaming stores of render_fwd's image outputs and streaming loads
+// of render_bwd's dL/dpixel (render.hip GSR_NT_OUT / GSR_NT_DPIX) measured no gain.
+#ifndef GSR_NT_SH
+#define GSR_NT_SH 1
+#endif
 template <int ROWS, int THREADS, bool SPLIT>
 // rowmask: bit r set = stage row r (rows left out are not read; their LDS contents are undefined).
 __device__ __forceinline__ void sh_stage_in(const ShAddr& sa, int r0, int rows, float* lds, int stride, int tid,
@@ -140,8 +147,15 @@ __device__ __forceinline__ void sh_stage_in(const ShAddr& sa, int r0, int rows, 
         for (int k = 0; k < ROWS * kShRowF / 4 / THREADS; k++) {
             const int i4 = k * THREADS + tid;
             const int d = i4 * 4, row = d / kShRowF, col = d - row * kShRowF;
-            if (i4 < n4 && ((rowmask >> row) & 1ull))
+            if (i4 < n4 && ((rowmask >> row) & 1ull)) {
+#if GSR_NT_SH
+                typedef float v4f __attribute__((ext_vector_type(4)));
+                *reinterpret_cast<v4f*>(&lds[row * stride + col]) =
+                    __builtin_nontemporal_load(reinterpret_cast<const v4f*>(src) + i4);
+#else
                 *reinterpret_cast<float4*>(&lds[row * stride + col]) = src[i4];
+#endif
+            }
         }
         return;
     } else {
@@ -172,6 +186,13 @@ __device__ __forceinline__ void sh_stage_in(const ShAddr& sa, int r0, int rows, 
     }
 }
 
+// SH rows are read once per pass (preprocess: 192 MB at 1M): non-temporal loads keep them from
+// displacing the lines the next kernels re-read (r2zx: preprocess 69.5 -> 62.7 us, bin_count
+// 45.6 -> 43.3, step -8 us).  Streaming stores of render_fwd's image outputs and streaming loads
+// of render_bwd's dL/dpixel (render.hip GSR_NT_OUT / GSR_NT_DPIX) measured no gain.
+#ifndef GSR_NT_SH
+#define GSR_NT_SH 1
+#endif
 template <int ROWS, int THREADS, bool SPLIT>
 // rowmask: bit r set = write row r (rows left out are not written).
 __device__ __forceinline__ void sh_stage_out(const ShGradAddr& ga, int r0, int rows, const float* lds, int stride,

@@ -58,6 +58,14 @@ constexpr int kBatch = 64;  // list entries staged per round (one per lane)
 #ifndef GSR_ATTR
 #define GSR_ATTR 0
 #endif
+// Cache policy A/B switches: non-temporal stores of the forward's image outputs, non-temporal
+// loads of the backward's dL/dpixel.
+#ifndef GSR_NT_OUT
+#define GSR_NT_OUT 0
+#endif
+#ifndef GSR_NT_DPIX
+#define GSR_NT_DPIX 0
+#endif
 
 GSR_STAMP_BUFFER(g_st_rfwd);
 GSR_STAMP_BUFFER(g_st_rbwd);
@@ -258,10 +266,17 @@ __global__ void __launch_bounds__(64) GSR_FWD_OCCUPANCY render_fwd_kernel(Render
             a.img.accum[NT + t] = C1[k];
             a.img.accum[2 * NT + t] = C2[k];
             a.img.accum[3 * NT + t] = D[k];
+#if GSR_NT_OUT  // the image outputs are not read again in the step: streaming stores
+            __builtin_nontemporal_store(C0[k] + T * a.bg[0], a.out_color + pix);
+            __builtin_nontemporal_store(C1[k] + T * a.bg[1], a.out_color + N + pix);
+            __builtin_nontemporal_store(C2[k] + T * a.bg[2], a.out_color + 2 * N + pix);
+            __builtin_nontemporal_store(D[k], a.out_invdepth + pix);
+#else
             a.out_color[pix] = C0[k] + T * a.bg[0];
             a.out_color[N + pix] = C1[k] + T * a.bg[1];
             a.out_color[2 * N + pix] = C2[k] + T * a.bg[2];
             a.out_invdepth[pix] = D[k];
+#endif
         }
     }
 
@@ -396,10 +411,17 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
         if (GSR_ATTR & 4) {
             g0[q] = g1[q] = g2[q] = gi[q] = c0[q] = c1[q] = c2[q] = cd[q] = fT[q] = 0.5f;
         } else {
+#if GSR_NT_DPIX  // read once per step: streaming loads
+            g0[q] = __builtin_nontemporal_load(a.dL_dpix + pix);
+            g1[q] = __builtin_nontemporal_load(a.dL_dpix + N + pix);
+            g2[q] = __builtin_nontemporal_load(a.dL_dpix + 2 * N + pix);
+            gi[q] = a.dL_dinvdepth ? __builtin_nontemporal_load(a.dL_dinvdepth + pix) : 0.f;
+#else
             g0[q] = a.dL_dpix[pix];
             g1[q] = a.dL_dpix[N + pix];
             g2[q] = a.dL_dpix[2 * N + pix];
             gi[q] = a.dL_dinvdepth ? a.dL_dinvdepth[pix] : 0.f;
+#endif
             c0[q] = a.img.accum[t];
             c1[q] = a.img.accum[NT + t];
             c2[q] = a.img.accum[2 * NT + t];
