@@ -22,6 +22,16 @@
 
 namespace gsr {
 
+// A/B: the gradient records are read once (gauss_reduce): streaming loads.
+#ifndef GSR_NT_REC
+#define GSR_NT_REC 0
+#endif
+#if GSR_NT_REC
+#define GSR_LD_REC(p) load_nt(p)
+#else
+#define GSR_LD_REC(p) (*(p))
+#endif
+
 // ---- 1. segmented sums of the per-instance records ------------------------------
 // One wave per 64 consecutive Gaussians.  Their records form one contiguous range
 // [E0, E1) (record index = rec_start[g] + k, k = the tile's row-major index in g's
@@ -114,18 +124,18 @@ __device__ __forceinline__ void reduce_records(int P, int g0, const uint32_t* __
     float4 x = make_float4(0.f, 0.f, 0.f, 0.f), y = x;
     float2 z = make_float2(0.f, 0.f);
     if (cur.has) {
-        x = recs.a[(size_t)kRecAB * (E0 + lane)];
-        y = recs.b[(size_t)kRecAB * (E0 + lane)];
-        z = recs.c[(size_t)kRecC * (E0 + lane)];
+        x = GSR_LD_REC(recs.a + (size_t)kRecAB * (E0 + lane));
+        y = GSR_LD_REC(recs.b + (size_t)kRecAB * (E0 + lane));
+        z = GSR_LD_REC(recs.c + (size_t)kRecC * (E0 + lane));
     }
     for (uint32_t base = E0; base < E1; base += 64) {
         const Slot nxt = base + 64 < E1 ? probe2(base + 64) : Slot{false, -1, lane};
         float4 nx = make_float4(0.f, 0.f, 0.f, 0.f), ny = nx;
         float2 nz = make_float2(0.f, 0.f);
         if (nxt.has) {
-            nx = recs.a[(size_t)kRecAB * (base + 64 + lane)];
-            ny = recs.b[(size_t)kRecAB * (base + 64 + lane)];
-            nz = recs.c[(size_t)kRecC * (base + 64 + lane)];
+            nx = GSR_LD_REC(recs.a + (size_t)kRecAB * (base + 64 + lane));
+            ny = GSR_LD_REC(recs.b + (size_t)kRecAB * (base + 64 + lane));
+            nz = GSR_LD_REC(recs.c + (size_t)kRecC * (base + 64 + lane));
         }
         // A chunk with no record adds nothing: skip its scan (uniform).  Behind saturated pixels
         // most instances have no record (5M@4K: 7.6M of 114.6M), so this is most chunks there.

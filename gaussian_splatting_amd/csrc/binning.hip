@@ -534,6 +534,15 @@ __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
     GSR_STAMP(g_st_scatter, blockIdx.x, 2);
 }
 
+// A/B: K4 reads each key once: streaming loads.
+#ifndef GSR_NT_KEYS
+#define GSR_NT_KEYS 0
+#endif
+#if GSR_NT_KEYS
+#define GSR_LD_KEY(p) __builtin_nontemporal_load(p)
+#else
+#define GSR_LD_KEY(p) (*(p))
+#endif
 // ---- K4 ---------------------------------------------------------------------
 // Bitonic sorting network over N2 = T * E keys, element i = thread * E + r held in
 // register a[r] (keys past the list are +infinity = ~0).  Exchange distance j:
@@ -635,7 +644,7 @@ __device__ __forceinline__ void sort_list(const u64* __restrict__ keys, uint32_t
     u64 a[E];
     const uint32_t i0 = threadIdx.x * E;
 #pragma unroll
-    for (int r = 0; r < E; r++) a[r] = i0 + r < n ? keys[lo + i0 + r] : ~0ull;
+    for (int r = 0; r < E; r++) a[r] = i0 + r < n ? GSR_LD_KEY(keys + lo + i0 + r) : ~0ull;
     bitonic_regs<T, E>(a, s_x);
 #pragma unroll
     for (int r = 0; r < E; r++)
@@ -747,7 +756,7 @@ __device__ bool bucket_sort_list(const u64* __restrict__ keys, uint32_t lo, uint
 #pragma unroll
     for (int e = 0; e < E; e++) {
         const uint32_t i = (uint32_t)e * T + tid;
-        k[e] = i < n ? keys[lo + i] : 0ull;
+        k[e] = i < n ? GSR_LD_KEY(keys + lo + i) : 0ull;
     }
 #pragma unroll
     for (int e = 0; e < E; e++) {

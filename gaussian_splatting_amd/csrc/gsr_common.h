@@ -331,6 +331,18 @@ template <uint32_t CTRL, uint32_t ROW_MASK, bool BOUND_ZERO>
 __device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROW_MASK, 0xf, BOUND_ZERO);
 }
+// Non-temporal (streaming) loads of vector types HIP defines as structs.
+__device__ __forceinline__ float4 load_nt(const float4* p) {
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    const v4f v = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ float2 load_nt(const float2* p) {
+    typedef float v2f __attribute__((ext_vector_type(2)));
+    const v2f v = __builtin_nontemporal_load(reinterpret_cast<const v2f*>(p));
+    return make_float2(v.x, v.y);
+}
+
 // Inclusive prefix sum / max over the wave: row_shr 1, 2, 4, 8 inside each 16-lane row, then
 // row_bcast:15 and row_bcast:31 carry the row totals up (identity 0).  Six VALU steps, no LDS.
 __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
