@@ -897,7 +897,13 @@ SideStream* side_stream() {
     SideStream& r = ss[dev];
     std::lock_guard<std::mutex> lk(r.mu);
     if (!r.ok && !r.s) {
-        r.ok = hipStreamCreateWithFlags(&r.s, hipStreamNonBlocking) == hipSuccess &&
+        // GSR_FILL_PRIO=1: the side stream at the device's highest priority, so the fill's few
+        // workgroups are dispatched ahead of render_bwd's queued ones (A/B switch)
+        const char* e = getenv("GSR_FILL_PRIO");
+        int lo = 0, hi = 0;
+        const bool prio = e && atoi(e) == 1 && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess;
+        r.ok = (prio ? hipStreamCreateWithPriority(&r.s, hipStreamNonBlocking, hi)
+                     : hipStreamCreateWithFlags(&r.s, hipStreamNonBlocking)) == hipSuccess &&
                hipEventCreateWithFlags(&r.fork, hipEventDisableTiming) == hipSuccess &&
                hipEventCreateWithFlags(&r.join, hipEventDisableTiming) == hipSuccess;
     }
