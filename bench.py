@@ -5,15 +5,23 @@
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 
 One step = ``_C.rasterize_gaussians`` + ``_C.rasterize_gaussians_backward`` for one
-view (+ the RCCL all-reduce of the flat 59-float-per-Gaussian gradient arena when
-N > 1), on synthetic inputs already resident in HBM.  Rank r
-renders view r (camera yawed by 5*r degrees), so per-GPU work is fixed as N grows
-("weak" scaling) and value = N * P * K / (max over ranks of the K-step time).
+view, on synthetic inputs already resident in HBM.  When N > 1
+the step also makes every rank's gradients the sum over all N views, by one of two
+exchanges over RCCL: the all-gather of the sparse per-view
+render-gradient blocks followed by the multi-view backward (``views``), or the
+all-reduce of the flat 59-float-per-Gaussian parameter-gradient arena (``allreduce``).
+``--exchange auto`` (the default) times both during the warm-up on this fabric, with the
+same collective count on every rank, and keeps the faster; the line's ``multi_gpu``
+object carries both timings and the pick.  Rank r renders view r (camera yawed by 5*r
+degrees), so per-GPU work is fixed as N grows ("weak" scaling) and value = N * P * K /
+(max over ranks of the K-step time).
 
 Rank 0 prints one JSON line.  It carries the roofline of the dominant kernel (its
 algorithmic bytes per launch / its mean duration from HIP events on the launch
-stream) and the CPU baseline: the oracle (C restatement of the reference,
-oracle/) timed on this host's cores on the same workload.
+stream), the host side of every step (``host``: forward call, the forward's wait for
+the instance count, backward enqueue, exchange), and the CPU baseline: the
+pure-PyTorch fallback rasterizer (oracle/torch_fallback.py) timed on one full frame
+on this host's cores, with the C restatement (oracle/) beside it.
 """
 from __future__ import annotations
 
@@ -69,29 +77,28 @@ def step_algorithmic_bytes(P, I, W, H, K):
 
 def cpu_baseline(cfg_name: str, P: int, W: int, H: int, forward_only: bool = False):
     """north_star's CPU baseline: the pure-PyTorch fallback rasterizer (oracle/torch_fallback.py, fp32)
-    on this host's cores, forward + autograd backward on the same frame as the GPU.  A bounded sample
-    (SURVEY.md 8d): preprocess, binning and the preprocess backward run in full; the render runs on a
-    stratified sample of the tiles and is scaled to the frame by list entries."""
+    on this host's cores, forward + autograd backward on the same frame as the GPU -- one FULL frame
+    (every tile rendered; SURVEY.md section 8d: 1 rep at configs 2/3, 5 forward reps at config 1),
+    after an untimed warm-up on a small tile sample."""
     from oracle import torch_fallback as tf
 
     scene, cam = syn.config_scene(cfg_name, seed=0, P=P)
     gc, gd = (None, None) if forward_only else syn.upstream_grads(H, W)
-    frac = 1.0 if P <= 100_000 else 0.25
-    reps = 5 if P <= 100_000 else 2
-    tf.splats_per_second(scene, cam, scene.sh_degree, gc, gd, tile_fraction=min(frac, 0.02))  # untimed warm-up
+    reps = 5 if P <= 100_000 else 1
+    tf.splats_per_second(scene, cam, scene.sh_degree, gc, gd, tile_fraction=0.02)  # untimed warm-up
     t0 = time.perf_counter()
-    value, t_frame, res = tf.splats_per_second(scene, cam, scene.sh_degree, gc, gd, tile_fraction=frac, reps=reps)
+    value, t_frame, res = tf.splats_per_second(scene, cam, scene.sh_degree, gc, gd, tile_fraction=1.0, reps=reps)
     wall = time.perf_counter() - t0
     threads = torch.get_num_threads()
     what = "forward" if forward_only else "forward + autograd backward"
-    sample = (f"{reps} reps of the full frame" if frac >= 1.0 else
-              f"{reps} reps; render on every {round(1 / frac)}th tile of the length-sorted order "
-              f"({res['rendered_instances']} of {res['num_rendered']} list entries), scaled by entries")
+    t = res["timings"]
     return {"value": value, "unit": "Gaussian-splats/s", "cores": threads, "host_cpus": os.cpu_count(),
             "kind": "port", "impl": "pure-PyTorch fallback rasterizer (oracle/torch_fallback.py, fp32)",
-            "sample": f"{cfg_name} ({P} Gaussians, {W}x{H}) {what}: {sample}; {t_frame:.2f} s per frame, "
-                      f"{wall:.1f} s timed, torch.get_num_threads() = {threads} (the box's OMP_NUM_THREADS share) "
-                      f"of os.cpu_count() = {os.cpu_count()}"}
+            "sample": f"{cfg_name} ({P} Gaussians, {W}x{H}) {what}: {reps} full frame(s), every tile rendered "
+                      f"({res['num_rendered']} list entries); {t_frame:.2f} s per frame (preprocess "
+                      f"{t['preprocess']:.2f}, binning {t['binning']:.2f}, render {t['render']:.2f}, preprocess "
+                      f"backward {t['preprocess_backward']:.2f} s), {wall:.1f} s timed, torch.get_num_threads() = "
+                      f"{threads} (the box's OMP_NUM_THREADS share) of os.cpu_count() = {os.cpu_count()}"}
 
 
 def cpu_baseline_c(cfg_name: str, P: int, W: int, H: int, threads: int, min_seconds: float = 8.0):
@@ -130,40 +137,74 @@ def cpu_only(cfg_name: str) -> None:
                       "cpu_baseline": base}), flush=True)
 
 
-def multi_rank_diagnostics(args, world, rank, views, ex, arena, per_rank, P, dev):
-    """N > 1: which exchange ran and why, its measured time alone (an untimed pass after the timed
-    region, every rank running the same collective count), the bytes each rank receives, and every
-    rank's own ms/step -- so a straggler or a wrong ``auto`` threshold shows in the record."""
+def multi_rank_diagnostics(args, world, exchange, ex, arena, per_rank, cand_ms, dev):
+    """N > 1: which exchange ran and why (the warm-up timings of both candidates when ``auto``), its
+    time alone (an untimed pass after the timed region, every rank running the same collective count),
+    the bytes each rank receives, and every rank's own ms/step -- so a straggler or a wrong pick shows
+    in the record."""
     reps = 5
     torch.cuda.synchronize()
     dist.barrier()
     t0 = time.perf_counter()
     for _ in range(reps):
-        if views:
+        if exchange == "views":
             ex.exchange()
+            ex.finish()
         else:
             arena.all_reduce()
     torch.cuda.synchronize()
     ms = torch.tensor([(time.perf_counter() - t0) / reps * 1e3], dtype=torch.float64, device=dev)
     dist.all_reduce(ms, op=dist.ReduceOp.MAX)
-    if views:
+    if exchange == "views":
         recv = ex.received_bytes()
-        why = (f"--exchange {args.exchange}: all-gather of "
-               + ("sparse view blocks (48 B per Gaussian with a non-zero render gradient; "
-                  f"{ex.last_entries} entries in the largest block)" if ex.sparse else "dense 44-B/Gaussian view blocks")
-               + (" -- auto picks it at every N: fewer received bytes than the 2(N-1)/N x 236 B/Gaussian all-reduce "
-                  "(DESIGN.md section 7)" if args.exchange == "auto" else ""))
+        what = ("all-gather of sparse view blocks (48 B per Gaussian with a non-zero render gradient; "
+                f"{ex.last_entries} entries gathered per rank at the capacity hint; "
+                f"{ex.resyncs} re-gathers after a hint below the count)" if ex.sparse and ex.last_entries else
+                "all-gather of dense 44-B/Gaussian view blocks") + " + the multi-view backward on every rank"
     else:
         recv = int(2 * (world - 1) / world * arena.flat.numel() * 4)
-        why = (f"--exchange {args.exchange}: RCCL all-reduce of the 59-float/Gaussian gradient arena"
-               + (" (auto picks it above 4 ranks, where the multi-view kernel's extra time would exceed the "
-                  "bytes saved at an assumed ~330 GB/s bus rate; DESIGN.md section 7)" if args.exchange == "auto"
-                  else ""))
-    return {"exchange": "views" if views else "allreduce", "why": why,
+        what = "RCCL all-reduce of the 59-float/Gaussian parameter-gradient arena"
+    if args.exchange == "auto":
+        why = ("--exchange auto: both exchanges timed in the warm-up on this fabric (whole steps, max over "
+               f"ranks, {args.auto_steps} steps each): " + ", ".join(f"{k} {v:.4f} ms/step" for k, v in cand_ms.items())
+               + f"; the faster is {exchange}")
+    else:
+        why = f"--exchange {args.exchange}"
+    return {"exchange": exchange, "what": what, "why": why, "candidates_ms_per_step": cand_ms or None,
             "exchange_ms": float(ms.item()), "received_bytes_per_rank": recv,
             "exchange_GBs_per_rank": recv / (float(ms.item()) * 1e-3) / 1e9 if ms.item() > 0 else None,
             "per_rank_ms_per_step": [round(e / args.steps * 1e3, 4) for e in per_rank],
             "backend": dist.get_backend()}
+
+
+class HostClock:
+    """Host-side timings of the timed steps (per step: the forward call, which includes its wait for
+    the instance count; forward return -> backward call; the backward call; the exchange), so every
+    run carries the evidence for a GPU that waits on the host."""
+
+    KEYS = ("forward_call", "fwd_return_to_bwd_call", "backward_call", "exchange", "step_wall")
+
+    def __init__(self):
+        self.t = {k: [] for k in self.KEYS}
+        self.gc_runs = 0
+        self.on = False
+
+    def add(self, k, dt):
+        if self.on:
+            self.t[k].append(dt * 1e3)
+
+    def summary(self, wait):
+        import statistics
+
+        out = {}
+        for k, v in self.t.items():
+            if v:
+                out[k + "_ms"] = {"mean": round(statistics.fmean(v), 4), "median": round(statistics.median(v), 4),
+                                  "max": round(max(v), 4)}
+        out["count_wait_ms"] = {"mean": round(wait["total_ms"] / wait["calls"], 4) if wait["calls"] else None,
+                                "max": round(wait["max_ms"], 4), "calls": wait["calls"]}
+        out["python_gc_collections"] = self.gc_runs
+        return out
 
 
 def main():
@@ -176,8 +217,10 @@ def main():
     ap.add_argument("--no-census", action="store_true",
                     help="skip the census pass (profiler runs: keeps its kernel instantiations out of the trace)")
     ap.add_argument("--exchange", choices=("auto", "views", "dense", "allreduce"), default="auto",
-                    help="N > 1: all-gather the sparse view blocks (views; auto picks it at every N), the dense "
-                         "view blocks (dense), or all-reduce the parameter gradients (DESIGN.md section 7)")
+                    help="N > 1: all-gather the sparse view blocks (views), the dense view blocks (dense), or "
+                         "all-reduce the parameter gradients (allreduce); auto times views and allreduce in the "
+                         "warm-up and keeps the faster (DESIGN.md section 7)")
+    ap.add_argument("--auto-steps", type=int, default=5, help="timed warm-up steps per candidate of --exchange auto")
     ap.add_argument("--cpu-threads", type=int, default=0, help="threads of the C-restatement figure (default 16)")
     ap.add_argument("--cpu-only", action="store_true",
                     help="no GPU: time the pure-PyTorch fallback forward on --config (BASELINE configs[0] plumbing)")
@@ -216,26 +259,42 @@ def main():
     bg = torch.zeros(3, device=dev)
     empty = torch.empty(0, device=dev)
     arena = GradArena(P, scene.shs.shape[1], dev)
-    views = world > 1 and args.exchange in ("auto", "views", "dense")
-    ex = ViewExchange(P, dev, sparse=args.exchange != "dense") if views else None
+    uses_views = world > 1 and args.exchange in ("auto", "views", "dense")
+    ex = ViewExchange(P, dev, sparse=args.exchange != "dense") if uses_views else None
+    # the exchange the steps run: fixed by --exchange, or (auto) picked by timing in the warm-up below
+    exchange = "none" if world == 1 else ("allreduce" if args.exchange == "allreduce" else
+                                          "views" if args.exchange in ("views", "dense") else "views")
+    clock = HostClock()
+    pc = time.perf_counter
 
     def step(collective=True):
+        t0 = pc()
         fwd = _C.rasterize_gaussians(bg, scene.means3D, empty, scene.opacities, scene.scales, scene.rotations, 1.0,
                                      empty, cam.viewmatrix, cam.projmatrix, cam.tanfovx, cam.tanfovy, H, W, scene.shs,
                                      Kdeg, cam.campos, False, False, False)
+        t1 = pc()
         nr, color, radii, geom, binning, img, invd = fwd
         bwd = (bg, scene.means3D, radii, empty, scene.opacities, scene.scales, scene.rotations, 1.0, empty,
                cam.viewmatrix, cam.projmatrix, cam.tanfovx, cam.tanfovy, gc, gd, scene.shs, Kdeg, cam.campos, geom, nr,
                binning, img, False, False)
-        if views and collective:  # N > 1: exchange the 44-B view blocks, every rank sums all views' gradients
+        t2 = pc()
+        if exchange == "views" and collective:  # sparse view blocks, every rank sums all views' gradients
             _C.rasterize_gaussians_backward_screen(*bwd, view_block=ex.local_block())
+            t3 = pc()
             ex.exchange(zero=arena.flat)  # the outputs zeroed beside the exchange; a live-list backward
             ex.views_backward(scene.means3D, None, scene.shs, Kdeg, scene.opacities, scene.scales, scene.rotations,
                               1.0, out=arena.views())
         else:
             _C.rasterize_gaussians_backward(*bwd, out=arena.views())
+            t3 = pc()
             if world > 1 and collective:
                 arena.all_reduce()
+        t4 = pc()
+        clock.add("forward_call", t1 - t0)
+        clock.add("fwd_return_to_bwd_call", t2 - t1)
+        clock.add("backward_call", t3 - t2)
+        if world > 1 and collective:
+            clock.add("exchange", t4 - t3)
         return nr
 
     # Untimed clock ramp: the GPU lowers its clock when idle and takes ~0.1 s of load to come back
@@ -251,6 +310,27 @@ def main():
     for _ in range(args.warmup):
         nr = step()
     torch.cuda.synchronize()
+    # --exchange auto at N > 1: time whole steps with each exchange on this fabric (the same number of
+    # steps and collectives on every rank, the max over ranks), keep the faster
+    cand_ms = {}
+    if world > 1 and args.exchange == "auto":
+        for cand in ("views", "allreduce"):
+            exchange = cand
+            for _ in range(2):
+                step()
+            torch.cuda.synchronize()
+            dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(args.auto_steps):
+                step()
+            torch.cuda.synchronize()
+            tt = torch.tensor([(time.perf_counter() - t0) / args.auto_steps * 1e3], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            cand_ms[cand] = float(tt.item())
+        exchange = min(cand_ms, key=cand_ms.get)
+        for _ in range(2):
+            step()
+        torch.cuda.synchronize()
     # Per-stage breakdown in a separate, untimed pass: every timed stage adds an event pair
     # (~10 us of idle GPU each), so the timed region below records events only around the
     # dominant kernel.
@@ -272,18 +352,31 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    import gc as _gc
+
+    def _gc_cb(phase, info):
+        if phase == "start" and clock.on:
+            clock.gc_runs += 1
+    _gc.callbacks.append(_gc_cb)
+    _lib.host_wait_stats(reset=True)
+    clock.on = True
     t0 = time.perf_counter()
     for i in range(args.steps):
+        ts = pc()
         # the dominant kernel's launches are timed live, on its own stream, on every `every`-th step
         if i % every == 0:
             _lib.profile_enable(True, stages=[dom])
         elif i % every == 1:
             _lib.profile_enable(False)
         nr = step()
+        clock.add("step_wall", pc() - ts)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    clock.on = False
+    _gc.callbacks.remove(_gc_cb)
+    host = clock.summary(_lib.host_wait_stats())
     _lib.profile_enable(False)
     dom_total, dom_calls = _lib.profile_collect()[dom]
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -294,7 +387,7 @@ def main():
         per_rank = [float(g.item()) for g in gathered]
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
-    multi = multi_rank_diagnostics(args, world, rank, views, ex, arena, per_rank, P, dev) if world > 1 else None
+    multi = multi_rank_diagnostics(args, world, exchange, ex, arena, per_rank, cand_ms, dev) if world > 1 else None
 
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
@@ -302,9 +395,10 @@ def main():
         dom_ms = dom_total / dom_calls if dom_calls else 0.0  # HIP events on the launch stream, timed region
         alg = algorithmic_bytes(dom, P, nr, W, H, K)
         traffic, traffic_src, kk = None, None, {}
-        if args.config == "1m_1080p_sh3" and os.path.exists(PMC_PROFILE):
+        if os.path.exists(PMC_PROFILE):
             prof = json.load(open(PMC_PROFILE))
-            kk = prof.get("kernels", {}).get(dom) or {}
+            kk = (prof.get("configs", {}).get(args.config) or
+                  (prof if prof.get("config", "1m_1080p_sh3") == args.config else {})).get("kernels", {}).get(dom) or {}
             if kk:
                 traffic = kk["hbm_read_bytes"] + kk["hbm_write_bytes"]
                 traffic_src = prof.get("source")
@@ -323,6 +417,10 @@ def main():
         # BASELINE.json's metric names the headline workload; another --config says its own
         metric = ("Gaussian-splats/sec fwd+bwd @1080p, 1M Gaussians" if args.config == "1m_1080p_sh3" else
                   f"Gaussian-splats/sec fwd+bwd @{W}x{H}, {P} Gaussians ({args.config}; not the headline metric)")
+        par = f"view-sharded x{world}"
+        if world > 1:
+            par += {"views": " + RCCL all-gather of " + ("sparse " if ex is not None and ex.sparse else "dense ")
+                    + "view blocks", "allreduce": " + RCCL all-reduce of the gradient arena"}[exchange]
         line = {
             "metric": metric,
             "value": value,
@@ -338,12 +436,12 @@ def main():
             "dtype": "fp32",
             "data": "synthetic (frustum-uniform Gaussians, SURVEY.md 8d; seed 0)",
             "config": {"workload": args.config, "gaussians": P, "width": W, "height": H, "sh_degree": Kdeg,
-                       "num_rendered": nr, "views": "one per GPU, yaw 5 deg x rank",
-                       "parallelism": f"view-sharded x{world}" + (
-                           "" if world == 1 else (" + RCCL all-gather of " + ("sparse " if ex.sparse else "")
-                                                  + "view blocks") if views else " + RCCL all-reduce")},
+                       "num_rendered": nr, "views": "one per GPU, yaw 5 deg x rank", "parallelism": par},
             "roofline": {"kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                         # counter bytes per launch over the launch time: the HBM rate the kernel really moves
+                         "traffic_frac": (traffic / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+                                          if traffic is not None and dom_ms > 0 else None),
                          "algorithmic_bytes_per_launch": alg, "mean_launch_ms": dom_ms, "timed_launches": int(dom_calls), "timed_every": every,
                          # what actually limits the render kernels: "hbm" above is the
                          # contract's roofline axis, not the limiter
@@ -352,6 +450,7 @@ def main():
                          "valu_issue_frac": valu_frac},
             "work": work,
             "stage_ms": {k: round(v, 4) for k, v in per_stage.items()},  # untimed breakdown pass
+            "host": host,
             "step_algorithmic_GBs": step_algorithmic_bytes(P, nr, W, H, K) / (ms_per_step * 1e-3) / 1e9,
         }
         if multi is not None:

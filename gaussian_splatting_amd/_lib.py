@@ -87,6 +87,10 @@ SIGNATURES = {
                                            _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gsr_debug_forward_state": (_i, [_i, _i, _i, _i, _i, ctypes.c_size_t, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gsr_forward_rebuilds": (ctypes.c_longlong, []),
+    "gsr_option_set": (_i, [ctypes.c_char_p, _i]),
+    "gsr_host_wait_stats": (_i, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                 ctypes.POINTER(ctypes.c_longlong), _i]),
+    "gsr_option_get": (_i, [ctypes.c_char_p]),
     "gsr_last_error": (ctypes.c_char_p, []),
     "gsr_version": (ctypes.c_char_p, []),
     "gsr_profile_enable": (_i, [_i]),
@@ -164,6 +168,51 @@ def check(rc: int, what: str) -> None:
 
 def version() -> str:
     return load().gsr_version().decode()
+
+
+# ---- runtime options (include/gsr.h gsr_option_set) ---------------------------------
+OPTIONS = ("fused_bin", "fwd_quads", "bwd_seg_ck", "host_total", "zero_fill", "live_list")
+
+
+def option_get(name: str) -> int:
+    v = int(load().gsr_option_get(name.encode()))
+    if v < 0:
+        raise GsrError(f"unknown libgsr option {name!r}")
+    return v
+
+
+def option_set(name: str, value: int) -> None:
+    check(load().gsr_option_set(name.encode(), int(value)), "option_set")
+
+
+class options:
+    """Context manager: set libgsr options for a block and restore them afterwards.
+
+        with _lib.options(zero_fill=2, live_list=0):
+            ...
+    """
+
+    def __init__(self, **values):
+        self.values = values
+        self.saved = {}
+
+    def __enter__(self):
+        for k, v in self.values.items():
+            self.saved[k] = option_get(k)
+            option_set(k, v)
+        return self
+
+    def __exit__(self, *exc):
+        for k, v in self.saved.items():
+            option_set(k, v)
+        return False
+
+
+def host_wait_stats(reset: bool = False) -> dict:
+    """Host time the forwards spent waiting for their instance count (include/gsr.h)."""
+    tot, mx, n = ctypes.c_double(0), ctypes.c_double(0), ctypes.c_longlong(0)
+    load().gsr_host_wait_stats(ctypes.byref(tot), ctypes.byref(mx), ctypes.byref(n), int(bool(reset)))
+    return {"total_ms": tot.value, "max_ms": mx.value, "calls": int(n.value)}
 
 
 # ---- stage profiler ---------------------------------------------------------------

@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstring>
 #include <atomic>
+#include <chrono>
 #include <mutex>
 #include <vector>
 
@@ -254,47 +255,84 @@ void carve_recs(char* base, size_t R, size_t P, gsr::GradRecs* recs, gsr::GradRe
     *total = align_up(c.off);
 }
 
-// Backward segment length in checkpoints (GSR_BWD_SEG_CK, default 1 = kCkStride entries per wave;
-// a large value gives one wave per tile, the schedule before checkpoints, for A/B runs).
-int bwd_segment_checkpoints() {
-    static const int v = [] {
-        const char* e = getenv("GSR_BWD_SEG_CK");
-        const int x = e ? atoi(e) : 1;
-        return x >= 1 ? (x > (1 << 20) ? (1 << 20) : x) : 1;
-    }();
-    return v;
-}
-
-// K2 folded into K3 in capacity mode (GSR_FUSED_BIN, default 1).
+// ---- runtime options (include/gsr.h gsr_option_set) ------------------------------
+// The library's alternative kernel paths.  Each default comes from GSR_<NAME> in the environment
+// at first use; gsr_option_set changes it for later calls (tests/test_gpu_options.py runs every
+// path against the oracle).
 #ifndef GSR_FUSED_BIN_DEFAULT
 #define GSR_FUSED_BIN_DEFAULT 1
 #endif
-bool fused_binning_mode() {
-    static const bool v = [] {
-        const char* e = getenv("GSR_FUSED_BIN");
-        return e ? atoi(e) != 0 : GSR_FUSED_BIN_DEFAULT != 0;
-    }();
-    return v;
+#ifndef GSR_ZERO_FILL_DEFAULT
+#define GSR_ZERO_FILL_DEFAULT 1
+#endif
+#ifndef GSR_LIVE_LIST_DEFAULT
+#define GSR_LIVE_LIST_DEFAULT 1
+#endif
+enum Opt { OPT_FUSED_BIN = 0, OPT_FWD_QUADS, OPT_BWD_SEG_CK, OPT_HOST_TOTAL, OPT_ZERO_FILL, OPT_LIVE_LIST, OPT_COUNT };
+struct OptionSpec {
+    const char* name;
+    const char* env;
+    int def, lo, hi;
+};
+const OptionSpec kOptions[OPT_COUNT] = {
+    {"fused_bin", "GSR_FUSED_BIN", GSR_FUSED_BIN_DEFAULT, 0, 1},
+    {"fwd_quads", "GSR_FWD_QUADS", 2, 2, 4},
+    {"bwd_seg_ck", "GSR_BWD_SEG_CK", 1, 1, 1 << 20},
+    {"host_total", "GSR_HOST_TOTAL", 1, 0, 1},
+    {"zero_fill", "GSR_ZERO_FILL", GSR_ZERO_FILL_DEFAULT, 0, 2},
+    {"live_list", "GSR_LIVE_LIST", GSR_LIVE_LIST_DEFAULT, 0, 1},
+};
+std::atomic<int> g_opt[OPT_COUNT];
+std::once_flag g_opt_once;
+
+void options_init() {
+    std::call_once(g_opt_once, [] {
+        for (int i = 0; i < OPT_COUNT; i++) {
+            const OptionSpec& o = kOptions[i];
+            int v = o.def;
+            if (const char* e = getenv(o.env)) {
+                const int x = atoi(e);
+                // out-of-range values clamp (a huge GSR_BWD_SEG_CK means "one unit per tile")
+                v = x < o.lo ? o.lo : x > o.hi ? o.hi : x;
+                if (i == OPT_FWD_QUADS) v = x == 4 ? 4 : 2;
+            }
+            g_opt[i].store(v, std::memory_order_relaxed);
+        }
+    });
 }
+
+int option(int id) {
+    options_init();
+    return g_opt[id].load(std::memory_order_relaxed);
+}
+
+int option_index(const char* name) {
+    if (!name) return -1;
+    for (int i = 0; i < OPT_COUNT; i++)
+        if (strcmp(name, kOptions[i].name) == 0) return i;
+    return -1;
+}
+
+// Backward segment length in checkpoints (1 = kCkStride entries per wave; a large value gives one
+// wave per tile, the schedule before checkpoints).
+int bwd_segment_checkpoints() { return option(OPT_BWD_SEG_CK); }
+
+// K2 folded into K3 in capacity mode.
+bool fused_binning_mode() { return option(OPT_FUSED_BIN) != 0; }
 
 // Per (host thread, device): a pinned 8-byte slot that num_rendered is copied into and the
 // event recorded behind that copy.  The host waits on the event -- i.e. for the binning
 // counts -- and not for the whole stream, so the render kernels queued behind the copy keep
 // the GPU busy while the host returns to Python and queues the backward.
-// By default the slot is coherent and mapped, and K2 stores the count into it itself
-// (`dev`), so no copy is queued behind K2; GSR_HOST_TOTAL=0 selects the copy (A/B runs).
+// The slot is coherent and mapped, and by default K2 stores the count into it itself
+// (`dev`), so no copy is queued behind K2; the "host_total" option 0 selects the copy.
 struct TotalReadback {
     unsigned long long* host = nullptr;
-    unsigned long long* dev = nullptr;  // device view of `host`, or null: copy instead
+    unsigned long long* mapped = nullptr;  // device view of `host`
+    unsigned long long* dev = nullptr;     // `mapped` when the kernels store the count, null: copy instead
     hipEvent_t ev = nullptr;
 };
-bool host_total_store() {
-    static const bool v = [] {
-        const char* e = getenv("GSR_HOST_TOTAL");
-        return !e || atoi(e) != 0;
-    }();
-    return v;
-}
+bool host_total_store() { return option(OPT_HOST_TOTAL) != 0; }
 int total_readback(TotalReadback** out) {
     constexpr int kMaxDevices = 64;
     thread_local TotalReadback slots[kMaxDevices];
@@ -303,13 +341,13 @@ int total_readback(TotalReadback** out) {
         return fail(GSR_ERR_HIP, "num_rendered readback: no current device");
     TotalReadback& r = slots[dev];
     if (!r.host) {
+        // always mapped + coherent, so the "host_total" option can switch between the kernels'
+        // own store (dev) and a queued copy (readback_dev() == null) from one call to the next
         void* h = nullptr;
-        const bool mapped = host_total_store();
-        if (hipHostMalloc(&h, sizeof(unsigned long long),
-                          mapped ? hipHostMallocMapped | hipHostMallocCoherent : hipHostMallocDefault) != hipSuccess)
+        if (hipHostMalloc(&h, sizeof(unsigned long long), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
             return fail(GSR_ERR_HIP, "num_rendered readback: hipHostMalloc failed");
         void* d = nullptr;
-        if (mapped && hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+        if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
             (void)hipHostFree(h);
             return fail(GSR_ERR_HIP, "num_rendered readback: hipHostGetDevicePointer failed");
         }
@@ -318,14 +356,17 @@ int total_readback(TotalReadback** out) {
             return fail(GSR_ERR_HIP, "num_rendered readback: hipEventCreate failed");
         }
         r.host = (unsigned long long*)h;
-        r.dev = (unsigned long long*)d;
+        r.mapped = (unsigned long long*)d;
     }
+    r.dev = host_total_store() ? r.mapped : nullptr;
     *out = &r;
     return GSR_OK;
 }
 
 // Forwards whose capacity hint was too small (the binning stage was redone), for gsr_forward_rebuilds().
 std::atomic<long long> g_rebuilds{0};
+// Host time spent waiting for the forward's instance count (gsr_host_wait_stats).
+std::atomic<long long> g_wait_ns{0}, g_wait_calls{0}, g_wait_max_ns{0};
 
 void* call_alloc(gsr_alloc_fn fn, void* ctx, size_t bytes) {
     if (!fn) return nullptr;
@@ -341,6 +382,35 @@ const char* gsr_last_error(void) { return g_err; }
 const char* gsr_version(void) { return "gsr 0.2.0 gfx950"; }
 
 long long gsr_forward_rebuilds(void) { return g_rebuilds.load(std::memory_order_relaxed); }
+
+int gsr_host_wait_stats(double* total_ms, double* max_ms, long long* calls, int reset) {
+    if (total_ms) *total_ms = (double)g_wait_ns.load(std::memory_order_relaxed) * 1e-6;
+    if (max_ms) *max_ms = (double)g_wait_max_ns.load(std::memory_order_relaxed) * 1e-6;
+    if (calls) *calls = g_wait_calls.load(std::memory_order_relaxed);
+    if (reset) {
+        g_wait_ns.store(0, std::memory_order_relaxed);
+        g_wait_max_ns.store(0, std::memory_order_relaxed);
+        g_wait_calls.store(0, std::memory_order_relaxed);
+    }
+    return GSR_OK;
+}
+
+int gsr_option_set(const char* name, int value) {
+    g_err[0] = 0;
+    const int i = option_index(name);
+    if (i < 0) return fail(GSR_ERR_ARGUMENT, "option_set: unknown option '%s'", name ? name : "(null)");
+    const OptionSpec& o = kOptions[i];
+    if (value < o.lo || value > o.hi || (i == OPT_FWD_QUADS && value != 2 && value != 4))
+        return fail(GSR_ERR_ARGUMENT, "option_set: %s = %d out of range [%d, %d]", name, value, o.lo, o.hi);
+    options_init();
+    g_opt[i].store(value, std::memory_order_relaxed);
+    return GSR_OK;
+}
+
+int gsr_option_get(const char* name) {
+    const int i = option_index(name);
+    return i < 0 ? -1 : option(i);
+}
 
 int gsr_fused_ssim_forward(int B, int CH, int H, int W, float C1, float C2, const float* img1, const float* img2,
                            float* ssim_map, float* dm_dmu1, float* dm_dsigma1_sq, float* dm_dsigma12, void* stream) {
@@ -746,7 +816,15 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
         return GSR_OK;
     };
     auto wait_total = [&](unsigned long long* total) -> int {
-        HIP_TRY(hipEventSynchronize(rb->ev), "num_rendered sync");
+        const auto t0 = std::chrono::steady_clock::now();
+        const hipError_t we = hipEventSynchronize(rb->ev);
+        const long long ns =
+            (long long)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+        g_wait_ns.fetch_add(ns, std::memory_order_relaxed);
+        g_wait_calls.fetch_add(1, std::memory_order_relaxed);
+        long long prev = g_wait_max_ns.load(std::memory_order_relaxed);
+        while (ns > prev && !g_wait_max_ns.compare_exchange_weak(prev, ns, std::memory_order_relaxed)) {}
+        HIP_TRY(we, "num_rendered sync");
         *total = *rb->host;
         if (*total > (unsigned long long)INT_MAX)
             return fail(GSR_ERR_OVERFLOW, "rasterize_forward: %llu tile instances exceed INT_MAX", *total);
@@ -790,7 +868,7 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
             ra.tile_join = geom.tile_join;
             ra.seg_ck = bwd_segment_checkpoints();
             ra.census = g_census;
-            HIP_TRY(launch_render_fwd(ra, stream), "render_fwd");
+            HIP_TRY(launch_render_fwd(ra, stream, option(OPT_FWD_QUADS)), "render_fwd");
         }
         return check_debug(debug, stream, "render_fwd");
     };
@@ -857,31 +935,12 @@ int gsr_rasterize_forward_ex(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_
 namespace {
 // The backward's dense outputs are zero-filled on a side stream that runs beside render_bwd
 // (VALU-bound: HBM is two-thirds idle under it); gauss_bwd then writes only the rows of
-// Gaussians with a non-zero render gradient (about 14% of a 1M@1080p view).  GSR_ZERO_FILL:
+// Gaussians with a non-zero render gradient (about 14% of a 1M@1080p view).  "zero_fill" option:
 // 1 (default) side stream, 2 main stream right before gauss_bwd, 0 gauss_bwd writes every row.
-#ifndef GSR_ZERO_FILL_DEFAULT
-#define GSR_ZERO_FILL_DEFAULT 1
-#endif
-// gauss_bwd over the list of Gaussians with a gradient (GSR_LIVE_LIST, default 1) or a lane per
+// "live_list": gauss_bwd over the list of Gaussians with a gradient (1, default) or a lane per
 // Gaussian (0), when the outputs are zero-filled.
-#ifndef GSR_LIVE_LIST_DEFAULT
-#define GSR_LIVE_LIST_DEFAULT 1
-#endif
-bool live_list_mode() {
-    static const bool v = [] {
-        const char* e = getenv("GSR_LIVE_LIST");
-        return e ? atoi(e) != 0 : GSR_LIVE_LIST_DEFAULT != 0;
-    }();
-    return v;
-}
-
-int zero_fill_mode() {
-    static const int v = [] {
-        const char* e = getenv("GSR_ZERO_FILL");
-        return e ? atoi(e) : GSR_ZERO_FILL_DEFAULT;
-    }();
-    return v;
-}
+bool live_list_mode() { return option(OPT_LIVE_LIST) != 0; }
+int zero_fill_mode() { return option(OPT_ZERO_FILL); }
 
 struct SideStream {
     std::mutex mu;  // one backward at a time per device uses the pair of events
@@ -897,13 +956,7 @@ SideStream* side_stream() {
     SideStream& r = ss[dev];
     std::lock_guard<std::mutex> lk(r.mu);
     if (!r.ok && !r.s) {
-        // GSR_FILL_PRIO=1: the side stream at the device's highest priority, so the fill's few
-        // workgroups are dispatched ahead of render_bwd's queued ones (A/B switch)
-        const char* e = getenv("GSR_FILL_PRIO");
-        int lo = 0, hi = 0;
-        const bool prio = e && atoi(e) == 1 && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess;
-        r.ok = (prio ? hipStreamCreateWithPriority(&r.s, hipStreamNonBlocking, hi)
-                     : hipStreamCreateWithFlags(&r.s, hipStreamNonBlocking)) == hipSuccess &&
+        r.ok = hipStreamCreateWithFlags(&r.s, hipStreamNonBlocking) == hipSuccess &&
                hipEventCreateWithFlags(&r.fork, hipEventDisableTiming) == hipSuccess &&
                hipEventCreateWithFlags(&r.join, hipEventDisableTiming) == hipSuccess;
     }
@@ -1016,13 +1069,34 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
     if (use_list && R == 0)
         HIP_TRY(hipMemsetAsync(live_count, 0, sizeof(uint32_t) * kLiveShards * kLiveCntStride, stream), "live count");
     SideStream* side = zmode == 1 && !debug && fill.count ? side_stream() : nullptr;
-    std::unique_lock<std::mutex> side_lock;
+    // Once the fill is queued on the side stream, `stream` must not run ahead of it on ANY return:
+    // the caller may free the outputs it writes as soon as this function fails, and the caching
+    // allocator would hand their memory to new work on `stream` while the fill still writes it.
+    struct SideJoin {
+        SideStream* side = nullptr;
+        hipStream_t stream = nullptr;
+        bool armed = false;
+        std::unique_lock<std::mutex> lock;
+        void join() {
+            if (!armed) return;
+            armed = false;
+            if (hipStreamWaitEvent(stream, side->join, 0) != hipSuccess) (void)hipStreamSynchronize(side->s);
+        }
+        ~SideJoin() { join(); }
+    } sj;
     if (side) {  // fork: the side stream starts after everything queued so far on `stream`
-        side_lock = std::unique_lock<std::mutex>(side->mu);
+        sj.lock = std::unique_lock<std::mutex>(side->mu);
+        sj.side = side;
+        sj.stream = stream;
         HIP_TRY(hipEventRecord(side->fork, stream), "zero fill fork");
         HIP_TRY(hipStreamWaitEvent(side->s, side->fork, 0), "zero fill fork");
-        HIP_TRY(launch_zero_fill(fill, side->s), "zero fill");
-        HIP_TRY(hipEventRecord(side->join, side->s), "zero fill join");
+        const hipError_t fe = launch_zero_fill(fill, side->s);
+        const hipError_t je = hipEventRecord(side->join, side->s);
+        if (fe != hipSuccess || je != hipSuccess) {
+            (void)hipStreamSynchronize(side->s);  // whatever was queued has finished
+            return fail(GSR_ERR_HIP, "zero fill: %s", hipGetErrorString(fe != hipSuccess ? fe : je));
+        }
+        sj.armed = true;
     }
 
     if (R > 0) {
@@ -1066,8 +1140,8 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
         ga.dL_dinvdepth = dL_dinvdepth; ga.dL_dmean3D = dL_dmean3D; ga.dL_dcov3D = dL_dcov3D;
         ga.dL_dsh = M > (dc ? 1 : 0) ? dL_dsh : nullptr; ga.dL_ddc = dc ? dL_ddc : nullptr; ga.dL_dscale = dL_dscale; ga.dL_drot = dL_drot;
         if (side) {  // join: gauss_bwd writes over the zeroed outputs
-            HIP_TRY(hipStreamWaitEvent(stream, side->join, 0), "zero fill join");
-            side_lock.unlock();
+            sj.join();
+            sj.lock.unlock();
         } else if (zmode) {
             HIP_TRY(launch_zero_fill(fill, stream), "zero fill");
         }

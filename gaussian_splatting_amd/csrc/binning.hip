@@ -373,7 +373,12 @@ __global__ void __launch_bounds__(kBinThreads) tile_scan_kernel(uint32_t tiles, 
                 const u64 lo = at < cap ? at : cap, hi = at + v[i] < cap ? at + v[i] : cap;
                 ranges[b + i] = make_uint2((uint32_t)lo, (uint32_t)hi);
                 tile_base[b + i] = (uint32_t)at;
-                if (v[i] > kSortWaveMax) {  // long list: one of the class kernels (K4)
+                // long list: one of the class kernels (K4).  Filed by the RAW count: on a truncated
+                // pass (capacity hint too small) a tile whose clamped length is <= kSortWaveMax is
+                // then sorted twice -- by tile_sort_kernel (which goes by the clamped length) and by
+                // its class kernel -- into the same order, and the pass is rebuilt exactly anyway
+                // (api.hip), so a tile may have two sorters only in a pass whose lists are discarded.
+                if (v[i] > kSortWaveMax) {
                     const int c = v[i] <= kClass0Max ? 0 : 1;
                     cls_list[(size_t)c * tiles + atomicAdd(&s_cls[c], 1u)] = b + i;
                 }
@@ -463,6 +468,7 @@ __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
             fs.total[0] = carry_t;
             if (fs.host_total) __hip_atomic_store(fs.host_total, carry_t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
+        // (classes by raw count, as K2: see the note there on truncated passes)
         // this workgroup's long-list tiles into the class lists: counted in LDS, one global atomic
         // per class reserves the workgroup's run (one global atomic per tile serialised ~30000
         // returning atomics on one counter at 4K: +340 us), then each tile takes its slot

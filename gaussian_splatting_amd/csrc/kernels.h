@@ -382,7 +382,8 @@ hipError_t launch_tile_sort(uint32_t tiles, const uint2* ranges, const GeomState
                             size_t cap, hipStream_t stream, bool zero_counts = false, uint32_t cells = 0);
 bool bin_fused_ok(uint32_t tiles);  // the fused form applies (LDS cursors)
 // render.hip
-hipError_t launch_render_fwd(const RenderFwdArgs& a, hipStream_t stream);
+// quads: 8x8 quadrants per wave, 2 (half tiles) or 4 (whole tiles; the "fwd_quads" option)
+hipError_t launch_render_fwd(const RenderFwdArgs& a, hipStream_t stream, int quads = 2);
 // a tile-major pixel plane (tile_px) -> image order [H][W], 4-byte elements (inspection only)
 hipError_t launch_untile(const uint32_t* src, uint32_t* dst, int W, int H, uint32_t gx, hipStream_t stream);
 hipError_t launch_render_bwd(const RenderBwdArgs& a, size_t max_units, hipStream_t stream);

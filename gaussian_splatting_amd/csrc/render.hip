@@ -332,22 +332,14 @@ hipError_t launch_untile(const uint32_t* src, uint32_t* dst, int W, int H, uint3
     return hipGetLastError();
 }
 
-// Quadrants per forward wave: 2 (half tiles) unless GSR_FWD_QUADS=4 (whole tiles, for A/B runs).
-static int fwd_quads_per_wave() {
-    static const int v = [] {
-        const char* e = getenv("GSR_FWD_QUADS");
-        return (e && atoi(e) == 4) ? 4 : 2;
-    }();
-    return v;
-}
-
-hipError_t launch_render_fwd(const RenderFwdArgs& a, hipStream_t stream) {
+// Quadrants per forward wave: 2 (half tiles) or 4 (whole tiles; the "fwd_quads" option, api.hip).
+hipError_t launch_render_fwd(const RenderFwdArgs& a, hipStream_t stream, int quads) {
     const uint32_t tiles = a.gx * a.gy;
     if (tiles == 0) return hipSuccess;
     const uint32_t groups = (tiles + 7) / 8;
     if (a.census)
         hipLaunchKernelGGL((render_fwd_kernel<2, true>), dim3(groups * 16), dim3(kWave), 0, stream, a);
-    else if (fwd_quads_per_wave() == 4)
+    else if (quads == 4)
         hipLaunchKernelGGL((render_fwd_kernel<4, false>), dim3(groups * 8), dim3(kWave), 0, stream, a);
     else
         hipLaunchKernelGGL((render_fwd_kernel<2, false>), dim3(groups * 16), dim3(kWave), 0, stream, a);

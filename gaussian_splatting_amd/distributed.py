@@ -2,13 +2,21 @@
 
 The reference trains on one GPU, one view per iteration (train.py:131-143).  Views
 are independent, so N ranks each render their own view with a replicated copy of
-the Gaussians, and exchange exactly one thing: the parameter gradients.  The six
-parameter groups of ``GaussianModel`` (``_xyz``, ``_features_dc``, ``_features_rest``,
-``_opacity``, ``_scaling``, ``_rotation``; scene/gaussian_model.py:235-242) are laid
-out back to back in one flat fp32 arena -- 59 floats per Gaussian at SH degree 3 --
-that the backward writes into directly, followed by ONE all-reduce over RCCL
-(backend "nccl" on ROCm).  Every rank then applies the same optimizer step, so the
-replicas stay identical without a broadcast.
+the Gaussians, and exchange one step's gradient information over RCCL (backend
+"nccl" on ROCm).  Two exchanges are provided:
+
+* ``GradArena.all_reduce`` -- north_star's form: the six parameter groups of
+  ``GaussianModel`` (``_xyz``, ``_features_dc``, ``_features_rest``, ``_opacity``,
+  ``_scaling``, ``_rotation``; scene/gaussian_model.py:235-242) back to back in one flat
+  fp32 arena (59 floats per Gaussian at SH degree 3) that the backward writes into
+  directly, reduced by ONE all-reduce;
+* ``ViewExchange`` -- the per-view render-gradient sums (10 floats of the Gaussians that
+  have one, ~14% of a 1M@1080p view) all-gathered, and the per-Gaussian backward run over
+  all gathered views on every rank.
+
+``bench.py --exchange auto`` times both in its warm-up on the real fabric and keeps the
+faster.  Either way every rank ends with the same summed gradients and applies the same
+optimizer step, so the replicas stay identical without a broadcast.
 """
 from __future__ import annotations
 
@@ -111,20 +119,25 @@ class ViewExchange:
 
     Instead of all-reducing the parameter gradients (``GradArena.all_reduce``: 2 (N-1)/N x 59
     floats per Gaussian through every rank's xGMI links), each rank writes its view's
-    per-Gaussian render-gradient sums into its block of ``gathered`` (``[N, block_floats]``,
-    ~44 B per Gaussian), ONE ``all_gather_into_tensor`` (in place) gives every rank all N
-    blocks, and ``_C.gauss_backward_views`` turns them into the summed parameter gradients on
-    every rank -- the same bytes in, the same kernel, so the replicas agree bit for bit.  At
-    N = 2 a rank receives 11 floats per Gaussian instead of 59; at N = 8, 77 instead of 103.
+    per-Gaussian render-gradient sums into a view block (~44 B per Gaussian), ONE
+    ``all_gather_into_tensor`` gives every rank all N blocks, and ``_C.gauss_backward_views``
+    turns them into the summed parameter gradients on every rank -- the same bytes in, the same
+    kernel, so the replicas agree bit for bit.  At N = 2 a rank receives 11 floats per Gaussian
+    instead of 59; at N = 8, 77 instead of 103.
 
     ``sparse=True`` (the default) sends the blocks packed (include/gsr.h, "Sparse view blocks"):
     only Gaussians with a non-zero render-gradient sum, 48 B each (~14% of a 1M@1080p frame's
-    Gaussians), all-gathered at the largest count over the ranks (one scalar all-reduce read by
-    the host); each rank then indexes the gathered packed blocks (one flag word per Gaussian and
-    view, ``_C.view_block_index``) and the multi-view backward reads the packed entries in place.
-    Left-out Gaussians had all-zero sums, so the result equals the dense exchange's bit for bit;
-    when a packed block would not be smaller than a dense one, the dense blocks are sent
-    (``last_entries`` is then None).
+    Gaussians).  The gather size is a capacity hint carried from earlier steps (a decaying maximum
+    of the largest packed block over the ranks, plus a margin), as the forward sizes its binning
+    buffer, so the host never waits for this step's count before queuing the collective: every
+    rank queues pack, the MAX of the counts (on the device), the all-gather at the hint, the
+    index and the multi-view backward, and only then (``finish``, called by ``views_backward``)
+    reads the step's largest count -- while the GPU still works through the queue.  A count over
+    the hint (rare: the view changed a lot) re-gathers at the exact size and reruns the index and
+    the backward, on every rank alike (they all read the same MAX).  The first exchange has no
+    hint and waits for the count first.  Left-out Gaussians had all-zero sums, so the result
+    equals the dense exchange's bit for bit; when a packed block would not be smaller than a dense
+    one, the dense blocks are sent (``last_entries`` is then None).
 
         ex = ViewExchange(P, device)
         _C.rasterize_gaussians_backward_screen(*backward_args, view_block=ex.local_block())
@@ -132,15 +145,21 @@ class ViewExchange:
         ex.views_backward(means3D, dc, sh, degree, opacities, scales, rotations, 1.0, out=arena.views())
     """
 
+    CAP_MARGIN = 1.05
+    CAP_DECAY = 0.98
+
     def __init__(self, P: int, device, group: Optional[dist.ProcessGroup] = None, sparse: bool = True):
         from . import _C
 
-        self.P, self.group, self.sparse = P, group, sparse and P > 0
+        self.P, self.group, self.sparse, self.device = P, group, sparse and P > 0, torch.device(device)
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.block_floats = _C.view_block_floats(P) if P > 0 else 0
-        self.gathered = torch.empty(self.world, self.block_floats, dtype=torch.float32, device=device)
-        self.last_entries = None  # sparse: entries of the largest packed block in the last exchange
+        self._gathered = None  # dense [N, block] buffer: allocated on first use (dense mode or fallback)
+        self.last_entries = None  # sparse: entries each rank sent in the last exchange
+        self.resyncs = 0          # sparse exchanges redone because the capacity hint was too small
+        self._cap_last = 0        # decaying maximum of the largest packed block (entries)
+        self._pending = None      # sparse: (hint used, whether the zero fill runs) until finish()
         if self.sparse:
             # this rank's dense block, its packed form (room for every Gaussian), the packed blocks
             # of all ranks, and the pack's scratch / count
@@ -150,28 +169,47 @@ class ViewExchange:
             nbytes = int(_lib_scratch_bytes(P))
             self._scratch = torch.empty(nbytes, dtype=torch.uint8, device=device)
             self._count = torch.zeros(1, dtype=torch.int32, device=device)
+            self._count64 = torch.zeros(1, dtype=torch.int64, device=device)
+            self._count_host = torch.zeros(1, dtype=torch.int64, pin_memory=True)
+            self._count_ev = torch.cuda.Event()
             self._flags = torch.empty(self.world, P, dtype=torch.int32, device=device)  # view_block_index
             self._live = torch.empty(_C.views_live_floats(P), dtype=torch.int32, device=device)
-        self._view_blocks, self._view_flags, self._view_live = self.gathered, None, None  # views_backward reads
+        self._view_blocks, self._view_flags, self._view_live = None, None, None  # views_backward reads
         self._side = None      # the stream zeroing the outputs during the exchange
         self._zeroed = None    # the flat output buffer it zeroes
+        self._last_bwd = None  # the arguments of the last views_backward (rerun after a resync)
+
+    @property
+    def gathered(self) -> torch.Tensor:
+        """All ranks' dense view blocks, [N, block_floats] (allocated on first use)."""
+        if self._gathered is None:
+            self._gathered = torch.empty(self.world, self.block_floats, dtype=torch.float32, device=self.device)
+        return self._gathered
 
     def local_block(self) -> torch.Tensor:
         """Where this rank's backward writes its view block."""
         return self._local if self.sparse else self.gathered[self.rank]
 
+    def capacity_hint(self) -> int:
+        """Entries the next sparse exchange gathers per rank (0: none yet, the count is waited for)."""
+        if self._cap_last <= 0:
+            return 0
+        return min(self.P, int(self._cap_last * self.CAP_MARGIN) + 1024)
+
+    def _note_count(self, n: int) -> None:
+        self._cap_last = max(int(n), int(self._cap_last * self.CAP_DECAY))
+
     def exchange(self, zero: Optional[torch.Tensor] = None) -> None:
-        """Give every rank all N view blocks in ``gathered``.
+        """Give every rank all N view blocks.
 
         Dense: one in-place ``all_gather_into_tensor`` of the blocks (44 B per Gaussian).
         Sparse (default): the block is packed to the Gaussians with a non-zero render gradient
-        (``_C.view_block_pack``, 48 B each, ~14% of a 1M@1080p view), the ranks agree on the
-        largest entry count (one scalar all-reduce, read by the host: the one synchronisation of
-        the exchange), ONE ``all_gather_into_tensor`` moves the packed blocks at that size, and
-        ``_C.view_block_index`` indexes the gathered packed blocks on every rank -- the same
-        gathered bytes, the same kernel, so the replicas stay bitwise equal, and
-        ``views_backward`` gives the dense exchange's result (a Gaussian left out had all-zero
-        sums).
+        (``_C.view_block_pack``, 48 B each, ~14% of a 1M@1080p view); the largest entry count over
+        the ranks is formed on the device (MAX all-reduce) and copied to pinned host memory without
+        waiting; ONE ``all_gather_into_tensor`` moves the packed blocks at the capacity hint; and
+        ``_C.view_block_index`` indexes them on every rank.  The host reads the count only in
+        ``finish`` -- after the multi-view backward is queued -- and redoes the exchange if the hint
+        was too small.  Without a hint (the first exchange) it waits for the count here.
 
         ``zero`` (optional): the flat buffer behind the ``out`` views later given to
         ``views_backward`` (e.g. ``GradArena.flat``).  It is zeroed on a second stream while the
@@ -179,8 +217,11 @@ class ViewExchange:
         view has a gradient for (a live list, ``_C.views_live_list``)."""
         from . import _C
 
-        self._view_blocks, self._view_flags, self._view_live = self.gathered, None, None
+        if self._pending is not None:
+            self.finish()
+        self._view_blocks, self._view_flags, self._view_live = None, None, None
         self._zeroed = None
+        self._last_bwd = None
         if zero is not None and self.sparse:
             cur = torch.cuda.current_stream(zero.device)
             if self._side is None:
@@ -193,39 +234,82 @@ class ViewExchange:
         if not self.sparse:
             if self.world > 1:
                 dist.all_gather_into_tensor(self.gathered.view(-1), self.local_block(), group=self.group)
+            self._view_blocks = self.gathered
             return
         _C.view_block_pack(self._local, self._packed, self._scratch, self._count, self.P)
-        if self.world == 1:
-            n = int(self._count.item())
+        self._count64.copy_(self._count)
+        if self.world > 1:
+            if dist.get_backend(self.group) == "nccl":
+                dist.all_reduce(self._count64, op=dist.ReduceOp.MAX, group=self.group)
+                self._count_host.copy_(self._count64, non_blocking=True)
+            else:  # gloo (CPU rehearsals): the collective needs a host tensor, i.e. a synchronisation
+                host = self._count64.cpu()
+                dist.all_reduce(host, op=dist.ReduceOp.MAX, group=self.group)
+                self._count_host.copy_(host)
         else:
-            cnt = self._count.to(torch.int64)
-            if dist.get_backend(self.group) != "nccl":
-                cnt = cnt.cpu()
-            dist.all_reduce(cnt, op=dist.ReduceOp.MAX, group=self.group)
-            n = int(cnt.item())
-        n = min(n, self.P)
+            self._count_host.copy_(self._count64, non_blocking=True)
+        self._count_ev.record()
+        hint = self.capacity_hint()
+        if hint == 0:  # no history: wait for this step's count (like the forward without a hint)
+            self._count_ev.synchronize()
+            hint = min(int(self._count_host.item()), self.P)
+        self._pending = (hint, True)
+        self._gather(hint)
+
+    def _gather(self, n: int) -> None:
+        """All-gather the packed blocks at ``n`` entries per rank (or the dense blocks if that is not
+        smaller), then index them."""
+        from . import _C
+
         size = _C.view_pack_floats(n)
-        self.last_entries = n
         if size >= self.block_floats:  # hardly any occlusion: the dense blocks are the smaller message
             self.gathered[self.rank].copy_(self._local)
             if self.world > 1:
                 dist.all_gather_into_tensor(self.gathered.view(-1), self.gathered[self.rank], group=self.group)
             self.last_entries = None
+            self._view_blocks, self._view_flags, self._view_live = self.gathered, None, None
             return
+        self.last_entries = n
         recv = self._recv[: self.world * size].view(self.world, size)
         if self.world > 1:
             dist.all_gather_into_tensor(recv.view(-1), self._packed[:size], group=self.group)
         else:
             recv[0].copy_(self._packed[:size])
         _C.view_block_index(recv, self._flags, self.P)
-        self._view_blocks, self._view_flags = recv, self._flags
+        self._view_blocks, self._view_flags, self._view_live = recv, self._flags, None
         if self._zeroed is not None:
             _C.views_live_list(self._flags, self._live, self.P)
             self._view_live = self._live
 
+    def finish(self) -> bool:
+        """Complete the last sparse exchange: read its largest count (queued as a non-blocking copy;
+        by now the GPU is usually past it) and, if it exceeded the gather's capacity, gather again
+        at the exact size -- rerunning the multi-view backward if it was already queued.  Returns
+        True if the exchange was redone.  Called by ``views_backward``; idempotent."""
+        if self._pending is None:
+            return False
+        hint, _ = self._pending
+        self._pending = None
+        self._count_ev.synchronize()
+        n = min(int(self._count_host.item()), self.P)  # a pinned host tensor: no device sync
+        self._note_count(n)
+        if n <= hint:
+            return False
+        self.resyncs += 1
+        self._gather(n)
+        if self._last_bwd is not None:
+            self._run_views_backward(*self._last_bwd)
+        return True
+
     def views_backward(self, means3D, dc, sh, degree, opacities, scales, rotations, scale_modifier, out) -> None:
         """The per-Gaussian backward summed over all ranks' views (``_C.gauss_backward_views`` over
-        what the last ``exchange`` gathered: dense view blocks, or packed blocks and their index)."""
+        what the last ``exchange`` gathered: dense view blocks, or packed blocks and their index).
+        Queues the kernel, then completes a sparse exchange (``finish``)."""
+        self._last_bwd = (means3D, dc, sh, degree, opacities, scales, rotations, scale_modifier, out)
+        self._run_views_backward(*self._last_bwd)
+        self.finish()
+
+    def _run_views_backward(self, means3D, dc, sh, degree, opacities, scales, rotations, scale_modifier, out):
         from . import _C
 
         if self._zeroed is not None:  # the outputs' zero fill (exchange(zero=...)) must be done

@@ -270,6 +270,28 @@ int gsr_debug_forward_state(int P, int width, int height, int R, int binning_cap
  * was redone with the exact count (gsr_rasterize_forward_ex). */
 long long gsr_forward_rebuilds(void);
 
+/* Host time the forwards spent waiting for their instance count (the one host synchronisation
+ * of a forward, CR/rasterizer_impl.cu:313; here an event behind the binning count): total and
+ * largest single wait in ms and the number of waits since the last reset (reset != 0 clears). */
+int gsr_host_wait_stats(double* total_ms, double* max_ms, long long* calls, int reset);
+
+/* Runtime options (no reference counterpart): the library's alternative kernel paths, readable
+ * and settable in-process so that every path it ships is parity-tested (tests/test_gpu_options.py).
+ * Each default comes from the environment variable GSR_<NAME> (upper case) at first use.
+ *   "fused_bin"  1|0    capacity-mode binning with the tile scan folded into the scatter (forward)
+ *   "fwd_quads"  2|4    8x8 quadrants per forward wave: half tiles | whole tiles
+ *   "bwd_seg_ck" 1..2^20 backward work unit length in 256-entry checkpoints; the forward writes the
+ *                        units, so a forward and its backward must run with the same value
+ *   "host_total" 1|0    the binning kernels store num_rendered into mapped host memory | a copy is queued
+ *   "zero_fill"  1|2|0  dense backward outputs zero-filled on a side stream | on the launch stream
+ *                        before gauss_bwd | not at all (gauss_bwd writes every row)
+ *   "live_list"  1|0    gauss_bwd over the list of Gaussians with a render gradient | a lane per Gaussian
+ *                        (only with zero_fill != 0)
+ * gsr_option_get returns -1 for an unknown name; gsr_option_set returns GSR_ERR_ARGUMENT for an
+ * unknown name or an out-of-range value.  Not synchronised against calls running on other threads. */
+int gsr_option_set(const char* name, int value);
+int gsr_option_get(const char* name);
+
 /* Message of the last error on this thread ("" if none). */
 const char* gsr_last_error(void);
 

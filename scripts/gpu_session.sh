@@ -48,7 +48,7 @@ for stage in "$@"; do
       bash scripts/pmc_session.sh "$TAG/pmc_$c" scripts/pmc_all.txt $c; rc=$?
       echo "pmc $c rc=$rc"; [ $rc -eq 0 ] || exit $rc ;;
     rehearse2)  # N=2 on one GPU (gloo collectives): the multi-rank bench path, both exchanges
-      for ex in views dense allreduce; do
+      for ex in auto views dense allreduce; do
         GSR_BENCH_SHARE_GPU=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
           --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 2 --exchange $ex \
           > "$OUT/rehearse2_$ex.json" 2> "$OUT/rehearse2_$ex.err"; rc=$?

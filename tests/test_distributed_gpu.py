@@ -7,7 +7,8 @@ two exchanges run for real:
     one all-reduce sums them;
   * ViewExchange -- each rank writes its view block (gsr_rasterize_backward_screen), one all-gather of the
     packed (sparse) blocks -- and of the dense ones -- and every rank runs gsr_gauss_backward_views over
-    both views.
+    both views; the sparse exchange again at its capacity hint (no wait for the count), and with a hint
+    forced below the count (the exchange is redone at the exact size).
 
 Both must equal the oracle's sum of the per-view gradients (unit-scale upstream gradient, the small-case
 bar max |diff| / max |ref| <= 2e-4), and the replicas must be bitwise identical after each exchange.
@@ -79,6 +80,23 @@ def _worker(rank, port, outdir):
             ex.views_backward(d("means3D"), None, d("shs"), inp["sh_degree"], d("opacities"), d("scales"),
                               d("rotations"), 1.0, out=arena2.views())
             torch.cuda.synchronize()
+            first = arena2.flat.clone()
+            if sparse:
+                # later steps gather at the capacity hint without waiting for the count; a hint below
+                # the count (forced here) is detected after the backward is queued and the exchange
+                # is redone at the exact size -- the same gradients bit for bit every time
+                assert ex.capacity_hint() > 0 and ex.resyncs == 0
+                for forced in (None, 8):
+                    if forced is not None:
+                        ex.capacity_hint = lambda: forced  # noqa: E731
+                    arena2.flat.fill_(float("nan"))
+                    ex.exchange(zero=arena2.flat)
+                    ex.views_backward(d("means3D"), None, d("shs"), inp["sh_degree"], d("opacities"), d("scales"),
+                                      d("rotations"), 1.0, out=arena2.views())
+                    torch.cuda.synchronize()
+                    assert torch.equal(arena2.flat, first), forced
+                assert ex.resyncs == 1, ex.resyncs
+                del ex.capacity_hint
             np.save(os.path.join(outdir, f"{mode}{rank}.npy"), arena2.flat.cpu().numpy())
             m2d = np.stack([ex.means2D_grad(r).cpu().numpy() for r in range(WORLD)])  # densification input
             np.save(os.path.join(outdir, f"m2d_{mode}{rank}.npy"), m2d)

@@ -14,8 +14,9 @@ frame on the host.  What is checked:
     max |diff| / max |ref| <= 2e-4 per tensor over every Gaussian not at a threshold flip.  A
     Gaussian is at a flip when its own blend at some pixel lies within the margins of a discrete
     threshold (oracle threshold_gaussians), or it shares a tile with a pixel whose last contributor
-    differs: a flip moves that pixel's whole term in or out of its gradient.  Those are counted and
-    printed with their own error;
+    differs: a flip moves that pixel's whole term in or out of its gradient.  Those are counted,
+    printed with their own error and held to max |diff| / max |ref| <= 2e-3; with the L1 upstream
+    gradient every Gaussian, flips included, is within 1e-5 absolute (north_star's bar);
   * bitwise determinism and the reference's colours-precomputed consistency switch.
 """
 import os
@@ -31,6 +32,8 @@ pytestmark = [pytest.mark.gpu, pytest.mark.slow]
 
 ATOL_PIX = 1e-5       # north_star: forward RGB within 1e-5 abs fp32
 RTOL_GRAD = 2e-4      # the small-case bar, unit upstream gradient
+RTOL_GRAD_FLIP = 2e-3  # Gaussians at a threshold flip (max |diff| / max |ref| per tensor)
+ATOL_GRAD_L1 = 1e-5   # every Gaussian, L1-mean upstream gradient (north_star's absolute bar)
 # threshold margins (oracle pixel_margins): a pixel within these of a discrete decision of the
 # reference's blend can legitimately fall either way under a different fp32 evaluation order
 MARGIN_POWER = 1e-5   # |power| (absolute)
@@ -158,9 +161,19 @@ def test_fullsize_backward(fullsize, upstream):
     print(f"[{fullsize['name']}/{upstream}] Gaussians at a threshold flip: {int(taint.sum())} "
           f"of {taint.size}; per tensor (max|ref|, max rel elsewhere, max rel at flips): "
           + "; ".join(f"{k} {s:.2e} {c:.2e} {t:.2e}" for k, s, c, t in rows))
+    worst = max(rows, key=lambda r: r[3])
+    print(f"[{fullsize['name']}/{upstream}] worst Gaussian at a flip: {worst[0]} rel {worst[3]:.2e} "
+          f"(bar {RTOL_GRAD_FLIP:.0e})")
     for k, s, c, t in rows:
         assert c <= RTOL_GRAD, (k, c)
-        assert np.isfinite(t)
+        # a flip moves one pixel's term of a Gaussian's sum; observed <= 9.6e-4 of max|ref| (r2zz)
+        assert t <= RTOL_GRAD_FLIP, (k, t)
+    if upstream == "l1":
+        # north_star's bar literally: 1e-5 absolute with the reference's L1-mean upstream gradient
+        # (train.py:155), over EVERY Gaussian, those at a threshold flip included
+        for k, got in zip(C.GRAD_NAMES, out):
+            dabs = float(np.abs(_np(got).astype(np.float64) - ref_g[k]).max())
+            assert dabs <= ATOL_GRAD_L1, (k, dabs)
     assert taint.mean() <= 0.05, taint.mean()
 
 

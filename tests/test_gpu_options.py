@@ -1,0 +1,90 @@
+"""Every alternative kernel path libgsr ships (include/gsr.h gsr_option_set) against the oracle.
+
+The library's runtime options select alternative paths of the forward and backward -- binning
+without the fused scan, whole-tile forward waves, longer backward work units, a queued copy of the
+instance count, the three zero-fill modes of the backward outputs and gauss_bwd without the live
+list.  Each path is a way a user can run the rasterizer, so each is held to the same bars as the
+default path (tests/test_gpu_parity.py), on cases that reach every binning sort class, in both the
+synchronising and the capacity-hint forward:
+  * integers identical to the f32 oracle: num_rendered, radii, the sorted tile lists;
+  * colour / inverse depth within 1e-5; gradients within 1e-5 absolute with the L1 upstream
+    gradient and 2e-4 of max |ref| with a unit one;
+  * and against the default path itself: bitwise equal, except the backward of "bwd_seg_ck",
+    whose work units start from other blend checkpoints (the same sums in another rounding).
+"""
+import numpy as np
+import pytest
+import torch
+
+from tests import common as C
+
+pytestmark = pytest.mark.gpu
+
+VARIANTS = {
+    "fused_bin=0": dict(fused_bin=0),
+    "fwd_quads=4": dict(fwd_quads=4),
+    "bwd_seg_ck=2": dict(bwd_seg_ck=2),
+    "bwd_seg_ck=max": dict(bwd_seg_ck=1 << 20),
+    "host_total=0": dict(host_total=0),
+    "zero_fill=0": dict(zero_fill=0),
+    "zero_fill=2": dict(zero_fill=2),
+    "live_list=0": dict(live_list=0),
+}
+CASES = ["sh3_scalerot", "antialiasing", "dense_opaque", "lists_1k_2k", "lists_4k_8k", "lists_over_8k"]
+
+
+def _np(t):
+    return t.detach().float().cpu().numpy()
+
+
+def _run(inp, case, grads, hint):
+    """Forward (synchronising, or with a capacity hint of the exact count) + two backwards."""
+    from gaussian_splatting_amd import _C as CM
+
+    key = (torch.cuda.current_device(), case.W, case.H)
+    CM._capacity.pop(key, None)
+    if hint:
+        ref = C.run_oracle(inp)
+        CM._capacity[key] = (case.P, ref.num_rendered)
+    fwd = C.run_gpu_forward(inp)
+    outs = [C.run_gpu_backward(inp, fwd, *g) for g in grads]
+    torch.cuda.synchronize()
+    CM._capacity.pop(key, None)
+    return fwd, outs
+
+
+@pytest.mark.parametrize("hint", [False, True], ids=["sync", "hint"])
+@pytest.mark.parametrize("case_name", CASES)
+@pytest.mark.parametrize("variant", sorted(VARIANTS))
+def test_option_path_matches_oracle(variant, case_name, hint):
+    from gaussian_splatting_amd import _C as CM
+    from gaussian_splatting_amd import _lib
+
+    case = next(c for c in C.SMALL_CASES if c.name == case_name)
+    inp = C.build(case)
+    ref = C.run_oracle(inp)
+    grads = (C.unit_grads(case.H, case.W), C.l1_grads(case.H, case.W))
+    base_fwd, base_outs = _run(inp, case, grads, hint)
+    with _lib.options(**VARIANTS[variant]):
+        fwd, outs = _run(inp, case, grads, hint)
+        st = CM.debug_forward_state(fwd, case.P)
+    nr, color, radii, *_, invd = fwd
+    assert nr == ref.num_rendered
+    np.testing.assert_array_equal(_np(radii).astype(np.int32), ref.radii)
+    np.testing.assert_array_equal(st["point_list"].numpy(), ref.handle.binning()["point_list"].astype(np.int64))
+    np.testing.assert_allclose(_np(color), ref.color, atol=1e-5, rtol=0)
+    np.testing.assert_allclose(_np(invd), ref.invdepth, atol=1e-5, rtol=0)
+    for (gc, gd), out, mode in zip(grads, outs, ("unit", "l1")):
+        r = ref.handle.backward(gc, gd)
+        for k, got in zip(C.GRAD_NAMES, out):
+            if mode == "l1":
+                np.testing.assert_allclose(_np(got), r[k], atol=1e-5, rtol=0, err_msg=f"{variant} {k}")
+            else:
+                assert C.rel_err(_np(got), r[k]) <= 2e-4, (variant, k, C.rel_err(_np(got), r[k]))
+    # against the default path
+    assert torch.equal(fwd[1], base_fwd[1]) and torch.equal(fwd[6], base_fwd[6]) and torch.equal(fwd[2], base_fwd[2])
+    if not variant.startswith("bwd_seg_ck"):
+        for out, base in zip(outs, base_outs):
+            for a, b in zip(out, base):
+                assert torch.equal(a, b), variant
+

@@ -275,11 +275,21 @@ def test_matches_golden_fixture(name):
     from gaussian_splatting_amd import _C as CM
     st = CM.debug_forward_state(fwd, inp["means3D"].shape[0])
     np.testing.assert_array_equal(st["point_list"].numpy(), ref32.handle.binning()["point_list"].astype(np.int64))
-    assert abs(nr - exp["num_rendered"]) <= 2
-    assert (_to_np(radii).astype(np.int32) != exp["radii"]).sum() <= 2
-    for got, e in ((_to_np(color), exp["color"]), (_to_np(invd), exp["invdepth"])):
-        d = np.abs(got - e)
-        assert (d <= ATOL_FWD).mean() >= 0.999 and d.mean() <= 1e-6, (name, d.max())
+    # the committed fixture's own integers: identical (no tolerance)
+    assert nr == int(exp["num_rendered"]), (name, nr, int(exp["num_rendered"]))
+    np.testing.assert_array_equal(_to_np(radii).astype(np.int64), exp["radii"].astype(np.int64))
+    # the full-size rule (tests/test_gpu_fullsize.py): every pixel over 1e-5 against the fixture is
+    # explained by a discrete threshold of the reference's blend that rounding flips -- its last
+    # contributor differs from the f32 oracle's, or the f32 oracle's walk over it lies within the
+    # margin of power = 0, alpha = 1/255 or T = 1e-4
+    d = np.maximum(np.abs(_to_np(color) - exp["color"]).max(0), np.abs(_to_np(invd) - exp["invdepth"])[0])
+    m = ref32.handle.pixel_margins()
+    near = (m["power"] < 1e-5) | (m["alpha"] < 1e-4) | (m["T"] < 1e-4)
+    nc_diff = st["n_contrib"].numpy() != ref32.handle.image()["n_contrib"].astype(np.int64)
+    unexplained = (d > ATOL_FWD) & ~(near | nc_diff)
+    assert not unexplained.any(), (name, int(unexplained.sum()), float(d[unexplained].max()))
+    print(f"[{name}] pixels over 1e-5: {int((d > ATOL_FWD).sum())}, all explained; max|diff| elsewhere "
+          f"{float(d[~(near | nc_diff)].max()) if (~(near | nc_diff)).any() else 0.0:.2e}")
     if grads is None:
         return
     out = C.run_gpu_backward(inp, fwd, *grads)

@@ -196,3 +196,20 @@ def test_product_path_never_touches_the_oracle():
                     if pat.search(code):
                         offenders.append("%s:%d: %s" % (os.path.relpath(f, ROOT), n, line.strip()))
     assert not offenders, "\n".join(offenders)
+
+
+def test_option_errors_and_restore():
+    """libgsr's runtime options (include/gsr.h gsr_option_set): range checks and the restoring
+    context manager; no GPU work (the paths themselves: tests/test_gpu_options.py)."""
+    from gaussian_splatting_amd import _lib
+
+    before = {k: _lib.option_get(k) for k in _lib.OPTIONS}
+    with pytest.raises(_lib.GsrError, match="unknown option"):
+        _lib.option_set("no_such_option", 1)
+    with pytest.raises(_lib.GsrError, match="out of range"):
+        _lib.option_set("fwd_quads", 3)
+    with pytest.raises(_lib.GsrError, match="out of range"):
+        _lib.option_set("zero_fill", 3)
+    with _lib.options(zero_fill=2, live_list=0):
+        assert _lib.option_get("zero_fill") == 2 and _lib.option_get("live_list") == 0
+    assert {k: _lib.option_get(k) for k in _lib.OPTIONS} == before

@@ -117,3 +117,32 @@ def test_train_false_and_accel_variant():
     _, e1, e2, e3 = fused_ssim_cuda.fusedssim(1e-4, 9e-4, a[None], b[None], True)
     ref = fused_ssim_cuda.fusedssim_backward(1e-4, 9e-4, a[None], b[None], g[None], e1, e2, e3)[0]
     assert torch.equal(_C.fusedssim_backward(1e-4, 9e-4, a, b, g), ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("padding", ["same", "valid"])
+def test_map_function_agrees_with_loss(padding):
+    """The package's two autograd functions: the map-level FusedSSIMMap, averaged, gives the loss
+    fused_ssim computes and the same dL/dimg1; train=False gives the value and refuses a backward;
+    an unknown padding raises (an AssertionError, as the reference's assert)."""
+    from fused_ssim import FusedSSIMMap, fused_ssim
+
+    g = torch.Generator().manual_seed(5)
+    a0 = torch.rand(2, 3, 37, 53, generator=g).cuda()
+    b = torch.rand(2, 3, 37, 53, generator=g).cuda()
+    a1 = a0.clone().requires_grad_(True)
+    a2 = a0.clone().requires_grad_(True)
+    loss = fused_ssim(a1, b, padding)
+    loss.backward()
+    m = FusedSSIMMap.apply(0.01 ** 2, 0.03 ** 2, a2, b, padding, True).mean()
+    m.backward()
+    torch.testing.assert_close(loss, m, rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(a1.grad, a2.grad, rtol=1e-5, atol=1e-9)
+    with torch.no_grad():
+        v = fused_ssim(a0, b, padding, train=False)
+    torch.testing.assert_close(v, loss.detach(), rtol=1e-6, atol=1e-7)
+    a3 = a0.clone().requires_grad_(True)
+    with pytest.raises(RuntimeError, match="train=False"):
+        fused_ssim(a3, b, padding, train=False).backward()
+    with pytest.raises(AssertionError):
+        fused_ssim(a0, b, "full")
