@@ -10,7 +10,9 @@ synchronising and the capacity-hint forward:
   * colour / inverse depth within 1e-5; gradients within 1e-5 absolute with the L1 upstream
     gradient and 2e-4 of max |ref| with a unit one;
   * and against the default path itself: bitwise equal, except the backward of "bwd_seg_ck",
-    whose work units start from other blend checkpoints (the same sums in another rounding).
+    whose work units start from other blend checkpoints (the same sums in another rounding), and
+    "fwd_quads=4", a separate instantiation of the forward kernel in which the compiler contracts
+    other multiply-adds into FMAs (the oracle bars above still hold it).
 """
 import numpy as np
 import pytest
@@ -82,7 +84,11 @@ def test_option_path_matches_oracle(variant, case_name, hint):
             else:
                 assert C.rel_err(_np(got), r[k]) <= 2e-4, (variant, k, C.rel_err(_np(got), r[k]))
     # against the default path
-    assert torch.equal(fwd[1], base_fwd[1]) and torch.equal(fwd[6], base_fwd[6]) and torch.equal(fwd[2], base_fwd[2])
+    assert torch.equal(fwd[2], base_fwd[2])
+    if variant == "fwd_quads=4":
+        assert float((fwd[1] - base_fwd[1]).abs().max()) <= 1e-6
+        return
+    assert torch.equal(fwd[1], base_fwd[1]) and torch.equal(fwd[6], base_fwd[6])
     if not variant.startswith("bwd_seg_ck"):
         for out, base in zip(outs, base_outs):
             for a, b in zip(out, base):
