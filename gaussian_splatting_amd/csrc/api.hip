@@ -156,6 +156,10 @@ gsr::GeomState carve_geom(char* base, int P, uint32_t gx, uint32_t gy, size_t* t
     g.unit_cnt = c.take<uint32_t>((size_t)kUnitLists * kUnitShards * kUnitCntStride);
     g.unit_part = c.take<uint2>((size_t)(kUnitLists - 1) * kUnitShards * unit_part_cap(tiles));
     g.tile_join = c.take<unsigned long long>(tiles);
+    g.sorted_len = c.take<uint32_t>(tiles);
+    g.redo_flag = c.take<uint32_t>(tiles);
+    g.redo_list = c.take<uint32_t>(tiles);
+    g.redo_cnt = c.take<uint32_t>(1);
     *total = align_up(c.off);
     return g;
 }

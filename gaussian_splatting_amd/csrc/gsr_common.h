@@ -95,6 +95,14 @@ struct GeomState {
     uint32_t* unit_cnt;
     uint2* unit_part;
     unsigned long long* tile_join;  // [tiles] the forward's half-tile waves combine their limits here (K2 zeroes)
+    // Reachable-prefix sort (binning.hip K4, the "sort_prefix" option): entries [0, sorted_len[t]) of
+    // tile t's list are in final order, the rest unsorted.  A forward wave that reaches sorted_len
+    // with pixels still blending files the tile for a redo (flag + list + count; K4 zeroes them):
+    // the tail is sorted and the tile rendered again (render.hip).
+    uint32_t* sorted_len;       // [tiles]
+    uint32_t* redo_flag;        // [tiles]
+    uint32_t* redo_list;        // [tiles]
+    uint32_t* redo_cnt;         // [1]
 };
 
 // Image state: per pixel and per tile.  The per-pixel planes are tile-major: pixel (x, y) of

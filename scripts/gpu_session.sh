@@ -25,6 +25,9 @@ for stage in "$@"; do
     bench)
       timeout -k 10 600 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"; rc=$?
       echo "bench rc=$rc"; cat "$OUT/bench.json"; tail -3 "$OUT/bench.err"; [ $rc -eq 0 ] || exit $rc ;;
+    cpuonly)  # BASELINE configs[0]: the pure-PyTorch fallback forward on this host, no GPU touched
+      timeout -k 10 600 python bench.py --cpu-only --config 10k_256_sh0 > "$OUT/cpu_only_10k_256_sh0.json" 2> "$OUT/cpu_only.err"; rc=$?
+      echo "cpuonly rc=$rc"; cat "$OUT/cpu_only_10k_256_sh0.json"; [ $rc -eq 0 ] || exit $rc ;;
     benchquick)
       timeout -k 10 600 python bench.py --no-cpu-baseline > "$OUT/bench.json" 2> "$OUT/bench.err"; rc=$?
       echo "bench rc=$rc"; cat "$OUT/bench.json"; tail -3 "$OUT/bench.err"; [ $rc -eq 0 ] || exit $rc ;;

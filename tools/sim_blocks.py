@@ -54,7 +54,8 @@ def main():
     lx, ly = lx.reshape(-1), ly.reshape(-1)
     quad = (ly // 8) * 2 + lx // 8       # 8x8 quadrant of each tile pixel
     blk = (ly // 4) * 4 + lx // 4        # 4x4 block
-    tot = dict(q_evals=0, b_iters=0, pairs=0, entries=0, b_lane_evals=0)
+    blk8x4 = (ly // 4) * 2 + lx // 8     # 8x4 half-quadrant blocks: 8 per tile
+    tot = dict(q_evals=0, b_iters=0, pairs=0, entries=0, b_lane_evals=0, h_iters=0, h_lane_evals=0)
     tiles = range(0, gx * gy, a.every)
     for t in tiles:
         s, e = ranges[t]
@@ -84,9 +85,15 @@ def main():
         bh = np.stack([hit[:, blk == k].any(1) for k in range(16)], 1) & (pos < blim[None, :])
         tot["q_evals"] += int(qh.sum())
         tot["b_lane_evals"] += int(bh.sum()) * 16
+        hlim = np.array([ncp[blk8x4 == k].max() for k in range(8)])
+        hh = np.stack([hit[:, blk8x4 == k].any(1) for k in range(8)], 1) & (pos < hlim[None, :])
+        tot["h_lane_evals"] += int(hh.sum()) * 32
         for b0 in range(0, lim, 64):
             bb = bh[b0:b0 + 64].reshape(-1, 4, 4)  # [entry, block row (slot), block column (group)]
             tot["b_iters"] += int(bb.sum(0).max(1).sum())
+            # two 32-lane halves: half h owns the 8x4 blocks of column h (4 slots, one per block row)
+            hb = hh[b0:b0 + 64].reshape(-1, 4, 2)
+            tot["h_iters"] += int(hb.sum(0).max(1).sum())
     q_lanes = tot["q_evals"] * 64
     b_lanes = tot["b_iters"] * 64
     print(f"{a.config}, every {a.every}th tile: entries {tot['entries']}, pairs with a gradient {tot['pairs']}")
@@ -94,6 +101,9 @@ def main():
     print(f"  4x4 block scheme: {tot['b_iters']} wave iterations ({tot['b_iters'] / tot['q_evals']:.3f} of the quadrant "
           f"evaluations), useful lanes {tot['pairs'] / b_lanes:.3f}; lane-evaluations of touched blocks alone "
           f"{tot['b_lane_evals'] / q_lanes:.3f} of the quadrant scheme's")
+    print(f"  8x4 blocks, two 32-lane halves: {tot['h_iters']} wave iterations ({tot['h_iters'] / tot['q_evals']:.3f}), "
+          f"useful lanes {tot['pairs'] / (tot['h_iters'] * 64):.3f}; touched-block lane-evaluations "
+          f"{tot['h_lane_evals'] / q_lanes:.3f}")
 
 
 if __name__ == "__main__":
