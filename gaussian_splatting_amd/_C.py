@@ -338,6 +338,23 @@ def debug_forward_state(fwd, P: int) -> dict:
             "n_contrib": torch.from_numpy(u(n_contrib)), "final_T": final_T.cpu()}
 
 
+def debug_sort_state(fwd, P: int) -> dict:
+    """The forward's reachable-prefix sort state (include/gsr.h gsr_debug_sort_state): ``sorted_len``
+    [tiles] (entries of each tile list in final order) and ``redo_count`` (tiles the forward
+    rendered again because a wave passed its sorted prefix); int64 CPU tensor / int."""
+    num_rendered, color, _radii, geom, binning, img, _inv = fwd
+    H, W = int(color.size(1)), int(color.size(2))
+    device = color.device
+    tiles = ((W + 15) // 16) * ((H + 15) // 16)
+    sl = torch.zeros(tiles, dtype=torch.int32, device=device)
+    rc = torch.zeros(1, dtype=torch.int32, device=device)
+    with torch.cuda.device(device):
+        r = _lib.load().gsr_debug_sort_state(int(P), W, H, geom.data_ptr(), sl.data_ptr(), rc.data_ptr(),
+                                             _stream_handle(device))
+    _lib.check(r, "debug_sort_state")
+    return {"sorted_len": sl.cpu().long(), "redo_count": int(rc.item())}
+
+
 def view_block_floats(P: int) -> int:
     """Floats in one view block (include/gsr.h, multi-GPU view exchange)."""
     return int(_lib.load().gsr_view_block_floats(int(P)))

@@ -87,6 +87,7 @@ SIGNATURES = {
                                            _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gsr_debug_forward_state": (_i, [_i, _i, _i, _i, _i, ctypes.c_size_t, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gsr_forward_rebuilds": (ctypes.c_longlong, []),
+    "gsr_debug_sort_state": (_i, [_i, _i, _i, _vp, _vp, _vp, _vp]),
     "gsr_option_set": (_i, [ctypes.c_char_p, _i]),
     "gsr_host_wait_stats": (_i, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                  ctypes.POINTER(ctypes.c_longlong), _i]),
@@ -171,7 +172,7 @@ def version() -> str:
 
 
 # ---- runtime options (include/gsr.h gsr_option_set) ---------------------------------
-OPTIONS = ("fused_bin", "fwd_quads", "bwd_seg_ck", "host_total", "zero_fill", "live_list")
+OPTIONS = ("fused_bin", "fwd_quads", "bwd_seg_ck", "host_total", "zero_fill", "live_list", "sort_prefix")
 
 
 def option_get(name: str) -> int:

@@ -272,7 +272,13 @@ void carve_recs(char* base, size_t R, size_t P, gsr::GradRecs* recs, gsr::GradRe
 #ifndef GSR_LIVE_LIST_DEFAULT
 #define GSR_LIVE_LIST_DEFAULT 1
 #endif
-enum Opt { OPT_FUSED_BIN = 0, OPT_FWD_QUADS, OPT_BWD_SEG_CK, OPT_HOST_TOTAL, OPT_ZERO_FILL, OPT_LIVE_LIST, OPT_COUNT };
+#ifndef GSR_SORT_PREFIX_DEFAULT
+#define GSR_SORT_PREFIX_DEFAULT 1024
+#endif
+enum Opt {
+    OPT_FUSED_BIN = 0, OPT_FWD_QUADS, OPT_BWD_SEG_CK, OPT_HOST_TOTAL, OPT_ZERO_FILL, OPT_LIVE_LIST, OPT_SORT_PREFIX,
+    OPT_COUNT
+};
 struct OptionSpec {
     const char* name;
     const char* env;
@@ -285,6 +291,7 @@ const OptionSpec kOptions[OPT_COUNT] = {
     {"host_total", "GSR_HOST_TOTAL", 1, 0, 1},
     {"zero_fill", "GSR_ZERO_FILL", GSR_ZERO_FILL_DEFAULT, 0, 2},
     {"live_list", "GSR_LIVE_LIST", GSR_LIVE_LIST_DEFAULT, 0, 1},
+    {"sort_prefix", "GSR_SORT_PREFIX", GSR_SORT_PREFIX_DEFAULT, 0, 1 << 30},
 };
 std::atomic<int> g_opt[OPT_COUNT];
 std::once_flag g_opt_once;
@@ -856,11 +863,14 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
             {
                 StageScope sc(ST_TILE_SORT, stream);
                 HIP_TRY(launch_tile_sort(tiles, img.ranges, geom, bin, C, stream, fused_now,
-                                         (uint32_t)bin_cell_count(gx, gy)),
+                                         (uint32_t)bin_cell_count(gx, gy),
+                                         g_census ? 0u : (uint32_t)option(OPT_SORT_PREFIX)),
                         "tile_sort");
             }
             if (int rc = check_debug(debug, stream, "tile_sort")) return rc;
         }
+        // (census runs sort whole lists: a redone tile's first pass would be counted twice)
+        const uint32_t prefix = g_census ? 0u : (uint32_t)option(OPT_SORT_PREFIX);
         {
             StageScope sc(ST_RENDER_FWD, stream);
             RenderFwdArgs ra{};
@@ -872,7 +882,17 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
             ra.tile_join = geom.tile_join;
             ra.seg_ck = bwd_segment_checkpoints();
             ra.census = g_census;
+            ra.sorted_len = geom.sorted_len;
+            ra.redo_flag = geom.redo_flag;
+            ra.redo_list = geom.redo_list;
+            ra.redo_cnt = geom.redo_cnt;
+            // (C == 0: no lists and no K4, so nothing is prefix-sorted and no redo state was reset)
+            if (C == 0) ra.sorted_len = nullptr;
             HIP_TRY(launch_render_fwd(ra, stream, option(OPT_FWD_QUADS)), "render_fwd");
+            if (prefix && C > 0) {  // the tiles whose walk passed their sorted prefix (usually none)
+                HIP_TRY(launch_tile_sort_redo(tiles, img.ranges, geom, bin, C, stream), "render_fwd redo sort");
+                HIP_TRY(launch_render_fwd_redo(ra, stream, option(OPT_FWD_QUADS)), "render_fwd redo");
+            }
         }
         return check_debug(debug, stream, "render_fwd");
     };
@@ -1322,7 +1342,6 @@ int gsr_debug_forward_state(int P, int width, int height, int R, int binning_cap
     using namespace gsr;
     g_err[0] = 0;
     hipStream_t stream = (hipStream_t)stream_;
-    (void)geom_buffer;
     if (P <= 0 || R < 0 || width <= 0 || height <= 0)
         return fail(GSR_ERR_ARGUMENT, "debug_forward_state: invalid sizes P=%d R=%d W=%d H=%d", P, R, width, height);
     if (!image_buffer || (R > 0 && !binning_buffer))
@@ -1344,11 +1363,33 @@ int gsr_debug_forward_state(int P, int width, int height, int R, int binning_cap
                               width, height, gx, stream),
                 "debug_forward_state final_T");
     if (point_list && R > 0) {
+        // the forward's sorted entries (masks included) and, where K4 sorted only a list's reachable
+        // prefix, the rest of the list sorted here into the copy
+        if (!geom_buffer) return fail(GSR_ERR_ARGUMENT, "debug_forward_state: point_list needs the geometry buffer");
         BinningState bin = carve_binning((char*)binning_buffer, C, &tmp);
-        HIP_TRY(hipMemcpyAsync(point_list, bin.gid_sorted, sizeof(uint32_t) * (size_t)R, hipMemcpyDeviceToDevice,
-                               stream),
+        GeomState geom = carve_geom((char*)const_cast<void*>(geom_buffer), P, gx, gy, &tmp);
+        HIP_TRY(launch_sorted_lists_copy(gx * gy, img.ranges, geom, bin, C, point_list, stream),
                 "debug_forward_state point_list");
     }
+    return GSR_OK;
+}
+
+int gsr_debug_sort_state(int P, int width, int height, const void* geom_buffer, unsigned int* sorted_len,
+                         unsigned int* redo_count, void* stream_) {
+    using namespace gsr;
+    g_err[0] = 0;
+    hipStream_t stream = (hipStream_t)stream_;
+    if (P <= 0 || width <= 0 || height <= 0 || !geom_buffer)
+        return fail(GSR_ERR_ARGUMENT, "debug_sort_state: invalid sizes or no geometry buffer");
+    const uint32_t gx = (width + kTile - 1) / kTile, gy = (height + kTile - 1) / kTile;
+    size_t tmp = 0;
+    GeomState geom = carve_geom((char*)const_cast<void*>(geom_buffer), P, gx, gy, &tmp);
+    if (sorted_len)
+        HIP_TRY(hipMemcpyAsync(sorted_len, geom.sorted_len, sizeof(uint32_t) * gx * gy, hipMemcpyDeviceToDevice, stream),
+                "debug_sort_state sorted_len");
+    if (redo_count)
+        HIP_TRY(hipMemcpyAsync(redo_count, geom.redo_cnt, sizeof(uint32_t), hipMemcpyDeviceToDevice, stream),
+                "debug_sort_state redo_count");
     return GSR_OK;
 }
 

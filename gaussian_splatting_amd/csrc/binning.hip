@@ -720,6 +720,7 @@ struct BucketLds {
     uint32_t start[NBMAX + 1];
     u64 red[2 * (T / 64)];
     uint32_t tmp[T / 64];
+    uint32_t m;  // entries sorted (prefix mode)
 };
 
 template <int T>
@@ -751,9 +752,14 @@ __device__ __forceinline__ void block_minmax_u64(u64& mn, u64& mx, u64* red) {
 // skewed.  The keys are loaded once, striped over the workgroup (all E loads of a thread in
 // flight together), and stay in registers until they are scattered to their bins.  The caller
 // must barrier before reusing the LDS.
+// Prefix mode (lim < n): only the bins that start below lim are scattered and ranked -- the
+// smallest *sorted = lim + (the rest of the bin lim falls in) keys, in final order at
+// gid_sorted[lo, lo + *sorted); the other entries are left unwritten.  The bins are the full key
+// range's, so the keys kept are exactly the smallest *sorted of the list.
 template <int T, int E, int NMAX, int NBMAX>
 __device__ bool bucket_sort_list(const u64* __restrict__ keys, uint32_t lo, uint32_t n,
-                                 uint32_t* __restrict__ gid_sorted, BucketLds<T, NMAX, NBMAX>& s) {
+                                 uint32_t* __restrict__ gid_sorted, BucketLds<T, NMAX, NBMAX>& s,
+                                 uint32_t lim = ~0u, uint32_t* sorted = nullptr) {
     static_assert(T * E <= NMAX, "LDS bucket buffer");
     const uint32_t tid = threadIdx.x;
     u64 k[E];
@@ -780,6 +786,7 @@ __device__ bool bucket_sort_list(const u64* __restrict__ keys, uint32_t lo, uint
     const uint32_t nb = (uint32_t)(range >> sh) + 1u;  // <= 2^lg bins
     const uint32_t per = (nb + T - 1) / T;            // bins per thread in the scan
     for (uint32_t i = tid; i < per * T + 1; i += T) s.start[i] = 0u;
+    if (tid == 0) s.m = n;  // the prefix ends at n unless a bin below crosses lim
     __syncthreads();
 #pragma unroll
     for (int e = 0; e < E; e++)
@@ -799,15 +806,24 @@ __device__ bool bucket_sort_list(const u64* __restrict__ keys, uint32_t lo, uint
     for (uint32_t c = 0; c < per; c++) {
         const uint32_t v = s.start[tid * per + c];
         s.start[tid * per + c] = at;
+        // the prefix ends with the bin lim falls in, or right before the nonempty bin starting at
+        // lim (one bin of the workgroup matches, if any)
+        if ((at < lim && lim < at + v) || (at == lim && v)) s.m = at < lim ? at + v : at;
         at += v;
     }
     if (tid == 0) s.start[nb] = n;  // bins past nb are empty and never looked up
     __syncthreads();
+    const uint32_t m = s.m;
 #pragma unroll
-    for (int e = 0; e < E; e++)
-        if ((uint32_t)e * T + tid < n) s.buf[s.start[(uint32_t)((k[e] - mn) >> sh)] + o[e]] = k[e];
+    for (int e = 0; e < E; e++) {
+        if ((uint32_t)e * T + tid < n) {
+            const uint32_t st = s.start[(uint32_t)((k[e] - mn) >> sh)];
+            if (st < m) s.buf[st + o[e]] = k[e];
+        }
+    }
     __syncthreads();
-    for (uint32_t j = tid; j < n; j += T) {
+    if (sorted && tid == 0) *sorted = m;
+    for (uint32_t j = tid; j < m; j += T) {
         const u64 kj = s.buf[j];
         const uint32_t b = (uint32_t)((kj - mn) >> sh);
         const uint32_t st = s.start[b], en = s.start[b + 1];
@@ -830,7 +846,10 @@ constexpr uint32_t kBucketMinN = GSR_BUCKET_MIN_N;
 __global__ void __launch_bounds__(64) tile_sort_kernel(const uint2* __restrict__ ranges,
                                                        const u64* __restrict__ keys, u64 cap,
                                                        uint32_t* __restrict__ gid_sorted,
-                                                       uint32_t* __restrict__ zero_cnt, uint32_t n_cells) {
+                                                       uint32_t* __restrict__ zero_cnt, uint32_t n_cells,
+                                                       uint32_t* __restrict__ sorted_len,
+                                                       uint32_t* __restrict__ redo_flag,
+                                                       uint32_t* __restrict__ redo_cnt) {
     __shared__ BucketLds<64, kSortWaveMax, kSortWaveMax / 2> s;
     if (zero_cnt && threadIdx.x == 0) {  // fused binning: K2's re-zeroing of the tile / cell counters
         zero_cnt[blockIdx.x] = 0u;
@@ -838,6 +857,11 @@ __global__ void __launch_bounds__(64) tile_sort_kernel(const uint2* __restrict__
     }
     const uint2 r = ranges[blockIdx.x];
     const uint32_t n = tile_len(r, cap);
+    if (threadIdx.x == 0) {  // the forward's redo state (render.hip), and this kernel's lists' lengths
+        redo_flag[blockIdx.x] = 0u;
+        if (blockIdx.x == 0) redo_cnt[0] = 0u;
+        if (n <= kSortWaveMax) sorted_len[blockIdx.x] = n;  // (longer lists: the class kernels)
+    }
     GSR_STAMP(g_st_sort, blockIdx.x, 0);
     GSR_STAMP_VAL(g_st_sort, blockIdx.x, 2, n);
     if (n <= 1) {
@@ -880,12 +904,18 @@ constexpr int kClassThreads = 256;
 template <int CLASS>
 constexpr int class_threads() { return CLASS == 0 ? GSR_CLASS0_THREADS : kClassThreads; }
 
+// lim: sort only the reachable prefix of each list (the "sort_prefix" option; ~0u = whole lists):
+// the bucket sort then ranks the smallest lim (+ the rest of a bin) keys and leaves the tail
+// unwritten, and sorted_len records how many entries are in order.  The skew fallbacks sort the
+// whole list.
 template <int CLASS>
 __global__ void __launch_bounds__(class_threads<CLASS>()) tile_sort_class_kernel(const uint2* __restrict__ ranges,
                                                                         u64* __restrict__ keys, u64 cap,
                                                                         uint32_t* __restrict__ gid_sorted,
                                                                         const uint32_t* __restrict__ list,
-                                                                        const uint32_t* __restrict__ count) {
+                                                                        const uint32_t* __restrict__ count,
+                                                                        uint32_t lim,
+                                                                        uint32_t* __restrict__ sorted_len) {
     constexpr int T = class_threads<CLASS>();
     constexpr int NMAX = CLASS == 0 ? (int)kClass0Max : (int)kBucketMax;
     constexpr int EF = CLASS == 0 ? NMAX / T : 16;  // the fallback network's keys per thread
@@ -894,19 +924,76 @@ __global__ void __launch_bounds__(class_threads<CLASS>()) tile_sort_class_kernel
     static_assert(CLASS != 0 || T * EF == NMAX, "class 0's fallback network covers the class");
     const uint32_t nb = count[0];
     for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
-        const uint2 r = ranges[list[b]];
+        const uint32_t t = list[b];
+        const uint2 r = ranges[t];
         const uint32_t n = tile_len(r, cap);  // may be shorter than its class when truncated by cap
         if (n <= 1) {
             if (n == 1 && threadIdx.x == 0) gid_sorted[r.x] = (uint32_t)keys[r.x];
-        } else if (n > (uint32_t)NMAX || !bucket_sort_list<T, NMAX / T>(keys, r.x, n, gid_sorted, s)) {
+            if (threadIdx.x == 0) sorted_len[t] = n;
+        } else if (n > (uint32_t)NMAX || !bucket_sort_list<T, NMAX / T>(keys, r.x, n, gid_sorted, s, lim,
+                                                                          sorted_len + t)) {
             __syncthreads();
             if (CLASS == 0 || n <= (uint32_t)T * EF)
                 sort_list<T, EF>(keys, r.x, n, gid_sorted, s.buf);
             else
                 sort_list_global(keys, r.x, n, gid_sorted);
+            if (threadIdx.x == 0) sorted_len[t] = n;
         }
         __syncthreads();  // the LDS is reused by the next tile
     }
+}
+
+// Whole-list sort of selected tiles, 256 threads per tile (any length: the bucket sort up to
+// kBucketMax keys, then a register network up to 4096, a global-memory network beyond).
+//  * redo (list != null): the tiles the forward filed because a wave reached the end of their
+//    sorted prefix with pixels still blending (render.hip); the full list goes to `out`
+//    (= gid_sorted), sorted_len becomes the whole length and the tile's half-wave join word is
+//    cleared, so the redo render starts the tile afresh.  Persistent; exits at once when the list
+//    is empty (the usual case).
+//  * inspection (list == null): every tile whose list is only prefix-sorted gets its whole sorted
+//    list in `out` (gsr_debug_forward_state's copy; the product's buffers are not written).
+__global__ void __launch_bounds__(kClassThreads) tile_sort_full_kernel(const uint2* __restrict__ ranges,
+                                                                      u64* __restrict__ keys, u64 cap,
+                                                                      uint32_t* __restrict__ out,
+                                                                      const uint32_t* __restrict__ list,
+                                                                      const uint32_t* __restrict__ count,
+                                                                      uint32_t tiles,
+                                                                      uint32_t* __restrict__ sorted_len,
+                                                                      unsigned long long* __restrict__ tile_join) {
+    constexpr int T = kClassThreads;
+    __shared__ BucketLds<T, kBucketMax, kBucketMax / 2> s;
+    const uint32_t nb = list ? count[0] : tiles;
+    for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
+        const uint32_t t = list ? list[b] : b;
+        const uint2 r = ranges[t];
+        const uint32_t n = tile_len(r, cap);
+        if (!list && sorted_len[t] >= n) continue;  // uniform: a whole-sorted list
+        if (n <= 1) {
+            if (n == 1 && threadIdx.x == 0) out[r.x] = (uint32_t)keys[r.x];
+        } else if (n > kBucketMax || !bucket_sort_list<T, kBucketMax / T>(keys, r.x, n, out, s)) {
+            __syncthreads();
+            if (n <= (uint32_t)T * 16)
+                sort_list<T, 16>(keys, r.x, n, out, s.buf);
+            else
+                sort_list_global(keys, r.x, n, out);
+        }
+        if (list && threadIdx.x == 0) {
+            sorted_len[t] = n;
+            tile_join[t] = 0ull;
+        }
+        __syncthreads();  // the LDS is reused by the next tile
+    }
+}
+
+// out[lo, lo + sorted_len) = gid_sorted[lo, ...) for every tile (gsr_debug_forward_state: the
+// product's sorted entries, with the quadrant masks the forward wrote into them).
+__global__ void __launch_bounds__(64) copy_sorted_prefix_kernel(const uint2* __restrict__ ranges, u64 cap,
+                                                                 const uint32_t* __restrict__ gid_sorted,
+                                                                 const uint32_t* __restrict__ sorted_len,
+                                                                 uint32_t* __restrict__ out) {
+    const uint2 r = ranges[blockIdx.x];
+    const uint32_t n = min(tile_len(r, cap), sorted_len[blockIdx.x]);
+    for (uint32_t i = threadIdx.x; i < n; i += 64) out[r.x + i] = gid_sorted[r.x + i];
 }
 
 // ---- launchers ----------------------------------------------------------------
@@ -999,17 +1086,36 @@ hipError_t launch_bin_scatter(int P, const GeomState& g, uint32_t gx, uint32_t g
 }
 
 hipError_t launch_tile_sort(uint32_t tiles, const uint2* ranges, const GeomState& g, const BinningState& b,
-                            size_t cap, hipStream_t stream, bool zero_counts, uint32_t cells) {
+                            size_t cap, hipStream_t stream, bool zero_counts, uint32_t cells, uint32_t prefix) {
     if (tiles == 0 || cap == 0) return hipSuccess;
     const u64 c = cap;
+    const uint32_t lim = prefix ? prefix : ~0u;
     hipLaunchKernelGGL(tile_sort_kernel, dim3(tiles), dim3(64), 0, stream, ranges, b.keys, c, b.gid_sorted,
-                       zero_counts ? g.tile_cnt : nullptr, cells);
+                       zero_counts ? g.tile_cnt : nullptr, cells, g.sorted_len, g.redo_flag, g.redo_cnt);
     // persistent class kernels: grids sized to fill the chip when their lists are long
     const auto grid = [&](uint32_t want) { return dim3(tiles < want ? tiles : want); };
     hipLaunchKernelGGL(tile_sort_class_kernel<0>, grid(2048), dim3(class_threads<0>()), 0, stream, ranges, b.keys, c,
-                       b.gid_sorted, g.cls_list, g.cls_count);
+                       b.gid_sorted, g.cls_list, g.cls_count, lim, g.sorted_len);
     hipLaunchKernelGGL(tile_sort_class_kernel<1>, grid(512), dim3(class_threads<1>()), 0, stream, ranges, b.keys, c,
-                       b.gid_sorted, g.cls_list + tiles, g.cls_count + 1);
+                       b.gid_sorted, g.cls_list + tiles, g.cls_count + 1, lim, g.sorted_len);
+    return hipGetLastError();
+}
+
+hipError_t launch_tile_sort_redo(uint32_t tiles, const uint2* ranges, const GeomState& g, const BinningState& b,
+                                 size_t cap, hipStream_t stream) {
+    if (tiles == 0 || cap == 0) return hipSuccess;
+    hipLaunchKernelGGL(tile_sort_full_kernel, dim3(tiles < 256 ? tiles : 256), dim3(kClassThreads), 0, stream, ranges,
+                       b.keys, (u64)cap, b.gid_sorted, g.redo_list, g.redo_cnt, tiles, g.sorted_len, g.tile_join);
+    return hipGetLastError();
+}
+
+hipError_t launch_sorted_lists_copy(uint32_t tiles, const uint2* ranges, const GeomState& g, const BinningState& b,
+                                    size_t cap, uint32_t* out, hipStream_t stream) {
+    if (tiles == 0 || cap == 0) return hipSuccess;
+    hipLaunchKernelGGL(tile_sort_full_kernel, dim3(tiles < 2048 ? tiles : 2048), dim3(kClassThreads), 0, stream,
+                       ranges, b.keys, (u64)cap, out, nullptr, nullptr, tiles, g.sorted_len, nullptr);
+    hipLaunchKernelGGL(copy_sorted_prefix_kernel, dim3(tiles), dim3(64), 0, stream, ranges, (u64)cap, b.gid_sorted,
+                       g.sorted_len, out);
     return hipGetLastError();
 }
 

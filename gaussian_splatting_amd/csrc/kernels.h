@@ -48,6 +48,11 @@ struct RenderFwdArgs {
     unsigned long long* tile_join;  // GeomState::tile_join
     int seg_ck;
     unsigned long long* census;     // diagnostic pair counts (gsr_census_set) or null
+    // reachable-prefix sort (GeomState): entries in order per tile, and the redo filing
+    const uint32_t* sorted_len;
+    uint32_t* redo_flag;
+    uint32_t* redo_list;
+    uint32_t* redo_cnt;
 };
 
 struct RenderBwdArgs {
@@ -378,12 +383,25 @@ hipError_t launch_bin_count(int P, const GeomState& g, uint32_t gx, uint32_t gy,
 hipError_t launch_bin_scatter(int P, const GeomState& g, uint32_t gx, uint32_t gy, const BinningState& b, size_t cap,
                               hipStream_t stream, uint2* ranges = nullptr, unsigned long long* host_total = nullptr,
                               bool fused = false);
+// prefix: sort only the first `prefix` (+ the rest of an LDS bin) entries of the lists longer than
+// one wave's sort (0: whole lists); GeomState::sorted_len records each list's sorted length.
 hipError_t launch_tile_sort(uint32_t tiles, const uint2* ranges, const GeomState& g, const BinningState& b,
-                            size_t cap, hipStream_t stream, bool zero_counts = false, uint32_t cells = 0);
+                            size_t cap, hipStream_t stream, bool zero_counts = false, uint32_t cells = 0,
+                            uint32_t prefix = 0);
+// The forward's redo of tiles whose walk passed their sorted prefix: whole-list sort of the filed
+// tiles (before launch_render_fwd_redo).
+hipError_t launch_tile_sort_redo(uint32_t tiles, const uint2* ranges, const GeomState& g, const BinningState& b,
+                                 size_t cap, hipStream_t stream);
+// Inspection: every tile's whole sorted list into `out` (the product's sorted entries, the rest
+// sorted here), without writing the forward's buffers.
+hipError_t launch_sorted_lists_copy(uint32_t tiles, const uint2* ranges, const GeomState& g, const BinningState& b,
+                                    size_t cap, uint32_t* out, hipStream_t stream);
 bool bin_fused_ok(uint32_t tiles);  // the fused form applies (LDS cursors)
 // render.hip
 // quads: 8x8 quadrants per wave, 2 (half tiles) or 4 (whole tiles; the "fwd_quads" option)
 hipError_t launch_render_fwd(const RenderFwdArgs& a, hipStream_t stream, int quads = 2);
+// the tiles filed for a redo (GeomState::redo_list), after launch_tile_sort_redo; exits at once if none
+hipError_t launch_render_fwd_redo(const RenderFwdArgs& a, hipStream_t stream, int quads = 2);
 // a tile-major pixel plane (tile_px) -> image order [H][W], 4-byte elements (inspection only)
 hipError_t launch_untile(const uint32_t* src, uint32_t* dst, int W, int H, uint32_t gx, hipStream_t stream);
 hipError_t launch_render_bwd(const RenderBwdArgs& a, size_t max_units, hipStream_t stream);

@@ -120,15 +120,18 @@ __device__ __forceinline__ float splat_alpha(float p2, float opacity, float& G) 
 // the same XCD (blocks are dealt round-robin over the 8 XCDs) and share its L2.
 // CENSUS (diagnostic instantiation, gsr_census_set): counts the work the blend does -- see
 // include/gsr.h "Census" for the counters -- with wave-uniform scalar counters, one atomic per wave.
+// Reachable-prefix sort (binning.hip K4): only entries [0, sorted_len) of a long list are in
+// order.  A part that reaches sorted_len with pixels still blending files its tile for a redo
+// (one flag per tile, so a tile is listed once) and stops without writing anything: after this
+// launch the tile's whole list is sorted and both parts render it again from the start
+// (render_fwd_redo_kernel).  The forward walks ~7% of a 4K tile's list and ~34% of a 1080p
+// one, so with a prefix of 1024 entries a redo is rare.
 template <int NQ, bool CENSUS>
-__global__ void __launch_bounds__(64) GSR_FWD_OCCUPANCY render_fwd_kernel(RenderFwdArgs a) {
+__device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const uint32_t tile, const int part) {
   {
     constexpr int NPART = 4 / NQ;
     constexpr uint32_t kPartMask = (1u << NQ) - 1u;
     const uint32_t tiles = a.gx * a.gy;
-    const uint32_t tile = (blockIdx.x / (8 * NPART)) * 8 + blockIdx.x % 8;
-    const int part = NPART == 1 ? 0 : (int)((blockIdx.x / 8) % NPART);
-    if (tile >= tiles) return;
     const int qbase = part * NQ;  // first quadrant of this part
     const int tile_x0 = (int)(tile % a.gx) * kTile, tile_y0 = (int)(tile / a.gx) * kTile;
     const int lane = threadIdx.x;
@@ -158,11 +161,12 @@ __global__ void __launch_bounds__(64) GSR_FWD_OCCUPANCY render_fwd_kernel(Render
 
     const uint2 range = a.ranges[tile];
     const int n = (int)(range.y - range.x);
+    const int ns = a.sorted_len ? min(n, (int)a.sorted_len[tile]) : n;  // entries in order
     unsigned long long c_staged = 0, c_eval = 0, c_alpha = 0, c_blend = 0, c_idle = 0;  // CENSUS only
-    for (int b0 = 0; b0 < n && alive; b0 += kBatch) {
-        if (CENSUS) c_staged += (unsigned long long)min(kBatch, n - b0);
+    for (int b0 = 0; b0 < ns && alive; b0 += kBatch) {
+        if (CENSUS) c_staged += (unsigned long long)min(kBatch, ns - b0);
         uint32_t qm = 0;
-        if (b0 + lane < n) {
+        if (b0 + lane < ns) {
             uint32_t* ent = a.gid_sorted + range.x + b0 + lane;  // Gaussian << 4 | quadrant mask
             const uint32_t gid = *ent >> kEntryMaskBits;
             const float4* rec = a.rec + (size_t)kRecRows * gid;
@@ -245,6 +249,10 @@ __global__ void __launch_bounds__(64) GSR_FWD_OCCUPANCY render_fwd_kernel(Render
         atomicAdd(&a.census[3], c_blend);
         atomicAdd(&a.census[9], c_idle);
     }
+    if (ns < n && alive) {  // uniform: the sorted prefix ran out with pixels still blending
+        if (lane == 0 && atomicOr(&a.redo_flag[tile], 1u) == 0u) a.redo_list[atomicAdd(a.redo_cnt, 1u)] = tile;
+        return;
+    }
     if (part == 0) {
         GSR_STAMP(g_st_rfwd, tile, 1);
         GSR_STAMP_RT(g_st_rfwd, tile, 5);
@@ -317,6 +325,25 @@ __global__ void __launch_bounds__(64) GSR_FWD_OCCUPANCY render_fwd_kernel(Render
   }
 }
 
+template <int NQ, bool CENSUS>
+__global__ void __launch_bounds__(64) GSR_FWD_OCCUPANCY render_fwd_kernel(RenderFwdArgs a) {
+    constexpr int NPART = 4 / NQ;
+    const uint32_t tile = (blockIdx.x / (8 * NPART)) * 8 + blockIdx.x % 8;
+    const int part = NPART == 1 ? 0 : (int)((blockIdx.x / 8) % NPART);
+    if (tile >= a.gx * a.gy) return;
+    render_fwd_tile<NQ, CENSUS>(a, tile, part);
+}
+
+// The redo of the tiles render_fwd_kernel filed (their whole lists sorted since, by
+// tile_sort_full_kernel): NPART blocks per tile, persistent over the redo list.
+template <int NQ, bool CENSUS>
+__global__ void __launch_bounds__(64) GSR_FWD_OCCUPANCY render_fwd_redo_kernel(RenderFwdArgs a) {
+    constexpr int NPART = 4 / NQ;
+    const uint32_t cnt = a.redo_cnt[0];
+    for (uint32_t i = blockIdx.x / NPART; i < cnt; i += gridDim.x / NPART)
+        render_fwd_tile<NQ, CENSUS>(a, a.redo_list[i], (int)(blockIdx.x % NPART));
+}
+
 __global__ void untile_kernel(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, int W, int H, uint32_t gx) {
     const int x = blockIdx.x * 16 + (threadIdx.x & 15), y = blockIdx.y * 16 + (threadIdx.x >> 4);
     if (x >= W || y >= H) return;
@@ -329,6 +356,18 @@ hipError_t launch_untile(const uint32_t* src, uint32_t* dst, int W, int H, uint3
     const uint32_t gy = (H + kTile - 1) / kTile;
     if (gx == 0 || gy == 0) return hipSuccess;
     hipLaunchKernelGGL(untile_kernel, dim3(gx, gy), dim3(256), 0, stream, src, dst, W, H, gx);
+    return hipGetLastError();
+}
+
+hipError_t launch_render_fwd_redo(const RenderFwdArgs& a, hipStream_t stream, int quads) {
+    if (a.gx * a.gy == 0) return hipSuccess;
+    constexpr uint32_t kTilesPerPass = 256;  // persistent: each block walks the list in steps of this
+    if (a.census)
+        hipLaunchKernelGGL((render_fwd_redo_kernel<2, true>), dim3(2 * kTilesPerPass), dim3(kWave), 0, stream, a);
+    else if (quads == 4)
+        hipLaunchKernelGGL((render_fwd_redo_kernel<4, false>), dim3(kTilesPerPass), dim3(kWave), 0, stream, a);
+    else
+        hipLaunchKernelGGL((render_fwd_redo_kernel<2, false>), dim3(2 * kTilesPerPass), dim3(kWave), 0, stream, a);
     return hipGetLastError();
 }
 

@@ -266,6 +266,13 @@ int gsr_debug_forward_state(int P, int width, int height, int R, int binning_cap
                             unsigned int* ranges, unsigned int* point_list, unsigned int* n_contrib, float* final_T,
                             void* stream);
 
+/* Inspection of the reachable-prefix sort ("sort_prefix" option): copies, on `stream`, device to
+ * device, the number of entries of each tile's list in final order (sorted_len [tiles]; the whole
+ * length unless K4 sorted only a prefix) and the number of tiles the forward redid because a wave
+ * passed the sorted prefix (redo_count [1]).  Either pointer may be NULL. */
+int gsr_debug_sort_state(int P, int width, int height, const void* geom_buffer, unsigned int* sorted_len,
+                         unsigned int* redo_count, void* stream);
+
 /* Number of forwards (process-wide) whose capacity hint was too small, so the binning stage
  * was redone with the exact count (gsr_rasterize_forward_ex). */
 long long gsr_forward_rebuilds(void);
@@ -287,6 +294,9 @@ int gsr_host_wait_stats(double* total_ms, double* max_ms, long long* calls, int 
  *                        before gauss_bwd | not at all (gauss_bwd writes every row)
  *   "live_list"  1|0    gauss_bwd over the list of Gaussians with a render gradient | a lane per Gaussian
  *                        (only with zero_fill != 0)
+ *   "sort_prefix" L|0   lists longer than 1024 entries: sort only their first L (+ the rest of a bucket)
+ *                        entries, the part the blend reaches, and redo the rare tile whose walk passes
+ *                        it | sort whole lists (default L = 1024)
  * gsr_option_get returns -1 for an unknown name; gsr_option_set returns GSR_ERR_ARGUMENT for an
  * unknown name or an out-of-range value.  Not synchronised against calls running on other threads. */
 int gsr_option_set(const char* name, int value);

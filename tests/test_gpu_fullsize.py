@@ -84,7 +84,12 @@ def test_fullsize_integers_identical(fullsize):
     nz = elen > 0
     np.testing.assert_array_equal(gr[nz, 0], er[nz, 0])  # (empty tiles: the reference leaves [0, 0))
     np.testing.assert_array_equal(st["point_list"].numpy(), rb["point_list"].astype(np.int64))
-    print(f"[{fullsize['name']}] num_rendered={nr} identical; {int(nz.sum())} non-empty tiles, lists identical")
+    from gaussian_splatting_amd import _C
+    ss = _C.debug_sort_state(fwd, fullsize["inp"]["means3D"].shape[0])
+    sl = ss["sorted_len"].numpy()
+    print(f"[{fullsize['name']}] num_rendered={nr} identical; {int(nz.sum())} non-empty tiles, lists identical "
+          f"(the product sorted {int(np.minimum(sl, glen).sum())} of {int(glen.sum())} entries, reachable prefixes of "
+          f"{int((sl < glen).sum())} long lists; {ss['redo_count']} tiles redone)")
 
 
 def _flips(fullsize):

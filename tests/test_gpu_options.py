@@ -31,6 +31,8 @@ VARIANTS = {
     "zero_fill=0": dict(zero_fill=0),
     "zero_fill=2": dict(zero_fill=2),
     "live_list=0": dict(live_list=0),
+    "sort_prefix=0": dict(sort_prefix=0),     # whole lists sorted
+    "sort_prefix=64": dict(sort_prefix=64),   # long lists sorted to 64 entries: most of their tiles redone
 }
 CASES = ["sh3_scalerot", "antialiasing", "dense_opaque", "lists_1k_2k", "lists_4k_8k", "lists_over_8k"]
 

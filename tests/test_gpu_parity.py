@@ -362,3 +362,47 @@ def test_census_counts_pairs(name):
     assert torch.equal(box["fwd"][1], fwd[1])
     for a, b in zip(box["out"], out):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("name,prefix", [("lists_1k_2k", 64), ("lists_2k_4k", 64), ("lists_4k_8k", 256),
+                                         ("lists_over_8k", 1024), ("lists_2k_4k", 1024)])
+def test_sort_prefix_and_redo(name, prefix):
+    """The reachable-prefix sort (binning.hip K4, "sort_prefix"): lists longer than one wave's sort are
+    sorted to `prefix` (+ a bucket's rest) entries only, and a tile whose forward walk passes that is
+    sorted whole and rendered again.  Checked: the prefix was applied (sorted_len < list length for
+    the long lists), the redo ran where the walk needed it, every list -- prefix as the product left
+    it, tail sorted for inspection -- equals the oracle's, and images and gradients are bitwise those
+    of whole-list sorting."""
+    from gaussian_splatting_amd import _C as CM
+    from gaussian_splatting_amd import _lib
+
+    case = next(c for c in C.SMALL_CASES if c.name == name)
+    inp = C.build(case)
+    ref = C.run_oracle(inp)
+    gc, gd = C.unit_grads(case.H, case.W)
+    with _lib.options(sort_prefix=0):
+        whole = _run_pair(inp, gc, gd)
+    with _lib.options(sort_prefix=prefix):
+        fwd = C.run_gpu_forward(inp)
+        out = C.run_gpu_backward(inp, fwd, gc, gd)
+        torch.cuda.synchronize()
+        st = CM.debug_sort_state(fwd, case.P)
+        lists = CM.debug_forward_state(fwd, case.P)
+    got = [fwd[0]] + [_to_np(fwd[i]) for i in (1, 2, 6)] + [_to_np(o) for o in out]
+    rng = lists["ranges"].numpy()
+    n = rng[:, 1] - rng[:, 0]
+    sl = st["sorted_len"].numpy()
+    long = n > 1024
+    assert long.any()
+    assert (sl[~long] == n[~long]).all()
+    assert (sl[long] >= np.minimum(prefix, n[long])).all() and (sl[long] <= n[long]).all()
+    cut = long & (prefix < n)
+    print(f"[{name} prefix {prefix}] long lists {int(long.sum())}, prefix-sorted {int((sl < n).sum())} "
+          f"(sorted {int(sl[long].sum())} of {int(n[long].sum())} entries), redone tiles {st['redo_count']}")
+    if prefix == 64:
+        assert st["redo_count"] > 0  # the blend walks past 64 entries in these dense tiles
+    assert cut.any()
+    np.testing.assert_array_equal(lists["point_list"].numpy(), ref.handle.binning()["point_list"].astype(np.int64))
+    assert got[0] == whole[0]
+    for a, b in zip(got[1:], whole[1:]):
+        np.testing.assert_array_equal(a, b)
