@@ -397,11 +397,11 @@ def main():
         traffic, traffic_src, kk = None, None, {}
         if os.path.exists(PMC_PROFILE):
             prof = json.load(open(PMC_PROFILE))
-            kk = (prof.get("configs", {}).get(args.config) or
-                  (prof if prof.get("config", "1m_1080p_sh3") == args.config else {})).get("kernels", {}).get(dom) or {}
+            entry = prof.get("configs", {}).get(args.config) or (prof if args.config == "1m_1080p_sh3" else {})
+            kk = entry.get("kernels", {}).get(dom) or {}
             if kk:
                 traffic = kk["hbm_read_bytes"] + kk["hbm_write_bytes"]
-                traffic_src = prof.get("source")
+                traffic_src = entry.get("source")
         achieved = alg / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
         valu_frac = None
         if traffic is not None and kk.get("valu_insts"):

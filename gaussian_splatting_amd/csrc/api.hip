@@ -331,6 +331,18 @@ int bwd_segment_checkpoints() { return option(OPT_BWD_SEG_CK); }
 // K2 folded into K3 in capacity mode.
 bool fused_binning_mode() { return option(OPT_FUSED_BIN) != 0; }
 
+// The reachable-prefix sort of long lists ("sort_prefix" option, binning.hip K4) for a binning
+// buffer of capacity C: on when the frame's lists are long -- mean length >= 2 L -- where sorting
+// only their first L entries saves most of K4 (5M@4K: tile_sort 0.70 -> 0.49 ms); off for shorter
+// lists, where it saves nothing and the two redo launches cost ~8 us (1M@1080p, r3c).  Census runs
+// sort whole lists (a redone tile's first pass would be counted twice).  The results are the same
+// either way.
+uint32_t sort_prefix_for(size_t C, uint32_t tiles) {
+    const uint32_t L = (uint32_t)option(OPT_SORT_PREFIX);
+    if (!L || g_census || tiles == 0) return 0u;
+    return C / tiles >= 2ull * L ? L : 0u;
+}
+
 // Per (host thread, device): a pinned 8-byte slot that num_rendered is copied into and the
 // event recorded behind that copy.  The host waits on the event -- i.e. for the binning
 // counts -- and not for the whole stream, so the render kernels queued behind the copy keep
@@ -863,14 +875,12 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
             {
                 StageScope sc(ST_TILE_SORT, stream);
                 HIP_TRY(launch_tile_sort(tiles, img.ranges, geom, bin, C, stream, fused_now,
-                                         (uint32_t)bin_cell_count(gx, gy),
-                                         g_census ? 0u : (uint32_t)option(OPT_SORT_PREFIX)),
+                                         (uint32_t)bin_cell_count(gx, gy), sort_prefix_for(C, tiles)),
                         "tile_sort");
             }
             if (int rc = check_debug(debug, stream, "tile_sort")) return rc;
         }
-        // (census runs sort whole lists: a redone tile's first pass would be counted twice)
-        const uint32_t prefix = g_census ? 0u : (uint32_t)option(OPT_SORT_PREFIX);
+        const uint32_t prefix = sort_prefix_for(C, tiles);
         {
             StageScope sc(ST_RENDER_FWD, stream);
             RenderFwdArgs ra{};

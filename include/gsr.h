@@ -294,9 +294,10 @@ int gsr_host_wait_stats(double* total_ms, double* max_ms, long long* calls, int 
  *                        before gauss_bwd | not at all (gauss_bwd writes every row)
  *   "live_list"  1|0    gauss_bwd over the list of Gaussians with a render gradient | a lane per Gaussian
  *                        (only with zero_fill != 0)
- *   "sort_prefix" L|0   lists longer than 1024 entries: sort only their first L (+ the rest of a bucket)
- *                        entries, the part the blend reaches, and redo the rare tile whose walk passes
- *                        it | sort whole lists (default L = 1024)
+ *   "sort_prefix" L|0   when the frame's mean list length is at least 2 L: of the lists longer than
+ *                        1024 entries sort only the first L (+ the rest of a bucket), the part the blend
+ *                        reaches, and redo the rare tile whose walk passes it | sort whole lists
+ *                        (default L = 1024)
  * gsr_option_get returns -1 for an unknown name; gsr_option_set returns GSR_ERR_ARGUMENT for an
  * unknown name or an out-of-range value.  Not synchronised against calls running on other threads. */
 int gsr_option_set(const char* name, int value);

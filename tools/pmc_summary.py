@@ -44,6 +44,8 @@ def main():
     ap.add_argument("dir")
     ap.add_argument("--out")
     ap.add_argument("--json", help="also write {kernel: {hbm_read_bytes, hbm_write_bytes, ...}} here")
+    ap.add_argument("--config", help="with --json: merge as configs[CONFIG] into the existing file (bench.py reads "
+                                     "the entry of the config it runs)")
     a = ap.parse_args()
     vals, meta = load(a.dir)
     table = {}
@@ -71,9 +73,16 @@ def main():
     if a.json:
         import json
 
+        entry = {"source": a.out or a.dir, "correction": "read = 2 x FETCH_SIZE KiB (gfx950), write = WRITE_SIZE KiB",
+                 "kernels": table}
+        if a.config:
+            doc = json.load(open(a.json)) if os.path.exists(a.json) else {}
+            doc.setdefault("configs", {})[a.config] = entry
+            if a.config == "1m_1080p_sh3":  # the headline config also at the top level (older readers)
+                doc.update(entry)
+            entry = doc
         with open(a.json, "w") as f:
-            json.dump({"source": a.out or a.dir, "correction": "read = 2 x FETCH_SIZE KiB (gfx950), write = WRITE_SIZE KiB",
-                       "kernels": table}, f, indent=1)
+            json.dump(entry, f, indent=1)
     if a.out:
         with open(a.out, "w") as f:
             f.write(f"# PMC summary ({a.dir}): mean per dispatch\n\n"
