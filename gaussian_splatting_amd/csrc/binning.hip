@@ -760,7 +760,8 @@ template <int T, int E, int NMAX, int NBMAX>
 __device__ bool bucket_sort_list(const u64* __restrict__ keys, uint32_t lo, uint32_t n,
                                  uint32_t* __restrict__ gid_sorted, BucketLds<T, NMAX, NBMAX>& s,
                                  uint32_t lim = ~0u, uint32_t* sorted = nullptr) {
-    static_assert(T * E <= NMAX, "LDS bucket buffer");
+    // T * E > NMAX: more keys in registers than the LDS buffer takes -- for prefix use; the sort
+    // fails (uniformly) when the prefix does not fit the buffer
     const uint32_t tid = threadIdx.x;
     u64 k[E];
     uint32_t o[E];
@@ -814,6 +815,7 @@ __device__ bool bucket_sort_list(const u64* __restrict__ keys, uint32_t lo, uint
     if (tid == 0) s.start[nb] = n;  // bins past nb are empty and never looked up
     __syncthreads();
     const uint32_t m = s.m;
+    if (T * E > NMAX && m > (uint32_t)NMAX) return false;  // uniform: the prefix overflows the buffer
 #pragma unroll
     for (int e = 0; e < E; e++) {
         if ((uint32_t)e * T + tid < n) {
@@ -937,6 +939,48 @@ __global__ void __launch_bounds__(class_threads<CLASS>()) tile_sort_class_kernel
                 sort_list<T, EF>(keys, r.x, n, gid_sorted, s.buf);
             else
                 sort_list_global(keys, r.x, n, gid_sorted);
+            if (threadIdx.x == 0) sorted_len[t] = n;
+        }
+        __syncthreads();  // the LDS is reused by the next tile
+    }
+}
+
+// Prefix mode (the "sort_prefix" option in force): every long list -- both class lists -- sorted
+// to its reachable prefix by one kernel whose LDS holds only the prefix (kPrefixBuf keys and up to
+// kPrefixBins bins: 24 KiB, twice the class-0 kernel's occupancy), the keys themselves in
+// registers (up to kBucketMax per tile).  Skewed bins, a prefix over the buffer or a list over
+// kBucketMax fall back to the global-memory network (whole list).
+#ifndef GSR_PREFIX_KERNEL
+#define GSR_PREFIX_KERNEL 1
+#endif
+constexpr int kPrefixBuf = 2048;
+constexpr int kPrefixBins = 2048;
+
+// E keys per thread: 16 for class 0's lists (<= 4096 keys), 32 for class 1's (<= kBucketMax).
+// (16 keys: at most 128 VGPRs, four workgroups per CU; the LDS would allow six)
+template <int E>
+__global__ void __launch_bounds__(kClassThreads) __attribute__((amdgpu_waves_per_eu(E <= 16 ? 4 : 2)))
+tile_sort_prefix_kernel(const uint2* __restrict__ ranges,
+                                                                        u64* __restrict__ keys, u64 cap,
+                                                                        uint32_t* __restrict__ gid_sorted,
+                                                                        const uint32_t* __restrict__ list,
+                                                                        const uint32_t* __restrict__ count,
+                                                                        uint32_t lim,
+                                                                        uint32_t* __restrict__ sorted_len) {
+    constexpr int T = kClassThreads;
+    __shared__ BucketLds<T, kPrefixBuf, kPrefixBins> s;
+    const uint32_t nb = count[0];
+    for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
+        const uint32_t t = list[b];
+        const uint2 r = ranges[t];
+        const uint32_t n = tile_len(r, cap);
+        if (n <= 1) {
+            if (n == 1 && threadIdx.x == 0) gid_sorted[r.x] = (uint32_t)keys[r.x];
+            if (threadIdx.x == 0) sorted_len[t] = n;
+        } else if (n > (uint32_t)(T * E) ||
+                   !bucket_sort_list<T, E>(keys, r.x, n, gid_sorted, s, lim, sorted_len + t)) {
+            __syncthreads();
+            sort_list_global(keys, r.x, n, gid_sorted);
             if (threadIdx.x == 0) sorted_len[t] = n;
         }
         __syncthreads();  // the LDS is reused by the next tile
@@ -1094,6 +1138,14 @@ hipError_t launch_tile_sort(uint32_t tiles, const uint2* ranges, const GeomState
                        zero_counts ? g.tile_cnt : nullptr, cells, g.sorted_len, g.redo_flag, g.redo_cnt);
     // persistent class kernels: grids sized to fill the chip when their lists are long
     const auto grid = [&](uint32_t want) { return dim3(tiles < want ? tiles : want); };
+    if (GSR_PREFIX_KERNEL && prefix) {
+        hipLaunchKernelGGL(tile_sort_prefix_kernel<kClass0Max / kClassThreads>, grid(4096), dim3(kClassThreads), 0,
+                           stream, ranges, b.keys, c, b.gid_sorted, g.cls_list, g.cls_count, lim, g.sorted_len);
+        hipLaunchKernelGGL(tile_sort_prefix_kernel<kBucketMax / kClassThreads>, grid(1024), dim3(kClassThreads), 0,
+                           stream, ranges, b.keys, c, b.gid_sorted, g.cls_list + tiles, g.cls_count + 1, lim,
+                           g.sorted_len);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(tile_sort_class_kernel<0>, grid(2048), dim3(class_threads<0>()), 0, stream, ranges, b.keys, c,
                        b.gid_sorted, g.cls_list, g.cls_count, lim, g.sorted_len);
     hipLaunchKernelGGL(tile_sort_class_kernel<1>, grid(512), dim3(class_threads<1>()), 0, stream, ranges, b.keys, c,
