@@ -406,3 +406,28 @@ def test_sort_prefix_and_redo(name, prefix):
     assert got[0] == whole[0]
     for a, b in zip(got[1:], whole[1:]):
         np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("P", [3000, 40000])
+def test_scatter_window_fallback_large_image(P):
+    """K3's cursors (binning.hip): an LDS window over the chunk's tile bounding box when it holds at
+    most 16384 tiles, global per-(chunk, tile) cursors otherwise.  A 2304x2048 frame has 18432
+    tiles: with 3000 Gaussians every chunk spans most of the screen (the global cursors), with
+    40000 the chunks are compact screen regions (the LDS windows).  Lists, image and gradients
+    against the oracle as for the small cases."""
+    case = C.Case("large_image", P=P, W=2304, H=2048, focal=1400.0, scale_range=(0.01, 0.08))
+    inp = C.build(case)
+    ref = C.run_oracle(inp, nthreads=8)
+    fwd = C.run_gpu_forward(inp)
+    torch.cuda.synchronize()
+    assert fwd[0] == ref.num_rendered
+    np.testing.assert_array_equal(_to_np(fwd[2]).astype(np.int32), ref.radii)
+    from gaussian_splatting_amd import _C as CM
+    st = CM.debug_forward_state(fwd, case.P)
+    np.testing.assert_array_equal(st["point_list"].numpy(), ref.handle.binning()["point_list"].astype(np.int64))
+    np.testing.assert_allclose(_to_np(fwd[1]), ref.color, atol=ATOL_FWD, rtol=0)
+    gc, gd = C.l1_grads(case.H, case.W)
+    out = C.run_gpu_backward(inp, fwd, gc, gd)
+    r = ref.handle.backward(gc, gd, nthreads=8)
+    for k, got in zip(C.GRAD_NAMES, out):
+        np.testing.assert_allclose(_to_np(got), r[k], atol=1e-5, rtol=0, err_msg=k)
