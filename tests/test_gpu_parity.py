@@ -425,9 +425,16 @@ def test_scatter_window_fallback_large_image(P):
     from gaussian_splatting_amd import _C as CM
     st = CM.debug_forward_state(fwd, case.P)
     np.testing.assert_array_equal(st["point_list"].numpy(), ref.handle.binning()["point_list"].astype(np.int64))
-    np.testing.assert_allclose(_to_np(fwd[1]), ref.color, atol=ATOL_FWD, rtol=0)
+    # a frame this size has a few pixels at a threshold flip (tests/test_gpu_fullsize.py's rule)
+    d = np.maximum(np.abs(_to_np(fwd[1]) - ref.color).max(0), np.abs(_to_np(fwd[6]) - ref.invdepth)[0])
+    m = ref.handle.pixel_margins(nthreads=8)
+    near = (m["power"] < 1e-5) | (m["alpha"] < 1e-4) | (m["T"] < 1e-4)
+    nc_diff = st["n_contrib"].numpy() != ref.handle.image()["n_contrib"].astype(np.int64)
+    unexplained = (d > ATOL_FWD) & ~(near | nc_diff)
+    assert not unexplained.any(), (int(unexplained.sum()), float(d[unexplained].max()))
     gc, gd = C.l1_grads(case.H, case.W)
     out = C.run_gpu_backward(inp, fwd, gc, gd)
     r = ref.handle.backward(gc, gd, nthreads=8)
     for k, got in zip(C.GRAD_NAMES, out):
         np.testing.assert_allclose(_to_np(got), r[k], atol=1e-5, rtol=0, err_msg=k)
+    print(f"[large_image P={P}] pixels over 1e-5: {int((d > ATOL_FWD).sum())}, all at threshold flips")
