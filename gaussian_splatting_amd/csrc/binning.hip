@@ -419,27 +419,15 @@ struct FusedScan {
     uint32_t* cls_count;
 };
 
-// K3's cursors live in LDS for a window of tiles: the tile bounding box of the chunk's rectangles
-// (K0's spatial order makes a chunk a compact screen region: a few hundred to a few thousand tiles).
-// kScatterWinMax words (64 KiB) leave room for two 1024-thread workgroups per CU where a cursor per
-// tile of a 4K frame (32400 tiles, 130 KiB) allowed one -- the walk is latency-bound (5M@4K r2zC:
-// 12% of wave cycles issuing).  A chunk whose box is larger (a huge splat) keeps its cursors in its
-// own row of chunk_off and takes global atomics.
-#ifndef GSR_SCATTER_WIN_MAX
-#define GSR_SCATTER_WIN_MAX 16384
-#endif
-constexpr uint32_t kScatterWinMax = GSR_SCATTER_WIN_MAX;
-
 template <bool LDS>
 __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
     int P, int chunk, const uint2* __restrict__ rect, const uint32_t* __restrict__ tiles_touched,
     const uint32_t* __restrict__ depth_key, const uint4* __restrict__ order, const uint32_t* __restrict__ n_visible,
     uint32_t tiles, uint32_t gx, uint32_t* __restrict__ tile_base,
-    uint32_t* __restrict__ chunk_off, const u64* __restrict__ chunk_total, u64* __restrict__ keys, u64 cap,
-    uint32_t* __restrict__ rec_start, float4* __restrict__ rec, FusedScan fs, uint32_t win_cap) {
-    extern __shared__ uint32_t s_cur[];  // win_cap words: the cursors of the chunk's tile window
+    const uint32_t* __restrict__ chunk_off, const u64* __restrict__ chunk_total, u64* __restrict__ keys, u64 cap,
+    uint32_t* __restrict__ rec_start, float4* __restrict__ rec, FusedScan fs) {
+    extern __shared__ uint32_t s_cur[];  // tiles words
     __shared__ u64 s_tmp[kBinWaves];
-    __shared__ uint32_t s_box[4];
     const int g0 = blockIdx.x * chunk, g1 = min(P, g0 + chunk);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     GSR_STAMP(g_st_scatter, blockIdx.x, 0);
@@ -447,50 +435,9 @@ __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
     // here (loads issued first, they land while the cursors load) instead of scanned in K2
     u64 before = 0;
     for (uint32_t c = threadIdx.x; c < blockIdx.x; c += blockDim.x) before += chunk_total[c];
-    // the chunk's positions [q0, q1) of the spatial order (K0), and their tile bounding box
-    const int V = (int)n_visible[0];
-    const int q0 = blockIdx.x * chunk, q1 = min(V, q0 + chunk);
-    uint32_t wx0 = 0, wy0 = 0, ww = 0, wh = 0;
-    bool win = false;  // uniform: the cursors fit the LDS window
-    if (LDS) {
-        if (threadIdx.x < 4) s_box[threadIdx.x] = threadIdx.x < 2 ? 0xffffu : 0u;
-        __syncthreads();
-        uint32_t x0 = 0xffffu, y0 = 0xffffu, x1 = 0u, y1 = 0u;
-        for (int p = q0 + (int)threadIdx.x; p < q1; p += kBinThreads) {
-            const uint4 o = order[p];
-            if (rect_tiles(make_uint2(o.y, o.z))) {
-                x0 = min(x0, o.y & 0xffffu);
-                y0 = min(y0, o.y >> 16);
-                x1 = max(x1, o.z & 0xffffu);
-                y1 = max(y1, o.z >> 16);
-            }
-        }
-        if (x1 > 0u) {
-            atomicMin(&s_box[0], x0);
-            atomicMin(&s_box[1], y0);
-            atomicMax(&s_box[2], x1);
-            atomicMax(&s_box[3], y1);
-        }
-        __syncthreads();
-        wx0 = s_box[0];
-        wy0 = s_box[1];
-        ww = s_box[2] > wx0 ? s_box[2] - wx0 : 0u;
-        wh = s_box[3] > wy0 ? s_box[3] - wy0 : 0u;
-        win = (u64)ww * wh <= (u64)win_cap;
-    }
-    uint32_t* const off_w = chunk_off + (size_t)blockIdx.x * tiles;  // this chunk's row (the fallback's cursors)
-    // the cursor of tile t (column tx, row ty) starts at c0: into the window, or the chunk's row
-    const auto set_cursor = [&](uint32_t t, uint32_t c0) {
-        if (win) {
-            const uint32_t tx = t % gx - wx0, ty = t / gx - wy0;  // (wrap to large values outside the box)
-            if (tx < ww && ty < wh) s_cur[ty * ww + tx] = c0;
-        } else {
-            off_w[t] = c0;
-        }
-    };
     if (LDS && fs.cnt) {
         // the tile starts (K2's scan, redone by every workgroup), then this chunk's cursors
-        const uint32_t* off = off_w;  // (read before the fallback overwrites: each entry by its own thread)
+        const uint32_t* off = chunk_off + (size_t)blockIdx.x * tiles;
         u64 carry_t = 0;
         for (uint32_t base = 0; base < tiles; base += kBinThreads * kScanV) {
             const uint32_t b = base + threadIdx.x * kScanV;
@@ -507,7 +454,7 @@ __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
 #pragma unroll
             for (int i = 0; i < kScanV; i++) {
                 if (b + i < tiles) {
-                    set_cursor(b + i, (uint32_t)at + off[b + i]);  // garbage where the chunk has no instance: unused
+                    s_cur[b + i] = (uint32_t)at + off[b + i];  // garbage where the chunk has no instance: unused
                     if (publish) {
                         const u64 lo = at < cap ? at : cap, hi = at + v[i] < cap ? at + v[i] : cap;
                         fs.ranges[b + i] = make_uint2((uint32_t)lo, (uint32_t)hi);
@@ -553,9 +500,9 @@ __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
     } else if (LDS) {
         // this chunk's cursors: tile start + the chunk's offset inside the tile (K1); entries of
         // tiles the chunk does not touch are garbage and never used
-        for (uint32_t i = threadIdx.x; i < tiles; i += blockDim.x) set_cursor(i, tile_base[i] + off_w[i]);
+        const uint32_t* off = chunk_off + (size_t)blockIdx.x * tiles;
+        for (uint32_t i = threadIdx.x; i < tiles; i += blockDim.x) s_cur[i] = tile_base[i] + off[i];
     }
-    if (LDS && !win) __threadfence();  // the row's cursors are in L2 before any thread's atomics
     // first record index of every Gaussian: chunk base + in-order scan of tiles_touched
     u64 carry = block_sum(before, s_tmp);
     for (int gb = g0; gb < g1; gb += kBinThreads) {
@@ -572,18 +519,18 @@ __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
     if (LDS) __syncthreads();
     GSR_STAMP(g_st_scatter, blockIdx.x, 1);
     // the keys: chunk positions [q0, q1) of the spatial order (K0), as K1 counted them
+    const int V = (int)n_visible[0];
+    const int q0 = blockIdx.x * chunk, q1 = min(V, q0 + chunk);
     for (int pb = q0 + wave * 64; pb < q1; pb += kBinThreads) {
         const int p = pb + lane;
         const uint4 o = p < q1 ? order[p] : make_uint4(0u, 0u, 0u, 0u);
         const uint32_t g = o.x, dk = o.w;
         const uint2 r = make_uint2(o.y, o.z);
         const uint32_t n = rect_tiles(r);
-        for_each_instance(n, r, gx, [&](bool valid, int owner, uint32_t t, uint32_t tx, uint32_t ty) {
+        for_each_instance(n, r, gx, [&](bool valid, int owner, uint32_t t, uint32_t, uint32_t) {
             const uint32_t kh = __shfl(dk, owner), kg = __shfl(g, owner);
             if (!valid) return;
-            const uint32_t pos = !LDS ? atomicAdd(&tile_base[t], 1u)
-                                 : win ? atomicAdd(&s_cur[__umul24(ty - wy0, ww) + (tx - wx0)], 1u)
-                                       : atomicAdd(&off_w[t], 1u);
+            const uint32_t pos = LDS ? atomicAdd(&s_cur[t], 1u) : atomicAdd(&tile_base[t], 1u);
             if (pos < cap) keys[pos] = ((u64)kh << 32) | (kg << kEntryMaskBits);  // cap: redone if exceeded
         });
     }
@@ -1167,19 +1114,18 @@ hipError_t launch_bin_scatter(int P, const GeomState& g, uint32_t gx, uint32_t g
     const int nchunks = bin_chunks(P, &chunk);
     const bool lds = tiles <= kLdsTilesMax;
     const dim3 grid(nchunks), block(kBinThreads);
-    const uint32_t win_cap = tiles < kScatterWinMax ? tiles : kScatterWinMax;
-    const size_t cur_bytes = lds ? win_cap * sizeof(uint32_t) : 0;
+    const size_t cur_bytes = lds ? tiles * sizeof(uint32_t) : 0;
     if (fused && !lds) return hipErrorInvalidValue;
     const FusedScan fs = fused ? FusedScan{g.tile_cnt, ranges, g.total, (u64*)host_total, g.cls_list, g.cls_count}
                                : FusedScan{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     if (lds)
         hipLaunchKernelGGL(tile_scatter_kernel<true>, grid, block, cur_bytes, stream, P, chunk, g.rect,
                            g.tiles_touched, g.depth_key, g.order, g.n_visible, tiles, gx, g.tile_base, g.chunk_off,
-                           g.chunk_total, b.keys, (u64)cap, g.rec_start, g.rec, fs, win_cap);
+                           g.chunk_total, b.keys, (u64)cap, g.rec_start, g.rec, fs);
     else
         hipLaunchKernelGGL(tile_scatter_kernel<false>, grid, block, 0, stream, P, chunk, g.rect, g.tiles_touched,
                            g.depth_key, g.order, g.n_visible, tiles, gx, g.tile_base, g.chunk_off, g.chunk_total,
-                           b.keys, (u64)cap, g.rec_start, g.rec, fs, 0u);
+                           b.keys, (u64)cap, g.rec_start, g.rec, fs);
     return hipGetLastError();
 }
 

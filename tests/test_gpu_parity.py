@@ -409,12 +409,10 @@ def test_sort_prefix_and_redo(name, prefix):
 
 
 @pytest.mark.parametrize("P", [3000, 40000])
-def test_scatter_window_fallback_large_image(P):
-    """K3's cursors (binning.hip): an LDS window over the chunk's tile bounding box when it holds at
-    most 16384 tiles, global per-(chunk, tile) cursors otherwise.  A 2304x2048 frame has 18432
-    tiles: with 3000 Gaussians every chunk spans most of the screen (the global cursors), with
-    40000 the chunks are compact screen regions (the LDS windows).  Lists, image and gradients
-    against the oracle as for the small cases."""
+def test_large_image(P):
+    """A 2304x2048 frame (18432 tiles: K3's LDS cursors hold 74 KiB), sparse (3000 Gaussians, every
+    binning chunk spanning most of the screen) and denser (40000): lists identical, the image by the
+    full-size threshold-flip rule, L1-gradient parity 1e-5."""
     case = C.Case("large_image", P=P, W=2304, H=2048, focal=1400.0, scale_range=(0.01, 0.08))
     inp = C.build(case)
     ref = C.run_oracle(inp, nthreads=8)
