@@ -193,7 +193,7 @@ class HostClock:
         if self.on:
             self.t[k].append(dt * 1e3)
 
-    def summary(self, wait):
+    def summary(self, lib):
         import statistics
 
         out = {}
@@ -201,8 +201,11 @@ class HostClock:
             if v:
                 out[k + "_ms"] = {"mean": round(statistics.fmean(v), 4), "median": round(statistics.median(v), 4),
                                   "max": round(max(v), 4)}
-        out["count_wait_ms"] = {"mean": round(wait["total_ms"] / wait["calls"], 4) if wait["calls"] else None,
-                                "max": round(wait["max_ms"], 4), "calls": wait["calls"]}
+        # inside the library (include/gsr.h gsr_host_stats): the count wait, and the whole forward /
+        # backward calls -- the Python side of a call is its call time minus these
+        for k, st in lib.items():
+            out[f"lib_{k}_ms"] = {"mean": round(st["total_ms"] / st["calls"], 4) if st["calls"] else None,
+                                  "max": round(st["max_ms"], 4), "calls": st["calls"]}
         out["python_gc_collections"] = self.gc_runs
         return out
 
@@ -358,7 +361,7 @@ def main():
         if phase == "start" and clock.on:
             clock.gc_runs += 1
     _gc.callbacks.append(_gc_cb)
-    _lib.host_wait_stats(reset=True)
+    _lib.host_stats(reset=True)
     clock.on = True
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -376,7 +379,7 @@ def main():
     elapsed = time.perf_counter() - t0
     clock.on = False
     _gc.callbacks.remove(_gc_cb)
-    host = clock.summary(_lib.host_wait_stats())
+    host = clock.summary(_lib.host_stats())
     _lib.profile_enable(False)
     dom_total, dom_calls = _lib.profile_collect()[dom]
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)

@@ -89,8 +89,7 @@ SIGNATURES = {
     "gsr_forward_rebuilds": (ctypes.c_longlong, []),
     "gsr_debug_sort_state": (_i, [_i, _i, _i, _vp, _vp, _vp, _vp]),
     "gsr_option_set": (_i, [ctypes.c_char_p, _i]),
-    "gsr_host_wait_stats": (_i, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
-                                 ctypes.POINTER(ctypes.c_longlong), _i]),
+    "gsr_host_stats": (_i, [ctypes.POINTER(ctypes.c_double), _i, _i]),
     "gsr_option_get": (_i, [ctypes.c_char_p]),
     "gsr_last_error": (ctypes.c_char_p, []),
     "gsr_version": (ctypes.c_char_p, []),
@@ -209,11 +208,13 @@ class options:
         return False
 
 
-def host_wait_stats(reset: bool = False) -> dict:
-    """Host time the forwards spent waiting for their instance count (include/gsr.h)."""
-    tot, mx, n = ctypes.c_double(0), ctypes.c_double(0), ctypes.c_longlong(0)
-    load().gsr_host_wait_stats(ctypes.byref(tot), ctypes.byref(mx), ctypes.byref(n), int(bool(reset)))
-    return {"total_ms": tot.value, "max_ms": mx.value, "calls": int(n.value)}
+def host_stats(reset: bool = False) -> dict:
+    """Host-side statistics of the library (include/gsr.h gsr_host_stats): for the forwards' count
+    waits, whole forward calls and whole backward calls, {calls, total_ms, max_ms}."""
+    v = (ctypes.c_double * 9)()
+    load().gsr_host_stats(v, 9, int(bool(reset)))
+    return {k: {"calls": int(v[3 * i]), "total_ms": v[3 * i + 1], "max_ms": v[3 * i + 2]}
+            for i, k in enumerate(("count_wait", "forward", "backward"))}
 
 
 # ---- stage profiler ---------------------------------------------------------------

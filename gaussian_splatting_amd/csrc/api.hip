@@ -388,8 +388,32 @@ int total_readback(TotalReadback** out) {
 
 // Forwards whose capacity hint was too small (the binning stage was redone), for gsr_forward_rebuilds().
 std::atomic<long long> g_rebuilds{0};
-// Host time spent waiting for the forward's instance count (gsr_host_wait_stats).
-std::atomic<long long> g_wait_ns{0}, g_wait_calls{0}, g_wait_max_ns{0};
+// Host-side statistics (gsr_host_stats): time the forwards waited for their instance count, and
+// the host time of whole forward / backward calls.
+struct HostStat {
+    std::atomic<long long> ns{0}, calls{0}, max_ns{0};
+    void add(long long v) {
+        ns.fetch_add(v, std::memory_order_relaxed);
+        calls.fetch_add(1, std::memory_order_relaxed);
+        long long prev = max_ns.load(std::memory_order_relaxed);
+        while (v > prev && !max_ns.compare_exchange_weak(prev, v, std::memory_order_relaxed)) {}
+    }
+    void reset() {
+        ns.store(0, std::memory_order_relaxed);
+        calls.store(0, std::memory_order_relaxed);
+        max_ns.store(0, std::memory_order_relaxed);
+    }
+};
+HostStat g_wait, g_fwd_host, g_bwd_host;
+struct HostTimer {  // adds the scope's host time to a HostStat
+    HostStat& st;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    explicit HostTimer(HostStat& s) : st(s) {}
+    ~HostTimer() {
+        st.add((long long)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0)
+                   .count());
+    }
+};
 
 void* call_alloc(gsr_alloc_fn fn, void* ctx, size_t bytes) {
     if (!fn) return nullptr;
@@ -406,15 +430,17 @@ const char* gsr_version(void) { return "gsr 0.2.0 gfx950"; }
 
 long long gsr_forward_rebuilds(void) { return g_rebuilds.load(std::memory_order_relaxed); }
 
-int gsr_host_wait_stats(double* total_ms, double* max_ms, long long* calls, int reset) {
-    if (total_ms) *total_ms = (double)g_wait_ns.load(std::memory_order_relaxed) * 1e-6;
-    if (max_ms) *max_ms = (double)g_wait_max_ns.load(std::memory_order_relaxed) * 1e-6;
-    if (calls) *calls = g_wait_calls.load(std::memory_order_relaxed);
-    if (reset) {
-        g_wait_ns.store(0, std::memory_order_relaxed);
-        g_wait_max_ns.store(0, std::memory_order_relaxed);
-        g_wait_calls.store(0, std::memory_order_relaxed);
-    }
+int gsr_host_stats(double* values, int n, int reset) {
+    const HostStat* st[3] = {&g_wait, &g_fwd_host, &g_bwd_host};
+    for (int k = 0; k < 3; k++)
+        for (int j = 0; j < 3; j++) {
+            const int i = 3 * k + j;
+            if (!values || i >= n) continue;
+            values[i] = j == 0 ? (double)st[k]->calls.load(std::memory_order_relaxed)
+                               : (double)(j == 1 ? st[k]->ns : st[k]->max_ns).load(std::memory_order_relaxed) * 1e-6;
+        }
+    if (reset)
+        for (auto* p : {&g_wait, &g_fwd_host, &g_bwd_host}) p->reset();
     return GSR_OK;
 }
 
@@ -734,6 +760,7 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
                  int antialiasing, int* radii, int debug, void* stream_, int* num_rendered, int capacity_hint,
                  int* binning_capacity, bool quantized = true) {
     using namespace gsr;
+    HostTimer host_time(g_fwd_host);
     g_err[0] = 0;
     hipStream_t stream = (hipStream_t)stream_;
     // _ex / _dc forwards lay the binning buffer out for a multiple of kCapQuantum (the backward
@@ -839,14 +866,11 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
         return GSR_OK;
     };
     auto wait_total = [&](unsigned long long* total) -> int {
-        const auto t0 = std::chrono::steady_clock::now();
-        const hipError_t we = hipEventSynchronize(rb->ev);
-        const long long ns =
-            (long long)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
-        g_wait_ns.fetch_add(ns, std::memory_order_relaxed);
-        g_wait_calls.fetch_add(1, std::memory_order_relaxed);
-        long long prev = g_wait_max_ns.load(std::memory_order_relaxed);
-        while (ns > prev && !g_wait_max_ns.compare_exchange_weak(prev, ns, std::memory_order_relaxed)) {}
+        hipError_t we;
+        {
+            HostTimer ht(g_wait);
+            we = hipEventSynchronize(rb->ev);
+        }
         HIP_TRY(we, "num_rendered sync");
         *total = *rb->host;
         if (*total > (unsigned long long)INT_MAX)
@@ -1008,6 +1032,7 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
                   void* scratch_ctx, void* stream_, int binning_capacity, size_t binning_bytes,
                   float* view_block = nullptr) {
     using namespace gsr;
+    HostTimer host_time(g_bwd_host);
     g_err[0] = 0;
     hipStream_t stream = (hipStream_t)stream_;
     // view_block: screen-space backward only -- the render-gradient sums, flags and camera go

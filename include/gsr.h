@@ -277,10 +277,12 @@ int gsr_debug_sort_state(int P, int width, int height, const void* geom_buffer, 
  * was redone with the exact count (gsr_rasterize_forward_ex). */
 long long gsr_forward_rebuilds(void);
 
-/* Host time the forwards spent waiting for their instance count (the one host synchronisation
- * of a forward, CR/rasterizer_impl.cu:313; here an event behind the binning count): total and
- * largest single wait in ms and the number of waits since the last reset (reset != 0 clears). */
-int gsr_host_wait_stats(double* total_ms, double* max_ms, long long* calls, int reset);
+/* Host-side statistics since the last reset (reset != 0 clears after reading), for finding time
+ * the GPU spends waiting on the host.  values[0..8] = for (a) the forwards' waits for their
+ * instance count (the one host synchronisation of a forward, CR/rasterizer_impl.cu:313; here an
+ * event behind the binning count), (b) whole forward calls, (c) whole backward calls: the number of
+ * calls, their total host time in ms and the longest one in ms.  Up to n values are written. */
+int gsr_host_stats(double* values, int n, int reset);
 
 /* Runtime options (no reference counterpart): the library's alternative kernel paths, readable
  * and settable in-process so that every path it ships is parity-tested (tests/test_gpu_options.py).
