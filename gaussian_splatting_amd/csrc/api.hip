@@ -175,7 +175,6 @@ gsr::ImageState carve_image(char* base, int W, int H, uint32_t tiles, size_t* to
     im.n_contrib = c.take<uint32_t>(NT);
     im.accum = c.take<float>(4 * NT);
     im.ranges = c.take<uint2>(tiles);
-    im.lim_key = c.take<unsigned long long>(tiles);
     *total = align_up(c.off);
     return im;
 }
@@ -248,7 +247,7 @@ void carve_recs(char* base, size_t R, size_t P, gsr::GradRecs* recs, gsr::GradRe
         recs->b = c.take<float4>(R);
         recs->c = c.take<float2>(R);
     }
-    recs->flag = GSR_REC_FLAG ? c.take<uint8_t>(R) : nullptr;
+    recs->flag = c.take<uint8_t>(R);
     sums->a = c.take<float4>(P);
     sums->b = c.take<float4>(P);
     sums->c = c.take<float2>(P);
@@ -1158,13 +1157,16 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
         sj.armed = true;
     }
 
+    // the records' content bytes: render_bwd sets those of the records it writes, gauss_reduce
+    // reads them to find the records (R bytes: 8 MB at 1M@1080p)
+    if (R > 0) HIP_TRY(hipMemsetAsync(recs.flag, 0, (size_t)R, stream), "record flags");
     if (R > 0) {
         StageScope sc(ST_RENDER_BWD, stream);
         RenderBwdArgs ra{};
         ra.W = width; ra.H = height; ra.gx = gx; ra.gy = gy; ra.ranges = img.ranges; ra.gid_sorted = bin.gid_sorted;
         ra.rec = geom.rec;
         ra.bg = background; ra.dL_dpix = dL_dpix; ra.dL_dinvdepth = dL_dinvdepths; ra.img = img; ra.recs = recs;
-        ra.ckpt = bin.ckpt; ra.depth_key = geom.depth_key; ra.seg_ck = seg_ck;
+        ra.ckpt = bin.ckpt; ra.seg_ck = seg_ck;
         ra.unit_cnt = geom.unit_cnt; ra.unit_part = geom.unit_part; ra.unit_full = bin.unit_full;
         ra.full_cap = (uint32_t)unit_full_cap(C);
         ra.census = g_census;
@@ -1174,7 +1176,7 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
     if (int rc = check_debug(debug, stream, "render_bwd")) return rc;
     {
         StageScope sc(ST_GAUSS_REDUCE, stream);
-        HIP_TRY(launch_gauss_reduce(P, geom, gx, img.lim_key, recs, sums, flags, radii, live, live_count, stream),
+        HIP_TRY(launch_gauss_reduce(P, geom, recs, sums, flags, radii, live, live_count, stream),
                 "gauss_reduce");
     }
     if (int rc = check_debug(debug, stream, "gauss_reduce")) return rc;

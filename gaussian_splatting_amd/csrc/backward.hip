@@ -37,21 +37,17 @@ namespace gsr {
 // [E0, E1) (record index = rec_start[g] + k, k = the tile's row-major index in g's
 // rectangle); it is read 64 records at a time with fully coalesced loads (one record
 // per lane) and each Gaussian's run is summed by a segmented scan over the wave, in a
-// fixed order, so the result does not depend on scheduling.  The render backward writes records only
-// for entries before each tile's last contributor; instance (g, tile t) has one iff
-// key(g) = depth bits << 32 | g <= lim_key[t] (tile lists are sorted by key), and
-// the others are read as zeros without touching memory (render.hip, "Entries at
-// positions >= limit").  Of those, only entries with a gradient term have a record with
-// content; the rest wrote a zero content byte (GSR_REC_FLAG) and are skipped too.
+// fixed order, so the result does not depend on scheduling.  A record exists iff its content
+// byte is set (render.hip writes records only for entries with a gradient term; the bytes are
+// zeroed before it, api.hip): a chunk of 64 instances none of which has a record -- most of them
+// behind saturated pixels, 5M@4K: 93% of the instances -- costs one coalesced 64-byte load and a
+// ballot; only a chunk holding records works out its owners and runs the scan.
 constexpr int kRecStride = 12;  // floats per Gaussian in the LDS hand-off of chunk totals (10 used), 48 B
 
 // Sums of the records of the wave's 64 consecutive Gaussians [g0, g0 + 64), one
 // Gaussian per lane (zeros for lanes past P).  s_rec: 64 * kRecStride floats of LDS.
 __device__ __forceinline__ void reduce_records(int P, int g0, const uint32_t* __restrict__ rec_start,
-                                               const uint32_t* __restrict__ tiles_touched,
-                                               const uint2* __restrict__ rect,
-                                               const uint32_t* __restrict__ depth_key, uint32_t gx,
-                                               const unsigned long long* __restrict__ lim_key, const GradRecs& recs,
+                                               const uint32_t* __restrict__ tiles_touched, const GradRecs& recs,
                                                float* s_rec, float4& sa, float4& sb, float2& sc) {
     const int lane = threadIdx.x;
     const int g = g0 + lane;
@@ -62,37 +58,32 @@ __device__ __forceinline__ void reduce_records(int P, int g0, const uint32_t* __
     const uint32_t n = valid ? tiles_touched[g] : 0u;
     const uint32_t my0 = valid ? rec_start[g] : E1;
     const uint32_t my1 = my0 + n;
-    uint32_t x0 = 0, y0 = 0, w = 1;
-    unsigned long long key = ~0ull;
-    if (n) {
-        const uint2 rr = rect[g];
-        x0 = rr.x & 0xffffu;
-        y0 = rr.x >> 16;
-        w = (rr.y & 0xffffu) - x0;
-        key = ((unsigned long long)depth_key[g] << 32) | (uint32_t)g;
-    }
     sa = make_float4(0.f, 0.f, 0.f, 0.f);
     sb = sa;
     sc = make_float2(0.f, 0.f);
-    // Whether slot e of a chunk has a record needs the tile's limit key: a dependent load.
     // Wave-parallel segmented sums: the chunk's 64 records stay in registers (one per lane);
     // a segmented inclusive scan over the wave (DPP row shifts and row broadcasts, the add
     // masked where the source lane belongs to another Gaussian) leaves each Gaussian's chunk
     // total in the last lane of its run, which hands it to the owner lane through LDS.  The
-    // cost no longer depends on the longest run in the chunk (a Gaussian touching hundreds
-    // of tiles made 63 lanes wait).  Chunk c + 1's records and limit keys load while chunk
-    // c is reduced.
+    // cost does not depend on the longest run in the chunk.  Chunk c + 1's content bytes and
+    // records load while chunk c is reduced.
     struct Slot {
         bool has;
         int owner, seg0;
     };
     // The owner of record e: the largest lane whose range starts at or before e.  Called for
     // consecutive chunks in order: lanes whose ranges start in the chunk mark the start (lane + 1)
-    // in LDS, a DPP max-scan spreads the marks, the previous chunk's last owner fills the rest
-    // (no dependent ds_bpermute chain; one wave's LDS accesses execute in order).
+    // in LDS, a DPP max-scan spreads the marks, the previous chunks' last owner fills the rest
+    // (no dependent ds_bpermute chain; one wave's LDS accesses execute in order).  A chunk
+    // without records only advances that carry: the last lane starting in it, by one ballot.
     __shared__ uint32_t s_mark[64];
     uint32_t carry = 0;
-    auto probe2 = [&](uint32_t base) -> Slot {
+    auto probe = [&](uint32_t base, bool has) -> Slot {
+        if (!__any(has)) {  // uniform
+            const unsigned long long st = __ballot(n && my0 < base + 64);
+            if (st) carry = 64u - (uint32_t)__clzll((long long)st);  // (lane + 1) of the last start
+            return Slot{false, -1, lane};
+        }
         const uint32_t e = base + lane;
         s_mark[lane] = 0u;
         __builtin_amdgcn_wave_barrier();
@@ -102,25 +93,13 @@ __device__ __forceinline__ void reduce_records(int P, int g0, const uint32_t* __
         __builtin_amdgcn_wave_barrier();
         carry = (uint32_t)__builtin_amdgcn_readlane((int)m, 63);
         const int owner = m ? (int)m - 1 : 0;
-        const uint32_t o0 = __shfl(my0, owner), ow = __shfl(w, owner), ox = __shfl(x0, owner),
-                       oy = __shfl(y0, owner);
-        const unsigned long long okey = __shfl(key, owner);
+        const uint32_t o0 = __shfl(my0, owner);
         if (e >= E1) return Slot{false, -1, lane};
-        const int seg0 = o0 > base ? (int)(o0 - base) : 0;
-        // k / ow by a float reciprocal (k < 2^24, ow <= 2^16: the estimate is off by at most one,
-        // fixed by one compare each way) instead of the integer-division sequence
-        const uint32_t k = e - o0;
-        uint32_t ty = (uint32_t)((float)k * __builtin_amdgcn_rcpf((float)ow));
-        ty = ty * ow > k ? ty - 1 : ty;
-        ty = (ty + 1) * ow <= k ? ty + 1 : ty;
-        const uint32_t tile = (oy + ty) * gx + ox + (k - ty * ow);
-        // GSR_REC_FLAG: a staged entry without a gradient term wrote its content byte only (the
-        // byte load does not wait for the limit key's)
-        const bool content = !GSR_REC_FLAG || recs.flag[e] != 0;
-        return Slot{okey <= lim_key[tile] && content, owner, seg0};
+        return Slot{has, owner, o0 > base ? (int)(o0 - base) : 0};
     };
+    const auto has_at = [&](uint32_t base) { return base + lane < E1 && recs.flag[base + lane] != 0; };
     float4* part = reinterpret_cast<float4*>(s_rec);  // [64][3] float4: a Gaussian's chunk total
-    Slot cur = E0 < E1 ? probe2(E0) : Slot{false, -1, lane};
+    Slot cur = E0 < E1 ? probe(E0, has_at(E0)) : Slot{false, -1, lane};
     float4 x = make_float4(0.f, 0.f, 0.f, 0.f), y = x;
     float2 z = make_float2(0.f, 0.f);
     if (cur.has) {
@@ -129,7 +108,7 @@ __device__ __forceinline__ void reduce_records(int P, int g0, const uint32_t* __
         z = GSR_LD_REC(recs.c + (size_t)kRecC * (E0 + lane));
     }
     for (uint32_t base = E0; base < E1; base += 64) {
-        const Slot nxt = base + 64 < E1 ? probe2(base + 64) : Slot{false, -1, lane};
+        const Slot nxt = base + 64 < E1 ? probe(base + 64, has_at(base + 64)) : Slot{false, -1, lane};
         float4 nx = make_float4(0.f, 0.f, 0.f, 0.f), ny = nx;
         float2 nz = make_float2(0.f, 0.f);
         if (nxt.has) {
@@ -137,8 +116,7 @@ __device__ __forceinline__ void reduce_records(int P, int g0, const uint32_t* __
             ny = GSR_LD_REC(recs.b + (size_t)kRecAB * (base + 64 + lane));
             nz = GSR_LD_REC(recs.c + (size_t)kRecC * (base + 64 + lane));
         }
-        // A chunk with no record adds nothing: skip its scan (uniform).  Behind saturated pixels
-        // most instances have no record (5M@4K: 7.6M of 114.6M), so this is most chunks there.
+        // A chunk with no record adds nothing: skip its scan (uniform).
         if (__any(cur.has)) {
         // segmented inclusive scan, one DPP step per distance (gsr_common.h wave_sum_to_lane63)
         const int r = lane & 15, row = lane >> 4;
@@ -182,9 +160,6 @@ __device__ __forceinline__ void reduce_records(int P, int g0, const uint32_t* __
 
 __global__ void __launch_bounds__(64) gauss_reduce_kernel(int P, const uint32_t* __restrict__ rec_start,
                                                           const uint32_t* __restrict__ tiles_touched,
-                                                          const uint2* __restrict__ rect,
-                                                          const uint32_t* __restrict__ depth_key, uint32_t gx,
-                                                          const unsigned long long* __restrict__ lim_key,
                                                           GradRecs recs, GradRecs sums, uint32_t* __restrict__ flags,
                                                           const int* __restrict__ radii,
                                                           const uint8_t* __restrict__ clamped,
@@ -194,8 +169,7 @@ __global__ void __launch_bounds__(64) gauss_reduce_kernel(int P, const uint32_t*
     const int g = blockIdx.x * 64 + (int)threadIdx.x;
     float4 sa, sb;
     float2 sc;
-    reduce_records(P, blockIdx.x * 64, rec_start, tiles_touched, rect, depth_key, gx, lim_key, recs, s_rec, sa, sb,
-                   sc);
+    reduce_records(P, blockIdx.x * 64, rec_start, tiles_touched, recs, s_rec, sa, sb, sc);
     if (g < P) {
         sums.a[g] = sa;
         sums.b[g] = sb;
@@ -221,13 +195,12 @@ __global__ void __launch_bounds__(64) gauss_reduce_kernel(int P, const uint32_t*
     }
 }
 
-hipError_t launch_gauss_reduce(int P, const GeomState& g, uint32_t gx, const unsigned long long* lim_key,
-                               const GradRecs& recs, const GradRecs& sums, uint32_t* flags, const int* radii,
-                               uint32_t* live, uint32_t* live_count, hipStream_t stream) {
+hipError_t launch_gauss_reduce(int P, const GeomState& g, const GradRecs& recs, const GradRecs& sums,
+                               uint32_t* flags, const int* radii, uint32_t* live, uint32_t* live_count,
+                               hipStream_t stream) {
     if (P == 0) return hipSuccess;
     hipLaunchKernelGGL(gauss_reduce_kernel, dim3((P + 63) / 64), dim3(64), 0, stream, P, g.rec_start, g.tiles_touched,
-                       g.rect, g.depth_key, gx, lim_key, recs, sums, flags, radii, g.clamped, live, live_count,
-                       live_list_cap((uint32_t)P));
+                       recs, sums, flags, radii, g.clamped, live, live_count, live_list_cap((uint32_t)P));
     return hipGetLastError();
 }
 

@@ -118,8 +118,6 @@ struct ImageState {
     uint32_t* n_contrib;  // [tiles * 256]
     float* accum;         // [4][tiles * 256]: colour r,g,b and inverse depth, without background
     uint2* ranges;        // [tiles]
-    unsigned long long* lim_key;  // [tiles] key (depth bits << 32 | index) of the entry at limit - 1, 0 if
-                                  // none: entries past it have no gradient record (backward.hip)
 };
 
 // Binning state: per instance (R, or the capacity the buffer was requested for).
@@ -189,15 +187,13 @@ struct GradRecs {
     float4* a;  // (dcolor.r, dcolor.g, dcolor.b, dinvdepth)
     float4* b;  // (dmean2D.x, dmean2D.y, dopacity_eff, dconic.b)
     float2* c;  // (dconic.a, dconic.c)
-    uint8_t* flag;  // per-instance records only (GSR_REC_FLAG): 1 = the record has content
+    uint8_t* flag;  // per-instance records only: 1 = the record exists (zeroed before render_bwd)
 };
-// A/B switch: the render backward writes a record only for an entry with a gradient term (~half
-// of the staged entries at 1M@1080p) and one content byte for every staged entry; the reduction
-// reads the byte and skips the record of an entry without content, instead of every staged
-// entry's 48-byte record, zeros included.
-#ifndef GSR_REC_FLAG
+// The render backward writes a record and its content byte only for an entry with a gradient term
+// (~half of the staged entries at 1M@1080p, 7.6M of 114.7M instances at 5M@4K); the content bytes
+// are zeroed before it, so gauss_reduce finds the records from the bytes alone (a coalesced 64-byte
+// load per 64 instances) and skips the rest.
 #define GSR_REC_FLAG 1
-#endif
 
 // The live list (backward scratch): the Gaussians with a gradient, appended by gauss_reduce for
 // the sparse gauss_bwd.  Sharded by reduction workgroup (one counter per 128-byte line): a single

@@ -67,7 +67,6 @@ struct RenderBwdArgs {
     ImageState img;
     GradRecs recs;
     const float* ckpt;                  // blend checkpoints written by the forward
-    const uint32_t* depth_key;          // per Gaussian (for the tile's lim_key)
     // work list: (tile, first checkpoint index) of each wave, written by the forward render
     const uint32_t* unit_cnt;
     const uint2* unit_part;
@@ -418,9 +417,9 @@ hipError_t launch_ssim_bwd(int planes, int H, int W, const float* img1, const fl
                            const float* dm_dmu1, const float* dm_ds11, const float* dm_ds12, float* dL_dimg1,
                            hipStream_t stream);
 // backward.hip
-hipError_t launch_gauss_reduce(int P, const GeomState& g, uint32_t gx, const unsigned long long* lim_key,
-                               const GradRecs& recs, const GradRecs& sums, uint32_t* flags, const int* radii,
-                               uint32_t* live, uint32_t* live_count, hipStream_t stream);
+hipError_t launch_gauss_reduce(int P, const GeomState& g, const GradRecs& recs, const GradRecs& sums,
+                               uint32_t* flags, const int* radii, uint32_t* live, uint32_t* live_count,
+                               hipStream_t stream);
 // multi-view backward over gathered view blocks (backward.hip section 4)
 struct ViewsBwdArgs {
     int P, D, M;

@@ -303,7 +303,6 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const ui
         if ((old >> 62) == 0) return;  // the other part finishes the tile
         lm = max(lm, (uint32_t)((old >> (31 * (part ^ 1))) & 0x7fffffffull));
     }
-    if (lane == 0 && lm == 0) a.img.lim_key[tile] = 0ull;  // (otherwise the backward's first unit writes it)
     // The backward's work list: units (tile, k * seg_ck) for the full segments of S entries below
     // the limit, then the last partial segment into one of four lists by length quarter.
     // Lanes 0 and 1 append in parallel (separate counters, gsr_common.h "work list").
@@ -507,13 +506,6 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
     const bool hi8 = (lane & 8) != 0, acc_wr = li == 0 || li == 8 || li == 15, acc_h4 = li == 15;
     const int acc_off = li == 0 ? slot_k : li == 8 ? 4 + slot_k : 8 + row;
 
-    if (start == 0 && lane == 0) {
-        // the key of the entry at limit - 1 (tiles with limit 0 get 0 from bwd_units_kernel): entries
-        // past it get no gradient record, and the per-Gaussian reduction recognises them by key (tile
-        // lists are sorted by depth bits << 32 | index; a visible Gaussian's depth bits are never 0)
-        const uint32_t gl = a.gid_sorted[range.x + limit - 1] >> kEntryMaskBits;
-        a.img.lim_key[tile] = ((unsigned long long)a.depth_key[gl] << 32) | gl;
-    }
     const uint32_t ttx = tile % a.gx, tty = tile / a.gx;
     unsigned long long c_staged = 0, c_eval = 0, c_alpha = 0, c_red = 0, c_idle = 0;  // CENSUS only
     // The ten per-entry sums stay zero between entries (reset after each reduction), so an entry
@@ -623,8 +615,8 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
         }
         __syncthreads();
         const bool content = (written >> lane) & 1ull;
-        if (GSR_REC_FLAG && has && !(GSR_ATTR & 1)) a.recs.flag[e] = content ? 1 : 0;
-        if (has && (content || !GSR_REC_FLAG) && !(GSR_ATTR & 1)) {
+        if (has && content && !(GSR_ATTR & 1)) {
+            a.recs.flag[e] = 1;  // (the bytes were zeroed before this kernel: api.hip)
             float4 ra = make_float4(0.f, 0.f, 0.f, 0.f), rb = ra;
             float2 rc = make_float2(0.f, 0.f);
             if (content) {
