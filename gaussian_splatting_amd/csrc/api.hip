@@ -232,7 +232,7 @@ bool resolve_capacity(int R, int capacity, size_t bytes, size_t* C) {
     return binning_bytes_for((size_t)R) == bytes;
 }
 
-// Backward scratch: per-tile limit keys, R per-instance records, P per-Gaussian sums.
+// Backward scratch: R per-instance records and their content bytes, P per-Gaussian sums, the live list.
 void carve_recs(char* base, size_t R, size_t P, gsr::GradRecs* recs, gsr::GradRecs* sums, uint32_t** live,
                 uint32_t** live_count, size_t* total) {
     using namespace gsr;
@@ -247,7 +247,7 @@ void carve_recs(char* base, size_t R, size_t P, gsr::GradRecs* recs, gsr::GradRe
         recs->b = c.take<float4>(R);
         recs->c = c.take<float2>(R);
     }
-    recs->flag = c.take<uint8_t>(R);
+    recs->flag = c.take<uint8_t>((R + 15) & ~(size_t)15);  // gauss_reduce reads it in aligned 16-byte words
     sums->a = c.take<float4>(P);
     sums->b = c.take<float4>(P);
     sums->c = c.take<float2>(P);

@@ -39,9 +39,9 @@ namespace gsr {
 // per lane) and each Gaussian's run is summed by a segmented scan over the wave, in a
 // fixed order, so the result does not depend on scheduling.  A record exists iff its content
 // byte is set (render.hip writes records only for entries with a gradient term; the bytes are
-// zeroed before it, api.hip): a chunk of 64 instances none of which has a record -- most of them
-// behind saturated pixels, 5M@4K: 93% of the instances -- costs one coalesced 64-byte load and a
-// ballot; only a chunk holding records works out its owners and runs the scan.
+// zeroed before it, api.hip): the range is scanned 1024 bytes per wave-wide load, and only the
+// 64-instance chunks that start at a record are loaded and reduced -- 5M@4K: 7.6M records of
+// 114.7M instances, the rest behind saturated pixels.
 constexpr int kRecStride = 12;  // floats per Gaussian in the LDS hand-off of chunk totals (10 used), 48 B
 
 // Sums of the records of the wave's 64 consecutive Gaussians [g0, g0 + 64), one
@@ -61,63 +61,51 @@ __device__ __forceinline__ void reduce_records(int P, int g0, const uint32_t* __
     sa = make_float4(0.f, 0.f, 0.f, 0.f);
     sb = sa;
     sc = make_float2(0.f, 0.f);
-    // Wave-parallel segmented sums: the chunk's 64 records stay in registers (one per lane);
+    // Wave-parallel segmented sums: a chunk's 64 records stay in registers (one per lane);
     // a segmented inclusive scan over the wave (DPP row shifts and row broadcasts, the add
     // masked where the source lane belongs to another Gaussian) leaves each Gaussian's chunk
     // total in the last lane of its run, which hands it to the owner lane through LDS.  The
-    // cost does not depend on the longest run in the chunk.  Chunk c + 1's content bytes and
-    // records load while chunk c is reduced.
+    // cost does not depend on the longest run in the chunk.
+    //
+    // Finding the records: the range is walked in windows of 1024 content bytes (one aligned
+    // 16-byte load per lane, a ballot); a window without records costs that load alone.  Inside
+    // a window each chunk starts AT the next record (found from the bytes already in registers),
+    // so runs of records fall into as few chunks as possible.
     struct Slot {
         bool has;
         int owner, seg0;
     };
-    // The owner of record e: the largest lane whose range starts at or before e.  Called for
-    // consecutive chunks in order: lanes whose ranges start in the chunk mark the start (lane + 1)
-    // in LDS, a DPP max-scan spreads the marks, the previous chunks' last owner fills the rest
-    // (no dependent ds_bpermute chain; one wave's LDS accesses execute in order).  A chunk
-    // without records only advances that carry: the last lane starting in it, by one ballot.
+    // The owner of record e in [base, base + 64): the largest lane whose (non-empty) range starts
+    // at or before e.  Lanes starting before the chunk: one ballot; lanes starting in it mark the
+    // start (lane + 1) in LDS and a DPP max-scan spreads the marks (one wave's LDS accesses
+    // execute in order, so no dependent ds_bpermute chain).
     __shared__ uint32_t s_mark[64];
-    uint32_t carry = 0;
-    auto probe = [&](uint32_t base, bool has) -> Slot {
-        if (!__any(has)) {  // uniform
-            const unsigned long long st = __ballot(n && my0 < base + 64);
-            if (st) carry = 64u - (uint32_t)__clzll((long long)st);  // (lane + 1) of the last start
-            return Slot{false, -1, lane};
-        }
+    auto chunk = [&](uint32_t base) -> Slot {
         const uint32_t e = base + lane;
+        const bool has = e < E1 && recs.flag[e] != 0;
+        const unsigned long long st = __ballot(n && my0 < base);
+        const uint32_t carry = st ? 64u - (uint32_t)__clzll((long long)st) : 0u;
         s_mark[lane] = 0u;
         __builtin_amdgcn_wave_barrier();
         if (n && my0 >= base && my0 < base + 64) s_mark[my0 - base] = (uint32_t)lane + 1u;
         __builtin_amdgcn_wave_barrier();
         const uint32_t m = max(wave_incl_max(s_mark[lane]), carry);
         __builtin_amdgcn_wave_barrier();
-        carry = (uint32_t)__builtin_amdgcn_readlane((int)m, 63);
         const int owner = m ? (int)m - 1 : 0;
         const uint32_t o0 = __shfl(my0, owner);
         if (e >= E1) return Slot{false, -1, lane};
         return Slot{has, owner, o0 > base ? (int)(o0 - base) : 0};
     };
-    const auto has_at = [&](uint32_t base) { return base + lane < E1 && recs.flag[base + lane] != 0; };
     float4* part = reinterpret_cast<float4*>(s_rec);  // [64][3] float4: a Gaussian's chunk total
-    Slot cur = E0 < E1 ? probe(E0, has_at(E0)) : Slot{false, -1, lane};
-    float4 x = make_float4(0.f, 0.f, 0.f, 0.f), y = x;
-    float2 z = make_float2(0.f, 0.f);
-    if (cur.has) {
-        x = GSR_LD_REC(recs.a + (size_t)kRecAB * (E0 + lane));
-        y = GSR_LD_REC(recs.b + (size_t)kRecAB * (E0 + lane));
-        z = GSR_LD_REC(recs.c + (size_t)kRecC * (E0 + lane));
-    }
-    for (uint32_t base = E0; base < E1; base += 64) {
-        const Slot nxt = base + 64 < E1 ? probe(base + 64, has_at(base + 64)) : Slot{false, -1, lane};
-        float4 nx = make_float4(0.f, 0.f, 0.f, 0.f), ny = nx;
-        float2 nz = make_float2(0.f, 0.f);
-        if (nxt.has) {
-            nx = GSR_LD_REC(recs.a + (size_t)kRecAB * (base + 64 + lane));
-            ny = GSR_LD_REC(recs.b + (size_t)kRecAB * (base + 64 + lane));
-            nz = GSR_LD_REC(recs.c + (size_t)kRecC * (base + 64 + lane));
+    auto reduce_chunk = [&](uint32_t base) {
+        const Slot cur = chunk(base);
+        float4 x = make_float4(0.f, 0.f, 0.f, 0.f), y = x;
+        float2 z = make_float2(0.f, 0.f);
+        if (cur.has) {
+            x = GSR_LD_REC(recs.a + (size_t)kRecAB * (base + lane));
+            y = GSR_LD_REC(recs.b + (size_t)kRecAB * (base + lane));
+            z = GSR_LD_REC(recs.c + (size_t)kRecC * (base + lane));
         }
-        // A chunk with no record adds nothing: skip its scan (uniform).
-        if (__any(cur.has)) {
         // segmented inclusive scan, one DPP step per distance (gsr_common.h wave_sum_to_lane63)
         const int r = lane & 15, row = lane >> 4;
         // the masks as 0/1 factors: v += shifted * m is one FMA (records are finite)
@@ -150,11 +138,41 @@ __device__ __forceinline__ void reduce_records(int P, int g0, const uint32_t* __
             sc.x += ww.x; sc.y += ww.y;
         }
         __syncthreads();
+    };
+    uint32_t base = E0;
+    while (base < E1) {  // uniform
+        // content bytes [wa, wa + 1024): lane l holds bytes wa + 16 l .. + 15 (the byte buffer is
+        // padded to a multiple of 16, api.hip carve_recs); bytes at or past E1 are another wave's
+        const uint32_t wa = base & ~15u, wend = wa + 1024u;
+        const uint32_t p = wa + 16u * (uint32_t)lane;
+        uint64_t lo = 0, hi = 0;
+        if (p < E1) {
+            const uint4 f = *reinterpret_cast<const uint4*>(recs.flag + p);
+            lo = (uint64_t)f.x | ((uint64_t)f.y << 32);
+            hi = (uint64_t)f.z | ((uint64_t)f.w << 32);
+            const uint32_t k = E1 - p;  // bytes of this lane below E1
+            if (k < 8) { lo &= (1ull << (8 * k)) - 1ull; hi = 0; }
+            else if (k < 16) hi &= (1ull << (8 * (k - 8))) - 1ull;  // k == 8 clears hi
         }
-        cur = nxt;
-        x = nx;
-        y = ny;
-        z = nz;
+        while (true) {
+            // drop the bytes below base (already reduced or before the range)
+            if (base > p) {
+                const uint32_t k = base - p;
+                if (k >= 16) { lo = 0; hi = 0; }
+                else if (k >= 8) { lo = 0; hi &= ~0ull << (8 * (k - 8)); }
+                else lo &= ~0ull << (8 * k);
+            }
+            const unsigned long long nz = __ballot((lo | hi) != 0ull);
+            if (!nz) {
+                base = wend;
+                break;
+            }
+            const uint32_t mine = p + (lo ? (uint32_t)__builtin_ctzll(lo) >> 3 : 8u + ((uint32_t)__builtin_ctzll(hi | (1ull << 63)) >> 3));
+            const uint32_t first = (uint32_t)__builtin_amdgcn_readlane((int)mine, __builtin_ctzll(nz));
+            reduce_chunk(first);
+            base = first + 64;
+            if (base >= wend) break;
+        }
     }
 }
 
