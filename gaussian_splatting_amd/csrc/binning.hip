@@ -7,8 +7,8 @@
 // list in (depth, index) order.  Here the same lists are built in four passes:
 //
 //   K1 tile_count    every workgroup owns a contiguous chunk of Gaussians and
-//                    counts its tile hits in an LDS histogram (two 16-bit
-//                    counters per word); the flush is one RETURNING atomic add
+//                    counts its tile hits in LDS (+1/-1 at each tile rectangle's
+//                    corners, then a 2-D prefix sum); the flush is one RETURNING atomic add
 //                    per (chunk, tile), whose result -- the chunk's offset inside
 //                    the tile's block -- is kept in chunk_off[chunk][tile];
 //   K2 tile_scan     one workgroup: exclusive scan of the tile counts (-> the
@@ -284,6 +284,68 @@ struct FusedZero {
     uint32_t* cls_count;
 };
 
+// K1 by rectangles (GSR_K1_RECT, the default with LDS counters): a chunk's per-tile counts are the
+// number of its Gaussians whose tile rectangle covers the tile, so each Gaussian adds +1 / -1 at its
+// rectangle's four corners of a 2-D difference array in LDS (one u32 per tile; a corner on the far
+// edge of the grid is dropped) and a 2-D inclusive prefix sum -- rows by DPP scans, one wave per row,
+// then columns in register blocks -- turns the differences into the counts.  Four LDS atomics per
+// Gaussian instead of one per instance (5M@4K: 20M instead of 114.7M) and no instance walk; the
+// counts are exactly the walk's, so everything downstream is unchanged.
+#ifndef GSR_K1_RECT
+#define GSR_K1_RECT 1
+#endif
+constexpr int kColBlock = 8;  // rows per register block of the column pass
+
+__device__ __forceinline__ void count_by_rectangles(int g0, int g1, const uint4* __restrict__ order, uint32_t tiles,
+                                                    uint32_t gx, uint32_t* s_d) {
+    const uint32_t gy = tiles / gx;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (uint32_t i = threadIdx.x; i < tiles; i += blockDim.x) s_d[i] = 0u;
+    __syncthreads();
+    for (int p = g0 + (int)threadIdx.x; p < g1; p += kBinThreads) {
+        uint32_t x0, y0, x1, y1;
+        const uint4 o = order[p];
+        unpack_rect(make_uint2(o.y, o.z), x0, y0, x1, y1);
+        if (x0 < x1 && y0 < y1) {  // (K0 orders only Gaussians with tiles)
+            atomicAdd(&s_d[y0 * gx + x0], 1u);
+            if (x1 < gx) atomicAdd(&s_d[y0 * gx + x1], ~0u);
+            if (y1 < gy) {
+                atomicAdd(&s_d[y1 * gx + x0], ~0u);
+                if (x1 < gx) atomicAdd(&s_d[y1 * gx + x1], 1u);
+            }
+        }
+    }
+    __syncthreads();
+    // rows (modular u32 arithmetic: every partial sum of a row is a count difference, the
+    // final values are counts)
+    for (uint32_t y = (uint32_t)wave; y < gy; y += kBinWaves) {
+        uint32_t carry = 0u;
+        for (uint32_t xb = 0; xb < gx; xb += 64) {
+            const uint32_t x = xb + (uint32_t)lane;
+            const uint32_t v = x < gx ? s_d[y * gx + x] : 0u;
+            const uint32_t incl = wave_incl_sum(v) + carry;
+            if (x < gx) s_d[y * gx + x] = incl;
+            carry = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        }
+    }
+    __syncthreads();
+    // columns: one thread per column, kColBlock independent loads per round trip
+    for (uint32_t x = threadIdx.x; x < gx; x += blockDim.x) {
+        uint32_t run = 0u;
+        for (uint32_t yb = 0; yb < gy; yb += kColBlock) {
+            uint32_t v[kColBlock];
+#pragma unroll
+            for (int i = 0; i < kColBlock; i++) v[i] = yb + i < gy ? s_d[(yb + i) * gx + x] : 0u;
+#pragma unroll
+            for (int i = 0; i < kColBlock; i++) {
+                run += v[i];
+                if (yb + i < gy) s_d[(yb + i) * gx + x] = run;
+            }
+        }
+    }
+    __syncthreads();
+}
+
 template <bool LDS>
 __global__ void __launch_bounds__(kBinThreads) tile_count_kernel(int P, int chunk, const uint2* __restrict__ rect,
                                                                  const uint32_t* __restrict__ tiles_touched,
@@ -291,7 +353,7 @@ __global__ void __launch_bounds__(kBinThreads) tile_count_kernel(int P, int chun
                                                                  const uint32_t* __restrict__ n_visible,
                                                                  uint32_t tiles, uint32_t gx, uint32_t* __restrict__ cnt,
                                                                  uint32_t* __restrict__ chunk_off, FusedZero fz) {
-    extern __shared__ uint32_t s_hist[];  // (tiles + 1) / 2 words: 16-bit counters (a chunk has < 65536 Gaussians)
+    extern __shared__ uint32_t s_hist[];  // by rectangles: tiles words; walk: (tiles + 1) / 2 words of 16-bit counters (a chunk has < 65536 Gaussians)
     if (fz.unit_cnt) {
         if (blockIdx.x == 0 && threadIdx.x < kUnitLists * kUnitShards) fz.unit_cnt[threadIdx.x * kUnitCntStride] = 0u;
         if (blockIdx.x == 0 && threadIdx.x < kSortClasses) fz.cls_count[threadIdx.x] = 0u;
@@ -303,6 +365,17 @@ __global__ void __launch_bounds__(kBinThreads) tile_count_kernel(int P, int chun
     const uint32_t words = (tiles + 1) / 2;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     GSR_STAMP(g_st_count, blockIdx.x, 0);
+    if (LDS && GSR_K1_RECT) {
+        count_by_rectangles(g0, g1, order, tiles, gx, s_hist);
+        GSR_STAMP(g_st_count, blockIdx.x, 2);
+        uint32_t* off = chunk_off + (size_t)blockIdx.x * tiles;
+        for (uint32_t i = threadIdx.x; i < tiles; i += blockDim.x) {
+            const uint32_t c = s_hist[i];
+            if (c) off[i] = atomicAdd(&cnt[i], c);
+        }
+        GSR_STAMP(g_st_count, blockIdx.x, 3);
+        return;
+    }
     if (LDS) {
         for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) s_hist[i] = 0;
         __syncthreads();
@@ -1090,7 +1163,8 @@ hipError_t launch_bin_count(int P, const GeomState& g, uint32_t gx, uint32_t gy,
                        cgx, g.cell_cnt, g.cell_off, g.chunk_total);
     hipLaunchKernelGGL(cell_scatter_kernel, grid, block, cell_bytes, stream, P, chunk, g.rect, g.tiles_touched,
                        cells, cgx, g.cell_cnt, g.cell_off, g.depth_key, g.order, g.n_visible);
-    const size_t hist_bytes = lds ? ((tiles + 1) / 2) * sizeof(uint32_t) : 0;
+    // K1's LDS: one u32 per tile (by rectangles) or two 16-bit walk counters per word
+    const size_t hist_bytes = !lds ? 0 : GSR_K1_RECT ? tiles * sizeof(uint32_t) : ((tiles + 1) / 2) * sizeof(uint32_t);
     if (fused && !lds) return hipErrorInvalidValue;  // the fused scan needs the LDS cursors
     const FusedZero fz = fused ? FusedZero{g.unit_cnt, g.tile_join, g.cls_count} : FusedZero{nullptr, nullptr, nullptr};
     if (lds)
