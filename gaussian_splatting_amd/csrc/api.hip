@@ -187,6 +187,7 @@ gsr::BinningState carve_binning(char* base, size_t C, size_t* total) {
     b.gid_sorted = c.take<uint32_t>(C);
     b.ckpt = c.take<float>((C / kCkStride + 1) * (size_t)kCkFloats);
     b.unit_full = c.take<uint2>(kUnitShards * unit_full_cap(C));
+    b.rec_flag = c.take<uint8_t>(((C + 15) & ~(size_t)15) + 16);  // K3 / gauss_reduce use aligned 16-byte words
     *total = align_up(c.off);
     return b;
 }
@@ -232,7 +233,8 @@ bool resolve_capacity(int R, int capacity, size_t bytes, size_t* C) {
     return binning_bytes_for((size_t)R) == bytes;
 }
 
-// Backward scratch: R per-instance records and their content bytes, P per-Gaussian sums, the live list.
+// Backward scratch: R per-instance records, P per-Gaussian sums, the live list (the records' content
+// bytes are in the binning buffer).
 void carve_recs(char* base, size_t R, size_t P, gsr::GradRecs* recs, gsr::GradRecs* sums, uint32_t** live,
                 uint32_t** live_count, size_t* total) {
     using namespace gsr;
@@ -247,7 +249,7 @@ void carve_recs(char* base, size_t R, size_t P, gsr::GradRecs* recs, gsr::GradRe
         recs->b = c.take<float4>(R);
         recs->c = c.take<float2>(R);
     }
-    recs->flag = c.take<uint8_t>((R + 15) & ~(size_t)15);  // gauss_reduce reads it in aligned 16-byte words
+    recs->flag = nullptr;  // in the binning buffer (BinningState::rec_flag)
     sums->a = c.take<float4>(P);
     sums->b = c.take<float4>(P);
     sums->c = c.take<float2>(P);
@@ -1157,9 +1159,9 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
         sj.armed = true;
     }
 
-    // the records' content bytes: render_bwd sets those of the records it writes, gauss_reduce
-    // reads them to find the records (R bytes: 8 MB at 1M@1080p)
-    if (R > 0) HIP_TRY(hipMemsetAsync(recs.flag, 0, (size_t)R, stream), "record flags");
+    // the records' content bytes (zeroed by the forward's K3): render_bwd sets those of the records
+    // it writes, gauss_reduce reads them to find the records
+    recs.flag = bin.rec_flag;
     if (R > 0) {
         StageScope sc(ST_RENDER_BWD, stream);
         RenderBwdArgs ra{};

@@ -498,7 +498,7 @@ __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
     const uint32_t* __restrict__ depth_key, const uint4* __restrict__ order, const uint32_t* __restrict__ n_visible,
     uint32_t tiles, uint32_t gx, uint32_t* __restrict__ tile_base,
     const uint32_t* __restrict__ chunk_off, const u64* __restrict__ chunk_total, u64* __restrict__ keys, u64 cap,
-    uint32_t* __restrict__ rec_start, float4* __restrict__ rec, FusedScan fs) {
+    uint32_t* __restrict__ rec_start, float4* __restrict__ rec, uint8_t* __restrict__ rec_flag, FusedScan fs) {
     extern __shared__ uint32_t s_cur[];  // tiles words
     __shared__ u64 s_tmp[kBinWaves];
     const int g0 = blockIdx.x * chunk, g1 = min(P, g0 + chunk);
@@ -578,6 +578,15 @@ __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
     }
     // first record index of every Gaussian: chunk base + in-order scan of tiles_touched
     u64 carry = block_sum(before, s_tmp);
+    if (rec_flag) {
+        // the gradient records' content bytes of this chunk's emission range [carry, carry + total),
+        // zeroed for the backward (render_bwd sets them): 16-byte words, rounded outward -- a word
+        // shared with the next chunk gets zeros from both.  Clamped to the capacity (a truncated pass
+        // is rebuilt).
+        const u64 e1 = min(carry + chunk_total[blockIdx.x], cap);
+        uint4* w = reinterpret_cast<uint4*>(rec_flag);
+        for (u64 i = carry / 16 + threadIdx.x; i < (e1 + 15) / 16; i += blockDim.x) w[i] = make_uint4(0u, 0u, 0u, 0u);
+    }
     for (int gb = g0; gb < g1; gb += kBinThreads) {
         const int g = gb + (int)threadIdx.x;
         const uint32_t n = g < g1 ? tiles_touched[g] : 0u;
@@ -1195,11 +1204,11 @@ hipError_t launch_bin_scatter(int P, const GeomState& g, uint32_t gx, uint32_t g
     if (lds)
         hipLaunchKernelGGL(tile_scatter_kernel<true>, grid, block, cur_bytes, stream, P, chunk, g.rect,
                            g.tiles_touched, g.depth_key, g.order, g.n_visible, tiles, gx, g.tile_base, g.chunk_off,
-                           g.chunk_total, b.keys, (u64)cap, g.rec_start, g.rec, fs);
+                           g.chunk_total, b.keys, (u64)cap, g.rec_start, g.rec, b.rec_flag, fs);
     else
         hipLaunchKernelGGL(tile_scatter_kernel<false>, grid, block, 0, stream, P, chunk, g.rect, g.tiles_touched,
                            g.depth_key, g.order, g.n_visible, tiles, gx, g.tile_base, g.chunk_off, g.chunk_total,
-                           b.keys, (u64)cap, g.rec_start, g.rec, fs);
+                           b.keys, (u64)cap, g.rec_start, g.rec, b.rec_flag, fs);
     return hipGetLastError();
 }
 

@@ -127,6 +127,8 @@ struct BinningState {
                                // (Gaussian << kEntryMaskBits | quadrant mask)
     float* ckpt;               // blend checkpoints, [C / kCkStride + 1][kCkFloats] (see below)
     uint2* unit_full;          // backward units covering full segments, [shard][unit_full_cap(C)]
+    uint8_t* rec_flag;         // per emission index: the gradient record's content byte (GradRecs::flag),
+                               // zeroed by K3, set by render_bwd, read by gauss_reduce; C + 16 bytes
 };
 
 // ---------------------------------------------------------------------------
@@ -187,12 +189,15 @@ struct GradRecs {
     float4* a;  // (dcolor.r, dcolor.g, dcolor.b, dinvdepth)
     float4* b;  // (dmean2D.x, dmean2D.y, dopacity_eff, dconic.b)
     float2* c;  // (dconic.a, dconic.c)
-    uint8_t* flag;  // per-instance records only: 1 = the record exists (zeroed before render_bwd)
+    uint8_t* flag;  // per-instance records only: 1 = the record exists (BinningState::rec_flag)
 };
 // The render backward writes a record and its content byte only for an entry with a gradient term
 // (~half of the staged entries at 1M@1080p, 7.6M of 114.7M instances at 5M@4K); the content bytes
-// are zeroed before it, so gauss_reduce finds the records from the bytes alone (a coalesced 64-byte
-// load per 64 instances) and skips the rest.
+// live in the binning buffer and are zeroed by the forward's K3 (each chunk clears its emission
+// range with 16-byte stores, no memset launch), so gauss_reduce finds the records from the bytes
+// alone (1024 per wave-wide load) and skips the rest.  Whether an entry has a gradient term depends
+// on the geometry only, not on the upstream gradient, so a second backward of the same forward sets
+// the same bytes.
 #define GSR_REC_FLAG 1
 
 // The live list (backward scratch): the Gaussians with a gradient, appended by gauss_reduce for
