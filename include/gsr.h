@@ -93,8 +93,11 @@ int gsr_rasterize_forward_ex(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_
  * forward's callbacks returned.  dL_dinvdepths ([1,H,W]) may be NULL, in which
  * case dL_dinvdepth must be NULL too.  dL_dconic ([P,4]) may be NULL.  Every
  * element of every non-NULL output is written (no pre-zeroing needed).
- * `scratch_alloc` provides 40 bytes per tile instance for the per-instance
- * gradient records. */
+ * `scratch_alloc` provides 48 bytes per tile instance for the per-instance
+ * gradient records, plus 40 bytes and a live-list slot per Gaussian.  The backward
+ * also sets the records' content bytes, which live in the forward's binning buffer
+ * (zeroed by the forward); they depend on the geometry only, so a second backward of
+ * the same forward (retain_graph) sets the same bytes. */
 int gsr_rasterize_backward(int P, int D, int M, int R, const float* background, int width, int height,
                            const float* means3D, const float* shs, const float* colors_precomp,
                            const float* opacities, const float* scales, float scale_modifier, const float* rotations,
