@@ -45,6 +45,10 @@ namespace gsr {
 
 constexpr int kBinThreads = 1024;
 constexpr int kBinWaves = kBinThreads / 64;
+#ifndef GSR_BIN_UNROLL
+#define GSR_BIN_UNROLL 4
+#endif
+constexpr int kBinUnroll = GSR_BIN_UNROLL;  // K0 / K1 Gaussians per thread per round (loads in flight together)
 constexpr uint32_t kLdsTilesMax = 36864;  // K3 keeps one u32 per tile in LDS (144 KiB)
 constexpr uint32_t kSortWaveMax = 1024;   // longest list tile_sort_kernel sorts (one wave per tile)
 // Longer lists go to two persistent 256-thread kernels walking K2's class lists: class 0
@@ -226,10 +230,21 @@ __global__ void __launch_bounds__(kBinThreads) cell_count_kernel(int P, int chun
     for (uint32_t i = threadIdx.x; i < cells; i += blockDim.x) s_c[i] = 0;
     __syncthreads();
     u64 mine = 0;
-    for (int g = g0 + (int)threadIdx.x; g < g1; g += kBinThreads) {
-        const uint32_t n = tiles_touched[g];
-        mine += n;
-        if (n) atomicAdd(&s_c[cell_of(rect[g], cgx)], 1u);
+    // kBinUnroll Gaussians per thread per round, their loads all issued before the LDS atomics
+    for (int gb = g0 + (int)threadIdx.x; gb < g1; gb += kBinUnroll * kBinThreads) {
+        uint32_t n[kBinUnroll];
+        uint2 r[kBinUnroll];
+#pragma unroll
+        for (int u = 0; u < kBinUnroll; u++) {
+            const int g = gb + u * kBinThreads;
+            n[u] = g < g1 ? tiles_touched[g] : 0u;
+            r[u] = g < g1 ? rect[g] : make_uint2(0u, 0u);
+        }
+#pragma unroll
+        for (int u = 0; u < kBinUnroll; u++) {
+            mine += n[u];
+            if (n[u]) atomicAdd(&s_c[cell_of(r[u], cgx)], 1u);
+        }
     }
     const u64 total = block_sum(mine, s_tmp);  // ends with a barrier: the histogram is complete
     if (threadIdx.x == 0) chunk_total[blockIdx.x] = total;
@@ -267,11 +282,22 @@ __global__ void __launch_bounds__(kBinThreads) cell_scatter_kernel(int P, int ch
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) n_visible[0] = carry;
     __syncthreads();
-    for (int g = g0 + (int)threadIdx.x; g < g1; g += kBinThreads)
-        if (tiles_touched[g]) {
-            const uint2 r = rect[g];
-            order[atomicAdd(&s_c[cell_of(r, cgx)], 1u)] = make_uint4((uint32_t)g, r.x, r.y, depth_key[g]);
+    for (int gb = g0 + (int)threadIdx.x; gb < g1; gb += kBinUnroll * kBinThreads) {
+        uint32_t n[kBinUnroll], dk[kBinUnroll];
+        uint2 r[kBinUnroll];
+#pragma unroll
+        for (int u = 0; u < kBinUnroll; u++) {
+            const int g = gb + u * kBinThreads;
+            n[u] = g < g1 ? tiles_touched[g] : 0u;
+            r[u] = g < g1 ? rect[g] : make_uint2(0u, 0u);
+            dk[u] = g < g1 ? depth_key[g] : 0u;
         }
+#pragma unroll
+        for (int u = 0; u < kBinUnroll; u++)
+            if (n[u])
+                order[atomicAdd(&s_c[cell_of(r[u], cgx)], 1u)] =
+                    make_uint4((uint32_t)(gb + u * kBinThreads), r[u].x, r[u].y, dk[u]);
+    }
 }
 
 // ---- K1 ---------------------------------------------------------------------
@@ -302,16 +328,25 @@ __device__ __forceinline__ void count_by_rectangles(int g0, int g1, const uint4*
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (uint32_t i = threadIdx.x; i < tiles; i += blockDim.x) s_d[i] = 0u;
     __syncthreads();
-    for (int p = g0 + (int)threadIdx.x; p < g1; p += kBinThreads) {
-        uint32_t x0, y0, x1, y1;
-        const uint4 o = order[p];
-        unpack_rect(make_uint2(o.y, o.z), x0, y0, x1, y1);
-        if (x0 < x1 && y0 < y1) {  // (K0 orders only Gaussians with tiles)
-            atomicAdd(&s_d[y0 * gx + x0], 1u);
-            if (x1 < gx) atomicAdd(&s_d[y0 * gx + x1], ~0u);
-            if (y1 < gy) {
-                atomicAdd(&s_d[y1 * gx + x0], ~0u);
-                if (x1 < gx) atomicAdd(&s_d[y1 * gx + x1], 1u);
+    for (int pb = g0 + (int)threadIdx.x; pb < g1; pb += kBinUnroll * kBinThreads) {
+        uint2 rr[kBinUnroll];
+#pragma unroll
+        for (int u = 0; u < kBinUnroll; u++) {
+            const int p = pb + u * kBinThreads;
+            const uint4 o = p < g1 ? order[p] : make_uint4(0u, 0u, 0u, 0u);
+            rr[u] = make_uint2(o.y, o.z);
+        }
+#pragma unroll
+        for (int u = 0; u < kBinUnroll; u++) {
+            uint32_t x0, y0, x1, y1;
+            unpack_rect(rr[u], x0, y0, x1, y1);
+            if (x0 < x1 && y0 < y1) {  // (K0 orders only Gaussians with tiles; padding lanes are empty)
+                atomicAdd(&s_d[y0 * gx + x0], 1u);
+                if (x1 < gx) atomicAdd(&s_d[y0 * gx + x1], ~0u);
+                if (y1 < gy) {
+                    atomicAdd(&s_d[y1 * gx + x0], ~0u);
+                    if (x1 < gx) atomicAdd(&s_d[y1 * gx + x1], 1u);
+                }
             }
         }
     }
