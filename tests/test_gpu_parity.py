@@ -408,12 +408,15 @@ def test_sort_prefix_and_redo(name, prefix):
         np.testing.assert_array_equal(a, b)
 
 
-@pytest.mark.parametrize("P", [3000, 40000])
-def test_large_image(P):
+@pytest.mark.parametrize("P,W,H", [(3000, 2304, 2048), (40000, 2304, 2048), (6000, 5120, 2048)],
+                         ids=["2304x2048_sparse", "2304x2048_dense", "5120x2048_global_cursors"])
+def test_large_image(P, W, H):
     """A 2304x2048 frame (18432 tiles: K3's LDS cursors hold 74 KiB), sparse (3000 Gaussians, every
-    binning chunk spanning most of the screen) and denser (40000): lists identical, the image by the
-    full-size threshold-flip rule, L1-gradient parity 1e-5."""
-    case = C.Case("large_image", P=P, W=2304, H=2048, focal=1400.0, scale_range=(0.01, 0.08))
+    binning chunk spanning most of the screen) and denser (40000); and a 5120x2048 frame (40960 tiles,
+    more than K1 / K3 keep in LDS: the binning falls back to global-memory counters and cursors and the
+    unfused tile scan).  Lists identical, the image by the full-size threshold-flip rule, L1-gradient
+    parity 1e-5."""
+    case = C.Case("large_image", P=P, W=W, H=H, focal=1400.0, scale_range=(0.01, 0.08))
     inp = C.build(case)
     ref = C.run_oracle(inp, nthreads=8)
     fwd = C.run_gpu_forward(inp)
@@ -435,4 +438,4 @@ def test_large_image(P):
     r = ref.handle.backward(gc, gd, nthreads=8)
     for k, got in zip(C.GRAD_NAMES, out):
         np.testing.assert_allclose(_to_np(got), r[k], atol=1e-5, rtol=0, err_msg=k)
-    print(f"[large_image P={P}] pixels over 1e-5: {int((d > ATOL_FWD).sum())}, all at threshold flips")
+    print(f"[large_image P={P} {W}x{H}] pixels over 1e-5: {int((d > ATOL_FWD).sum())}, all at threshold flips")
