@@ -985,6 +985,9 @@ __device__ __forceinline__ void views_sh_band(const ViewsBwdArgs& a, int idx, fl
     }
 }
 
+#ifndef GSR_VIEWS_ONE_PASS
+#define GSR_VIEWS_ONE_PASS 1
+#endif
 template <int SH_MODE, bool PACKED, bool LIST = false>
 // 3 waves per SIMD (the LDS limit of the SH staging): the register allocator then spills a
 // few values but the per-view latency chains overlap better (8 views: 0.50 -> 0.44 ms, r1af)
@@ -1063,10 +1066,20 @@ __global__ void __launch_bounds__(64) GSR_VIEWS_OCCUPANCY gauss_bwd_views_kernel
     if constexpr (SH_MODE != kShGlobal) __syncthreads();  // the staged SH rows are read for the last time
     float* row = SH_MODE != kShGlobal ? &s_sh[lane * kShStride] : nullptr;
     if (valid) {
+#if GSR_VIEWS_ONE_PASS
+        // one walk over the views for every band: phase 1's registers are dead here, so the 48
+        // accumulators fit under its peak (four walks -- one per band -- cost 0.12 of 0.28 ms at 8
+        // views, r3z)
+        if (a.D > 2) views_sh_band<0, 16, SH_MODE, PACKED>(a, idx, mean, row, sh_dst);
+        else if (a.D > 1) views_sh_band<0, 9, SH_MODE, PACKED>(a, idx, mean, row, sh_dst);
+        else if (a.D > 0) views_sh_band<0, 4, SH_MODE, PACKED>(a, idx, mean, row, sh_dst);
+        else views_sh_band<0, 1, SH_MODE, PACKED>(a, idx, mean, row, sh_dst);
+#else
         views_sh_band<0, 1, SH_MODE, PACKED>(a, idx, mean, row, sh_dst);
         if (a.D > 0) views_sh_band<1, 4, SH_MODE, PACKED>(a, idx, mean, row, sh_dst);
         if (a.D > 1) views_sh_band<4, 9, SH_MODE, PACKED>(a, idx, mean, row, sh_dst);
         if (a.D > 2) views_sh_band<9, 16, SH_MODE, PACKED>(a, idx, mean, row, sh_dst);
+#endif
         const int K = (a.D + 1) * (a.D + 1);
         if constexpr (SH_MODE != kShGlobal) {
             for (int k = K; k < 16; k++) row[3 * k] = row[3 * k + 1] = row[3 * k + 2] = 0.f;
