@@ -988,6 +988,9 @@ __device__ __forceinline__ void views_sh_band(const ViewsBwdArgs& a, int idx, fl
 #ifndef GSR_VIEWS_ONE_PASS
 #define GSR_VIEWS_ONE_PASS 1
 #endif
+#ifndef GSR_VIEWS_FLAG_PREFETCH
+#define GSR_VIEWS_FLAG_PREFETCH 1
+#endif
 template <int SH_MODE, bool PACKED, bool LIST = false>
 // 3 waves per SIMD (the LDS limit of the SH staging): the register allocator then spills a
 // few values but the per-view latency chains overlap better (8 views: 0.50 -> 0.44 ms, r1af)
@@ -1039,10 +1042,18 @@ __global__ void __launch_bounds__(64) GSR_VIEWS_OCCUPANCY gauss_bwd_views_kernel
         float3 dmean = make_float3(0.f, 0.f, 0.f), dscale = dmean;
         float4 drot = make_float4(0.f, 0.f, 0.f, 0.f);
         float dop = 0.f;
+#if GSR_VIEWS_FLAG_PREFETCH  // (the next view's flag word loads while this view is evaluated)
+        uint32_t flags_next = a.n_views > 0 ? view_flag<PACKED>(a, a.blocks, 0, idx) : 0u;
+#endif
 #pragma unroll 1
         for (int v = 0; v < a.n_views; v++) {
             const float* blk = a.blocks + (size_t)v * a.block_floats;
+#if GSR_VIEWS_FLAG_PREFETCH
+            const uint32_t flags = flags_next;
+            if (v + 1 < a.n_views) flags_next = view_flag<PACKED>(a, blk + a.block_floats, v + 1, idx);
+#else
             const uint32_t flags = view_flag<PACKED>(a, blk, v, idx);
+#endif
             if (!(flags & 1u)) continue;  // not visible in view v: no gradient from it
             const ViewCam cam{blk + kViewCamView, blk + kViewCamProj, blk + kViewCamPos, blk[kViewCamTanX],
                               blk[kViewCamTanY],  blk[kViewCamFocalX], blk[kViewCamFocalY],
