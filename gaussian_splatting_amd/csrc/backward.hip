@@ -39,7 +39,7 @@ namespace gsr {
 // per lane) and each Gaussian's run is summed by a segmented scan over the wave, in a
 // fixed order, so the result does not depend on scheduling.  A record exists iff its content
 // byte is set (render.hip writes records only for entries with a gradient term; the bytes are
-// zeroed before it, api.hip): the range is scanned 1024 bytes per wave-wide load, and only the
+// zeroed by the forward's K3, binning.hip): the range is scanned 1024 bytes per wave-wide load, and only the
 // 64-instance chunks that start at a record are loaded and reduced -- 5M@4K: 7.6M records of
 // 114.7M instances, the rest behind saturated pixels.
 constexpr int kRecStride = 12;  // floats per Gaussian in the LDS hand-off of chunk totals (10 used), 48 B

@@ -616,7 +616,7 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
         __syncthreads();
         const bool content = (written >> lane) & 1ull;
         if (has && content && !(GSR_ATTR & 1)) {
-            a.recs.flag[e] = 1;  // (the bytes were zeroed before this kernel: api.hip)
+            a.recs.flag[e] = 1;  // (the bytes were zeroed by the forward's K3, binning.hip)
             float4 ra = make_float4(0.f, 0.f, 0.f, 0.f), rb = ra;
             float2 rc = make_float2(0.f, 0.f);
             if (content) {
