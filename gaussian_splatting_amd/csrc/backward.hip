@@ -42,6 +42,9 @@ namespace gsr {
 // zeroed by the forward's K3, binning.hip): the range is scanned 1024 bytes per wave-wide load, and only the
 // 64-instance chunks that start at a record are loaded and reduced -- 5M@4K: 7.6M records of
 // 114.7M instances, the rest behind saturated pixels.
+#ifndef GSR_REDUCE_WIN_LDS
+#define GSR_REDUCE_WIN_LDS 1
+#endif
 constexpr int kRecStride = 12;  // floats per Gaussian in the LDS hand-off of chunk totals (10 used), 48 B
 
 // Sums of the records of the wave's 64 consecutive Gaussians [g0, g0 + 64), one
@@ -80,9 +83,19 @@ __device__ __forceinline__ void reduce_records(int P, int g0, const uint32_t* __
     // start (lane + 1) in LDS and a DPP max-scan spreads the marks (one wave's LDS accesses
     // execute in order, so no dependent ds_bpermute chain).
     __shared__ uint32_t s_mark[64];
+#if GSR_REDUCE_WIN_LDS
+    // the current window's content bytes (masked at E1), mirrored in LDS: a chunk's record test is
+    // an LDS byte read inside the window (a global reload only for the part past its end)
+    __shared__ __attribute__((aligned(16))) uint8_t s_win[1024];
+#endif
+    uint32_t wa = 0;  // the current window's first byte
     auto chunk = [&](uint32_t base) -> Slot {
         const uint32_t e = base + lane;
+#if GSR_REDUCE_WIN_LDS
+        const bool has = e < E1 && (e - wa < 1024u ? s_win[e - wa] != 0 : recs.flag[e] != 0);
+#else
         const bool has = e < E1 && recs.flag[e] != 0;
+#endif
         const unsigned long long st = __ballot(n && my0 < base);
         const uint32_t carry = st ? 64u - (uint32_t)__clzll((long long)st) : 0u;
         s_mark[lane] = 0u;
@@ -143,7 +156,8 @@ __device__ __forceinline__ void reduce_records(int P, int g0, const uint32_t* __
     while (base < E1) {  // uniform
         // content bytes [wa, wa + 1024): lane l holds bytes wa + 16 l .. + 15 (the byte buffer is
         // padded to a multiple of 16, api.hip carve_recs); bytes at or past E1 are another wave's
-        const uint32_t wa = base & ~15u, wend = wa + 1024u;
+        wa = base & ~15u;
+        const uint32_t wend = wa + 1024u;
         const uint32_t p = wa + 16u * (uint32_t)lane;
         uint64_t lo = 0, hi = 0;
         if (p < E1) {
@@ -154,6 +168,12 @@ __device__ __forceinline__ void reduce_records(int P, int g0, const uint32_t* __
             if (k < 8) { lo &= (1ull << (8 * k)) - 1ull; hi = 0; }
             else if (k < 16) hi &= (1ull << (8 * (k - 8))) - 1ull;  // k == 8 clears hi
         }
+#if GSR_REDUCE_WIN_LDS
+        __builtin_amdgcn_wave_barrier();  // the previous window's readers are done (in-order LDS)
+        reinterpret_cast<uint4*>(s_win)[lane] =
+            make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+        __builtin_amdgcn_wave_barrier();
+#endif
         while (true) {
             // drop the bytes below base (already reduced or before the range)
             if (base > p) {
