@@ -527,6 +527,15 @@ struct FusedScan {
     uint32_t* cls_count;
 };
 
+// Store-cost attribution builds only (GSR_K3_ATTR): K3 writes its keys a second
+// time into a scratch buffer, scattered as the real stores (1) or coalesced (2).
+#ifndef GSR_K3_ATTR
+#define GSR_K3_ATTR 0
+#endif
+#if GSR_K3_ATTR
+__device__ u64* g_k3_scratch;
+#endif
+
 template <bool LDS>
 __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
     int P, int chunk, const uint2* __restrict__ rect, const uint32_t* __restrict__ tiles_touched,
@@ -638,6 +647,9 @@ __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
     // the keys: chunk positions [q0, q1) of the spatial order (K0), as K1 counted them
     const int V = (int)n_visible[0];
     const int q0 = blockIdx.x * chunk, q1 = min(V, q0 + chunk);
+#if GSR_K3_ATTR
+    u64 attr_ctr = 0;
+#endif
     for (int pb = q0 + wave * 64; pb < q1; pb += kBinThreads) {
         const int p = pb + lane;
         const uint4 o = p < q1 ? order[p] : make_uint4(0u, 0u, 0u, 0u);
@@ -649,6 +661,16 @@ __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
             if (!valid) return;
             const uint32_t pos = LDS ? atomicAdd(&s_cur[t], 1u) : atomicAdd(&tile_base[t], 1u);
             if (pos < cap) keys[pos] = ((u64)kh << 32) | (kg << kEntryMaskBits);  // cap: redone if exceeded
+#if GSR_K3_ATTR == 1  // attribution: the same scattered stores again, into a scratch buffer
+            if (pos < cap) g_k3_scratch[pos] = ((u64)kh << 32) | (kg << kEntryMaskBits);
+#elif GSR_K3_ATTR == 2  // attribution: as many stores again, coalesced (lane-contiguous per step)
+            {
+                const u64 region = cap / ((u64)gridDim.x * kBinWaves);
+                const u64 at = ((u64)blockIdx.x * kBinWaves + (u64)wave) * region;
+                g_k3_scratch[at + (attr_ctr + (u64)lane) % region] = ((u64)kh << 32) | (kg << kEntryMaskBits);
+                attr_ctr += 64;
+            }
+#endif
         });
     }
 #ifdef GSR_STAMPS
@@ -1236,6 +1258,16 @@ hipError_t launch_bin_scatter(int P, const GeomState& g, uint32_t gx, uint32_t g
     if (fused && !lds) return hipErrorInvalidValue;
     const FusedScan fs = fused ? FusedScan{g.tile_cnt, ranges, g.total, (u64*)host_total, g.cls_list, g.cls_count}
                                : FusedScan{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+#if GSR_K3_ATTR
+    static u64* scratch = nullptr;
+    static size_t scratch_cap = 0;
+    if (cap > scratch_cap) {
+        if (scratch) (void)hipFree(scratch);
+        if (hipMalloc(&scratch, cap * sizeof(u64)) != hipSuccess) return hipErrorOutOfMemory;
+        scratch_cap = cap;
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_k3_scratch), &scratch, sizeof(scratch)) != hipSuccess) return hipErrorUnknown;
+    }
+#endif
     if (lds)
         hipLaunchKernelGGL(tile_scatter_kernel<true>, grid, block, cur_bytes, stream, P, chunk, g.rect,
                            g.tiles_touched, g.depth_key, g.order, g.n_visible, tiles, gx, g.tile_base, g.chunk_off,
