@@ -224,6 +224,8 @@ def main():
                          "all-reduce the parameter gradients (allreduce); auto times views and allreduce in the "
                          "warm-up and keeps the faster (DESIGN.md section 7)")
     ap.add_argument("--auto-steps", type=int, default=5, help="timed warm-up steps per candidate of --exchange auto")
+    ap.add_argument("--separate-sh", action="store_true",
+                    help="SH as train.py's separate_sh path passes it: dc [P,1,3] + rest [P,M-1,3] (3DGS-accel surface)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="threads of the C-restatement figure (default 16)")
     ap.add_argument("--cpu-only", action="store_true",
                     help="no GPU: time the pure-PyTorch fallback forward on --config (BASELINE configs[0] plumbing)")
@@ -261,7 +263,15 @@ def main():
     gc, gd = gc.to(dev), gd.to(dev)
     bg = torch.zeros(3, device=dev)
     empty = torch.empty(0, device=dev)
-    arena = GradArena(P, scene.shs.shape[1], dev)
+    # SH layout: one [P,M,3] tensor (the vendored rasterizer), or dc + rest as train.py's separate_sh path
+    # hands them over (gaussian_renderer/__init__.py:106-125)
+    if args.separate_sh:
+        sh_dc, sh_rest = scene.shs[:, :1].contiguous(), scene.shs[:, 1:].contiguous()
+        sh_in = (sh_dc, sh_rest)
+    else:
+        sh_dc, sh_rest = None, scene.shs
+        sh_in = (scene.shs,)
+    arena = GradArena(P, scene.shs.shape[1], dev, separate_sh=args.separate_sh)
     uses_views = world > 1 and args.exchange in ("auto", "views", "dense")
     ex = ViewExchange(P, dev, sparse=args.exchange != "dense") if uses_views else None
     # the exchange the steps run: fixed by --exchange, or (auto) picked by timing in the warm-up below
@@ -273,19 +283,19 @@ def main():
     def step(collective=True):
         t0 = pc()
         fwd = _C.rasterize_gaussians(bg, scene.means3D, empty, scene.opacities, scene.scales, scene.rotations, 1.0,
-                                     empty, cam.viewmatrix, cam.projmatrix, cam.tanfovx, cam.tanfovy, H, W, scene.shs,
+                                     empty, cam.viewmatrix, cam.projmatrix, cam.tanfovx, cam.tanfovy, H, W, *sh_in,
                                      Kdeg, cam.campos, False, False, False)
         t1 = pc()
         nr, color, radii, geom, binning, img, invd = fwd
         bwd = (bg, scene.means3D, radii, empty, scene.opacities, scene.scales, scene.rotations, 1.0, empty,
-               cam.viewmatrix, cam.projmatrix, cam.tanfovx, cam.tanfovy, gc, gd, scene.shs, Kdeg, cam.campos, geom, nr,
+               cam.viewmatrix, cam.projmatrix, cam.tanfovx, cam.tanfovy, gc, gd, *sh_in, Kdeg, cam.campos, geom, nr,
                binning, img, False, False)
         t2 = pc()
         if exchange == "views" and collective:  # sparse view blocks, every rank sums all views' gradients
             _C.rasterize_gaussians_backward_screen(*bwd, view_block=ex.local_block())
             t3 = pc()
             ex.exchange(zero=arena.flat)  # the outputs zeroed beside the exchange; a live-list backward
-            ex.views_backward(scene.means3D, None, scene.shs, Kdeg, scene.opacities, scene.scales, scene.rotations,
+            ex.views_backward(scene.means3D, sh_dc, sh_rest, Kdeg, scene.opacities, scene.scales, scene.rotations,
                               1.0, out=arena.views())
         else:
             _C.rasterize_gaussians_backward(*bwd, out=arena.views())
@@ -439,7 +449,8 @@ def main():
             "dtype": "fp32",
             "data": "synthetic (frustum-uniform Gaussians, SURVEY.md 8d; seed 0)",
             "config": {"workload": args.config, "gaussians": P, "width": W, "height": H, "sh_degree": Kdeg,
-                       "num_rendered": nr, "views": "one per GPU, yaw 5 deg x rank", "parallelism": par},
+                       "num_rendered": nr, "views": "one per GPU, yaw 5 deg x rank", "parallelism": par,
+                       "sh_layout": "dc + rest (separate_sh)" if args.separate_sh else "one [P,M,3] tensor"},
             "roofline": {"kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          # counter bytes per launch over the launch time: the HBM rate the kernel really moves

@@ -41,7 +41,13 @@ def _newest_input_mtime() -> float:
 # (radius, getRect's tile rectangle, tiles_touched, hence num_rendered and the tile lists) then
 # comes from the same individually rounded operations as the reference's and the oracle's
 # (oracle/Makefile builds with -ffp-contract=off), so those integers are identical, not close.
+# backward.hip: contraction inside each expression only (-ffp-contract=on, not HIP's default
+# "fast", which fuses a multiply into an add wherever the backend's DAG sees both) and no SLP
+# vectorisation (it also splits fmuladd pairs into a packed multiply plus a scalar add): an
+# expression then rounds the same way whatever code surrounds it, so the split and combined SH
+# layouts' kernels give bitwise-equal gradients (tests/test_separate_sh.py).
 FILE_FLAGS = {"render.hip": ["-fno-slp-vectorize"],
+              "backward.hip": ["-fno-slp-vectorize", "-ffp-contract=on"],
               "preprocess.hip": ["-fno-slp-vectorize", "-ffp-contract=off"]}
 
 

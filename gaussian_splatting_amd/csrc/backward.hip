@@ -327,11 +327,13 @@ constexpr int kShStride = 52;  // padded LDS row stride: conflict-free ds_read/w
 
 // ---- per-view gradient math (one Gaussian, one view) ----------------------------
 // computeCov2DCUDA with its re-derived tail, the screen-space mean chain, the SH colour
-// backward and the scale/rotation backward, from the view's summed render gradients.
-// Used once per (Gaussian, view) by gauss_bwd_views_kernel.  It is the same math as
-// gauss_bwd_kernel's body, which keeps its own inline copy: there the outputs are stored as
-// soon as they are formed, and routing the single-view kernel through this function
-// measured 118 -> 124 us (r1af).  Keep the two in step.
+// backward and the scale/rotation backward, from the view's summed render gradients.  The one
+// copy of this math: gauss_bwd_kernel runs it once per Gaussian, gauss_bwd_views_kernel once
+// per (Gaussian, view).  The outputs leave through the caller's sink as soon as each is formed
+// (the single-view kernel stores them there and then, which keeps its register peak down; the
+// multi-view kernel sums them over the views).  Sink interface:
+//   dop(float)  dcov(const float (&)[6])  dmean(float3)  scale_rot(bool have, float3, float4)
+//   sh_defer(float3 view vector, float3 masked colour gradient)   (kShDefer only)
 struct ViewCam {
     const float* V;       // viewmatrix, 16 floats (column-major)
     const float* Pm;      // projmatrix
@@ -346,19 +348,36 @@ struct GaussIn {
     float4 q;              // rotation (when have_scales)
     const float* cov3D;    // 6 floats, or null
     float scale_modifier;
-    float opacity;         // for the AA chain
+    const float* opacity;  // the Gaussian's opacity (read by the AA chain only)
 };
-struct ViewOut {
-    float3 dmean;
-    float dop;
-    float dcov[6];
-    float3 dscale;
-    float4 drot;
-};
+// SH colour backward of view_backward (when do_sh: the colours came from SH, not precomputed):
+// now (through the accessor, adding the view-direction term to dL/dmean3D), or deferred (the
+// caller runs it later from what sink.sh_defer receives, then stores dL/dmean3D itself).
+enum { kShNow = 1, kShDefer = 2 };
 
+// d(normalize(v))/dv applied to the direction gradient (dnormvdv, CR/auxiliary.h:129-139),
+// added to dmean.
+__device__ __forceinline__ void add_dir_grad(float3 v, float ddx, float ddy, float ddz, float3& dmean) {
+    const float sum2 = v.x * v.x + v.y * v.y + v.z * v.z;
+    const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
+    dmean.x += ((sum2 - v.x * v.x) * ddx - v.y * v.x * ddy - v.z * v.x * ddz) * invsum32;
+    dmean.y += (-v.x * v.y * ddx + (sum2 - v.y * v.y) * ddy - v.z * v.y * ddz) * invsum32;
+    dmean.z += (-v.x * v.z * ddx - v.y * v.z * ddy + (sum2 - v.z * v.z) * ddz) * invsum32;
+}
+
+// SH colour backward for view vector v (mean - campos) and colour gradient g: dL/dSH through the
+// accessor, the direction term added to dmean (CR/backward.cu:12-146).
 template <class ShAcc>
+__device__ __forceinline__ void sh_dir_backward(const ShAcc& sh, int D, int M, float3 v, float3 g, float3& dmean) {
+    const float len = sqrtf(v.x * v.x + v.y * v.y + v.z * v.z);
+    float ddx, ddy, ddz;
+    sh_backward(sh, D, M, v.x / len, v.y / len, v.z / len, g, ddx, ddy, ddz);
+    add_dir_grad(v, ddx, ddy, ddz, dmean);
+}
+
+template <int SHM, class ShAcc, class Sink>
 __device__ __forceinline__ void view_backward(const ViewCam& c, const GaussIn& gi, float4 sa, float4 sb, float2 sc,
-                                              uint8_t cm, bool do_sh, int D, int M, const ShAcc& sh, ViewOut& o) {
+                                              uint8_t cm, bool do_sh, int D, int M, const ShAcc& sh, Sink& out) {
     const float3 dcol = make_float3(sa.x, sa.y, sa.z);
     const float dinvd = sa.w;
     const float m2x = sb.x, m2y = sb.y;
@@ -420,7 +439,7 @@ __device__ __forceinline__ void view_backward(const ViewCam& c, const GaussIn& g
         c_yy += h_var;
         const float det_cov_plus_h_cov = c_xx * c_yy - c_xy * c_xy;
         const float h = sqrtf(fmaxf(0.000025f, det_cov / det_cov_plus_h_cov));
-        const float d_h = dop * gi.opacity;
+        const float d_h = dop * *gi.opacity;
         dop = dop * h;
         d_inside_root = (det_cov / det_cov_plus_h_cov) <= 0.000025f ? 0.f : d_h / (2.f * h);
     } else {
@@ -444,7 +463,7 @@ __device__ __forceinline__ void view_backward(const ViewCam& c, const GaussIn& g
         dL_dc_yy += denom2inv * (-c_xx * c_xx * dcc + 2.f * c_xx * c_xy * dcb + (denom - c_xx * c_yy) * dca);
         dL_dc_xy += denom2inv * 2.f * (c_xy * c_yy * dca - (denom + 2.f * c_xy * c_xy) * dcb + c_xx * c_xy * dcc);
     }
-    o.dop = dop;
+    out.dop(dop);
 
     // tail: cov2D = A Sigma A^T  ->  dL/dcov3D (6 stored entries) and dL/dA
     const float ga = dL_dc_xx, gb = dL_dc_xy, gc = dL_dc_yy;
@@ -455,7 +474,7 @@ __device__ __forceinline__ void view_backward(const ViewCam& c, const GaussIn& g
     dcov[1] = 2.f * A0[0] * A0[1] * ga + (A0[0] * A1[1] + A0[1] * A1[0]) * gb + 2.f * A1[0] * A1[1] * gc;
     dcov[2] = 2.f * A0[0] * A0[2] * ga + (A0[0] * A1[2] + A0[2] * A1[0]) * gb + 2.f * A1[0] * A1[2] * gc;
     dcov[4] = 2.f * A0[2] * A0[1] * ga + (A0[1] * A1[2] + A0[2] * A1[1]) * gb + 2.f * A1[1] * A1[2] * gc;
-    for (int k = 0; k < 6; k++) o.dcov[k] = dcov[k];
+    out.dcov(dcov);
 
     float dA0[3], dA1[3];
     for (int k = 0; k < 3; k++) {
@@ -486,21 +505,16 @@ __device__ __forceinline__ void view_backward(const ViewCam& c, const GaussIn& g
     dmean.y += (Pm[4] * m_w - Pm[7] * mul1) * m2x + (Pm[5] * m_w - Pm[7] * mul2) * m2y;
     dmean.z += (Pm[8] * m_w - Pm[11] * mul1) * m2x + (Pm[9] * m_w - Pm[11] * mul2) * m2y;
 
-    // ---- SH colour backward (CR/backward.cu:12-146)
+    // ---- SH colour backward (CR/backward.cu:12-146), the clamp mask zeroing its channels (:26-28)
     if (do_sh) {
         const float3 v = make_float3(mean.x - c.campos[0], mean.y - c.campos[1], mean.z - c.campos[2]);
-        const float len = sqrtf(v.x * v.x + v.y * v.y + v.z * v.z);
         const float3 g = make_float3((cm & 1) ? 0.f : dcol.x, (cm & 2) ? 0.f : dcol.y, (cm & 4) ? 0.f : dcol.z);
-        float ddx, ddy, ddz;
-        sh_backward(sh, D, M, v.x / len, v.y / len, v.z / len, g, ddx, ddy, ddz);
-        // dnormvdv (CR/auxiliary.h:129-139)
-        const float sum2 = v.x * v.x + v.y * v.y + v.z * v.z;
-        const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
-        dmean.x += ((sum2 - v.x * v.x) * ddx - v.y * v.x * ddy - v.z * v.x * ddz) * invsum32;
-        dmean.y += (-v.x * v.y * ddx + (sum2 - v.y * v.y) * ddy - v.z * v.y * ddz) * invsum32;
-        dmean.z += (-v.x * v.z * ddx - v.y * v.z * ddy + (sum2 - v.z * v.z) * ddz) * invsum32;
+        if constexpr (SHM == kShNow)
+            sh_dir_backward(sh, D, M, v, g, dmean);
+        else
+            out.sh_defer(v, g);
     }
-    o.dmean = dmean;
+    out.dmean(dmean);
 
     // ---- scale / rotation backward (CR/backward.cu:296-365, called when scales are given, :427-428)
     if (gi.have_scales) {
@@ -522,7 +536,7 @@ __device__ __forceinline__ void view_backward(const ViewCam& c, const GaussIn& g
         const float ds0 = Rg[0][0] * dMt[0][0] + Rg[1][0] * dMt[0][1] + Rg[2][0] * dMt[0][2];
         const float ds1 = Rg[0][1] * dMt[1][0] + Rg[1][1] * dMt[1][1] + Rg[2][1] * dMt[1][2];
         const float ds2 = Rg[0][2] * dMt[2][0] + Rg[1][2] * dMt[2][1] + Rg[2][2] * dMt[2][2];
-        o.dscale = make_float3(ds0, ds1, ds2);
+        const float3 dscale = make_float3(ds0, ds1, ds2);
         for (int i = 0; i < 3; i++)
             for (int kk = 0; kk < 3; kk++) dMt[i][kk] *= s[i];
         float4 dq;
@@ -534,10 +548,9 @@ __device__ __forceinline__ void view_backward(const ViewCam& c, const GaussIn& g
                2.f * z * (dMt[1][2] + dMt[2][1]) - 4.f * y * (dMt[2][2] + dMt[0][0]);
         dq.w = 2.f * r_ * (dMt[0][1] - dMt[1][0]) + 2.f * x * (dMt[2][0] + dMt[0][2]) +
                2.f * y * (dMt[1][2] + dMt[2][1]) - 4.f * z * (dMt[1][1] + dMt[0][0]);
-        o.drot = dq;
+        out.scale_rot(true, dscale, dq);
     } else {
-        o.dscale = make_float3(0.f, 0.f, 0.f);
-        o.drot = make_float4(0.f, 0.f, 0.f, 0.f);
+        out.scale_rot(false, make_float3(0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f));
     }
 }
 
@@ -633,213 +646,65 @@ __global__ void __launch_bounds__(64) GSR_GB_OCCUPANCY gauss_bwd_kernel(GaussBwd
         }
     }
     if (visible) {
-        // ---- summed render gradients of this Gaussian (loaded above)
-        const float3 dcol = make_float3(sa.x, sa.y, sa.z);
-        const float dinvd = sa.w;
-        const float m2x = sb.x, m2y = sb.y;
-        float dop = sb.z;
-        // dL/dconic in the reference's convention (CR/backward.cu:604-606)
-        const float dca = sc.x, dcb = sb.w, dcc = sc.y;
-        store3(a.dL_dmean2D, idx, m2x, m2y, 0.f);
-        store3(a.dL_dcolor, idx, dcol.x, dcol.y, dcol.z);
-        if (a.dL_dconic) reinterpret_cast<float4*>(a.dL_dconic)[idx] = make_float4(dca, dcb, 0.f, dcc);
-        if (a.dL_dinvdepth) a.dL_dinvdepth[idx] = dinvd;
+        // ---- summed render gradients of this Gaussian (loaded above): colour, inverse depth,
+        // mean2D, opacity, and dL/dconic in the reference's convention (CR/backward.cu:604-606)
+        store3(a.dL_dmean2D, idx, sb.x, sb.y, 0.f);
+        store3(a.dL_dcolor, idx, sa.x, sa.y, sa.z);
+        if (a.dL_dconic) reinterpret_cast<float4*>(a.dL_dconic)[idx] = make_float4(sc.x, sb.w, 0.f, sc.y);
+        if (a.dL_dinvdepth) a.dL_dinvdepth[idx] = sa.w;
 
-        // ---- computeCov2DCUDA
-        const float* V = a.viewmatrix;
-        const float3 mean = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
-        float3 t = xform_point_4x3(mean, V);
-        const float limx = 1.3f * a.tan_fovx, limy = 1.3f * a.tan_fovy;
-        const float txtz = t.x / t.z, tytz = t.y / t.z;
-        t.x = fminf(limx, fmaxf(-limx, txtz)) * t.z;
-        t.y = fminf(limy, fmaxf(-limy, tytz)) * t.z;
-        const float x_grad_mul = txtz < -limx || txtz > limx ? 0.f : 1.f;
-        const float y_grad_mul = tytz < -limy || tytz > limy ? 0.f : 1.f;
-        const float fx = a.focal_x, fy = a.focal_y;
-        const float j00 = fx / t.z, j02 = -(fx * t.x) / (t.z * t.z);
-        const float j11 = fy / t.z, j12 = -(fy * t.y) / (t.z * t.z);
-        // A = J * Rv, rows A0 (x) and A1 (y); Rv rows (V0,V4,V8) (V1,V5,V9) (V2,V6,V10)
-        const float A0[3] = {j00 * V[0] + j02 * V[2], j00 * V[4] + j02 * V[6], j00 * V[8] + j02 * V[10]};
-        const float A1[3] = {j11 * V[1] + j12 * V[2], j11 * V[5] + j12 * V[6], j11 * V[9] + j12 * V[10]};
-
-        float cov[6];
-        float3 sc3 = make_float3(0.f, 0.f, 0.f);
-        float4 q = make_float4(1.f, 0.f, 0.f, 0.f);
+        // ---- computeCov2DCUDA, the mean chain, SH and scale/rotation (view_backward, one view)
+        const ViewCam cam{a.viewmatrix, a.projmatrix, a.campos, a.tan_fovx, a.tan_fovy,
+                          a.focal_x,    a.focal_y,    a.antialiasing, a.have_invdepth};
+        GaussIn gi;
+        gi.mean = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
+        gi.have_scales = a.scales != nullptr;
+        gi.sc3 = make_float3(0.f, 0.f, 0.f);
+        gi.q = make_float4(1.f, 0.f, 0.f, 0.f);
         if (a.scales) {
-            sc3 = make_float3(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]);
-            q = reinterpret_cast<const float4*>(a.rotations)[idx];
+            gi.sc3 = make_float3(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]);
+            gi.q = reinterpret_cast<const float4*>(a.rotations)[idx];
         }
-        if (a.cov3D_precomp) {
-            for (int k = 0; k < 6; k++) cov[k] = a.cov3D_precomp[6 * idx + k];
-        } else {
-            const float r_ = q.x, x = q.y, y = q.z, z = q.w;
-            const float sx = a.scale_modifier * sc3.x, sy = a.scale_modifier * sc3.y, sz = a.scale_modifier * sc3.z;
-            const float L00 = (1.f - 2.f * (y * y + z * z)) * sx, L01 = 2.f * (x * y - r_ * z) * sy,
-                        L02 = 2.f * (x * z + r_ * y) * sz;
-            const float L10 = 2.f * (x * y + r_ * z) * sx, L11 = (1.f - 2.f * (x * x + z * z)) * sy,
-                        L12 = 2.f * (y * z - r_ * x) * sz;
-            const float L20 = 2.f * (x * z - r_ * y) * sx, L21 = 2.f * (y * z + r_ * x) * sy,
-                        L22 = (1.f - 2.f * (x * x + y * y)) * sz;
-            cov[0] = L00 * L00 + L01 * L01 + L02 * L02;
-            cov[1] = L00 * L10 + L01 * L11 + L02 * L12;
-            cov[2] = L00 * L20 + L01 * L21 + L02 * L22;
-            cov[3] = L10 * L10 + L11 * L11 + L12 * L12;
-            cov[4] = L10 * L20 + L11 * L21 + L12 * L22;
-            cov[5] = L20 * L20 + L21 * L21 + L22 * L22;
-        }
-        const float SA0[3] = {cov[0] * A0[0] + cov[1] * A0[1] + cov[2] * A0[2],
-                              cov[1] * A0[0] + cov[3] * A0[1] + cov[4] * A0[2],
-                              cov[2] * A0[0] + cov[4] * A0[1] + cov[5] * A0[2]};
-        const float SA1[3] = {cov[0] * A1[0] + cov[1] * A1[1] + cov[2] * A1[2],
-                              cov[1] * A1[0] + cov[3] * A1[1] + cov[4] * A1[2],
-                              cov[2] * A1[0] + cov[4] * A1[1] + cov[5] * A1[2]};
-        float c_xx = A0[0] * SA0[0] + A0[1] * SA0[1] + A0[2] * SA0[2];
-        const float c_xy = A0[0] * SA1[0] + A0[1] * SA1[1] + A0[2] * SA1[2];
-        float c_yy = A1[0] * SA1[0] + A1[1] * SA1[1] + A1[2] * SA1[2];
-
-        constexpr float h_var = 0.3f;
-        float d_inside_root = 0.f;
-        if (a.antialiasing) {
-            const float det_cov = c_xx * c_yy - c_xy * c_xy;
-            c_xx += h_var;
-            c_yy += h_var;
-            const float det_cov_plus_h_cov = c_xx * c_yy - c_xy * c_xy;
-            const float h = sqrtf(fmaxf(0.000025f, det_cov / det_cov_plus_h_cov));
-            const float d_h = dop * a.opacities[idx];
-            dop = dop * h;
-            d_inside_root = (det_cov / det_cov_plus_h_cov) <= 0.000025f ? 0.f : d_h / (2.f * h);
-        } else {
-            c_xx += h_var;
-            c_yy += h_var;
-        }
-        float dL_dc_xx = 0.f, dL_dc_xy = 0.f, dL_dc_yy = 0.f;
-        if (a.antialiasing) {
-            // the reference's formula (CR/backward.cu:256-270), at the dilated x, y as written there
-            const float x = c_xx, y = c_yy, z = c_xy, w = h_var;
-            const float qd = w * w + w * (x + y) + x * y - z * z;
-            const float denom_f = d_inside_root / (qd * qd);
-            dL_dc_xx = w * (w * y + y * y + z * z) * denom_f;
-            dL_dc_yy = w * (w * x + x * x + z * z) * denom_f;
-            dL_dc_xy = -2.f * w * z * (w + x + y) * denom_f;
-        }
-        const float denom = c_xx * c_yy - c_xy * c_xy;
-        const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
-        if (denom2inv != 0.f) {
-            dL_dc_xx += denom2inv * (-c_yy * c_yy * dca + 2.f * c_xy * c_yy * dcb + (denom - c_xx * c_yy) * dcc);
-            dL_dc_yy += denom2inv * (-c_xx * c_xx * dcc + 2.f * c_xx * c_xy * dcb + (denom - c_xx * c_yy) * dca);
-            dL_dc_xy += denom2inv * 2.f * (c_xy * c_yy * dca - (denom + 2.f * c_xy * c_xy) * dcb + c_xx * c_xy * dcc);
-        }
-        a.dL_dopacity[idx] = dop;
-
-        // tail: cov2D = A Sigma A^T  ->  dL/dcov3D (6 stored entries) and dL/dA
-        const float ga = dL_dc_xx, gb = dL_dc_xy, gc = dL_dc_yy;
-        float dcov[6];
-        dcov[0] = A0[0] * A0[0] * ga + A0[0] * A1[0] * gb + A1[0] * A1[0] * gc;
-        dcov[3] = A0[1] * A0[1] * ga + A0[1] * A1[1] * gb + A1[1] * A1[1] * gc;
-        dcov[5] = A0[2] * A0[2] * ga + A0[2] * A1[2] * gb + A1[2] * A1[2] * gc;
-        dcov[1] = 2.f * A0[0] * A0[1] * ga + (A0[0] * A1[1] + A0[1] * A1[0]) * gb + 2.f * A1[0] * A1[1] * gc;
-        dcov[2] = 2.f * A0[0] * A0[2] * ga + (A0[0] * A1[2] + A0[2] * A1[0]) * gb + 2.f * A1[0] * A1[2] * gc;
-        dcov[4] = 2.f * A0[2] * A0[1] * ga + (A0[1] * A1[2] + A0[2] * A1[1]) * gb + 2.f * A1[1] * A1[2] * gc;
-        for (int k = 0; k < 6; k++) a.dL_dcov3D[6 * idx + k] = dcov[k];
-
-        float dA0[3], dA1[3];
-        for (int k = 0; k < 3; k++) {
-            dA0[k] = 2.f * ga * SA0[k] + gb * SA1[k];
-            dA1[k] = 2.f * gc * SA1[k] + gb * SA0[k];
-        }
-        const float dJ00 = dA0[0] * V[0] + dA0[1] * V[4] + dA0[2] * V[8];
-        const float dJ02 = dA0[0] * V[2] + dA0[1] * V[6] + dA0[2] * V[10];
-        const float dJ11 = dA1[0] * V[1] + dA1[1] * V[5] + dA1[2] * V[9];
-        const float dJ12 = dA1[0] * V[2] + dA1[1] * V[6] + dA1[2] * V[10];
-        const float tz = 1.f / t.z, tz2 = tz * tz, tz3 = tz2 * tz;
-        const float dL_dtx = x_grad_mul * -fx * tz2 * dJ02;
-        const float dL_dty = y_grad_mul * -fy * tz2 * dJ12;
-        float dL_dtz =
-            -fx * tz2 * dJ00 - fy * tz2 * dJ11 + (2.f * fx * t.x) * tz3 * dJ02 + (2.f * fy * t.y) * tz3 * dJ12;
-        if (a.have_invdepth) dL_dtz -= dinvd / (t.z * t.z);
-        // transformVec4x3Transpose (CR/auxiliary.h:109-117)
-        float3 dmean = make_float3(V[0] * dL_dtx + V[1] * dL_dty + V[2] * dL_dtz,
-                                   V[4] * dL_dtx + V[5] * dL_dty + V[6] * dL_dtz,
-                                   V[8] * dL_dtx + V[9] * dL_dty + V[10] * dL_dtz);
-
-        // ---- screen-space mean -> 3-D mean through the projection (CR/backward.cu:403-420)
-        const float* Pm = a.projmatrix;
-        const float4 m_hom = xform_point_4x4(mean, Pm);
-        const float m_w = 1.0f / (m_hom.w + 0.0000001f);
-        const float mul1 = m_hom.x * m_w * m_w, mul2 = m_hom.y * m_w * m_w;
-        dmean.x += (Pm[0] * m_w - Pm[3] * mul1) * m2x + (Pm[1] * m_w - Pm[3] * mul2) * m2y;
-        dmean.y += (Pm[4] * m_w - Pm[7] * mul1) * m2x + (Pm[5] * m_w - Pm[7] * mul2) * m2y;
-        dmean.z += (Pm[8] * m_w - Pm[11] * mul1) * m2x + (Pm[9] * m_w - Pm[11] * mul2) * m2y;
-
-        // ---- SH colour backward (CR/backward.cu:12-146)
-        if (kShLate && (a.shs || a.dc)) {
-            sh_late = true;
-            sh_v = make_float3(mean.x - a.campos[0], mean.y - a.campos[1], mean.z - a.campos[2]);
-            const uint8_t cm = a.geom.clamped[idx];
-            sh_g = make_float3((cm & 1) ? 0.f : dcol.x, (cm & 2) ? 0.f : dcol.y, (cm & 4) ? 0.f : dcol.z);
-        } else if (a.shs || a.dc) {
-            const float3 v = make_float3(mean.x - a.campos[0], mean.y - a.campos[1], mean.z - a.campos[2]);
-            const float len = sqrtf(v.x * v.x + v.y * v.y + v.z * v.z);
-            const uint8_t cm = a.geom.clamped[idx];
-            const float3 g = make_float3((cm & 1) ? 0.f : dcol.x, (cm & 2) ? 0.f : dcol.y, (cm & 4) ? 0.f : dcol.z);
-            float ddx, ddy, ddz;
-            if constexpr (SH_MODE != kShGlobal) {
-                sh_backward(ShLds{&s_sh[lane * kShStride]}, a.D, M, v.x / len, v.y / len, v.z / len, g, ddx, ddy,
-                            ddz);
-            } else {
-                sh_backward(ShGlobal{sh_src, sh_dst, idx}, a.D, M, v.x / len, v.y / len, v.z / len, g, ddx, ddy, ddz);
+        gi.cov3D = a.cov3D_precomp ? a.cov3D_precomp + 6 * idx : nullptr;
+        gi.scale_modifier = a.scale_modifier;
+        gi.opacity = a.opacities + idx;
+        // outputs stored as they are formed; dL/dmean3D waits for a deferred SH pass
+        struct Sink {
+            const GaussBwdArgs& a;
+            int idx;
+            bool& sh_late;
+            float3 &sh_v, &sh_g, &dmean_late;
+            __device__ __forceinline__ void dop(float v) const { a.dL_dopacity[idx] = v; }
+            __device__ __forceinline__ void dcov(const float (&d)[6]) const {
+                for (int k = 0; k < 6; k++) a.dL_dcov3D[6 * idx + k] = d[k];
             }
-            // dnormvdv (CR/auxiliary.h:129-139)
-            const float sum2 = v.x * v.x + v.y * v.y + v.z * v.z;
-            const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
-            dmean.x += ((sum2 - v.x * v.x) * ddx - v.y * v.x * ddy - v.z * v.x * ddz) * invsum32;
-            dmean.y += (-v.x * v.y * ddx + (sum2 - v.y * v.y) * ddy - v.z * v.y * ddz) * invsum32;
-            dmean.z += (-v.x * v.z * ddx - v.y * v.z * ddy + (sum2 - v.z * v.z) * ddz) * invsum32;
-        } else if (a.dL_dsh || a.dL_ddc) {
+            __device__ __forceinline__ void sh_defer(float3 v, float3 g) const {
+                sh_late = true;
+                sh_v = v;
+                sh_g = g;
+            }
+            __device__ __forceinline__ void dmean(float3 m) const {
+                if (sh_late)
+                    dmean_late = m;  // stored after the SH pass adds the direction term
+                else
+                    store3(a.dL_dmean3D, idx, m.x, m.y, m.z);
+            }
+            __device__ __forceinline__ void scale_rot(bool have, float3 ds, float4 dq) const {
+                if (have || a.dL_dscale) store3(a.dL_dscale, idx, ds.x, ds.y, ds.z);
+                if (have || a.dL_drot) reinterpret_cast<float4*>(a.dL_drot)[idx] = dq;
+            }
+        } sink{a, idx, sh_late, sh_v, sh_g, dmean_late};
+        const bool do_sh = a.shs || a.dc;
+        const uint8_t cm = do_sh ? a.geom.clamped[idx] : 0;
+        if constexpr (kShLate)
+            view_backward<kShDefer>(cam, gi, sa, sb, sc, cm, do_sh, a.D, M, ShLds{nullptr}, sink);
+        else if constexpr (SH_MODE != kShGlobal)
+            view_backward<kShNow>(cam, gi, sa, sb, sc, cm, do_sh, a.D, M, ShLds{&s_sh[lane * kShStride]}, sink);
+        else
+            view_backward<kShNow>(cam, gi, sa, sb, sc, cm, do_sh, a.D, M, ShGlobal{sh_src, sh_dst, idx}, sink);
+        if (!do_sh && (a.dL_dsh || a.dL_ddc)) {  // colours precomputed: dL/dSH is zero
             const ShGlobal acc{sh_src, sh_dst, idx};
             for (int k = 0; k < M; k++) acc.store(k, make_float3(0.f, 0.f, 0.f));
-        }
-        if (sh_late)
-            dmean_late = dmean;  // stored after the SH pass adds the direction term
-        else
-            store3(a.dL_dmean3D, idx, dmean.x, dmean.y, dmean.z);
-
-        // ---- scale / rotation backward (CR/backward.cu:296-365, called when scales are given, :427-428)
-        if (a.scales) {
-            const float r_ = q.x, x = q.y, y = q.z, z = q.w;
-            // Rg[col][row] = the reference's GLM rotation (R_std transposed)
-            const float Rg[3][3] = {{1.f - 2.f * (y * y + z * z), 2.f * (x * y - r_ * z), 2.f * (x * z + r_ * y)},
-                                    {2.f * (x * y + r_ * z), 1.f - 2.f * (x * x + z * z), 2.f * (y * z - r_ * x)},
-                                    {2.f * (x * z - r_ * y), 2.f * (y * z + r_ * x), 1.f - 2.f * (x * x + y * y)}};
-            const float s[3] = {a.scale_modifier * sc3.x, a.scale_modifier * sc3.y, a.scale_modifier * sc3.z};
-            const float dS[3][3] = {{dcov[0], 0.5f * dcov[1], 0.5f * dcov[2]},
-                                    {0.5f * dcov[1], dcov[3], 0.5f * dcov[4]},
-                                    {0.5f * dcov[2], 0.5f * dcov[4], dcov[5]}};
-            // dMt[r][c] = dL_dM[c][r], dL_dM = 2 M dSigma (GLM product), M[k][r] = s_r Rg[k][r]
-            float dMt[3][3];
-            for (int c = 0; c < 3; c++)
-                for (int rr = 0; rr < 3; rr++)
-                    dMt[rr][c] = 2.f * s[rr] * (Rg[0][rr] * dS[c][0] + Rg[1][rr] * dS[c][1] + Rg[2][rr] * dS[c][2]);
-            // dot(Rt[i], dL_dMt[i]) -- the reference leaves the scale modifier out here
-            const float ds0 = Rg[0][0] * dMt[0][0] + Rg[1][0] * dMt[0][1] + Rg[2][0] * dMt[0][2];
-            const float ds1 = Rg[0][1] * dMt[1][0] + Rg[1][1] * dMt[1][1] + Rg[2][1] * dMt[1][2];
-            const float ds2 = Rg[0][2] * dMt[2][0] + Rg[1][2] * dMt[2][1] + Rg[2][2] * dMt[2][2];
-            store3(a.dL_dscale, idx, ds0, ds1, ds2);
-            for (int i = 0; i < 3; i++)
-                for (int kk = 0; kk < 3; kk++) dMt[i][kk] *= s[i];
-            float4 dq;
-            dq.x = 2.f * z * (dMt[0][1] - dMt[1][0]) + 2.f * y * (dMt[2][0] - dMt[0][2]) +
-                   2.f * x * (dMt[1][2] - dMt[2][1]);
-            dq.y = 2.f * y * (dMt[1][0] + dMt[0][1]) + 2.f * z * (dMt[2][0] + dMt[0][2]) +
-                   2.f * r_ * (dMt[1][2] - dMt[2][1]) - 4.f * x * (dMt[2][2] + dMt[1][1]);
-            dq.z = 2.f * x * (dMt[1][0] + dMt[0][1]) + 2.f * r_ * (dMt[2][0] - dMt[0][2]) +
-                   2.f * z * (dMt[1][2] + dMt[2][1]) - 4.f * y * (dMt[2][2] + dMt[0][0]);
-            dq.w = 2.f * r_ * (dMt[0][1] - dMt[1][0]) + 2.f * x * (dMt[2][0] + dMt[0][2]) +
-                   2.f * y * (dMt[1][2] + dMt[2][1]) - 4.f * z * (dMt[1][1] + dMt[0][0]);
-            reinterpret_cast<float4*>(a.dL_drot)[idx] = dq;
-        } else {
-            if (a.dL_dscale) store3(a.dL_dscale, idx, 0.f, 0.f, 0.f);
-            if (a.dL_drot) reinterpret_cast<float4*>(a.dL_drot)[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
     }
 
@@ -860,16 +725,15 @@ __global__ void __launch_bounds__(64) GSR_GB_OCCUPANCY gauss_bwd_kernel(GaussBwd
             if ((lane >> 5) == half && idx < a.P) {
                 float* row = &s_sh[(lane & 31) * kShStride];
                 if (sh_late) {
-                    const float len = sqrtf(sh_v.x * sh_v.x + sh_v.y * sh_v.y + sh_v.z * sh_v.z);
-                    float ddx, ddy, ddz;
-                    sh_backward(ShLds{row}, a.D, M, sh_v.x / len, sh_v.y / len, sh_v.z / len, sh_g, ddx, ddy, ddz);
-                    const float3 v = sh_v;
-                    const float sum2 = v.x * v.x + v.y * v.y + v.z * v.z;
-                    const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
+                    // split layout: pin the view vector here -- otherwise the compiler evaluates the SH
+                    // basis ahead of the row gather and the barrier, and the values held across it push
+                    // the list kernel to 1-3 waves per SIMD.  (The pin moves no arithmetic: with SLP
+                    // vectorisation off and contraction per expression, build.py, both layouts round
+                    // alike -- test_separate_sh.)
+                    float3 v = sh_v;
+                    if constexpr (SH_MODE == kShLdsSplit) asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z));
                     float3 dm = dmean_late;
-                    dm.x += ((sum2 - v.x * v.x) * ddx - v.y * v.x * ddy - v.z * v.x * ddz) * invsum32;
-                    dm.y += (-v.x * v.y * ddx + (sum2 - v.y * v.y) * ddy - v.z * v.y * ddz) * invsum32;
-                    dm.z += (-v.x * v.z * ddx - v.y * v.z * ddy + (sum2 - v.z * v.z) * ddz) * invsum32;
+                    sh_dir_backward(ShLds{row}, a.D, M, v, sh_g, dm);
                     store3(a.dL_dmean3D, idx, dm.x, dm.y, dm.z);
                 } else if (!a.sparse || SH_MODE == kShLdsSplit) {  // split: see sh_stage_out
                     for (int k = 0; k < kShRowF; k += 4)
@@ -1056,12 +920,25 @@ __global__ void __launch_bounds__(64) GSR_VIEWS_OCCUPANCY gauss_bwd_views_kernel
         gi.q = reinterpret_cast<const float4*>(a.rotations)[idx];
         gi.cov3D = nullptr;
         gi.scale_modifier = a.scale_modifier;
-        gi.opacity = a.opacities[idx];
+        gi.opacity = a.opacities + idx;
         const ShReadOnly<SH_MODE != kShGlobal> shr{SH_MODE != kShGlobal ? &s_sh[lane * kShStride] : nullptr, sh_src,
                                                    idx};
-        float3 dmean = make_float3(0.f, 0.f, 0.f), dscale = dmean;
-        float4 drot = make_float4(0.f, 0.f, 0.f, 0.f);
-        float dop = 0.f;
+        // the parameter gradients summed over the views (dL/dcov3D is not an output here)
+        struct Sink {
+            float3 dmean_sum = make_float3(0.f, 0.f, 0.f), dscale_sum = make_float3(0.f, 0.f, 0.f);
+            float4 drot_sum = make_float4(0.f, 0.f, 0.f, 0.f);
+            float dop_sum = 0.f;
+            __device__ __forceinline__ void dop(float v) { dop_sum += v; }
+            __device__ __forceinline__ void dcov(const float (&)[6]) {}
+            __device__ __forceinline__ void sh_defer(float3, float3) {}
+            __device__ __forceinline__ void dmean(float3 m) {
+                dmean_sum.x += m.x; dmean_sum.y += m.y; dmean_sum.z += m.z;
+            }
+            __device__ __forceinline__ void scale_rot(bool, float3 ds, float4 dq) {
+                dscale_sum.x += ds.x; dscale_sum.y += ds.y; dscale_sum.z += ds.z;
+                drot_sum.x += dq.x; drot_sum.y += dq.y; drot_sum.z += dq.z; drot_sum.w += dq.w;
+            }
+        } sink;
 #if GSR_VIEWS_FLAG_PREFETCH  // (the next view's flag word loads while this view is evaluated)
         uint32_t flags_next = a.n_views > 0 ? view_flag<PACKED>(a, a.blocks, 0, idx) : 0u;
 #endif
@@ -1081,17 +958,12 @@ __global__ void __launch_bounds__(64) GSR_VIEWS_OCCUPANCY gauss_bwd_views_kernel
             float4 sa, sb;
             float2 sc;
             view_sums<PACKED>(a, blk, flags, idx, sa, sb, sc);
-            ViewOut o;
-            view_backward(cam, gi, sa, sb, sc, (uint8_t)((flags >> 1) & 7u), true, a.D, M, shr, o);
-            dmean.x += o.dmean.x; dmean.y += o.dmean.y; dmean.z += o.dmean.z;
-            dop += o.dop;
-            dscale.x += o.dscale.x; dscale.y += o.dscale.y; dscale.z += o.dscale.z;
-            drot.x += o.drot.x; drot.y += o.drot.y; drot.z += o.drot.z; drot.w += o.drot.w;
+            view_backward<kShNow>(cam, gi, sa, sb, sc, (uint8_t)((flags >> 1) & 7u), true, a.D, M, shr, sink);
         }
-        store3(a.dL_dmean3D, idx, dmean.x, dmean.y, dmean.z);
-        a.dL_dopacity[idx] = dop;
-        store3(a.dL_dscale, idx, dscale.x, dscale.y, dscale.z);
-        reinterpret_cast<float4*>(a.dL_drot)[idx] = drot;
+        store3(a.dL_dmean3D, idx, sink.dmean_sum.x, sink.dmean_sum.y, sink.dmean_sum.z);
+        a.dL_dopacity[idx] = sink.dop_sum;
+        store3(a.dL_dscale, idx, sink.dscale_sum.x, sink.dscale_sum.y, sink.dscale_sum.z);
+        reinterpret_cast<float4*>(a.dL_drot)[idx] = sink.drot_sum;
     }
     // ---- phase 2: dL/dSH band by band (CR/backward.cu:43-127 products, summed over views)
     if constexpr (SH_MODE != kShGlobal) __syncthreads();  // the staged SH rows are read for the last time

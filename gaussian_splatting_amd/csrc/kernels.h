@@ -246,10 +246,20 @@ __device__ __forceinline__ void sh_stage_out(const ShGradAddr& ga, int r0, int r
 // the live-list backward's rows.  Combined layout: 16-byte pieces (12 per row, rows are 16-byte
 // aligned); split layout: dwords (45-float rest rows are only 4-byte aligned) plus the dc triple.
 // All lanes must call them (the row owners' indices travel by shuffle).
+// Loop unrolling of the gathers (the live-list gauss_bwd's SH rows).  Fully unrolled, the split
+// layout's 45-float rows take ~23 dword iterations whose addresses the compiler precomputes and
+// keeps live across the kernel: 308 VGPRs, one wave per SIMD.  One iteration at a time: 90.
+#define GSR_PRAGMA(x) _Pragma(#x)
+#ifndef GSR_GATHER_UNROLL_SPLIT
+#define GSR_GATHER_UNROLL_SPLIT 1
+#endif
+#ifndef GSR_GATHER_UNROLL_COMB
+#define GSR_GATHER_UNROLL_COMB 12
+#endif
 template <int ROWS, int THREADS, bool SPLIT>
 __device__ __forceinline__ void sh_gather_in(const ShAddr& sa, int g, int row0, float* lds, int stride, int tid) {
     if constexpr (!SPLIT) {
-#pragma unroll
+GSR_PRAGMA(unroll GSR_GATHER_UNROLL_COMB)
         for (int k = 0; k < ROWS * (kShRowF / 4) / THREADS; k++) {
             const int i4 = k * THREADS + tid, row = i4 / (kShRowF / 4), c4 = i4 - row * (kShRowF / 4);
             const int gr = __shfl(g, row0 + row);
@@ -258,11 +268,13 @@ __device__ __forceinline__ void sh_gather_in(const ShAddr& sa, int g, int row0, 
                     reinterpret_cast<const float4*>(sa.shs + (size_t)gr * kShRowF)[c4];
         }
     } else {
+GSR_PRAGMA(unroll GSR_GATHER_UNROLL_SPLIT)
         for (int k = 0; k < (ROWS * kShRestF + THREADS - 1) / THREADS; k++) {
             const int d = k * THREADS + tid, row = min(d / kShRestF, ROWS - 1), c = d - row * kShRestF;
             const int gr = __shfl(g, row0 + row);
             if (d < ROWS * kShRestF && gr >= 0) lds[row * stride + 3 + c] = sa.shs[(size_t)gr * kShRestF + c];
         }
+GSR_PRAGMA(unroll GSR_GATHER_UNROLL_SPLIT)
         for (int k = 0; k < (ROWS * 3 + THREADS - 1) / THREADS; k++) {
             const int d = k * THREADS + tid, row = min(d / 3, ROWS - 1), c = d - row * 3;
             const int gr = __shfl(g, row0 + row);
@@ -275,7 +287,7 @@ template <int ROWS, int THREADS, bool SPLIT>
 __device__ __forceinline__ void sh_gather_out(const ShGradAddr& ga, int g, int row0, const float* lds, int stride,
                                               int tid) {
     if constexpr (!SPLIT) {
-#pragma unroll
+GSR_PRAGMA(unroll GSR_GATHER_UNROLL_COMB)
         for (int k = 0; k < ROWS * (kShRowF / 4) / THREADS; k++) {
             const int i4 = k * THREADS + tid, row = i4 / (kShRowF / 4), c4 = i4 - row * (kShRowF / 4);
             const int gr = __shfl(g, row0 + row);
@@ -284,11 +296,13 @@ __device__ __forceinline__ void sh_gather_out(const ShGradAddr& ga, int g, int r
                     *reinterpret_cast<const float4*>(&lds[row * stride + 4 * c4]);
         }
     } else {
+GSR_PRAGMA(unroll GSR_GATHER_UNROLL_SPLIT)
         for (int k = 0; k < (ROWS * kShRestF + THREADS - 1) / THREADS; k++) {
             const int d = k * THREADS + tid, row = min(d / kShRestF, ROWS - 1), c = d - row * kShRestF;
             const int gr = __shfl(g, row0 + row);
             if (d < ROWS * kShRestF && gr >= 0) ga.dsh[(size_t)gr * kShRestF + c] = lds[row * stride + 3 + c];
         }
+GSR_PRAGMA(unroll GSR_GATHER_UNROLL_SPLIT)
         for (int k = 0; k < (ROWS * 3 + THREADS - 1) / THREADS; k++) {
             const int d = k * THREADS + tid, row = min(d / 3, ROWS - 1), c = d - row * 3;
             const int gr = __shfl(g, row0 + row);

@@ -122,6 +122,7 @@ template <int SH_MODE>
 __global__ void __launch_bounds__(kPreThreads) preprocess_kernel(PreprocessArgs a) {
     __shared__ __attribute__((aligned(16))) float s_buf[SH_MODE != kShGlobal ? kShHalfRows * kShRowStride : 64 * 16];
     static_assert(kShHalfRows * kShRowStride >= 64 * 16, "the record block reuses the SH buffer");
+    static_assert(kShHalfRows * kShRowStride >= kShHalfRows * (kShRestF + 3), "the split staging fits the buffer");
     const int lane = threadIdx.x;
     const int g0 = blockIdx.x * kPreThreads;
     const int idx = g0 + lane;
@@ -195,19 +196,55 @@ __global__ void __launch_bounds__(kPreThreads) preprocess_kernel(PreprocessArgs 
     }
     if (a.colors_precomp) {
         if (ok) rgb = make_float3(a.colors_precomp[3 * idx], a.colors_precomp[3 * idx + 1], a.colors_precomp[3 * idx + 2]);
-    } else if constexpr (SH_MODE != kShGlobal) {
+    } else if constexpr (SH_MODE == kShLdsCombined) {
         const ShAddr sa{a.shs, a.dc, a.M};
 #pragma unroll
         for (int half = 0; half < 2; half++) {
             const int rows = min(kShHalfRows, nvalid - half * kShHalfRows);
             if (rows > 0) {  // wave-uniform
-                sh_stage_in<kShHalfRows, kPreThreads, SH_MODE == kShLdsSplit>(sa, g0 + half * kShHalfRows, rows, s_buf, kShRowStride, lane);
+                sh_stage_in<kShHalfRows, kPreThreads, false>(sa, g0 + half * kShHalfRows, rows, s_buf, kShRowStride, lane);
                 __syncthreads();
                 if ((lane >> 5) == half && ok) {
                     const float* row = &s_buf[(lane & 31) * kShRowStride];
                     float3 sh[16];
 #pragma unroll
                     for (int k = 0; k < 16; k++) sh[k] = make_float3(row[3 * k], row[3 * k + 1], row[3 * k + 2]);
+                    rgb = sh_to_rgb(a.D, sh, dir.x, dir.y, dir.z);
+                }
+                __syncthreads();
+            }
+        }
+    } else if constexpr (SH_MODE == kShLdsSplit) {
+        // dc + rest (train.py's separate_sh path): the half's 32 rest rows (45 floats each) are one
+        // contiguous range in global memory and are kept contiguous in LDS too (row stride 45,
+        // odd: conflict-free reads), so they move as 16-byte pieces; the dc triples go to their own
+        // area behind them.  (Scattering the rest floats behind each row's dc triple took scalar
+        // LDS stores and per-float row divisions: 83 vs 63 us for the combined layout at 1M.)
+        float* s_rest = s_buf;                         // [32][45]
+        float* s_dc = s_buf + kShHalfRows * kShRestF;  // [32][3]
+#pragma unroll
+        for (int half = 0; half < 2; half++) {
+            const int rows = min(kShHalfRows, nvalid - half * kShHalfRows);
+            if (rows > 0) {  // wave-uniform
+                const int r0 = g0 + half * kShHalfRows;
+                typedef float v4f __attribute__((ext_vector_type(4)));
+                const v4f* rest = reinterpret_cast<const v4f*>(a.shs + (size_t)r0 * kShRestF);
+                const int nf = rows * kShRestF, n4 = nf >> 2;
+#pragma unroll
+                for (int k = 0; k < (kShHalfRows * kShRestF / 4 + kPreThreads - 1) / kPreThreads; k++) {
+                    const int i4 = k * kPreThreads + lane;
+                    if (i4 < n4) reinterpret_cast<v4f*>(s_rest)[i4] = __builtin_nontemporal_load(rest + i4);
+                }
+                if (lane < (nf & 3)) s_rest[n4 * 4 + lane] = a.shs[(size_t)r0 * kShRestF + n4 * 4 + lane];
+                for (int i = lane; i < rows * 3; i += kPreThreads) s_dc[i] = __builtin_nontemporal_load(a.dc + (size_t)r0 * 3 + i);
+                __syncthreads();
+                if ((lane >> 5) == half && ok) {
+                    const float* rr = &s_rest[(lane & 31) * kShRestF];
+                    const float* dr = &s_dc[(lane & 31) * 3];
+                    float3 sh[16];
+                    sh[0] = make_float3(dr[0], dr[1], dr[2]);
+#pragma unroll
+                    for (int k = 1; k < 16; k++) sh[k] = make_float3(rr[3 * k - 3], rr[3 * k - 2], rr[3 * k - 1]);
                     rgb = sh_to_rgb(a.D, sh, dir.x, dir.y, dir.z);
                 }
                 __syncthreads();

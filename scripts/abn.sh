@@ -1,10 +1,10 @@
 #!/bin/bash
 # Interleaved A/B of library variants: ROUNDS rounds of (every libgsr*.so in turn: bench stage times),
 # so clock / box drift hits every variant alike.  Parity of each variant: tests/test_gpu_parity.py once.
-# Usage: scripts/abn.sh TAG ROUNDS [CONFIG]
+# Usage: scripts/abn.sh TAG ROUNDS [CONFIG] [EXTRA BENCH FLAGS]
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-ROOT=$(pwd); OUT=$ROOT/gpurun_out/$1; R=${2:-2}; CFG=${3:-1m_1080p_sh3}; mkdir -p "$OUT"
+ROOT=$(pwd); OUT=$ROOT/gpurun_out/$1; R=${2:-2}; CFG=${3:-1m_1080p_sh3}; XF=${4:-}; mkdir -p "$OUT"
 LIBS="$ROOT/gaussian_splatting_amd/lib/libgsr.so $(ls $ROOT/gaussian_splatting_amd/lib/libgsr_*.so 2>/dev/null)"
 for lib in $LIBS; do
   v=$(basename $lib .so)
@@ -14,7 +14,7 @@ done
 for r in $(seq 1 $R); do
   for lib in $LIBS; do
     v=$(basename $lib .so)
-    GSR_LIBRARY=$lib timeout -k 10 300 python bench.py --config $CFG --no-cpu-baseline --no-census --steps 40 > "$OUT/bench_${v}_$r.json" 2> "$OUT/bench_${v}_$r.err"; rc=$?
+    GSR_LIBRARY=$lib timeout -k 10 300 python bench.py --config $CFG $XF --no-cpu-baseline --no-census --steps 40 > "$OUT/bench_${v}_$r.json" 2> "$OUT/bench_${v}_$r.err"; rc=$?
     [ $rc -eq 0 ] || { tail -3 "$OUT/bench_${v}_$r.err"; exit $rc; }
     python -c "import json; d=json.load(open('$OUT/bench_${v}_$r.json')); s=d['stage_ms']; print('$r $v', round(d['ms_per_step'],4), ' '.join(f'{k}={v*1e3:.1f}' for k,v in s.items()))"
   done
