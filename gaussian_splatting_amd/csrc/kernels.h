@@ -246,13 +246,11 @@ __device__ __forceinline__ void sh_stage_out(const ShGradAddr& ga, int r0, int r
 // the live-list backward's rows.  Combined layout: 16-byte pieces (12 per row, rows are 16-byte
 // aligned); split layout: dwords (45-float rest rows are only 4-byte aligned) plus the dc triple.
 // All lanes must call them (the row owners' indices travel by shuffle).
-// Loop unrolling of the gathers (the live-list gauss_bwd's SH rows).  Fully unrolled, the split
-// layout's 45-float rows take ~23 dword iterations whose addresses the compiler precomputes and
-// keeps live across the kernel: 308 VGPRs, one wave per SIMD.  One iteration at a time: 90.
+// Split layout: a row's floats are copied by the lanes that own the row (immediate offsets from one
+// address).  (Striped over the wave -- one dword of the block per lane and iteration -- the
+// fully unrolled loop kept ~23 iterations' addresses live across the kernel: 308 VGPRs, one wave
+// per SIMD; one iteration at a time serialised the loads.)
 #define GSR_PRAGMA(x) _Pragma(#x)
-#ifndef GSR_GATHER_UNROLL_SPLIT
-#define GSR_GATHER_UNROLL_SPLIT 1
-#endif
 #ifndef GSR_GATHER_UNROLL_COMB
 #define GSR_GATHER_UNROLL_COMB 12
 #endif
@@ -268,17 +266,29 @@ GSR_PRAGMA(unroll GSR_GATHER_UNROLL_COMB)
                     reinterpret_cast<const float4*>(sa.shs + (size_t)gr * kShRowF)[c4];
         }
     } else {
-GSR_PRAGMA(unroll GSR_GATHER_UNROLL_SPLIT)
-        for (int k = 0; k < (ROWS * kShRestF + THREADS - 1) / THREADS; k++) {
-            const int d = k * THREADS + tid, row = min(d / kShRestF, ROWS - 1), c = d - row * kShRestF;
-            const int gr = __shfl(g, row0 + row);
-            if (d < ROWS * kShRestF && gr >= 0) lds[row * stride + 3 + c] = sa.shs[(size_t)gr * kShRestF + c];
-        }
-GSR_PRAGMA(unroll GSR_GATHER_UNROLL_SPLIT)
-        for (int k = 0; k < (ROWS * 3 + THREADS - 1) / THREADS; k++) {
-            const int d = k * THREADS + tid, row = min(d / 3, ROWS - 1), c = d - row * 3;
-            const int gr = __shfl(g, row0 + row);
-            if (d < ROWS * 3 && gr >= 0) lds[row * stride + c] = sa.dc[(size_t)gr * 3 + c];
+        // THREADS / ROWS lanes per row, each copying its share of the row's 45 rest floats (one base
+        // address, immediate offsets, every load independent) and the last of them the dc triple
+        static_assert(THREADS % ROWS == 0, "whole lanes per row");
+        constexpr int L = THREADS / ROWS, PER = (kShRestF + L - 1) / L;
+        const int row = tid / L, part = tid % L;
+        const int gr = __shfl(g, row0 + row);
+        if (gr >= 0) {
+            const float* src = sa.shs + (size_t)gr * kShRestF + part * PER;
+            float* dst = lds + row * stride + 3 + part * PER;
+            const int n = kShRestF - part * PER;  // >= PER except for the last part
+            float v[PER];
+#pragma unroll
+            for (int c = 0; c < PER; c++) v[c] = c < n ? src[c] : 0.f;
+#pragma unroll
+            for (int c = 0; c < PER; c++)
+                if (c < n) dst[c] = v[c];
+            if (part == L - 1) {
+                const float* d3 = sa.dc + (size_t)gr * 3;
+                const float x = d3[0], y = d3[1], z = d3[2];
+                lds[row * stride] = x;
+                lds[row * stride + 1] = y;
+                lds[row * stride + 2] = z;
+            }
         }
     }
 }
@@ -296,17 +306,23 @@ GSR_PRAGMA(unroll GSR_GATHER_UNROLL_COMB)
                     *reinterpret_cast<const float4*>(&lds[row * stride + 4 * c4]);
         }
     } else {
-GSR_PRAGMA(unroll GSR_GATHER_UNROLL_SPLIT)
-        for (int k = 0; k < (ROWS * kShRestF + THREADS - 1) / THREADS; k++) {
-            const int d = k * THREADS + tid, row = min(d / kShRestF, ROWS - 1), c = d - row * kShRestF;
-            const int gr = __shfl(g, row0 + row);
-            if (d < ROWS * kShRestF && gr >= 0) ga.dsh[(size_t)gr * kShRestF + c] = lds[row * stride + 3 + c];
-        }
-GSR_PRAGMA(unroll GSR_GATHER_UNROLL_SPLIT)
-        for (int k = 0; k < (ROWS * 3 + THREADS - 1) / THREADS; k++) {
-            const int d = k * THREADS + tid, row = min(d / 3, ROWS - 1), c = d - row * 3;
-            const int gr = __shfl(g, row0 + row);
-            if (d < ROWS * 3 && gr >= 0) ga.ddc[(size_t)gr * 3 + c] = lds[row * stride + c];
+        static_assert(THREADS % ROWS == 0, "whole lanes per row");
+        constexpr int L = THREADS / ROWS, PER = (kShRestF + L - 1) / L;
+        const int row = tid / L, part = tid % L;
+        const int gr = __shfl(g, row0 + row);
+        if (gr >= 0) {
+            const float* src = lds + row * stride + 3 + part * PER;
+            float* dst = ga.dsh + (size_t)gr * kShRestF + part * PER;
+            const int n = kShRestF - part * PER;
+#pragma unroll
+            for (int c = 0; c < PER; c++)
+                if (c < n) dst[c] = src[c];
+            if (part == L - 1) {
+                float* d3 = ga.ddc + (size_t)gr * 3;
+                d3[0] = lds[row * stride];
+                d3[1] = lds[row * stride + 1];
+                d3[2] = lds[row * stride + 2];
+            }
         }
     }
 }
