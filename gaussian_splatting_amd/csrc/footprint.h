@@ -47,8 +47,11 @@ __device__ __forceinline__ float rect_min_form(float a, float b, float c, float 
 // Q <= 2 ln(255 o), with the same relative/absolute margin the box uses (preprocess.hip), so
 // the test stays conservative under fp32 rounding of the per-pixel evaluation.  Degenerate
 // conics keep the box result.  Runs while staging, one list entry per lane.
-__device__ __forceinline__ uint32_t quad_bits_exact(float4 v0, float4 v1, float4 v2, int tile_x0, int tile_y0) {
-    uint32_t q = quad_bits(v1, v2, tile_x0, tile_y0);
+// `only`: the quadrants to test (the others' bits come back clear) -- a half-tile render wave
+// tests its own two.
+__device__ __forceinline__ uint32_t quad_bits_exact(float4 v0, float4 v1, float4 v2, int tile_x0, int tile_y0,
+                                                    uint32_t only = 0xfu) {
+    uint32_t q = quad_bits(v1, v2, tile_x0, tile_y0) & only;
     const float a = v0.z, b = v0.w, c = v1.x, o = v1.y;
     if (q == 0 || !(a > 0.f && c > 0.f && a * c - b * b > 0.f) || !(o > 0.f)) return q;
     const float tau = fmaxf(0.f, __logf(255.f * o)) * 1.001f + 0.01f;
@@ -56,6 +59,7 @@ __device__ __forceinline__ uint32_t quad_bits_exact(float4 v0, float4 v1, float4
     const float ra = 1.f / a, rc = 1.f / c;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
+        if (!(only & (1u << k))) continue;  // (compile-time after inlining with a constant mask)
         if (!(q & (1u << k))) continue;
         const float x0 = (float)(tile_x0 + (k & 1) * 8) - v0.x, y0 = (float)(tile_y0 + (k >> 1) * 8) - v0.y;
         if (rect_min_form(a, b, c, ra, rc, x0, x0 + 7.f, y0, y0 + 7.f) > lim) q &= ~(1u << k);

@@ -46,6 +46,11 @@ constexpr int kBatch = 64;  // list entries staged per round (one per lane)
 #ifndef GSR_BWD_ANYSKIP
 #define GSR_BWD_ANYSKIP 1
 #endif
+// A/B switch: a half-tile forward wave tests only its own two quadrants of each entry's footprint
+// and ORs those bits into the entry (the other half adds its own).
+#ifndef GSR_FWD_OWN_BITS
+#define GSR_FWD_OWN_BITS 1
+#endif
 // A/B switch: the backward's ten per-entry sums carried across entries (zeroed after each
 // reduction) instead of declared per entry.
 #ifndef GSR_BWD_CARRY_R
@@ -173,11 +178,24 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const ui
             const float4 v0 = rec[0], v1 = rec[1], v2 = rec[2];
             s_xy[lane] = make_float4(v0.x, v0.y, v1.y, v1.z);
             s_col[lane] = v2;
+#if GSR_FWD_OWN_BITS
+            // this part's quadrants only; the backward (which visits only staged entries) gets every
+            // part's bits OR-ed into the entry K4 wrote with clear mask bits.  A part that stopped
+            // before an entry leaves its bits clear there: its pixels all ended earlier, so the
+            // backward has retired those slots by then (slot limits from n_contrib).
+            qm = quad_bits_exact(v0, v1, v2, tile_x0, tile_y0, kPartMask << qbase);
+            s_cq[lane] = stage_conic(v0, v1, qm >> qbase);
+            if (NPART == 1)
+                *ent = (gid << kEntryMaskBits) | qm;
+            else if (qm)
+                __hip_atomic_fetch_or(ent, qm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
             qm = quad_bits_exact(v0, v1, v2, tile_x0, tile_y0);
             s_cq[lane] = stage_conic(v0, v1, (qm >> qbase) & kPartMask);
             // all four bits, for the backward (which visits only staged entries); with two parts
             // both may store the entry, the same value
             *ent = (gid << kEntryMaskBits) | qm;
+#endif
         }
         __syncthreads();
         // Blend checkpoint (gsr_common.h): the state before entry b0, stored after this batch's
