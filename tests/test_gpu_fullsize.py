@@ -207,6 +207,36 @@ def test_fullsize_colors_precomp_matches_sh(fullsize):
     assert float(d.mean()) <= 1e-6
 
 
+def test_fullsize_separate_sh_bitwise(fullsize):
+    """The SH layout train.py passes (separate_sh: dc [P,1,3] + rest [P,15,3], the 3DGS-accel entry points)
+    gives the combined layout's image and gradients bit for bit at full size -- its own staging paths
+    (preprocess's contiguous rest rows, the live-list gauss_bwd's row gathers) over every wave of a real frame."""
+    from gaussian_splatting_amd import _C
+
+    inp, fwd, out = fullsize["inp"], fullsize["fwd"], fullsize["out_unit"]
+    dev = fwd[1].device
+    sh = inp["shs"].to(dev)
+    dc, rest = sh[:, :1].contiguous(), sh[:, 1:].contiguous()
+    d = lambda k: C._dev(inp[k], dev)  # noqa: E731
+    sep = _C.rasterize_gaussians(d("bg"), d("means3D"), d("colors_precomp"), d("opacities"), d("scales"),
+                                 d("rotations"), 1.0, d("cov3D_precomp"), d("viewmatrix"), d("projmatrix"),
+                                 inp["tanfovx"], inp["tanfovy"], inp["H"], inp["W"], dc, rest, inp["sh_degree"],
+                                 d("campos"), False, False, False)
+    assert sep[0] == fwd[0]
+    assert torch.equal(sep[1], fwd[1]) and torch.equal(sep[2], fwd[2]) and torch.equal(sep[6], fwd[6])
+    gc, gd = (t.to(dev) for t in fullsize["unit"])
+    nr, _, radii, geom, binning, img, _ = sep
+    g = _C.rasterize_gaussians_backward(d("bg"), d("means3D"), radii, d("colors_precomp"), d("opacities"),
+                                        d("scales"), d("rotations"), 1.0, d("cov3D_precomp"), d("viewmatrix"),
+                                        d("projmatrix"), inp["tanfovx"], inp["tanfovy"], gc, gd, dc, rest,
+                                        inp["sh_degree"], d("campos"), geom, nr, binning, img, False, False)
+    torch.cuda.synchronize()
+    for k, name in enumerate(["dL_dmeans2D", "dL_dcolors", "dL_dopacity", "dL_dmeans3D", "dL_dcov3D"]):
+        assert torch.equal(g[k], out[k]), name
+    assert torch.equal(g[5], out[5][:, :1]) and torch.equal(g[6], out[5][:, 1:]), "dL_ddc / dL_dsh"
+    assert torch.equal(g[7], out[6]) and torch.equal(g[8], out[7]), "dL_dscales / dL_drotations"
+
+
 def _sh_eval(sh, dirs, deg):
     """utils/sh_utils.py:57-112 restated (same polynomial and constants as CR/auxiliary.h:23-40)."""
     C0, C1 = 0.28209479177387814, 0.4886025119029199
