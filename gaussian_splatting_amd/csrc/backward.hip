@@ -208,19 +208,22 @@ __global__ void __launch_bounds__(64) gauss_reduce_kernel(int P, const uint32_t*
     float4 sa, sb;
     float2 sc;
     reduce_records(P, blockIdx.x * 64, rec_start, tiles_touched, recs, s_rec, sa, sb, sc);
-    if (g < P) {
+    // a Gaussian with a gradient (gauss_bwd's condition)
+    const bool lv = g < P && radii[g] > 0 &&
+                    ((sa.x != 0.f) | (sa.y != 0.f) | (sa.z != 0.f) | (sa.w != 0.f) | (sb.x != 0.f) |
+                     (sb.y != 0.f) | (sb.z != 0.f) | (sb.w != 0.f) | (sc.x != 0.f) | (sc.y != 0.f));
+    // With a live list (single view) gauss_bwd reads the sums of the listed Gaussians only, so the
+    // other ~87% (zeros) are not written; a view block (flags) or the dense backward reads every row.
+    if (g < P && (!live || flags || lv)) {
         sums.a[g] = sa;
         sums.b[g] = sb;
         sums.c[g] = sc;
-        // view-block flag word (gauss_bwd_views_kernel): bit 0 visible, bits 1-3 the SH clamp mask
-        if (flags) flags[g] = (radii[g] > 0 ? 1u : 0u) | ((uint32_t)(clamped[g] & 7u) << 1);
     }
+    // view-block flag word (gauss_bwd_views_kernel): bit 0 visible, bits 1-3 the SH clamp mask
+    if (g < P && flags) flags[g] = (radii[g] > 0 ? 1u : 0u) | ((uint32_t)(clamped[g] & 7u) << 1);
     if (live) {
-        // append the Gaussians with a gradient (gauss_bwd's condition) to the live list: one
-        // atomic per wave; the list order varies from run to run, each entry's result does not
-        const bool lv = g < P && radii[g] > 0 &&
-                        ((sa.x != 0.f) | (sa.y != 0.f) | (sa.z != 0.f) | (sa.w != 0.f) | (sb.x != 0.f) |
-                         (sb.y != 0.f) | (sb.z != 0.f) | (sb.w != 0.f) | (sc.x != 0.f) | (sc.y != 0.f));
+        // append them to the live list: one atomic per wave; the list order varies from run to run,
+        // each entry's result does not
         const unsigned long long m = __ballot(lv);
         if (m) {  // uniform
             const int lane = threadIdx.x;
