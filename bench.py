@@ -207,6 +207,14 @@ class HostClock:
             out[f"lib_{k}_ms"] = {"mean": round(st["total_ms"] / st["calls"], 4) if st["calls"] else None,
                                   "max": round(st["max_ms"], 4), "calls": st["calls"]}
         out["python_gc_collections"] = self.gc_runs
+        # the steps whose wall time is well above the median (a host stall leaves the GPU idle): step
+        # index, step wall / forward call / backward call (ms), so a slow run carries which step and call
+        walls = self.t["step_wall"]
+        if walls:
+            med = statistics.median(walls)
+            slow = [i for i, w in enumerate(walls) if w > 1.3 * med]
+            out["slow_steps"] = [[i, round(walls[i], 3), round(self.t["forward_call"][i], 3),
+                                  round(self.t["backward_call"][i], 3)] for i in slow[:8]]
         return out
 
 

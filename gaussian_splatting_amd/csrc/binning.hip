@@ -24,7 +24,7 @@
 //   K4 tile_sort     per tile, a bitonic network held in registers (exchanges
 //                    inside a lane, across lanes by swizzle/permute, across
 //                    waves through LDS), writing the Gaussian ids -- the tile
-//                    lists the render passes walk.  One wave per tile up to 1024
+//                    lists the render passes walk.  Two waves per tile up to 1024
 //                    keys; longer lists go to persistent kernels walking K2's
 //                    class lists.
 //
@@ -50,7 +50,7 @@ constexpr int kBinWaves = kBinThreads / 64;
 #endif
 constexpr int kBinUnroll = GSR_BIN_UNROLL;  // K0 / K1 Gaussians per thread per round (loads in flight together)
 constexpr uint32_t kLdsTilesMax = 36864;  // K3 keeps one u32 per tile in LDS (144 KiB)
-constexpr uint32_t kSortWaveMax = 1024;   // longest list tile_sort_kernel sorts (one wave per tile)
+constexpr uint32_t kSortWaveMax = 1024;   // longest list tile_sort_kernel sorts (one workgroup of kSortT per tile)
 // Longer lists go to two persistent 256-thread kernels walking K2's class lists: class 0
 // (1024, 4096], class 1 (> 4096; bucket sort up to 8192 keys, a network in global memory
 // beyond).
@@ -976,22 +976,31 @@ __device__ bool bucket_sort_list(const u64* __restrict__ keys, uint32_t lo, uint
     return true;
 }
 
-// Lists of up to kSortWaveMax keys: one wave per tile.  Short lists (<= kBucketMinN) are
+// Lists of up to kSortWaveMax keys: one workgroup (kSortT threads) per tile.  Short lists (<= kBucketMinN) are
 // sorted by a bitonic network in registers (no LDS, no barrier); longer ones by the bucket
 // sort, with the register network as its skew fallback.
 #ifndef GSR_BUCKET_MIN_N
 #define GSR_BUCKET_MIN_N 128
 #endif
 constexpr uint32_t kBucketMinN = GSR_BUCKET_MIN_N;
+// Threads per tile of the bucket sort below: 128 = two waves per tile, each holding half of the
+// tile's keys (the same LDS per tile as one wave, half the serial chain per thread: tile_sort
+// 66.6 -> 55.6-58.1 us at 1M@1080p against one wave, 62 us with four; r3y1).  The register
+// network for short or skewed lists runs on the first wave alone.
+#ifndef GSR_SORT_T
+#define GSR_SORT_T 128
+#endif
+constexpr int kSortT = GSR_SORT_T;
+static_assert(kSortT == 64 || kSortT == 128 || kSortT == 256, "tile_sort_kernel: 1, 2 or 4 waves");
 
-__global__ void __launch_bounds__(64) tile_sort_kernel(const uint2* __restrict__ ranges,
+__global__ void __launch_bounds__(kSortT) tile_sort_kernel(const uint2* __restrict__ ranges,
                                                        const u64* __restrict__ keys, u64 cap,
                                                        uint32_t* __restrict__ gid_sorted,
                                                        uint32_t* __restrict__ zero_cnt, uint32_t n_cells,
                                                        uint32_t* __restrict__ sorted_len,
                                                        uint32_t* __restrict__ redo_flag,
                                                        uint32_t* __restrict__ redo_cnt) {
-    __shared__ BucketLds<64, kSortWaveMax, kSortWaveMax / 2> s;
+    __shared__ BucketLds<kSortT, kSortWaveMax, kSortWaveMax / 2> s;
     if (zero_cnt && threadIdx.x == 0) {  // fused binning: K2's re-zeroing of the tile / cell counters
         zero_cnt[blockIdx.x] = 0u;
         if (blockIdx.x < n_cells) zero_cnt[gridDim.x + blockIdx.x] = 0u;
@@ -1011,14 +1020,15 @@ __global__ void __launch_bounds__(64) tile_sort_kernel(const uint2* __restrict__
     }
     if (n > kSortWaveMax) return;  // a class kernel's list (K2)
     if (n > kBucketMinN) {  // uniform
-        const bool done = n <= 256   ? bucket_sort_list<64, 4>(keys, r.x, n, gid_sorted, s)
-                          : n <= 512 ? bucket_sort_list<64, 8>(keys, r.x, n, gid_sorted, s)
-                                     : bucket_sort_list<64, 16>(keys, r.x, n, gid_sorted, s);
+        const bool done = n <= 256   ? bucket_sort_list<kSortT, 256 / kSortT>(keys, r.x, n, gid_sorted, s)
+                          : n <= 512 ? bucket_sort_list<kSortT, 512 / kSortT>(keys, r.x, n, gid_sorted, s)
+                                     : bucket_sort_list<kSortT, 1024 / kSortT>(keys, r.x, n, gid_sorted, s);
         if (done) {
             GSR_STAMP(g_st_sort, blockIdx.x, 1);
             return;
         }
     }
+    if (kSortT > 64 && threadIdx.x >= 64) return;  // (no barrier follows: the network is one wave's)
     if (n <= 64)
         sort_list<64, 1>(keys, r.x, n, gid_sorted, nullptr);
     else if (n <= 128)
@@ -1284,7 +1294,7 @@ hipError_t launch_tile_sort(uint32_t tiles, const uint2* ranges, const GeomState
     if (tiles == 0 || cap == 0) return hipSuccess;
     const u64 c = cap;
     const uint32_t lim = prefix ? prefix : ~0u;
-    hipLaunchKernelGGL(tile_sort_kernel, dim3(tiles), dim3(64), 0, stream, ranges, b.keys, c, b.gid_sorted,
+    hipLaunchKernelGGL(tile_sort_kernel, dim3(tiles), dim3(kSortT), 0, stream, ranges, b.keys, c, b.gid_sorted,
                        zero_counts ? g.tile_cnt : nullptr, cells, g.sorted_len, g.redo_flag, g.redo_cnt);
     // persistent class kernels: grids sized to fill the chip when their lists are long
     const auto grid = [&](uint32_t want) { return dim3(tiles < want ? tiles : want); };
