@@ -1105,10 +1105,15 @@ __global__ void __launch_bounds__(class_threads<CLASS>()) tile_sort_class_kernel
 constexpr int kPrefixBuf = 2048;
 constexpr int kPrefixBins = 2048;
 
-// E keys per thread: 16 for class 0's lists (<= 4096 keys), 32 for class 1's (<= kBucketMax).
-// (16 keys: at most 128 VGPRs, four workgroups per CU; the LDS would allow six)
-template <int E>
-__global__ void __launch_bounds__(kClassThreads) __attribute__((amdgpu_waves_per_eu(E <= 16 ? 4 : 2)))
+// T threads x E keys per thread: 256 x 16 for class 0's lists (<= 4096 keys), 256 x 32 for class 1's
+// (<= kBucketMax).  16 keys in at most 96 VGPRs: five workgroups per CU (the LDS would allow six;
+// 80 VGPRs spill): tile_sort 372-373 -> 357-360 us at 5M@4K against four; 512 x 8 measured 450
+// (six waves per SIMD) and 397 us (eight) (r3y3).
+#ifndef GSR_PREFIX_WAVES
+#define GSR_PREFIX_WAVES 5
+#endif
+template <int T, int E>
+__global__ void __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(E <= 16 ? GSR_PREFIX_WAVES : 2)))
 tile_sort_prefix_kernel(const uint2* __restrict__ ranges,
                                                                         u64* __restrict__ keys, u64 cap,
                                                                         uint32_t* __restrict__ gid_sorted,
@@ -1116,7 +1121,6 @@ tile_sort_prefix_kernel(const uint2* __restrict__ ranges,
                                                                         const uint32_t* __restrict__ count,
                                                                         uint32_t lim,
                                                                         uint32_t* __restrict__ sorted_len) {
-    constexpr int T = kClassThreads;
     __shared__ BucketLds<T, kPrefixBuf, kPrefixBins> s;
     const uint32_t nb = count[0];
     for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
@@ -1299,9 +1303,9 @@ hipError_t launch_tile_sort(uint32_t tiles, const uint2* ranges, const GeomState
     // persistent class kernels: grids sized to fill the chip when their lists are long
     const auto grid = [&](uint32_t want) { return dim3(tiles < want ? tiles : want); };
     if (GSR_PREFIX_KERNEL && prefix) {
-        hipLaunchKernelGGL(tile_sort_prefix_kernel<kClass0Max / kClassThreads>, grid(4096), dim3(kClassThreads), 0,
+        hipLaunchKernelGGL((tile_sort_prefix_kernel<kClassThreads, kClass0Max / kClassThreads>), grid(4096), dim3(kClassThreads), 0,
                            stream, ranges, b.keys, c, b.gid_sorted, g.cls_list, g.cls_count, lim, g.sorted_len);
-        hipLaunchKernelGGL(tile_sort_prefix_kernel<kBucketMax / kClassThreads>, grid(1024), dim3(kClassThreads), 0,
+        hipLaunchKernelGGL((tile_sort_prefix_kernel<kClassThreads, kBucketMax / kClassThreads>), grid(1024), dim3(kClassThreads), 0,
                            stream, ranges, b.keys, c, b.gid_sorted, g.cls_list + tiles, g.cls_count + 1, lim,
                            g.sorted_len);
         return hipGetLastError();
