@@ -171,7 +171,8 @@ def version() -> str:
 
 
 # ---- runtime options (include/gsr.h gsr_option_set) ---------------------------------
-OPTIONS = ("fused_bin", "fwd_quads", "bwd_seg_ck", "host_total", "zero_fill", "live_list", "sort_prefix")
+OPTIONS = ("fused_bin", "fwd_quads", "bwd_seg_ck", "host_total", "zero_fill", "live_list", "sort_prefix",
+           "count_wait")
 
 
 def option_get(name: str) -> int:

@@ -276,9 +276,12 @@ void carve_recs(char* base, size_t R, size_t P, gsr::GradRecs* recs, gsr::GradRe
 #ifndef GSR_SORT_PREFIX_DEFAULT
 #define GSR_SORT_PREFIX_DEFAULT 1024
 #endif
+#ifndef GSR_COUNT_WAIT_DEFAULT
+#define GSR_COUNT_WAIT_DEFAULT 1
+#endif
 enum Opt {
     OPT_FUSED_BIN = 0, OPT_FWD_QUADS, OPT_BWD_SEG_CK, OPT_HOST_TOTAL, OPT_ZERO_FILL, OPT_LIVE_LIST, OPT_SORT_PREFIX,
-    OPT_COUNT
+    OPT_COUNT_WAIT, OPT_COUNT
 };
 struct OptionSpec {
     const char* name;
@@ -293,6 +296,7 @@ const OptionSpec kOptions[OPT_COUNT] = {
     {"zero_fill", "GSR_ZERO_FILL", GSR_ZERO_FILL_DEFAULT, 0, 2},
     {"live_list", "GSR_LIVE_LIST", GSR_LIVE_LIST_DEFAULT, 0, 1},
     {"sort_prefix", "GSR_SORT_PREFIX", GSR_SORT_PREFIX_DEFAULT, 0, 1 << 30},
+    {"count_wait", "GSR_COUNT_WAIT", GSR_COUNT_WAIT_DEFAULT, 0, 1},
 };
 std::atomic<int> g_opt[OPT_COUNT];
 std::once_flag g_opt_once;
@@ -385,6 +389,25 @@ int total_readback(TotalReadback** out) {
     r.dev = host_total_store() ? r.mapped : nullptr;
     *out = &r;
     return GSR_OK;
+}
+
+// The forward's wait for its instance count ("count_wait" option).  1: poll the event from this
+// thread (up to kCountSpinMs, then block) -- the count lands ~0.6 ms after the call starts, while
+// the GPU still has the previous backward and this forward's binning to run, and a blocking wait
+// sleeps until the completion interrupt wakes the thread; on a busy host that wake-up was seen to
+// take 2 ms (bench slow_steps, r3y4), idling a GPU whose queue holds only the 0.27 ms of sort and
+// render behind the count.  0: hipEventSynchronize (HIP's short active wait, then the interrupt).
+constexpr int kCountSpinMs = 20;
+hipError_t wait_count_event(hipEvent_t ev) {
+    if (option(OPT_COUNT_WAIT)) {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (;;) {
+            const hipError_t q = hipEventQuery(ev);
+            if (q != hipErrorNotReady) return q;
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(kCountSpinMs)) break;
+        }
+    }
+    return hipEventSynchronize(ev);
 }
 
 // Forwards whose capacity hint was too small (the binning stage was redone), for gsr_forward_rebuilds().
@@ -870,7 +893,7 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
         hipError_t we;
         {
             HostTimer ht(g_wait);
-            we = hipEventSynchronize(rb->ev);
+            we = wait_count_event(rb->ev);
         }
         HIP_TRY(we, "num_rendered sync");
         *total = *rb->host;

@@ -303,6 +303,8 @@ int gsr_host_stats(double* values, int n, int reset);
  *                        1024 entries sort only the first L (+ the rest of a bucket), the part the blend
  *                        reaches, and redo the rare tile whose walk passes it | sort whole lists
  *                        (default L = 1024)
+ *   "count_wait" 1|0    the forward polls the event behind the instance count (20 ms at most, then
+ *                        blocks) | blocks in hipEventSynchronize (woken by the completion interrupt)
  * gsr_option_get returns -1 for an unknown name; gsr_option_set returns GSR_ERR_ARGUMENT for an
  * unknown name or an out-of-range value.  Not synchronised against calls running on other threads. */
 int gsr_option_set(const char* name, int value);

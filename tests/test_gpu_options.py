@@ -33,6 +33,7 @@ VARIANTS = {
     "live_list=0": dict(live_list=0),
     "sort_prefix=0": dict(sort_prefix=0),     # whole lists sorted
     "sort_prefix=64": dict(sort_prefix=64),   # long lists sorted to 64 entries: most of their tiles redone
+    "count_wait=0": dict(count_wait=0),       # the blocking wait for the instance count
 }
 CASES = ["sh3_scalerot", "antialiasing", "dense_opaque", "lists_1k_2k", "lists_4k_8k", "lists_over_8k"]
 
