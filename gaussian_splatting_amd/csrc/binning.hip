@@ -895,7 +895,11 @@ __device__ __forceinline__ void block_minmax_u64(u64& mn, u64& mx, u64* red) {
 // smallest *sorted = lim + (the rest of the bin lim falls in) keys, in final order at
 // gid_sorted[lo, lo + *sorted); the other entries are left unwritten.  The bins are the full key
 // range's, so the keys kept are exactly the smallest *sorted of the list.
-template <int T, int E, int NMAX, int NBMAX>
+// Window mode (WIN, whole lists longer than the LDS buffer): the bins are scattered and ranked in
+// windows of whole bins of at most NMAX keys each, in order, reusing the buffer; it fails (uniformly,
+// after writing part of the list -- the caller's fallback rewrites all of it) when one bin alone
+// exceeds the buffer.
+template <int T, int E, int NMAX, int NBMAX, bool WIN = false>
 __device__ bool bucket_sort_list(const u64* __restrict__ keys, uint32_t lo, uint32_t n,
                                  uint32_t* __restrict__ gid_sorted, BucketLds<T, NMAX, NBMAX>& s,
                                  uint32_t lim = ~0u, uint32_t* sorted = nullptr) {
@@ -953,6 +957,43 @@ __device__ bool bucket_sort_list(const u64* __restrict__ keys, uint32_t lo, uint
     }
     if (tid == 0) s.start[nb] = n;  // bins past nb are empty and never looked up
     __syncthreads();
+    if constexpr (WIN) {
+        for (uint32_t w0 = 0; w0 < n;) {  // uniform
+            // the window [w0, w1): up to the start of the bin that straddles w0 + NMAX, if one does
+            const uint32_t cut = w0 + (uint32_t)NMAX;
+            if (tid == 0) s.m = cut < n ? cut : n;
+            __syncthreads();
+            if (cut < n)
+                for (uint32_t c = 0; c < per; c++) {
+                    const uint32_t b = tid * per + c;
+                    if (s.start[b] < cut && cut < s.start[b + 1]) atomicMin(&s.m, s.start[b]);
+                }
+            __syncthreads();
+            const uint32_t w1 = s.m;
+            if (w1 <= w0) return false;  // uniform: one bin holds more keys than the buffer
+#pragma unroll
+            for (int e = 0; e < E; e++) {
+                if ((uint32_t)e * T + tid < n) {
+                    const uint32_t st = s.start[(uint32_t)((k[e] - mn) >> sh)];
+                    if (st >= w0 && st < w1) s.buf[st - w0 + o[e]] = k[e];
+                }
+            }
+            __syncthreads();
+            for (uint32_t j = tid; j < w1 - w0; j += T) {
+                const u64 kj = s.buf[j];
+                const uint32_t b = (uint32_t)((kj - mn) >> sh);
+                const uint32_t st = s.start[b] - w0, en = s.start[b + 1] - w0;
+                uint32_t c = 0;
+#pragma unroll 4
+                for (uint32_t q = st; q < en; q++) c += s.buf[q] < kj ? 1u : 0u;
+                gid_sorted[lo + w0 + st + c] = (uint32_t)kj;
+            }
+            __syncthreads();  // the buffer and s.m are reused by the next window
+            w0 = w1;
+        }
+        if (sorted && tid == 0) *sorted = n;
+        return true;
+    }
     const uint32_t m = s.m;
     if (T * E > NMAX && m > (uint32_t)NMAX) return false;  // uniform: the prefix overflows the buffer
 #pragma unroll
@@ -1140,6 +1181,39 @@ tile_sort_prefix_kernel(const uint2* __restrict__ ranges,
     }
 }
 
+// Class 0 in whole-list mode: the prefix kernel's layout -- the keys in registers, an LDS buffer of
+// kPrefixBuf keys (24 KiB: five workgroups per CU, against three for the 41-KiB class-0 kernel) --
+// with the bins ranked in windows of at most kPrefixBuf keys; a skewed list or one bin over the
+// buffer takes the global-memory network.  tile_sort 57.5-57.9 -> 52.3-52.4 us at 1M@1080p (r3y6);
+// GSR_CLASS0_WINDOW=0 builds the class-0 kernel instead.
+#ifndef GSR_CLASS0_WINDOW
+#define GSR_CLASS0_WINDOW 1
+#endif
+__global__ void __launch_bounds__(kClassThreads) __attribute__((amdgpu_waves_per_eu(GSR_PREFIX_WAVES)))
+tile_sort_window_kernel(const uint2* __restrict__ ranges, u64* __restrict__ keys, u64 cap,
+                        uint32_t* __restrict__ gid_sorted, const uint32_t* __restrict__ list,
+                        const uint32_t* __restrict__ count, uint32_t* __restrict__ sorted_len) {
+    constexpr int T = kClassThreads, E = kClass0Max / kClassThreads;
+    __shared__ BucketLds<T, kPrefixBuf, kPrefixBins> s;
+    const uint32_t nb = count[0];
+    for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
+        const uint32_t t = list[b];
+        const uint2 r = ranges[t];
+        const uint32_t n = tile_len(r, cap);
+        if (n <= 1) {
+            if (n == 1 && threadIdx.x == 0) gid_sorted[r.x] = (uint32_t)keys[r.x];
+            if (threadIdx.x == 0) sorted_len[t] = n;
+        } else if (n > (uint32_t)(T * E) ||
+                   !bucket_sort_list<T, E, kPrefixBuf, kPrefixBins, true>(keys, r.x, n, gid_sorted, s, ~0u,
+                                                                         sorted_len + t)) {
+            __syncthreads();
+            sort_list_global(keys, r.x, n, gid_sorted);
+            if (threadIdx.x == 0) sorted_len[t] = n;
+        }
+        __syncthreads();  // the LDS is reused by the next tile
+    }
+}
+
 // Whole-list sort of selected tiles, 256 threads per tile (any length: the bucket sort up to
 // kBucketMax keys, then a register network up to 4096, a global-memory network beyond).
 //  * redo (list != null): the tiles the forward filed because a wave reached the end of their
@@ -1310,8 +1384,12 @@ hipError_t launch_tile_sort(uint32_t tiles, const uint2* ranges, const GeomState
                            g.sorted_len);
         return hipGetLastError();
     }
-    hipLaunchKernelGGL(tile_sort_class_kernel<0>, grid(2048), dim3(class_threads<0>()), 0, stream, ranges, b.keys, c,
-                       b.gid_sorted, g.cls_list, g.cls_count, lim, g.sorted_len);
+    if (GSR_CLASS0_WINDOW)
+        hipLaunchKernelGGL(tile_sort_window_kernel, grid(2048), dim3(kClassThreads), 0, stream, ranges, b.keys, c,
+                           b.gid_sorted, g.cls_list, g.cls_count, g.sorted_len);
+    else
+        hipLaunchKernelGGL(tile_sort_class_kernel<0>, grid(2048), dim3(class_threads<0>()), 0, stream, ranges, b.keys,
+                           c, b.gid_sorted, g.cls_list, g.cls_count, lim, g.sorted_len);
     hipLaunchKernelGGL(tile_sort_class_kernel<1>, grid(512), dim3(class_threads<1>()), 0, stream, ranges, b.keys, c,
                        b.gid_sorted, g.cls_list + tiles, g.cls_count + 1, lim, g.sorted_len);
     return hipGetLastError();
