@@ -1268,10 +1268,14 @@ __global__ void __launch_bounds__(64) copy_sorted_prefix_kernel(const uint2* __r
 }
 
 // ---- launchers ----------------------------------------------------------------
+// Most binning chunks (A/B: GSR_BIN_CHUNKS_MAX).
+#ifndef GSR_BIN_CHUNKS_MAX
+#define GSR_BIN_CHUNKS_MAX 256
+#endif
 int bin_chunks(int P, int* chunk) {
     // ~256 chunks (enough workgroups for the chip), each < 65536 Gaussians (16-bit LDS counters)
     int n = (P + 1023) / 1024;
-    if (n > 256) n = 256;
+    if (n > GSR_BIN_CHUNKS_MAX) n = GSR_BIN_CHUNKS_MAX;
     if (n < 1) n = 1;
     int c = (P + n - 1) / n;
     if (c > 65535) {
