@@ -28,6 +28,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -75,6 +76,20 @@ def step_algorithmic_bytes(P, I, W, H, K):
     return (304 + 36 * K) * P + 132 * I + 48 * W * H
 
 
+def cpu_threads():
+    """Threads for the CPU baselines: the process's real CPU set (``os.sched_getaffinity``), capped by the
+    box's OMP_NUM_THREADS share when one is set (a GPU lease's worker-pool share; the affinity mask may
+    still show the whole machine).  Returns (threads, facts for the bench line)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:  # not Linux
+        aff = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS")
+    share = int(omp) if omp and omp.isdigit() and int(omp) > 0 else None
+    threads = max(1, min(aff, share) if share else aff)
+    return threads, {"affinity_cpus": aff, "omp_num_threads": share, "host_cpus": os.cpu_count()}
+
+
 def cpu_baseline(cfg_name: str, P: int, W: int, H: int, forward_only: bool = False):
     """north_star's CPU baseline: the pure-PyTorch fallback rasterizer (oracle/torch_fallback.py, fp32)
     on this host's cores, forward + autograd backward on the same frame as the GPU -- one FULL frame
@@ -82,6 +97,8 @@ def cpu_baseline(cfg_name: str, P: int, W: int, H: int, forward_only: bool = Fal
     after an untimed warm-up on a small tile sample."""
     from oracle import torch_fallback as tf
 
+    threads, cpus = cpu_threads()
+    torch.set_num_threads(threads)
     scene, cam = syn.config_scene(cfg_name, seed=0, P=P)
     gc, gd = (None, None) if forward_only else syn.upstream_grads(H, W)
     reps = 5 if P <= 100_000 else 1
@@ -89,16 +106,17 @@ def cpu_baseline(cfg_name: str, P: int, W: int, H: int, forward_only: bool = Fal
     t0 = time.perf_counter()
     value, t_frame, res = tf.splats_per_second(scene, cam, scene.sh_degree, gc, gd, tile_fraction=1.0, reps=reps)
     wall = time.perf_counter() - t0
-    threads = torch.get_num_threads()
     what = "forward" if forward_only else "forward + autograd backward"
     t = res["timings"]
-    return {"value": value, "unit": "Gaussian-splats/s", "cores": threads, "host_cpus": os.cpu_count(),
+    return {"value": value, "unit": "Gaussian-splats/s", "cores": torch.get_num_threads(), **cpus,
             "kind": "port", "impl": "pure-PyTorch fallback rasterizer (oracle/torch_fallback.py, fp32)",
             "sample": f"{cfg_name} ({P} Gaussians, {W}x{H}) {what}: {reps} full frame(s), every tile rendered "
                       f"({res['num_rendered']} list entries); {t_frame:.2f} s per frame (preprocess "
                       f"{t['preprocess']:.2f}, binning {t['binning']:.2f}, render {t['render']:.2f}, preprocess "
-                      f"backward {t['preprocess_backward']:.2f} s), {wall:.1f} s timed, torch.get_num_threads() = "
-                      f"{threads} (the box's OMP_NUM_THREADS share) of os.cpu_count() = {os.cpu_count()}"}
+                      f"backward {t['preprocess_backward']:.2f} s), {wall:.1f} s timed on {torch.get_num_threads()} torch "
+                      f"threads: the process's CPU set ({cpus['affinity_cpus']} CPUs, os.sched_getaffinity), capped "
+                      f"by the box's OMP_NUM_THREADS share ({cpus['omp_num_threads']}); os.cpu_count() = "
+                      f"{cpus['host_cpus']}"}
 
 
 def cpu_baseline_c(cfg_name: str, P: int, W: int, H: int, threads: int, min_seconds: float = 8.0):
@@ -118,7 +136,8 @@ def cpu_baseline_c(cfg_name: str, P: int, W: int, H: int, threads: int, min_seco
         total += time.perf_counter() - t0
         reps += 1
         del r
-    return {"value": reps * P / total, "unit": "Gaussian-splats/s", "cores": threads, "kind": "port",
+    return {"value": reps * P / total, "unit": "Gaussian-splats/s", "cores": threads, **cpu_threads()[1],
+            "kind": "port",
             "impl": "C restatement (oracle/gsr_oracle.c, float32, OpenMP)",
             "sample": f"{reps} full {cfg_name} frames ({P} Gaussians, {W}x{H}), forward+backward, "
                       f"{total:.1f} s on {threads} OpenMP threads"}
@@ -218,7 +237,45 @@ class HostClock:
         return out
 
 
-def main():
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_command(n: int, argv, port: int) -> list:
+    """The command that runs this bench as ``n`` ranks, one process per GPU (the driver's own form:
+    ``torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1``)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+def maybe_launch(args, argv) -> int | None:
+    """``--gpus N`` with N > 1 and no torch.distributed environment: start the N ranks as a CHILD
+    process (torch.distributed.run) and return its exit code -- the caller exits with it.  Runs before
+    anything touches the GPU (the library loads lazily; torch.cuda is not called), so this process holds
+    no HIP context.  Returns None when this process is itself a rank (or N == 1).  Inside a rank, a
+    WORLD_SIZE different from --gpus is an error (exit 2), never a silent one-rank run."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None:
+        if args.gpus > 1:
+            cmd = launch_command(args.gpus, argv, _free_port())
+            print(f"[bench] --gpus {args.gpus}: launching {args.gpus} ranks: {' '.join(cmd)}", file=sys.stderr,
+                  flush=True)
+            env = dict(os.environ)
+            env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this host driver
+            return subprocess.run(cmd, env=env).returncode
+        return None
+    if int(env_world) != args.gpus:
+        print(f"[bench] error: WORLD_SIZE={env_world} but --gpus {args.gpus}: the rank count the launcher "
+              f"started differs from the one requested", file=sys.stderr, flush=True)
+        return 2
+    return None
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -234,7 +291,7 @@ def main():
     ap.add_argument("--auto-steps", type=int, default=5, help="timed warm-up steps per candidate of --exchange auto")
     ap.add_argument("--separate-sh", action="store_true",
                     help="SH as train.py's separate_sh path passes it: dc [P,1,3] + rest [P,M-1,3] (3DGS-accel surface)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="threads of the C-restatement figure (default 16)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="threads of the C-restatement figure (default: the process's CPU set, capped by OMP_NUM_THREADS)")
     ap.add_argument("--cpu-only", action="store_true",
                     help="no GPU: time the pure-PyTorch fallback forward on --config (BASELINE configs[0] plumbing)")
     ap.add_argument("--roofline-every", type=int, default=4,
@@ -242,7 +299,19 @@ def main():
                          "leaves the GPU idle for a few us; 1 = every step)")
     ap.add_argument("--ramp-seconds", type=float, default=0.3,
                     help="untimed steps before the warmup, until the GPU clock has ramped up (DVFS)")
-    args = ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def main():
+    argv = sys.argv[1:]
+    args = parse_args(argv)
+    if args.gpus < 1:
+        print("[bench] error: --gpus must be >= 1", file=sys.stderr)
+        sys.exit(2)
+    if not args.cpu_only:
+        rc = maybe_launch(args, argv)
+        if rc is not None:
+            sys.exit(rc)
     if args.cpu_only:
         cpu_only(args.config)
         return
@@ -254,13 +323,34 @@ def main():
     # collectives -- exercises the N > 1 code path, not its speed
     rehearse = os.environ.get("GSR_BENCH_SHARE_GPU", "0") == "1"
     gpu = 0 if rehearse else local_rank
+    ndev = torch.cuda.device_count()  # counts devices without initialising HIP on this image
+    if gpu >= ndev:
+        print(f"[bench] error: rank {rank} (local rank {local_rank}) needs cuda:{gpu} but {ndev} device(s) are "
+              "visible", file=sys.stderr, flush=True)
+        sys.exit(2)
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
+    ranks_seen = 1
     if world > 1:
         if rehearse:
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=dev)
+        # the rank count the collective backend really connects: a SUM of ones over the group
+        one = torch.ones(1, dtype=torch.int64, device=dev)
+        dist.all_reduce(one)
+        ranks_seen = int(one.item())
+        if ranks_seen != world or dist.get_world_size() != world:
+            print(f"[bench] error: {dist.get_backend()} saw {ranks_seen} ranks (world size "
+                  f"{dist.get_world_size()}), expected {world}", file=sys.stderr, flush=True)
+            sys.exit(2)
+        dev_ids = torch.tensor([gpu], dtype=torch.int64, device=dev)
+        all_ids = [torch.zeros_like(dev_ids) for _ in range(world)]
+        dist.all_gather(all_ids, dev_ids)
+        rank_devices = [int(t.item()) for t in all_ids]
+        if not rehearse and len(set(rank_devices)) != world:
+            print(f"[bench] error: ranks share devices {rank_devices}", file=sys.stderr, flush=True)
+            sys.exit(2)
 
     cfg = syn.CONFIGS[args.config]
     P, W, H, Kdeg = cfg["P"], cfg["width"], cfg["height"], cfg["sh_degree"]
@@ -409,6 +499,9 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     multi = multi_rank_diagnostics(args, world, exchange, ex, arena, per_rank, cand_ms, dev) if world > 1 else None
+    if multi is not None:
+        multi.update({"ranks_seen_by_backend": ranks_seen, "rank_devices": rank_devices,
+                      "visible_devices_per_rank": ndev, "shared_gpu_rehearsal": rehearse})
 
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
@@ -479,7 +572,7 @@ def main():
             line["multi_gpu"] = multi
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.config, P, W, H)
-            line["cpu_baseline_c"] = cpu_baseline_c(args.config, P, W, H, args.cpu_threads or min(16, os.cpu_count() or 1))
+            line["cpu_baseline_c"] = cpu_baseline_c(args.config, P, W, H, args.cpu_threads or cpu_threads()[0])
         else:
             line["cpu_baseline"] = None
         print(json.dumps(line), flush=True)

@@ -12,7 +12,8 @@ import re
 import threading
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("GSR_LIBRARY", os.path.join(_PKG, "lib", "libgsr.so"))
+DEFAULT_LIB = os.path.join(_PKG, "lib", "libgsr.so")
+LIB_PATH = os.environ.get("GSR_LIBRARY", DEFAULT_LIB)
 INCLUDE_DIR = os.path.join(os.path.dirname(_PKG), "include")
 HEADER_PATH = os.path.join(INCLUDE_DIR, "gsr.h")
 HEADERS = [os.path.join(INCLUDE_DIR, h) for h in ("gsr.h", "gsr_knn.h", "gsr_ssim.h", "gsr_adam.h", "gsr_densify.h", "gsr_ply.h")]
@@ -93,6 +94,7 @@ SIGNATURES = {
     "gsr_option_get": (_i, [ctypes.c_char_p]),
     "gsr_last_error": (ctypes.c_char_p, []),
     "gsr_version": (ctypes.c_char_p, []),
+    "gsr_build_id": (ctypes.c_char_p, []),
     "gsr_profile_enable": (_i, [_i]),
     "gsr_profile_collect": (_i, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong), _i]),
     "gsr_profile_reset": (None, []),
@@ -156,6 +158,14 @@ def load():
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
+        if LIB_PATH == DEFAULT_LIB and os.environ.get("GSR_SKIP_BUILD_ID_CHECK", "0") != "1":
+            # the in-tree library must be the build of THIS tree's sources (build.py input_hash)
+            from gaussian_splatting_amd import build as _build
+
+            want, got = _build.input_hash(), lib.gsr_build_id().decode()
+            if got != want:
+                raise GsrError(f"{LIB_PATH} was built from other sources (build id {got[:16]}, this tree "
+                               f"{want[:16]}); rebuild it with `python -m gaussian_splatting_amd.build`")
         _lib = lib
     return _lib
 
@@ -168,6 +178,11 @@ def check(rc: int, what: str) -> None:
 
 def version() -> str:
     return load().gsr_version().decode()
+
+
+def build_id() -> str:
+    """sha256 of the sources and flags the loaded library was compiled from (include/gsr.h gsr_build_id)."""
+    return load().gsr_build_id().decode()
 
 
 # ---- runtime options (include/gsr.h gsr_option_set) ---------------------------------

@@ -13,7 +13,9 @@
 #include <cstring>
 #include <atomic>
 #include <chrono>
+#include <algorithm>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "../../include/gsr.h"
@@ -138,6 +140,7 @@ gsr::GeomState carve_geom(char* base, int P, uint32_t gx, uint32_t gy, size_t* t
     g.rec_start = c.take<uint32_t>(P);
     g.clamped = c.take<uint8_t>(P);
     g.status = c.take<uint32_t>(4);
+    g.fwd_seg_ck = g.status + 2;
     const uint32_t tiles = gx * gy;
     const size_t cells = bin_cell_count(gx, gy);
     g.tile_cnt = c.take<uint32_t>(tiles + cells);
@@ -295,7 +298,7 @@ const OptionSpec kOptions[OPT_COUNT] = {
     {"host_total", "GSR_HOST_TOTAL", 1, 0, 1},
     {"zero_fill", "GSR_ZERO_FILL", GSR_ZERO_FILL_DEFAULT, 0, 2},
     {"live_list", "GSR_LIVE_LIST", GSR_LIVE_LIST_DEFAULT, 0, 1},
-    {"sort_prefix", "GSR_SORT_PREFIX", GSR_SORT_PREFIX_DEFAULT, 0, 1 << 30},
+    {"sort_prefix", "GSR_SORT_PREFIX", GSR_SORT_PREFIX_DEFAULT, 0, (int)gsr::kSortPrefixMax},
     {"count_wait", "GSR_COUNT_WAIT", GSR_COUNT_WAIT_DEFAULT, 0, 1},
 };
 std::atomic<int> g_opt[OPT_COUNT];
@@ -329,10 +332,6 @@ int option_index(const char* name) {
     return -1;
 }
 
-// Backward segment length in checkpoints (1 = kCkStride entries per wave; a large value gives one
-// wave per tile, the schedule before checkpoints).
-int bwd_segment_checkpoints() { return option(OPT_BWD_SEG_CK); }
-
 // K2 folded into K3 in capacity mode.
 bool fused_binning_mode() { return option(OPT_FUSED_BIN) != 0; }
 
@@ -342,8 +341,11 @@ bool fused_binning_mode() { return option(OPT_FUSED_BIN) != 0; }
 // lists, where it saves nothing and the two redo launches cost ~8 us (1M@1080p, r3c).  Census runs
 // sort whole lists (a redone tile's first pass would be counted twice).  The results are the same
 // either way.
-uint32_t sort_prefix_for(size_t C, uint32_t tiles) {
-    const uint32_t L = (uint32_t)option(OPT_SORT_PREFIX);
+// L <= kSortPrefixMax (the option's range): the prefix kernel's LDS holds 2 kSortPrefixMax keys, so a
+// prefix plus the rest of its last bucket fits (a longer one would send every long list to the
+// global-memory fallback sort).
+uint32_t sort_prefix_for(size_t C, uint32_t tiles, uint32_t L) {
+    L = std::min(L, gsr::kSortPrefixMax);
     if (!L || g_census || tiles == 0) return 0u;
     return C / tiles >= 2ull * L ? L : 0u;
 }
@@ -361,7 +363,7 @@ struct TotalReadback {
     hipEvent_t ev = nullptr;
 };
 bool host_total_store() { return option(OPT_HOST_TOTAL) != 0; }
-int total_readback(TotalReadback** out) {
+int total_readback(TotalReadback** out, bool kernel_store) {
     constexpr int kMaxDevices = 64;
     thread_local TotalReadback slots[kMaxDevices];
     int dev = 0;
@@ -386,7 +388,7 @@ int total_readback(TotalReadback** out) {
         r.host = (unsigned long long*)h;
         r.mapped = (unsigned long long*)d;
     }
-    r.dev = host_total_store() ? r.mapped : nullptr;
+    r.dev = kernel_store ? r.mapped : nullptr;
     *out = &r;
     return GSR_OK;
 }
@@ -397,14 +399,21 @@ int total_readback(TotalReadback** out) {
 // sleeps until the completion interrupt wakes the thread; on a busy host that wake-up was seen to
 // take 2 ms (bench slow_steps, r3y4), idling a GPU whose queue holds only the 0.27 ms of sort and
 // render behind the count.  0: hipEventSynchronize (HIP's short active wait, then the interrupt).
+// The poll spins for kCountSpinUs, then yields the core between queries (std::this_thread::yield:
+// returns at once when nothing else wants the core, so a lone rank still sees the count within a
+// query's latency, while eight ranks per node plus RCCL proxy and loader threads get the cores
+// they need), and after kCountSpinMs falls back to the blocking wait.
 constexpr int kCountSpinMs = 20;
-hipError_t wait_count_event(hipEvent_t ev) {
-    if (option(OPT_COUNT_WAIT)) {
+constexpr int kCountSpinUs = 100;
+hipError_t wait_count_event(hipEvent_t ev, bool poll) {
+    if (poll) {
         const auto t0 = std::chrono::steady_clock::now();
         for (;;) {
             const hipError_t q = hipEventQuery(ev);
             if (q != hipErrorNotReady) return q;
-            if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(kCountSpinMs)) break;
+            const auto dt = std::chrono::steady_clock::now() - t0;
+            if (dt > std::chrono::milliseconds(kCountSpinMs)) break;
+            if (dt > std::chrono::microseconds(kCountSpinUs)) std::this_thread::yield();
         }
     }
     return hipEventSynchronize(ev);
@@ -451,6 +460,11 @@ extern "C" {
 const char* gsr_last_error(void) { return g_err; }
 
 const char* gsr_version(void) { return "gsr 0.2.0 gfx950"; }
+
+#ifndef GSR_BUILD_ID
+#define GSR_BUILD_ID "unknown"
+#endif
+const char* gsr_build_id(void) { return GSR_BUILD_ID; }
 
 long long gsr_forward_rebuilds(void) { return g_rebuilds.load(std::memory_order_relaxed); }
 
@@ -787,6 +801,13 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
     HostTimer host_time(g_fwd_host);
     g_err[0] = 0;
     hipStream_t stream = (hipStream_t)stream_;
+    // every option is read ONCE per call: gsr_option_set may run on another thread, and the launches
+    // of one forward (K4's prefix and the redo, the render's part protocol, the work list's segment
+    // length) must agree with each other
+    const int opt_quads = option(OPT_FWD_QUADS), opt_seg_ck = option(OPT_BWD_SEG_CK);
+    const uint32_t opt_prefix = (uint32_t)option(OPT_SORT_PREFIX);
+    const bool opt_fused = fused_binning_mode(), opt_host_total = host_total_store();
+    const bool opt_count_poll = option(OPT_COUNT_WAIT) != 0;
     // _ex / _dc forwards lay the binning buffer out for a multiple of kCapQuantum (the backward
     // recovers it from the buffer's size); gsr_rasterize_forward keeps the exact C = R layout
     const auto capacity_for = [quantized](size_t c) {
@@ -861,11 +882,11 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
     // exact mode: counts first (ranges unclamped), then the host reads R
     const size_t kNoCap = ~(size_t)0;
     TotalReadback* rb = nullptr;
-    if (int rc = total_readback(&rb)) return rc;
+    if (int rc = total_readback(&rb, opt_host_total)) return rc;
     // capacity mode: the binning buffer's capacity, known up front (the ranges are clamped to it)
     const size_t C_hint = capacity_hint > 0 ? capacity_for((size_t)capacity_hint) : 0;
     // capacity mode with LDS cursors: K2 folded into K3 (binning.hip FusedScan)
-    const bool fused = capacity_hint > 0 && bin_fused_ok(tiles) && fused_binning_mode();
+    const bool fused = capacity_hint > 0 && bin_fused_ok(tiles) && opt_fused;
     {
         StageScope sc(ST_BIN_COUNT, stream);
         HIP_TRY(launch_bin_count(P, geom, gx, gy, img.ranges, capacity_hint > 0 ? C_hint : kNoCap,
@@ -893,7 +914,7 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
         hipError_t we;
         {
             HostTimer ht(g_wait);
-            we = wait_count_event(rb->ev);
+            we = wait_count_event(rb->ev, opt_count_poll);
         }
         HIP_TRY(we, "num_rendered sync");
         *total = *rb->host;
@@ -907,6 +928,7 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
         char* bbase = (char*)call_alloc(binning_alloc, binning_ctx, bin_bytes);
         if (!bbase) return fail(GSR_ERR_ALLOC, "rasterize_forward: binning buffer allocation failed");
         BinningState bin = carve_binning(bbase, C, &bin_bytes);
+        const uint32_t prefix = C > 0 ? sort_prefix_for(C, tiles, opt_prefix) : 0u;  // K4 and the redo agree
         {
             // always launched: besides the keys (none when C == 0) it writes every Gaussian's
             // first record index, which the backward's reduction reads even when nothing
@@ -923,12 +945,11 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
             {
                 StageScope sc(ST_TILE_SORT, stream);
                 HIP_TRY(launch_tile_sort(tiles, img.ranges, geom, bin, C, stream, fused_now,
-                                         (uint32_t)bin_cell_count(gx, gy), sort_prefix_for(C, tiles)),
+                                         (uint32_t)bin_cell_count(gx, gy), prefix),
                         "tile_sort");
             }
             if (int rc = check_debug(debug, stream, "tile_sort")) return rc;
         }
-        const uint32_t prefix = sort_prefix_for(C, tiles);
         {
             StageScope sc(ST_RENDER_FWD, stream);
             RenderFwdArgs ra{};
@@ -938,7 +959,8 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
             ra.unit_cnt = geom.unit_cnt; ra.unit_part = geom.unit_part; ra.unit_full = bin.unit_full;
             ra.full_cap = (uint32_t)unit_full_cap(C);
             ra.tile_join = geom.tile_join;
-            ra.seg_ck = bwd_segment_checkpoints();
+            ra.seg_ck = opt_seg_ck;
+            ra.seg_ck_out = geom.fwd_seg_ck;
             ra.census = g_census;
             ra.sorted_len = geom.sorted_len;
             ra.redo_flag = geom.redo_flag;
@@ -946,10 +968,10 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
             ra.redo_cnt = geom.redo_cnt;
             // (C == 0: no lists and no K4, so nothing is prefix-sorted and no redo state was reset)
             if (C == 0) ra.sorted_len = nullptr;
-            HIP_TRY(launch_render_fwd(ra, stream, option(OPT_FWD_QUADS)), "render_fwd");
+            HIP_TRY(launch_render_fwd(ra, stream, opt_quads), "render_fwd");
             if (prefix && C > 0) {  // the tiles whose walk passed their sorted prefix (usually none)
                 HIP_TRY(launch_tile_sort_redo(tiles, img.ranges, geom, bin, C, stream), "render_fwd redo sort");
-                HIP_TRY(launch_render_fwd_redo(ra, stream, option(OPT_FWD_QUADS)), "render_fwd redo");
+                HIP_TRY(launch_render_fwd_redo(ra, stream, opt_quads), "render_fwd redo");
             }
         }
         return check_debug(debug, stream, "render_fwd");
@@ -1105,8 +1127,9 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
     BinningState bin = carve_binning((char*)binning_buffer, C, &tmp);
     size_t rec_bytes = 0;
     GradRecs recs{}, sums{};
-    const int seg_ck = bwd_segment_checkpoints();
-    const size_t max_units = R > 0 ? bwd_max_units((size_t)R, tiles, seg_ck) : 0;
+    // the forward recorded the segment length its work list uses (GeomState::fwd_seg_ck); the grid is
+    // sized for the shortest segments (seg_ck = 1), so it covers whatever the forward used
+    const size_t max_units = R > 0 ? bwd_max_units((size_t)R, tiles, 1) : 0;
     uint32_t *live = nullptr, *live_count = nullptr;
     carve_recs(nullptr, (size_t)R, (size_t)P, &recs, &sums, &live, &live_count, &rec_bytes);
     char* rbase = (char*)call_alloc(scratch_alloc, scratch_ctx, rec_bytes);
@@ -1191,7 +1214,7 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
         ra.W = width; ra.H = height; ra.gx = gx; ra.gy = gy; ra.ranges = img.ranges; ra.gid_sorted = bin.gid_sorted;
         ra.rec = geom.rec;
         ra.bg = background; ra.dL_dpix = dL_dpix; ra.dL_dinvdepth = dL_dinvdepths; ra.img = img; ra.recs = recs;
-        ra.ckpt = bin.ckpt; ra.seg_ck = seg_ck;
+        ra.ckpt = bin.ckpt; ra.seg_ck = geom.fwd_seg_ck;
         ra.unit_cnt = geom.unit_cnt; ra.unit_part = geom.unit_part; ra.unit_full = bin.unit_full;
         ra.full_cap = (uint32_t)unit_full_cap(C);
         ra.census = g_census;

@@ -1144,6 +1144,7 @@ __global__ void __launch_bounds__(class_threads<CLASS>()) tile_sort_class_kernel
 #define GSR_PREFIX_KERNEL 1
 #endif
 constexpr int kPrefixBuf = 2048;
+static_assert(kPrefixBuf >= 2 * (int)kSortPrefixMax, "a prefix plus the rest of its bucket fits the LDS buffer");
 constexpr int kPrefixBins = 2048;
 
 // T threads x E keys per thread: 256 x 16 for class 0's lists (<= 4096 keys), 256 x 32 for class 1's

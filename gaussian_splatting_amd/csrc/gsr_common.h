@@ -77,7 +77,9 @@ struct GeomState {
     uint2* rect;                // getRect, packed: (min.x | min.y << 16, max.x | max.y << 16)
     uint32_t* rec_start;        // first gradient-record index (exclusive scan of tiles_touched)
     uint8_t* clamped;           // SH clamp mask, 3 bits (CR/forward.cu:74-76)
-    uint32_t* status;           // device status word (prefiltered violation, ...)
+    uint32_t* status;           // device status words: [0] prefiltered violation, [2] fwd_seg_ck
+    uint32_t* fwd_seg_ck;       // status + 2: checkpoints per backward segment of the forward's work list
+                                // (render_fwd writes it, render_bwd reads it: the two always agree)
     // binning scratch (binning.hip)
     uint32_t* tile_cnt;         // [tiles] instances per tile; cell_cnt follows it (one memset)
     uint32_t* cell_cnt;         // [cells] visible Gaussians per screen cell (spatial order, binning.hip K0)

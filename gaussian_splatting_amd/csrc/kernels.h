@@ -47,6 +47,7 @@ struct RenderFwdArgs {
     uint32_t full_cap;     // unit_full_cap(binning capacity): stride of unit_full's shards
     unsigned long long* tile_join;  // GeomState::tile_join
     int seg_ck;
+    uint32_t* seg_ck_out;           // GeomState::fwd_seg_ck: seg_ck recorded for the backward
     unsigned long long* census;     // diagnostic pair counts (gsr_census_set) or null
     // reachable-prefix sort (GeomState): entries in order per tile, and the redo filing
     const uint32_t* sorted_len;
@@ -72,7 +73,8 @@ struct RenderBwdArgs {
     const uint2* unit_part;
     const uint2* unit_full;
     uint32_t full_cap;
-    int seg_ck;                         // checkpoints per backward segment (segment = seg_ck * kCkStride)
+    const uint32_t* seg_ck;             // GeomState::fwd_seg_ck: checkpoints per backward segment as the
+                                        // forward that built the work list used it (segment = seg_ck * kCkStride)
     unsigned long long* census;         // diagnostic pair counts (gsr_census_set) or null
     uint32_t* live_count;               // the live list's shard counters, zeroed here, or null
 };
@@ -437,6 +439,8 @@ hipError_t launch_render_bwd(const RenderBwdArgs& a, size_t max_units, hipStream
 // backward work list: one unit per (tile, segment of seg_ck * kCkStride entries below the tile's limit),
 // written by the forward render; at most R / (seg_ck kCkStride) + tiles of them
 size_t bwd_max_units(size_t R, uint32_t tiles, int seg_ck);
+// Longest reachable prefix K4 sorts ("sort_prefix" option range; binning.hip kPrefixBuf holds twice it).
+constexpr uint32_t kSortPrefixMax = 1024;
 // knn.hip
 size_t knn_scratch_bytes(int P);
 hipError_t launch_knn(int P, const float* pts, float* out, void* scratch, hipStream_t stream);

@@ -347,6 +347,7 @@ __global__ void __launch_bounds__(64) GSR_FWD_OCCUPANCY render_fwd_kernel(Render
     constexpr int NPART = 4 / NQ;
     const uint32_t tile = (blockIdx.x / (8 * NPART)) * 8 + blockIdx.x % 8;
     const int part = NPART == 1 ? 0 : (int)((blockIdx.x / 8) % NPART);
+    if (blockIdx.x == 0 && threadIdx.x == 0) *a.seg_ck_out = (uint32_t)a.seg_ck;  // for the backward
     if (tile >= a.gx * a.gy) return;
     render_fwd_tile<NQ, CENSUS>(a, tile, part);
 }
@@ -509,7 +510,7 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
         slim[q] = __builtin_amdgcn_readlane((int)wave_incl_max((uint32_t)nc[q]), 63);  // DPP max over the wave
     }
     const int limit = max(max(slim[0], slim[1]), max(slim[2], slim[3]));
-    const int end = min(limit, start + a.seg_ck * kCkStride);
+    const int end = min(limit, start + (int)uniform_u32(*a.seg_ck) * kCkStride);  // the forward's segments
     uint32_t live = 0;     // slots still reachable at the current position (uniform)
     int next_lim = limit;  // smallest slot limit among live slots
 #pragma unroll
@@ -671,6 +672,8 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
   }
 }
 
+// (the backward sizes its grid with seg_ck = 1, the most units any forward can append: the forward's
+// own seg_ck is on the device only; surplus blocks exit at the unit lookup)
 size_t bwd_max_units(size_t R, uint32_t tiles, int seg_ck) { return R / ((size_t)seg_ck * kCkStride) + tiles; }
 
 hipError_t launch_render_bwd(const RenderBwdArgs& a, size_t max_units, hipStream_t stream) {

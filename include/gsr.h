@@ -292,19 +292,23 @@ int gsr_host_stats(double* values, int n, int reset);
  * Each default comes from the environment variable GSR_<NAME> (upper case) at first use.
  *   "fused_bin"  1|0    capacity-mode binning with the tile scan folded into the scatter (forward)
  *   "fwd_quads"  2|4    8x8 quadrants per forward wave: half tiles | whole tiles
- *   "bwd_seg_ck" 1..2^20 backward work unit length in 256-entry checkpoints; the forward writes the
- *                        units, so a forward and its backward must run with the same value
+ *   "bwd_seg_ck" 1..2^20 backward work unit length in 256-entry checkpoints; read by the forward, which
+ *                        writes the units and records the value for its backward (a backward always
+ *                        walks the segments its own forward made, whatever the option is by then)
  *   "host_total" 1|0    the binning kernels store num_rendered into mapped host memory | a copy is queued
  *   "zero_fill"  1|2|0  dense backward outputs zero-filled on a side stream | on the launch stream
  *                        before gauss_bwd | not at all (gauss_bwd writes every row)
  *   "live_list"  1|0    gauss_bwd over the list of Gaussians with a render gradient | a lane per Gaussian
  *                        (only with zero_fill != 0)
- *   "sort_prefix" L|0   when the frame's mean list length is at least 2 L: of the lists longer than
+ *   "sort_prefix" L|0   (L in 1..1024) when the frame's mean list length is at least 2 L: of the lists longer than
  *                        1024 entries sort only the first L (+ the rest of a bucket), the part the blend
  *                        reaches, and redo the rare tile whose walk passes it | sort whole lists
  *                        (default L = 1024)
- *   "count_wait" 1|0    the forward polls the event behind the instance count (20 ms at most, then
- *                        blocks) | blocks in hipEventSynchronize (woken by the completion interrupt)
+ *   "count_wait" 1|0    the forward polls the event behind the instance count (spins 100 us, then yields
+ *                        the core between polls; 20 ms at most, then blocks) | blocks in
+ *                        hipEventSynchronize (woken by the completion interrupt)
+ * Every option is read once per forward / backward call, so a concurrent gsr_option_set never splits
+ * one call's launches between two values.
  * gsr_option_get returns -1 for an unknown name; gsr_option_set returns GSR_ERR_ARGUMENT for an
  * unknown name or an out-of-range value.  Not synchronised against calls running on other threads. */
 int gsr_option_set(const char* name, int value);
@@ -315,6 +319,12 @@ const char* gsr_last_error(void);
 
 /* Library version string, e.g. "gsr 0.1.0 gfx950". */
 const char* gsr_version(void);
+
+/* The build's input hash: sha256 (hex) over every source, header and compiler flag the library was
+ * compiled from (gaussian_splatting_amd/build.py input_hash), compiled into the library.  The loader
+ * compares it with the hash of the tree it runs from, so a library built from other sources is
+ * detected instead of used (no reference counterpart). */
+const char* gsr_build_id(void);
 
 /* Per-stage device timing with hipEvents recorded on the launch stream.
  * stage_mask selects the stages to time (bit s = stage s, -1 = all, 0 = off);

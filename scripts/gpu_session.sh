@@ -50,6 +50,12 @@ for stage in "$@"; do
       c=${stage#pmccfg:}
       bash scripts/pmc_session.sh "$TAG/pmc_$c" scripts/pmc_all.txt $c; rc=$?
       echo "pmc $c rc=$rc"; [ $rc -eq 0 ] || exit $rc ;;
+    launch2)  # bench.py --gpus 2 launching its own ranks (child torch.distributed.run), on one GPU with gloo
+      GSR_BENCH_SHARE_GPU=1 timeout -k 10 300 python bench.py --gpus 2 --steps 5 --warmup 2 \
+        > "$OUT/launch2.json" 2> "$OUT/launch2.err"; rc=$?
+      echo "launch2 rc=$rc"; cat "$OUT/launch2.json"; tail -3 "$OUT/launch2.err"; [ $rc -eq 0 ] || exit $rc ;;
+    cpus)  # the CPU set the baselines run on
+      python -c "import os; print('affinity', len(os.sched_getaffinity(0)), 'cpu_count', os.cpu_count(), 'OMP', os.environ.get('OMP_NUM_THREADS'))" | tee "$OUT/cpus.txt" ;;
     rehearse2)  # N=2 on one GPU (gloo collectives): the multi-rank bench path, both exchanges
       for ex in auto views dense allreduce; do
         GSR_BENCH_SHARE_GPU=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \

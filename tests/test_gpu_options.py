@@ -97,3 +97,33 @@ def test_option_path_matches_oracle(variant, case_name, hint):
             for a, b in zip(out, base):
                 assert torch.equal(a, b), variant
 
+
+
+@pytest.mark.parametrize("seg_ck", [2, 1 << 20])
+@pytest.mark.parametrize("case_name", ["lists_1k_2k", "lists_over_8k"])
+def test_seg_ck_set_around_forward_only(seg_ck, case_name):
+    """the backward walks the work units its OWN forward wrote.  A forward run with
+    bwd_seg_ck = k and a backward run after the option is restored (and the reverse) must give the
+    gradients of a forward + backward both run with k -- no segment counted twice, none left out."""
+    from gaussian_splatting_amd import _lib
+
+    case = next(c for c in C.SMALL_CASES if c.name == case_name)
+    inp = C.build(case)
+    ref = C.run_oracle(inp)
+    gc, gd = C.l1_grads(case.H, case.W)
+    with _lib.options(bwd_seg_ck=seg_ck):
+        fwd_k = C.run_gpu_forward(inp)
+        both_k = C.run_gpu_backward(inp, fwd_k, gc, gd)
+    split_k = C.run_gpu_backward(inp, fwd_k, gc, gd)  # option back at the default
+    fwd_1 = C.run_gpu_forward(inp)
+    with _lib.options(bwd_seg_ck=seg_ck):
+        split_1 = C.run_gpu_backward(inp, fwd_1, gc, gd)  # forward at the default, backward under k
+    both_1 = C.run_gpu_backward(inp, fwd_1, gc, gd)
+    torch.cuda.synchronize()
+    r = ref.handle.backward(gc, gd)
+    for a, b in zip(split_k, both_k):
+        assert torch.equal(a, b)
+    for a, b in zip(split_1, both_1):
+        assert torch.equal(a, b)
+    for k, got in zip(C.GRAD_NAMES, split_k):
+        np.testing.assert_allclose(_np(got), r[k], atol=1e-5, rtol=0, err_msg=k)

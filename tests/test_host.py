@@ -210,6 +210,25 @@ def test_option_errors_and_restore():
         _lib.option_set("fwd_quads", 3)
     with pytest.raises(_lib.GsrError, match="out of range"):
         _lib.option_set("zero_fill", 3)
+    # the reachable prefix is bounded by the prefix sort's LDS buffer: 1024 at most
+    _lib.option_set("sort_prefix", 1024)
+    with pytest.raises(_lib.GsrError, match="out of range"):
+        _lib.option_set("sort_prefix", 1025)
+    _lib.option_set("sort_prefix", before["sort_prefix"])
     with _lib.options(zero_fill=2, live_list=0):
         assert _lib.option_get("zero_fill") == 2 and _lib.option_get("live_list") == 0
     assert {k: _lib.option_get(k) for k in _lib.OPTIONS} == before
+
+
+def test_library_is_the_build_of_this_tree():
+    """freshness is decided by a hash of the sources, headers and flags (not by
+    mtimes), stored beside the library and compiled into it; the loaded library carries this tree's."""
+    from gaussian_splatting_amd import _lib, build
+
+    if _lib.LIB_PATH != _lib.DEFAULT_LIB:
+        pytest.skip("GSR_LIBRARY selects a variant build")
+    want = build.input_hash()
+    assert _lib.build_id() == want
+    with open(_lib.DEFAULT_LIB + ".inputs") as f:
+        assert f.read().strip() == want
+    assert build.input_hash(extra=("-DX=1",)) != want  # flags are part of the identity
