@@ -24,8 +24,12 @@ _LIBS: dict = {}
 
 
 def build(force: bool = False) -> None:
-    """Compile both precision variants with the committed Makefile (gcc + OpenMP)."""
-    targets = [os.path.join(_BUILD, f"liboracle_{p}.so") for p in ("f32", "f64")]
+    """Compile the variants with the committed Makefile (gcc + OpenMP): f32 and f64 without FP
+    contraction (the oracle), and f32fma -- float32 with every multiply-add the compiler can fuse
+    contracted into an FMA, as nvcc's default --fmad=true builds the reference (RI/setup.py passes
+    only -I).  f32fma only measures how sensitive the integer outputs are to contraction
+    (tools/fma_sensitivity.py); it is not a parity oracle."""
+    targets = [os.path.join(_BUILD, f"liboracle_{p}.so") for p in ("f32", "f64", "f32fma")]
     src = os.path.join(_HERE, "gsr_oracle.c")
     if not force and all(os.path.exists(t) and os.path.getmtime(t) >= os.path.getmtime(src) for t in targets):
         return
@@ -37,10 +41,10 @@ def _lib(precision: str):
         return _LIBS[precision]
     build()
     lib = ctypes.CDLL(os.path.join(_BUILD, f"liboracle_{precision}.so"))
-    pre = "oracle32_" if precision == "f32" else "oracle64_"
+    pre = "oracle32_" if precision.startswith("f32") else "oracle64_"
     vp = ctypes.c_void_p
     i = ctypes.c_int
-    r = ctypes.c_float if precision == "f32" else ctypes.c_double
+    r = ctypes.c_float if precision.startswith("f32") else ctypes.c_double
     fwd = getattr(lib, pre + "forward")
     fwd.restype = vp
     fwd.argtypes = [i, i, i, vp, i, i, vp, vp, vp, vp, vp, r, vp, vp, vp, vp, vp, r, r, i, i, vp, vp, vp, vp, i]
@@ -104,7 +108,7 @@ class OracleHandle:
     def __init__(self, precision, h, P, M, W, H):
         self.precision, self.h, self.P, self.M, self.W, self.H = precision, h, P, M, W, H
         self._lib, self._pre, _ = _lib(precision)
-        self.dtype = np.float32 if precision == "f32" else np.float64
+        self.dtype = np.float32 if precision.startswith("f32") else np.float64
 
     def __del__(self):
         try:
@@ -213,7 +217,7 @@ def forward(
 ) -> ForwardResult:
     """Forward pass of the restatement; argument meaning follows GaussianRasterizer / _C.rasterize_gaussians."""
     lib, pre, rtype = _lib(precision)
-    dt = np.float32 if precision == "f32" else np.float64
+    dt = np.float32 if precision.startswith("f32") else np.float64
     m3 = _arr(means3D, dt)
     P = 0 if m3 is None else m3.reshape(-1, 3).shape[0]
     sh = _arr(shs, dt)
@@ -239,7 +243,7 @@ def cov3d(scales, rotations, scale_modifier: float = 1.0, precision: str = "f32"
     """computeCov3D (CR/forward.cu:149-190): upper triangle [P, 6] of (S R)^T (S R); rotations are used
     as given (the reference's kernel does not normalise them)."""
     lib, pre, rtype = _lib(precision)
-    dt = np.float32 if precision == "f32" else np.float64
+    dt = np.float32 if precision.startswith("f32") else np.float64
     s = _arr(scales, dt)
     q = _arr(rotations, dt)
     P = 0 if s is None else s.reshape(-1, 3).shape[0]
@@ -250,7 +254,7 @@ def cov3d(scales, rotations, scale_modifier: float = 1.0, precision: str = "f32"
 
 def mark_visible(means3D, viewmatrix, precision: str = "f32") -> np.ndarray:
     lib, pre, _ = _lib(precision)
-    dt = np.float32 if precision == "f32" else np.float64
+    dt = np.float32 if precision.startswith("f32") else np.float64
     m3 = _arr(means3D, dt)
     P = 0 if m3 is None else m3.reshape(-1, 3).shape[0]
     out = np.zeros(max(P, 1), np.uint8)
