@@ -271,7 +271,10 @@ void carve_recs(char* base, size_t R, size_t P, gsr::GradRecs* recs, gsr::GradRe
 #define GSR_FUSED_BIN_DEFAULT 1
 #endif
 #ifndef GSR_ZERO_FILL_DEFAULT
-#define GSR_ZERO_FILL_DEFAULT 1
+#define GSR_ZERO_FILL_DEFAULT 3
+#endif
+#ifndef GSR_FUSED_FILL_BLOCKS
+#define GSR_FUSED_FILL_BLOCKS 256  // one-wave fill blocks in render_bwd's launch (the side-stream kernel: 64 x 4 waves)
 #endif
 #ifndef GSR_LIVE_LIST_DEFAULT
 #define GSR_LIVE_LIST_DEFAULT 1
@@ -296,10 +299,10 @@ const OptionSpec kOptions[OPT_COUNT] = {
     {"fwd_quads", "GSR_FWD_QUADS", 2, 2, 4},
     {"bwd_seg_ck", "GSR_BWD_SEG_CK", 1, 1, 1 << 20},
     {"host_total", "GSR_HOST_TOTAL", 1, 0, 1},
-    {"zero_fill", "GSR_ZERO_FILL", GSR_ZERO_FILL_DEFAULT, 0, 2},
+    {"zero_fill", "GSR_ZERO_FILL", GSR_ZERO_FILL_DEFAULT, 0, 3},
     {"live_list", "GSR_LIVE_LIST", GSR_LIVE_LIST_DEFAULT, 0, 1},
     {"sort_prefix", "GSR_SORT_PREFIX", GSR_SORT_PREFIX_DEFAULT, 0, (int)gsr::kSortPrefixMax},
-    {"count_wait", "GSR_COUNT_WAIT", GSR_COUNT_WAIT_DEFAULT, 0, 1},
+    {"count_wait", "GSR_COUNT_WAIT", GSR_COUNT_WAIT_DEFAULT, 0, 2},
 };
 std::atomic<int> g_opt[OPT_COUNT];
 std::once_flag g_opt_once;
@@ -417,6 +420,21 @@ hipError_t wait_count_event(hipEvent_t ev, bool poll) {
         }
     }
     return hipEventSynchronize(ev);
+}
+
+// "count_wait" 2: poll the mapped count slot until it leaves `pending` (the kernel's system-scope
+// store), with the same spin-then-yield pacing; after kCountSlotMs the stream itself is waited for
+// (a stalled or faulted stream then reports its error instead of the poll spinning on).
+constexpr int kCountSlotMs = 2000;
+hipError_t wait_count_slot(const unsigned long long* slot, unsigned long long pending, hipStream_t stream) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        if (__atomic_load_n(slot, __ATOMIC_ACQUIRE) != pending) return hipSuccess;
+        const auto dt = std::chrono::steady_clock::now() - t0;
+        if (dt > std::chrono::milliseconds(kCountSlotMs)) break;
+        if (dt > std::chrono::microseconds(kCountSpinUs)) std::this_thread::yield();
+    }
+    return hipStreamSynchronize(stream);
 }
 
 // Forwards whose capacity hint was too small (the binning stage was redone), for gsr_forward_rebuilds().
@@ -807,7 +825,7 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
     const int opt_quads = option(OPT_FWD_QUADS), opt_seg_ck = option(OPT_BWD_SEG_CK);
     const uint32_t opt_prefix = (uint32_t)option(OPT_SORT_PREFIX);
     const bool opt_fused = fused_binning_mode(), opt_host_total = host_total_store();
-    const bool opt_count_poll = option(OPT_COUNT_WAIT) != 0;
+    const int opt_count_wait = option(OPT_COUNT_WAIT);
     // _ex / _dc forwards lay the binning buffer out for a multiple of kCapQuantum (the backward
     // recovers it from the buffer's size); gsr_rasterize_forward keeps the exact C = R layout
     const auto capacity_for = [quantized](size_t c) {
@@ -887,6 +905,13 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
     const size_t C_hint = capacity_hint > 0 ? capacity_for((size_t)capacity_hint) : 0;
     // capacity mode with LDS cursors: K2 folded into K3 (binning.hip FusedScan)
     const bool fused = capacity_hint > 0 && bin_fused_ok(tiles) && opt_fused;
+    // "count_wait" 2 (capacity mode, the kernels storing the count into the mapped slot): no event
+    // behind the count -- the host polls the slot itself, reset to a sentinel before the launch that
+    // stores it, so the stream carries no marker (an event's marker left the GPU idle ~6 us between
+    // the scatter and the sort, r4a trace)
+    const bool poll_slot = opt_count_wait == 2 && capacity_hint > 0 && rb->dev;
+    constexpr unsigned long long kSlotPending = ~0ull;
+    if (poll_slot) __atomic_store_n(rb->host, kSlotPending, __ATOMIC_RELEASE);
     {
         StageScope sc(ST_BIN_COUNT, stream);
         HIP_TRY(launch_bin_count(P, geom, gx, gy, img.ranges, capacity_hint > 0 ? C_hint : kNoCap,
@@ -904,6 +929,7 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
     // mark num_rendered (K2 stores it into the host slot, or a copy is queued); wait_total()
     // waits for that mark only
     auto queue_total = [&]() -> int {
+        if (poll_slot) return GSR_OK;
         if (!rb->dev)
             HIP_TRY(hipMemcpyAsync(rb->host, geom.total, sizeof(*rb->host), hipMemcpyDeviceToHost, stream),
                     "num_rendered copy");
@@ -914,10 +940,13 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
         hipError_t we;
         {
             HostTimer ht(g_wait);
-            we = wait_count_event(rb->ev, opt_count_poll);
+            we = poll_slot ? wait_count_slot(rb->host, kSlotPending, stream)
+                           : wait_count_event(rb->ev, opt_count_wait != 0);
         }
         HIP_TRY(we, "num_rendered sync");
-        *total = *rb->host;
+        *total = __atomic_load_n(rb->host, __ATOMIC_ACQUIRE);
+        if (*total == kSlotPending)
+            return fail(GSR_ERR_HIP, "rasterize_forward: the stream finished without storing the instance count");
         if (*total > (unsigned long long)INT_MAX)
             return fail(GSR_ERR_OVERFLOW, "rasterize_forward: %llu tile instances exceed INT_MAX", *total);
         return GSR_OK;
@@ -1040,7 +1069,9 @@ namespace {
 // The backward's dense outputs are zero-filled on a side stream that runs beside render_bwd
 // (VALU-bound: HBM is two-thirds idle under it); gauss_bwd then writes only the rows of
 // Gaussians with a non-zero render gradient (about 14% of a 1M@1080p view).  "zero_fill" option:
-// 1 (default) side stream, 2 main stream right before gauss_bwd, 0 gauss_bwd writes every row.
+// 3 (default) fill blocks in render_bwd's own launch (no events: each fork / join event left the GPU
+// idle for 6-7 us, r4a), 1 side stream, 2 main stream right before gauss_bwd, 0 gauss_bwd writes
+// every row.
 // "live_list": gauss_bwd over the list of Gaussians with a gradient (1, default) or a lane per
 // Gaussian (0), when the outputs are zero-filled.
 bool live_list_mode() { return option(OPT_LIVE_LIST) != 0; }
@@ -1219,6 +1250,10 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
         ra.full_cap = (uint32_t)unit_full_cap(C);
         ra.census = g_census;
         ra.live_count = live_count;  // zeroed by its first workgroup
+        if (zmode == 3 && fill.count) {  // the zero fill rides in this launch
+            ra.fill = fill;
+            ra.fill_blocks = GSR_FUSED_FILL_BLOCKS;
+        }
         HIP_TRY(launch_render_bwd(ra, max_units, stream), "render_bwd");
     }
     if (int rc = check_debug(debug, stream, "render_bwd")) return rc;
@@ -1251,7 +1286,7 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
         if (side) {  // join: gauss_bwd writes over the zeroed outputs
             sj.join();
             sj.lock.unlock();
-        } else if (zmode) {
+        } else if (zmode == 1 || zmode == 2 || (zmode == 3 && R == 0)) {  // (3 with R = 0: no render_bwd launch)
             HIP_TRY(launch_zero_fill(fill, stream), "zero fill");
         }
         ga.sparse = zmode ? 1 : 0;

@@ -1289,31 +1289,9 @@ hipError_t launch_view_header(float* blk, const float* view, const float* proj, 
 #ifndef GSR_FILL_BLOCKS
 #define GSR_FILL_BLOCKS 64
 #endif
-#ifndef GSR_FILL_NT
-#define GSR_FILL_NT 1
-#endif
 __global__ void __launch_bounds__(256) zero_fill_kernel(FillArgs f) {
-    const unsigned long long tid = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
-    const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
-    for (int s = 0; s < f.count; s++) {
-        float* p = f.ptr[s];
-        const unsigned long long n = f.n[s];
-        const unsigned long long head = ((16 - (reinterpret_cast<uintptr_t>(p) & 15)) & 15) / 4;
-        const unsigned long long h = head < n ? head : n;
-        const unsigned long long n4 = (n - h) / 4;
-        float4* body = reinterpret_cast<float4*>(p + h);
-        for (unsigned long long i = tid; i < n4; i += stride) {
-#if GSR_FILL_NT  // streaming stores: the zeros do not displace render_bwd's lines from L2 / MALL
-            typedef float v4f __attribute__((ext_vector_type(4)));
-            __builtin_nontemporal_store((v4f){0.f, 0.f, 0.f, 0.f}, reinterpret_cast<v4f*>(body + i));
-#else
-            body[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-#endif
-        }
-        if (tid < h) p[tid] = 0.f;
-        const unsigned long long t0 = h + 4 * n4;
-        if (tid < n - t0) p[t0 + tid] = 0.f;
-    }
+    zero_fill_part(f, (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x,
+                   (unsigned long long)gridDim.x * blockDim.x);
 }
 
 hipError_t launch_zero_fill(const FillArgs& f, hipStream_t stream) {

@@ -56,6 +56,15 @@ struct RenderFwdArgs {
     uint32_t* redo_cnt;
 };
 
+// Zero-fill of up to kFillSegs float ranges (the backward's dense outputs), zeroed beside render_bwd
+// (VALU-bound, it leaves HBM bandwidth idle): "zero_fill" option, api.hip.
+constexpr int kFillSegs = 12;
+struct FillArgs {
+    float* ptr[kFillSegs];
+    unsigned long long n[kFillSegs];  // floats
+    int count;
+};
+
 struct RenderBwdArgs {
     int W, H;
     uint32_t gx, gy;
@@ -77,6 +86,11 @@ struct RenderBwdArgs {
                                         // forward that built the work list used it (segment = seg_ck * kCkStride)
     unsigned long long* census;         // diagnostic pair counts (gsr_census_set) or null
     uint32_t* live_count;               // the live list's shard counters, zeroed here, or null
+    // "zero_fill" = 3: the first fill_blocks blocks of the launch zero the backward's dense outputs
+    // (one wave each, beside the render waves) instead of a side-stream kernel forked and joined by
+    // events -- each event left the GPU idle for 6-7 us (r4a trace)
+    uint32_t fill_blocks;
+    FillArgs fill;
 };
 
 struct GaussBwdArgs {
@@ -115,15 +129,37 @@ struct GaussBwdArgs {
     uint32_t live_cap;           // entries per shard (live_list_cap)
 };
 
-// Zero-fill of up to kFillSegs float ranges (the backward's dense outputs), run on a side
-// stream while render_bwd (VALU-bound) leaves HBM bandwidth idle.
-constexpr int kFillSegs = 12;
-struct FillArgs {
-    float* ptr[kFillSegs];
-    unsigned long long n[kFillSegs];  // floats
-    int count;
-};
 hipError_t launch_zero_fill(const FillArgs& f, hipStream_t stream);
+
+// The fill's body, shared by zero_fill_kernel and the fill blocks fused into render_bwd's launch
+// ("zero_fill" = 3): thread `tid` of `stride` zeroes its share of every range -- 16-byte stores over
+// each range's aligned body (non-temporal: 236 MB of zeros written through the caches evicted the
+// records and pixel state render_bwd and gauss_reduce re-read, r2zv), dwords for the unaligned head
+// and tail.
+#ifndef GSR_FILL_NT
+#define GSR_FILL_NT 1
+#endif
+__device__ __forceinline__ void zero_fill_part(const FillArgs& f, unsigned long long tid, unsigned long long stride) {
+    for (int s = 0; s < f.count; s++) {
+        float* p = f.ptr[s];
+        const unsigned long long n = f.n[s];
+        const unsigned long long head = ((16 - (reinterpret_cast<uintptr_t>(p) & 15)) & 15) / 4;
+        const unsigned long long h = head < n ? head : n;
+        const unsigned long long n4 = (n - h) / 4;
+        float4* body = reinterpret_cast<float4*>(p + h);
+        for (unsigned long long i = tid; i < n4; i += stride) {
+#if GSR_FILL_NT
+            typedef float v4f __attribute__((ext_vector_type(4)));
+            __builtin_nontemporal_store((v4f){0.f, 0.f, 0.f, 0.f}, reinterpret_cast<v4f*>(body + i));
+#else
+            body[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+#endif
+        }
+        if (tid < h) p[tid] = 0.f;
+        const unsigned long long t0 = h + 4 * n4;
+        if (tid < n - t0) p[t0 + tid] = 0.f;
+    }
+}
 
 // ---- SH rows through LDS (preprocess and gauss_bwd, M = 16) -----------------------
 // LDS row r holds the 48 floats [coefficient 0..15][3] of Gaussian r0 + r at

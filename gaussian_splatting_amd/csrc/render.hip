@@ -413,6 +413,11 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
     // fill the slots that free up last -- no tile's full list ever sits on one SIMD.
     if (blockIdx.x == 0 && threadIdx.x < kLiveShards && a.live_count)  // gauss_reduce appends
         a.live_count[threadIdx.x * kLiveCntStride] = 0u;
+    if (blockIdx.x < a.fill_blocks) {  // uniform: a fill block (RenderBwdArgs::fill)
+        zero_fill_part(a.fill, (unsigned long long)blockIdx.x * kWave + threadIdx.x,
+                       (unsigned long long)a.fill_blocks * kWave);
+        return;
+    }
     uint2 unit;
     {  // full segments first, then the partial ones, longest quarter first; shards in order.
         // All 40 list counters in one vector load, an inclusive DPP scan, and a ballot find the
@@ -422,7 +427,7 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
         const int lane = threadIdx.x;
         const uint32_t c = lane < nl ? a.unit_cnt[lane * kUnitCntStride] : 0u;
         const uint32_t incl = wave_incl_sum(c);
-        const uint32_t i = blockIdx.x;
+        const uint32_t i = blockIdx.x - a.fill_blocks;
         const int l = __popcll(__ballot(lane < nl && incl <= i));  // lists wholly before unit i
         if (l >= nl) return;  // past the lists (the grid is sized for the worst case)
         const uint32_t before = l ? (uint32_t)__builtin_amdgcn_readlane((int)incl, l - 1) : 0u;
@@ -440,7 +445,10 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
     const float pxf0 = (float)(tile_x0 + lx), pyf0 = (float)(tile_y0 + ly);  // this lane's pixel in quadrant 0
 
     __shared__ float4 s_xy[kBatch], s_cq[kBatch], s_col[kBatch];  // as in the forward
-    __shared__ float4 s_acc[kBatch][3];                           // per entry: the 10 reduced sums (r8, r9 in 2 parts)
+    // per entry: the 10 reduced sums (r8, r9 in 2 parts), three float4 planes indexed by entry like the
+    // staged rows, so a reduction's store address is the entry's row offset (already scalar for the
+    // row reads) plus a per-lane constant (an [entry][3] layout cost a quarter-rate v_mad_u64_u32)
+    __shared__ float4 s_acc[3][kBatch];
     GSR_STAMP(g_st_rbwd, blockIdx.x, 0);
     GSR_STAMP_HWID(g_st_rbwd, blockIdx.x);
     GSR_STAMP_RT(g_st_rbwd, blockIdx.x, 4);
@@ -524,6 +532,7 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
     const int row = lane >> 4, slot_k = ((row & 1) << 1) | (row >> 1), li = lane & 15;
     const bool hi8 = (lane & 8) != 0, acc_wr = li == 0 || li == 8 || li == 15, acc_h4 = li == 15;
     const int acc_off = li == 0 ? slot_k : li == 8 ? 4 + slot_k : 8 + row;
+    const int acc_lane = (acc_off >> 2) * (4 * kBatch) + (acc_off & 3);  // float offset in s_acc, entry 0
 
     const uint32_t ttx = tile % a.gx, tty = tile / a.gx;
     unsigned long long c_staged = 0, c_eval = 0, c_alpha = 0, c_red = 0, c_idle = 0;  // CENSUS only
@@ -624,7 +633,7 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
                 // rows of w0: r0 r2 r1 r3; w1: r4 r6 r5 r7; h4: r8 r8 r9 r9
                 const float f = half_row_allsum(eight_fold(row_fold(h0, h1), row_fold(h2, h3), hi8));
                 const float g4 = row_allsum(h4);
-                if (acc_wr) reinterpret_cast<float*>(&s_acc[j][0])[acc_off] = acc_h4 ? g4 : f;
+                if (acc_wr) reinterpret_cast<float*>(s_acc)[j * 4 + acc_lane] = acc_h4 ? g4 : f;
 #if GSR_BWD_CARRY_R
                 r0 = r1 = r2 = r3 = r4 = r5 = r6 = r7 = r8 = r9 = 0.f;
 #endif
@@ -639,7 +648,7 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
             float4 ra = make_float4(0.f, 0.f, 0.f, 0.f), rb = ra;
             float2 rc = make_float2(0.f, 0.f);
             if (content) {
-                const float4 A = s_acc[lane][0], B = s_acc[lane][1], Cc = s_acc[lane][2];
+                const float4 A = s_acc[0][lane], B = s_acc[1][lane], Cc = s_acc[2][lane];
                 // dL/dmean2D in NDC units (x 0.5 W, 0.5 H, CR/backward.cu:509-510,600-601);
                 // dL/dconic with the reference's -0.5 factors (CR/backward.cu:604-606).  (Applying
                 // these linear maps per Gaussian in gauss_reduce instead measured +10 us in all, r2o.)
@@ -649,12 +658,16 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
                                  -0.5f * (float)a.H * o * (cc * B.y + cb * B.x), s9, -0.5f * o * B.w);
                 rc = make_float2(-0.5f * o * B.z, -0.5f * o * s8);
             }
-            a.recs.a[(size_t)kRecAB * e] = ra;
-            a.recs.b[(size_t)kRecAB * e] = rb;
-            if (GSR_REC_AOS)  // the whole 16-byte slot: full-width stores only
-                reinterpret_cast<float4*>(a.recs.c)[(size_t)kRecAB * e] = make_float4(rc.x, rc.y, 0.f, 0.f);
-            else
+            if (GSR_REC_AOS) {  // one 48-byte record (a, b, c + pad at recs.a + 0/1/2): one address, full-width stores
+                float4* r = a.recs.a + (size_t)kRecAB * e;
+                r[0] = ra;
+                r[1] = rb;
+                r[2] = make_float4(rc.x, rc.y, 0.f, 0.f);
+            } else {
+                a.recs.a[e] = ra;
+                a.recs.b[e] = rb;
                 a.recs.c[e] = rc;
+            }
         }
         __syncthreads();
     }
@@ -678,10 +691,11 @@ size_t bwd_max_units(size_t R, uint32_t tiles, int seg_ck) { return R / ((size_t
 
 hipError_t launch_render_bwd(const RenderBwdArgs& a, size_t max_units, hipStream_t stream) {
     if (max_units == 0) return hipSuccess;
+    const uint32_t grid = (uint32_t)max_units + a.fill_blocks;  // fill blocks first, then the units
     if (a.census)
-        hipLaunchKernelGGL(render_bwd_kernel<true>, dim3((uint32_t)max_units), dim3(kWave), 0, stream, a);
+        hipLaunchKernelGGL(render_bwd_kernel<true>, dim3(grid), dim3(kWave), 0, stream, a);
     else
-        hipLaunchKernelGGL(render_bwd_kernel<false>, dim3((uint32_t)max_units), dim3(kWave), 0, stream, a);
+        hipLaunchKernelGGL(render_bwd_kernel<false>, dim3(grid), dim3(kWave), 0, stream, a);
     return hipGetLastError();
 }
 

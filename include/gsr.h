@@ -296,17 +296,19 @@ int gsr_host_stats(double* values, int n, int reset);
  *                        writes the units and records the value for its backward (a backward always
  *                        walks the segments its own forward made, whatever the option is by then)
  *   "host_total" 1|0    the binning kernels store num_rendered into mapped host memory | a copy is queued
- *   "zero_fill"  1|2|0  dense backward outputs zero-filled on a side stream | on the launch stream
- *                        before gauss_bwd | not at all (gauss_bwd writes every row)
+ *   "zero_fill"  3|1|2|0 dense backward outputs zero-filled by extra blocks of render_bwd's launch
+ *                        (default) | on a side stream | on the launch stream before gauss_bwd | not at
+ *                        all (gauss_bwd writes every row)
  *   "live_list"  1|0    gauss_bwd over the list of Gaussians with a render gradient | a lane per Gaussian
  *                        (only with zero_fill != 0)
  *   "sort_prefix" L|0   (L in 1..1024) when the frame's mean list length is at least 2 L: of the lists longer than
  *                        1024 entries sort only the first L (+ the rest of a bucket), the part the blend
  *                        reaches, and redo the rare tile whose walk passes it | sort whole lists
  *                        (default L = 1024)
- *   "count_wait" 1|0    the forward polls the event behind the instance count (spins 100 us, then yields
- *                        the core between polls; 20 ms at most, then blocks) | blocks in
- *                        hipEventSynchronize (woken by the completion interrupt)
+ *   "count_wait" 2|1|0  capacity-hinted forwards: no event behind the instance count, the host polls the
+ *                        mapped count slot the binning kernel stores into (spins 100 us, then yields the
+ *                        core between polls) | polls the event recorded behind the count (20 ms at most,
+ *                        then blocks) | blocks in hipEventSynchronize (woken by the completion interrupt)
  * Every option is read once per forward / backward call, so a concurrent gsr_option_set never splits
  * one call's launches between two values.
  * gsr_option_get returns -1 for an unknown name; gsr_option_set returns GSR_ERR_ARGUMENT for an

@@ -4,7 +4,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/$1; shift; mkdir -p "$OUT"
-for rep in 1 2; do
+for rep in $(seq 1 ${REPS:-2}); do
   i=0
   for envs in "$@"; do
     i=$((i+1))

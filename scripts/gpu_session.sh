@@ -54,6 +54,9 @@ for stage in "$@"; do
       GSR_BENCH_SHARE_GPU=1 timeout -k 10 300 python bench.py --gpus 2 --steps 5 --warmup 2 \
         > "$OUT/launch2.json" 2> "$OUT/launch2.err"; rc=$?
       echo "launch2 rc=$rc"; cat "$OUT/launch2.json"; tail -3 "$OUT/launch2.err"; [ $rc -eq 0 ] || exit $rc ;;
+    stamps)  # per-workgroup timelines of the binning and render kernels (needs libgsr_stamps.so, built beforehand)
+      GSR_LIBRARY=$ROOT/gaussian_splatting_amd/lib/libgsr_stamps.so timeout -k 10 300 python tools/stamps.py > "$OUT/stamps.json" 2> "$OUT/stamps.err"; rc=$?
+      echo "stamps rc=$rc"; tail -c 3000 "$OUT/stamps.json"; [ $rc -eq 0 ] || exit $rc ;;
     cpus)  # the CPU set the baselines run on
       python -c "import os; print('affinity', len(os.sched_getaffinity(0)), 'cpu_count', os.cpu_count(), 'OMP', os.environ.get('OMP_NUM_THREADS'))" | tee "$OUT/cpus.txt" ;;
     rehearse2)  # N=2 on one GPU (gloo collectives): the multi-rank bench path, both exchanges

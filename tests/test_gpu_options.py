@@ -29,11 +29,13 @@ VARIANTS = {
     "bwd_seg_ck=max": dict(bwd_seg_ck=1 << 20),
     "host_total=0": dict(host_total=0),
     "zero_fill=0": dict(zero_fill=0),
+    "zero_fill=1": dict(zero_fill=1),         # side stream, forked / joined by events
     "zero_fill=2": dict(zero_fill=2),
     "live_list=0": dict(live_list=0),
     "sort_prefix=0": dict(sort_prefix=0),     # whole lists sorted
     "sort_prefix=64": dict(sort_prefix=64),   # long lists sorted to 64 entries: most of their tiles redone
     "count_wait=0": dict(count_wait=0),       # the blocking wait for the instance count
+    "count_wait=2": dict(count_wait=2),       # no event: the host polls the mapped count slot
 }
 CASES = ["sh3_scalerot", "antialiasing", "dense_opaque", "lists_1k_2k", "lists_4k_8k", "lists_over_8k"]
 

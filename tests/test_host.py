@@ -209,7 +209,7 @@ def test_option_errors_and_restore():
     with pytest.raises(_lib.GsrError, match="out of range"):
         _lib.option_set("fwd_quads", 3)
     with pytest.raises(_lib.GsrError, match="out of range"):
-        _lib.option_set("zero_fill", 3)
+        _lib.option_set("zero_fill", 4)
     # the reachable prefix is bounded by the prefix sort's LDS buffer: 1024 at most
     _lib.option_set("sort_prefix", 1024)
     with pytest.raises(_lib.GsrError, match="out of range"):
