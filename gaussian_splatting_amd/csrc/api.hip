@@ -283,7 +283,7 @@ void carve_recs(char* base, size_t R, size_t P, gsr::GradRecs* recs, gsr::GradRe
 #define GSR_SORT_PREFIX_DEFAULT 1024
 #endif
 #ifndef GSR_COUNT_WAIT_DEFAULT
-#define GSR_COUNT_WAIT_DEFAULT 1
+#define GSR_COUNT_WAIT_DEFAULT 2
 #endif
 enum Opt {
     OPT_FUSED_BIN = 0, OPT_FWD_QUADS, OPT_BWD_SEG_CK, OPT_HOST_TOTAL, OPT_ZERO_FILL, OPT_LIVE_LIST, OPT_SORT_PREFIX,

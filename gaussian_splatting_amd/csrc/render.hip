@@ -77,7 +77,12 @@ GSR_STAMP_BUFFER(g_st_rbwd);
 
 // Occupancy target of the backward (waves per SIMD).  One wave per tile means 8160
 // waves at 1080p for 1024 SIMDs; the register budget decides how many run at once.
-#ifdef GSR_BWD_WAVES
+// Six waves per SIMD (80 VGPRs): without the hint the fused zero-fill blocks (RenderBwdArgs::fill)
+// took the kernel to 82 VGPRs, i.e. five waves; 0 = no hint.
+#ifndef GSR_BWD_WAVES
+#define GSR_BWD_WAVES 6
+#endif
+#if GSR_BWD_WAVES
 #define GSR_BWD_OCCUPANCY __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVES, GSR_BWD_WAVES)))
 #else
 #define GSR_BWD_OCCUPANCY
@@ -111,10 +116,20 @@ __device__ __forceinline__ float splat_alpha(float p2, float opacity, float& G) 
 // terminated (skipped entries leave T alone).  A finished pixel therefore blends with weight 0
 // without any mask bookkeeping, and the only wave-level decisions are "does any
 // lane of this slot blend this splat" and "is any pixel of this slot still live".
+// SGPR budget of the forward: at .sgpr_count 82-96 the hardware admits 7 one-wave workgroups per
+// SIMD, at <= 80 eight (MI355X_MICROARCH.md "Residency"); the VGPRs (61) allow eight.
+#ifndef GSR_FWD_SGPRS
+#define GSR_FWD_SGPRS 80  // r4b: render_fwd 199-200 -> 195-197 us (8 SGPRs spill to VGPR lanes, prologue only); 0 = off
+#endif
+#if GSR_FWD_SGPRS
+#define GSR_FWD_SGPR_ATTR __attribute__((amdgpu_num_sgpr(GSR_FWD_SGPRS)))
+#else
+#define GSR_FWD_SGPR_ATTR
+#endif
 #ifdef GSR_FWD_WAVES
 #define GSR_FWD_OCCUPANCY __attribute__((amdgpu_waves_per_eu(GSR_FWD_WAVES, GSR_FWD_WAVES)))
 #else
-#define GSR_FWD_OCCUPANCY
+#define GSR_FWD_OCCUPANCY GSR_FWD_SGPR_ATTR
 #endif
 // One wave per PART of a tile: NQ = 4 quadrants (the whole 16x16 tile) or NQ = 2 (its top or
 // bottom half).  Each lane owns one pixel in each of the part's NQ quadrants ("slots").  With
