@@ -57,6 +57,12 @@ constexpr int kBatch = 64;  // list entries staged per round (one per lane)
 #define GSR_BWD_CARRY_R 0
 #endif
 
+// Each lane's tile-list entry of the NEXT batch is loaded during the current batch's walk, so a
+// batch's staging waits for one round trip (the splat records) instead of two (entry, then record).
+#ifndef GSR_PF_ENTRY
+#define GSR_PF_ENTRY 1
+#endif
+
 // Traffic attribution builds only (results are wrong in them): GSR_ATTR bit 0
 // drops the backward's record / content-byte stores, bit 1 its checkpoint loads, bit 2 its
 // per-pixel state loads other than n_contrib.  The control flow is unchanged in all three.
@@ -183,12 +189,14 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const ui
     const int n = (int)(range.y - range.x);
     const int ns = a.sorted_len ? min(n, (int)a.sorted_len[tile]) : n;  // entries in order
     unsigned long long c_staged = 0, c_eval = 0, c_alpha = 0, c_blend = 0, c_idle = 0;  // CENSUS only
+    uint32_t ent_next = GSR_PF_ENTRY && lane < ns ? a.gid_sorted[range.x + lane] : 0u;  // (GSR_PF_ENTRY)
     for (int b0 = 0; b0 < ns && alive; b0 += kBatch) {
         if (CENSUS) c_staged += (unsigned long long)min(kBatch, ns - b0);
         uint32_t qm = 0;
         if (b0 + lane < ns) {
             uint32_t* ent = a.gid_sorted + range.x + b0 + lane;  // Gaussian << 4 | quadrant mask
-            const uint32_t gid = *ent >> kEntryMaskBits;
+            // (the other part may be OR-ing its mask bits into *ent: only the Gaussian bits are used)
+            const uint32_t gid = (GSR_PF_ENTRY ? ent_next : *ent) >> kEntryMaskBits;
             const float4* rec = a.rec + (size_t)kRecRows * gid;
             const float4 v0 = rec[0], v1 = rec[1], v2 = rec[2];
             s_xy[lane] = make_float4(v0.x, v0.y, v1.y, v1.z);
@@ -212,6 +220,7 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const ui
             *ent = (gid << kEntryMaskBits) | qm;
 #endif
         }
+        if (GSR_PF_ENTRY && b0 + kBatch + lane < ns) ent_next = a.gid_sorted[range.x + b0 + kBatch + lane];
         __syncthreads();
         // Blend checkpoint (gsr_common.h): the state before entry b0, stored after this batch's
         // loads have landed.  vmcnt counts stores too, so stores issued ahead of the loads would
@@ -556,13 +565,15 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
 #if GSR_BWD_CARRY_R
     float r0 = 0.f, r1 = 0.f, r2 = 0.f, r3 = 0.f, r4 = 0.f, r5 = 0.f, r6 = 0.f, r7 = 0.f, r8 = 0.f, r9 = 0.f;
 #endif
+    uint32_t ent_next = GSR_PF_ENTRY && start + lane < end ? a.gid_sorted[range.x + start + lane] : 0u;
     for (int b0 = start; b0 < end; b0 += kBatch) {
         const bool has = b0 + lane < end;
         if (CENSUS) c_staged += (unsigned long long)min(kBatch, end - b0);
         uint32_t qm = 0, e = 0;
         float ca = 0.f, cb = 0.f, cc = 0.f, o = 0.f;  // this lane's entry: raw conic and opacity, for the flush
         if (has) {
-            const uint32_t ent = a.gid_sorted[range.x + b0 + lane];  // Gaussian << 4 | quadrant mask
+            // Gaussian << 4 | quadrant mask (GSR_PF_ENTRY: loaded during the previous batch)
+            const uint32_t ent = GSR_PF_ENTRY ? ent_next : a.gid_sorted[range.x + b0 + lane];
             const float4* rec = a.rec + (size_t)kRecRows * (ent >> kEntryMaskBits);
             const float4 v0 = rec[0], v1 = rec[1], v2 = rec[2], v3 = rec[3];
             // this instance's emission index (row 3: tile rectangle and first emission)
@@ -577,6 +588,7 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
             qm = ent & kEntryMask;
             s_cq[lane] = stage_conic(v0, v1, qm);
         }
+        if (GSR_PF_ENTRY && b0 + kBatch + lane < end) ent_next = a.gid_sorted[range.x + b0 + kBatch + lane];
         __syncthreads();
         unsigned long long todo = __ballot(qm != 0);
         unsigned long long written = 0;

@@ -20,6 +20,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="5m_4k_sh3")
     ap.add_argument("--chunks", type=int, default=256)
+    ap.add_argument("--order", choices=("row", "morton"), default="row",
+                    help="cell order of K0's spatial sort: row-major cells or Z-order (Morton) cells")
     args = ap.parse_args()
     scene, cam = syn.config_scene(args.config, seed=0)
     W, H = cam.width, cam.height
@@ -38,7 +40,13 @@ def main():
     print("instances", n.sum(), "num_rendered", r.num_rendered)
     vis = np.nonzero(n > 0)[0]
     cgx = (gx + 3) // 4
-    cell = (((y0 + y1) >> 1) // 4) * cgx + ((x0 + x1) >> 1) // 4
+    cx, cy = ((x0 + x1) >> 1) // 4, ((y0 + y1) >> 1) // 4
+    if args.order == "row":
+        cell = cy * cgx + cx
+    else:
+        cell = np.zeros_like(cx)
+        for b in range(16):
+            cell |= ((cx >> b) & 1) << (2 * b) | ((cy >> b) & 1) << (2 * b + 1)
     order = vis[np.argsort(cell[vis], kind="stable")]
     P = len(n)
     chunk = -(-P // args.chunks)
