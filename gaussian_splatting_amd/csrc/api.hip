@@ -990,6 +990,7 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
             ra.tile_join = geom.tile_join;
             ra.seg_ck = opt_seg_ck;
             ra.seg_ck_out = geom.fwd_seg_ck;
+            ra.fault = geom.status + 1;
             ra.census = g_census;
             ra.sorted_len = geom.sorted_len;
             ra.redo_flag = geom.redo_flag;

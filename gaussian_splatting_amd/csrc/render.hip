@@ -152,15 +152,42 @@ __device__ __forceinline__ float splat_alpha(float p2, float opacity, float& G) 
 // launch the tile's whole list is sorted and both parts render it again from the start
 // (render_fwd_redo_kernel).  The forward walks ~7% of a 4K tile's list and ~34% of a 1080p
 // one, so with a prefix of 1024 entries a redo is rare.
-template <int NQ, bool CENSUS>
+//
+// SHARED (NQ = 2 only; GSR_FWD_SHARED): the two half-tile waves are one 128-thread workgroup and
+// stage each 64-entry batch ONCE, into a ring of NB batch slots in LDS: the first part to need
+// batch k claims slot k % NB (an LDS compare-and-swap), loads the entries' records, tests the
+// footprint against the quadrants of both parts (of the other part only while it still runs) and
+// publishes the slot (a release store of its tag); the other part finds it staged.  No workgroup
+// barrier after the first: a part that runs ahead is held back only when it would overwrite a
+// slot the other part has not finished walking (NB - 1 batches of lead), and a part whose pixels
+// are all done leaves the protocol (done = kDoneAll) and the other stages alone.  The entries'
+// mask bits are written once, by the stager (no atomic OR).  No deadlock: a part waiting to reuse
+// a slot has claimed nothing, and a claimed slot is staged without waiting.
+#ifndef GSR_FWD_SHARED
+#define GSR_FWD_SHARED 0
+#endif
+#ifndef GSR_FWD_SHARED_NB
+#define GSR_FWD_SHARED_NB 3
+#endif
+constexpr int kDoneAll = 1 << 30;
+__device__ __forceinline__ int lds_load_acq(int* p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_store_rel(int* p, int v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+template <int NQ, bool CENSUS, bool SHARED = false>
 __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const uint32_t tile, const int part) {
   {
+    static_assert(!SHARED || NQ == 2, "shared staging pairs the two half-tile parts");
     constexpr int NPART = 4 / NQ;
     constexpr uint32_t kPartMask = (1u << NQ) - 1u;
+    constexpr int NB = SHARED ? GSR_FWD_SHARED_NB : 1;  // batch slots in LDS
     const uint32_t tiles = a.gx * a.gy;
     const int qbase = part * NQ;  // first quadrant of this part
     const int tile_x0 = (int)(tile % a.gx) * kTile, tile_y0 = (int)(tile / a.gx) * kTile;
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & (kWave - 1);
     const int lx = lane & 7, ly = lane >> 3;
     const float pxf0 = (float)(tile_x0 + lx), pyf0 = (float)(tile_y0 + ly);  // this lane's pixel in quadrant 0
     if (part == 0) {
@@ -169,7 +196,13 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const ui
         GSR_STAMP_RT(g_st_rfwd, tile, 4);
     }
 
-    __shared__ float4 s_xy[kBatch], s_cq[kBatch], s_col[kBatch];  // (x, y, o, 1/z), (A, B, C, quads), rgb
+    __shared__ float4 s_xy[NB][kBatch], s_cq[NB][kBatch], s_col[NB][kBatch];  // (x, y, o, 1/z), (A, B, C, quads), rgb
+    __shared__ int s_tag[NB], s_claim[NB], s_done[2];  // SHARED: slot k % NB holds batch s_tag; batches walked
+    if (SHARED) {
+        if (threadIdx.x < NB) s_tag[threadIdx.x] = s_claim[threadIdx.x] = (int)threadIdx.x - NB;
+        if (threadIdx.x < 2) s_done[threadIdx.x] = 0;
+        __syncthreads();  // (both parts are running here; the only workgroup barrier)
+    }
 
     float Tl[NQ], Tc[NQ], C0[NQ], C1[NQ], C2[NQ], D[NQ];
     uint32_t last[NQ];
@@ -189,39 +222,82 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const ui
     const int n = (int)(range.y - range.x);
     const int ns = a.sorted_len ? min(n, (int)a.sorted_len[tile]) : n;  // entries in order
     unsigned long long c_staged = 0, c_eval = 0, c_alpha = 0, c_blend = 0, c_idle = 0;  // CENSUS only
-    uint32_t ent_next = GSR_PF_ENTRY && lane < ns ? a.gid_sorted[range.x + lane] : 0u;  // (GSR_PF_ENTRY)
-    for (int b0 = 0; b0 < ns && alive; b0 += kBatch) {
-        if (CENSUS) c_staged += (unsigned long long)min(kBatch, ns - b0);
+    constexpr bool kPf = GSR_PF_ENTRY && !SHARED;
+    uint32_t ent_next = kPf && lane < ns ? a.gid_sorted[range.x + lane] : 0u;  // (GSR_PF_ENTRY)
+    int bk = 0;  // batch index
+    for (int b0 = 0; b0 < ns && alive; b0 += kBatch, bk++) {
+        const int sl = SHARED ? bk % NB : 0;
+        if (CENSUS && !SHARED) c_staged += (unsigned long long)min(kBatch, ns - b0);
         uint32_t qm = 0;
-        if (b0 + lane < ns) {
+        if (SHARED) {
+            // acquire batch bk in slot sl (uniform decisions).  Bounded: a protocol fault (none is
+            // known) ends this part's walk with a flag in the status word instead of hanging the GPU
+            uint32_t spins = 0;
+            for (;; spins++) {
+                if (spins > (1u << 22)) {
+                    if (lane == 0) atomicOr(a.fault, 1u);
+                    alive = 0;
+                    break;
+                }
+                if (lds_load_acq(&s_tag[sl]) == bk) break;  // staged, by either part
+                const bool mine_to_stage = s_claim[sl] != bk &&
+                                           (bk < NB || lds_load_acq(&s_done[part ^ 1]) > bk - NB);  // slot free
+                if (mine_to_stage) {
+                    int prev = 0;
+                    if (lane == 0) prev = atomicCAS(&s_claim[sl], bk - NB, bk);
+                    if (__builtin_amdgcn_readfirstlane(prev) == bk - NB) {
+                        if (CENSUS) c_staged += (unsigned long long)min(kBatch, ns - b0);
+                        if (b0 + lane < ns) {
+                            uint32_t* ent = a.gid_sorted + range.x + b0 + lane;
+                            const uint32_t gid = *ent >> kEntryMaskBits;
+                            const float4* rec = a.rec + (size_t)kRecRows * gid;
+                            const float4 v0 = rec[0], v1 = rec[1], v2 = rec[2];
+                            // both parts' quadrants, the other's only while it runs
+                            const uint32_t only = (kPartMask << qbase) |
+                                                  (lds_load_acq(&s_done[part ^ 1]) < kDoneAll ? kPartMask << (NQ - qbase) : 0u);
+                            const uint32_t q4 = quad_bits_exact(v0, v1, v2, tile_x0, tile_y0, only);
+                            s_xy[sl][lane] = make_float4(v0.x, v0.y, v1.y, v1.z);
+                            s_col[sl][lane] = v2;
+                            s_cq[sl][lane] = stage_conic(v0, v1, q4);
+                            *ent = (gid << kEntryMaskBits) | q4;  // for the backward, all parts' bits at once
+                        }
+                        lds_store_rel(&s_tag[sl], bk);
+                        break;
+                    }
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (!alive) break;
+            qm = __float_as_uint(s_cq[sl][lane].w);  // (all four bits; this part's are taken below)
+        } else if (b0 + lane < ns) {
             uint32_t* ent = a.gid_sorted + range.x + b0 + lane;  // Gaussian << 4 | quadrant mask
             // (the other part may be OR-ing its mask bits into *ent: only the Gaussian bits are used)
-            const uint32_t gid = (GSR_PF_ENTRY ? ent_next : *ent) >> kEntryMaskBits;
+            const uint32_t gid = (kPf ? ent_next : *ent) >> kEntryMaskBits;
             const float4* rec = a.rec + (size_t)kRecRows * gid;
             const float4 v0 = rec[0], v1 = rec[1], v2 = rec[2];
-            s_xy[lane] = make_float4(v0.x, v0.y, v1.y, v1.z);
-            s_col[lane] = v2;
+            s_xy[0][lane] = make_float4(v0.x, v0.y, v1.y, v1.z);
+            s_col[0][lane] = v2;
 #if GSR_FWD_OWN_BITS
             // this part's quadrants only; the backward (which visits only staged entries) gets every
             // part's bits OR-ed into the entry K4 wrote with clear mask bits.  A part that stopped
             // before an entry leaves its bits clear there: its pixels all ended earlier, so the
             // backward has retired those slots by then (slot limits from n_contrib).
             qm = quad_bits_exact(v0, v1, v2, tile_x0, tile_y0, kPartMask << qbase);
-            s_cq[lane] = stage_conic(v0, v1, qm >> qbase);
+            s_cq[0][lane] = stage_conic(v0, v1, qm >> qbase);
             if (NPART == 1)
                 *ent = (gid << kEntryMaskBits) | qm;
             else if (qm)
                 __hip_atomic_fetch_or(ent, qm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #else
             qm = quad_bits_exact(v0, v1, v2, tile_x0, tile_y0);
-            s_cq[lane] = stage_conic(v0, v1, (qm >> qbase) & kPartMask);
+            s_cq[0][lane] = stage_conic(v0, v1, (qm >> qbase) & kPartMask);
             // all four bits, for the backward (which visits only staged entries); with two parts
             // both may store the entry, the same value
             *ent = (gid << kEntryMaskBits) | qm;
 #endif
         }
-        if (GSR_PF_ENTRY && b0 + kBatch + lane < ns) ent_next = a.gid_sorted[range.x + b0 + kBatch + lane];
-        __syncthreads();
+        if (kPf && b0 + kBatch + lane < ns) ent_next = a.gid_sorted[range.x + b0 + kBatch + lane];
+        if (!SHARED) __syncthreads();
         // Blend checkpoint (gsr_common.h): the state before entry b0, stored after this batch's
         // loads have landed.  vmcnt counts stores too, so stores issued ahead of the loads would
         // make the staging wait for them; here they drain while the batch blends.  A part writes
@@ -243,8 +319,8 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const ui
         while (todo && alive) {
             const int j = __builtin_ctzll(todo);
             todo &= todo - 1;
-            const float4 xy = s_xy[j], cq = s_cq[j], col = s_col[j];
-            const uint32_t m = uniform_u32(__float_as_uint(cq.w)) & alive;
+            const float4 xy = s_xy[sl][j], cq = s_cq[sl][j], col = s_col[sl][j];
+            const uint32_t m = (SHARED ? uniform_u32(__float_as_uint(cq.w)) >> qbase : uniform_u32(__float_as_uint(cq.w))) & alive;
             const uint32_t pos1 = (uint32_t)(b0 + j + 1);
 #pragma unroll
             for (int k = 0; k < NQ; k++) {
@@ -279,11 +355,16 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const ui
                 if (!__any(Tl[k] > 0.f)) alive &= ~(1u << k);
             }
         }
-        __syncthreads();
+        if (SHARED) {
+            if (lane == 0) lds_store_rel(&s_done[part], bk + 1);  // slot sl may be restaged for bk + NB
+        } else {
+            __syncthreads();
+        }
 #ifdef GSR_STAMPS
-        if (threadIdx.x == 0 && part == 0) g_st_rfwd[(size_t)tile * kStampSlots + 3] = (unsigned long long)(b0 + kBatch);
+        if (lane == 0 && part == 0) g_st_rfwd[(size_t)tile * kStampSlots + 3] = (unsigned long long)(b0 + kBatch);
 #endif
     }
+    if (SHARED && lane == 0) lds_store_rel(&s_done[part], kDoneAll);  // the other part stages alone from here
     if (CENSUS && lane == 0) {
         atomicAdd(&a.census[0], c_staged);
         atomicAdd(&a.census[1], c_eval);
@@ -376,6 +457,20 @@ __global__ void __launch_bounds__(64) GSR_FWD_OCCUPANCY render_fwd_kernel(Render
     render_fwd_tile<NQ, CENSUS>(a, tile, part);
 }
 
+// Shared staging (GSR_FWD_SHARED): one 128-thread workgroup per tile, its two waves the halves.
+// (72 VGPRs at seven waves per SIMD: the staging of both parts' footprints holds more registers
+// beside the blend state; left alone the compiler took 84, five waves)
+#ifndef GSR_FWD_SHARED_WAVES
+#define GSR_FWD_SHARED_WAVES 7
+#endif
+template <bool CENSUS>
+__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(GSR_FWD_SHARED_WAVES, GSR_FWD_SHARED_WAVES)))
+GSR_FWD_SGPR_ATTR render_fwd_shared_kernel(RenderFwdArgs a) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *a.seg_ck_out = (uint32_t)a.seg_ck;  // for the backward
+    if (blockIdx.x >= a.gx * a.gy) return;  // (uniform over the workgroup)
+    render_fwd_tile<2, CENSUS, true>(a, blockIdx.x, (int)(threadIdx.x >> 6));
+}
+
 // The redo of the tiles render_fwd_kernel filed (their whole lists sorted since, by
 // tile_sort_full_kernel): NPART blocks per tile, persistent over the redo list.
 template <int NQ, bool CENSUS>
@@ -418,7 +513,12 @@ hipError_t launch_render_fwd(const RenderFwdArgs& a, hipStream_t stream, int qua
     const uint32_t tiles = a.gx * a.gy;
     if (tiles == 0) return hipSuccess;
     const uint32_t groups = (tiles + 7) / 8;
-    if (a.census)
+    if (GSR_FWD_SHARED && quads == 2) {
+        if (a.census)
+            hipLaunchKernelGGL((render_fwd_shared_kernel<true>), dim3(tiles), dim3(2 * kWave), 0, stream, a);
+        else
+            hipLaunchKernelGGL((render_fwd_shared_kernel<false>), dim3(tiles), dim3(2 * kWave), 0, stream, a);
+    } else if (a.census)
         hipLaunchKernelGGL((render_fwd_kernel<2, true>), dim3(groups * 16), dim3(kWave), 0, stream, a);
     else if (quads == 4)
         hipLaunchKernelGGL((render_fwd_kernel<4, false>), dim3(groups * 8), dim3(kWave), 0, stream, a);
