@@ -210,8 +210,22 @@ __device__ __forceinline__ void for_each_instance(uint32_t n, uint2 r, uint32_t 
 // runs instead of a few bytes per (chunk, tile) across the whole image.
 constexpr uint32_t kCell = 4;
 
+// GSR_CELL_MORTON: cells in Z order (Morton code of the cell column and row, over the power-of-two
+// square that holds the grid), so a chunk of the order covers a square-ish block of cells rather than
+// a strip of a cell row (5M@4K: 936 instead of 1062 tiles per chunk, tools/k3_runs.py --order).
+#ifndef GSR_CELL_MORTON
+#define GSR_CELL_MORTON 0
+#endif
+__host__ __device__ inline uint32_t spread_bits16(uint32_t x) {
+    x &= 0xffffu;
+    x = (x | (x << 8)) & 0x00ff00ffu;
+    x = (x | (x << 4)) & 0x0f0f0f0fu;
+    x = (x | (x << 2)) & 0x33333333u;
+    return (x | (x << 1)) & 0x55555555u;
+}
 __device__ __forceinline__ uint32_t cell_of(uint2 r, uint32_t cgx) {
     const uint32_t cx = ((r.x & 0xffffu) + (r.y & 0xffffu)) >> 1, cy = ((r.x >> 16) + (r.y >> 16)) >> 1;
+    if (GSR_CELL_MORTON) return spread_bits16(cx / kCell) | (spread_bits16(cy / kCell) << 1);
     return (cy / kCell) * cgx + cx / kCell;
 }
 
@@ -1294,7 +1308,13 @@ size_t bin_chunk_count(int P) {
 
 uint32_t bin_cells(uint32_t gx, uint32_t gy, uint32_t* cgx) {
     *cgx = (gx + kCell - 1) / kCell;
-    return *cgx * ((gy + kCell - 1) / kCell);
+    const uint32_t cgy = (gy + kCell - 1) / kCell;
+    if (GSR_CELL_MORTON) {  // Morton codes of the cells: the power-of-two square around the grid
+        uint32_t side = 1;
+        while (side < *cgx || side < cgy) side <<= 1;
+        return side * side;
+    }
+    return *cgx * cgy;
 }
 
 bool bin_fused_ok(uint32_t tiles) { return tiles <= kLdsTilesMax; }

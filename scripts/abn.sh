@@ -5,7 +5,12 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd); OUT=$ROOT/gpurun_out/$1; R=${2:-2}; CFG=${3:-1m_1080p_sh3}; XF=${4:-}; mkdir -p "$OUT"
-LIBS="$ROOT/gaussian_splatting_amd/lib/libgsr.so $(ls $ROOT/gaussian_splatting_amd/lib/libgsr_*.so 2>/dev/null)"
+# VARIANTS="a b" restricts the side libraries to libgsr_a.so libgsr_b.so (default: every libgsr_*.so)
+if [ -n "${VARIANTS:-}" ]; then
+  LIBS="$ROOT/gaussian_splatting_amd/lib/libgsr.so $(for v in $VARIANTS; do echo $ROOT/gaussian_splatting_amd/lib/libgsr_$v.so; done)"
+else
+  LIBS="$ROOT/gaussian_splatting_amd/lib/libgsr.so $(ls $ROOT/gaussian_splatting_amd/lib/libgsr_*.so 2>/dev/null)"
+fi
 for lib in $LIBS; do
   v=$(basename $lib .so)
   GSR_LIBRARY=$lib timeout -k 10 600 python -m pytest tests/test_gpu_parity.py -m gpu -q -x > "$OUT/pytest_$v.log" 2>&1; rc=$?
