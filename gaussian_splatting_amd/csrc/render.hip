@@ -268,7 +268,8 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const ui
                 __builtin_amdgcn_s_sleep(1);
             }
             if (!alive) break;
-            qm = __float_as_uint(s_cq[sl][lane].w);  // (all four bits; this part's are taken below)
+            // (all four bits, this part's taken below; lanes past the list hold a stale slot: none)
+            qm = b0 + lane < ns ? __float_as_uint(s_cq[sl][lane].w) : 0u;
         } else if (b0 + lane < ns) {
             uint32_t* ent = a.gid_sorted + range.x + b0 + lane;  // Gaussian << 4 | quadrant mask
             // (the other part may be OR-ing its mask bits into *ent: only the Gaussian bits are used)
