@@ -214,7 +214,7 @@ constexpr uint32_t kCell = 4;
 // square that holds the grid), so a chunk of the order covers a square-ish block of cells rather than
 // a strip of a cell row (5M@4K: 936 instead of 1062 tiles per chunk, tools/k3_runs.py --order).
 #ifndef GSR_CELL_MORTON
-#define GSR_CELL_MORTON 0
+#define GSR_CELL_MORTON 1  // r4c: bin_scatter 852-855 -> 827-831 us at 5M@4K, 1M unchanged
 #endif
 __host__ __device__ inline uint32_t spread_bits16(uint32_t x) {
     x &= 0xffffu;

@@ -83,10 +83,11 @@ GSR_STAMP_BUFFER(g_st_rbwd);
 
 // Occupancy target of the backward (waves per SIMD).  One wave per tile means 8160
 // waves at 1080p for 1024 SIMDs; the register budget decides how many run at once.
-// Six waves per SIMD (80 VGPRs): without the hint the fused zero-fill blocks (RenderBwdArgs::fill)
-// took the kernel to 82 VGPRs, i.e. five waves; 0 = no hint.
+// Occupancy hint (0 = none): with the fused zero-fill blocks (RenderBwdArgs::fill) the kernel takes
+// 82 VGPRs, five waves per SIMD; GSR_BWD_WAVES=6 holds it at 79 (six), which measured the same
+// (r4c: 0.7626 vs 0.7610 ms/step, render_bwd 284-289 us either way) -- not occupancy-bound.
 #ifndef GSR_BWD_WAVES
-#define GSR_BWD_WAVES 6
+#define GSR_BWD_WAVES 0
 #endif
 #if GSR_BWD_WAVES
 #define GSR_BWD_OCCUPANCY __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVES, GSR_BWD_WAVES)))
@@ -163,6 +164,9 @@ __device__ __forceinline__ float splat_alpha(float p2, float opacity, float& G) 
 // are all done leaves the protocol (done = kDoneAll) and the other stages alone.  The entries'
 // mask bits are written once, by the stager (no atomic OR).  No deadlock: a part waiting to reuse
 // a slot has claimed nothing, and a claimed slot is staged without waiting.
+// Measured (r4c, 1M@1080p, three interleaved rounds): render_fwd 236-240 us against 194-196 for the
+// two independent half-tile waves -- seven waves per SIMD instead of eight (the staging of both
+// parts' footprints needs 72 VGPRs), and a part that runs ahead waits for slot reuse.  Off.
 #ifndef GSR_FWD_SHARED
 #define GSR_FWD_SHARED 0
 #endif
