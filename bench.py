@@ -508,6 +508,11 @@ def main():
         value = world * P * args.steps / elapsed
         dom_ms = dom_total / dom_calls if dom_calls else 0.0  # HIP events on the launch stream, timed region
         alg = algorithmic_bytes(dom, P, nr, W, H, K)
+        # zero_fill = 3 (the default): the zero fill of the backward's dense outputs rides in render_bwd's
+        # launch (api.hip), so its bytes are that launch's too: 4 B x (means2D 3, opacity 1, colour 3,
+        # inverse depth 1, means3D 3, cov3D 6, SH 3K, scale 3, rotation 4) per Gaussian
+        fill_bytes = 4.0 * P * (24 + 3 * K) if dom == "render_bwd" and _lib.option_get("zero_fill") == 3 else 0.0
+        alg += fill_bytes
         traffic, traffic_src, kk = None, None, {}
         if os.path.exists(PMC_PROFILE):
             prof = json.load(open(PMC_PROFILE))
@@ -557,7 +562,8 @@ def main():
                          # counter bytes per launch over the launch time: the HBM rate the kernel really moves
                          "traffic_frac": (traffic / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
                                           if traffic is not None and dom_ms > 0 else None),
-                         "algorithmic_bytes_per_launch": alg, "mean_launch_ms": dom_ms, "timed_launches": int(dom_calls), "timed_every": every,
+                         "algorithmic_bytes_per_launch": alg, "fused_zero_fill_bytes": fill_bytes,
+                         "mean_launch_ms": dom_ms, "timed_launches": int(dom_calls), "timed_every": every,
                          # what actually limits the render kernels: "hbm" above is the
                          # contract's roofline axis, not the limiter
                          "limiter": ("VALU issue + latency (per (pixel, splat) pair work)"
