@@ -711,7 +711,10 @@ __global__ void __launch_bounds__(64) GSR_GB_OCCUPANCY gauss_bwd_kernel(GaussBwd
         }
     }
 
-    if constexpr (kShLate) {
+#ifndef GSR_GB_TIMING_NOSH
+#define GSR_GB_TIMING_NOSH 0  // timing builds only (results wrong): skip the deferred SH pass
+#endif
+    if constexpr (kShLate && !GSR_GB_TIMING_NOSH) {
         // SH backward, half a wave at a time through LDS: coalesced stage-in of 32 rows,
         // their lanes evaluate it in place, coalesced write-back of the 32 dL/dSH rows
         const unsigned long long need = __ballot(sh_late);  // rows whose SH is read at all
