@@ -35,7 +35,7 @@ VARIANTS = {
     "sort_prefix=0": dict(sort_prefix=0),     # whole lists sorted
     "sort_prefix=64": dict(sort_prefix=64),   # long lists sorted to 64 entries: most of their tiles redone
     "count_wait=0": dict(count_wait=0),       # the blocking wait for the instance count
-    "count_wait=2": dict(count_wait=2),       # no event: the host polls the mapped count slot
+    "count_wait=1": dict(count_wait=1),       # the host polls an event behind the count (default 2: the slot)
 }
 CASES = ["sh3_scalerot", "antialiasing", "dense_opaque", "lists_1k_2k", "lists_4k_8k", "lists_over_8k"]
 
