@@ -567,15 +567,6 @@ __device__ __forceinline__ void view_backward(const ViewCam& c, const GaussIn& g
 // With GSR_GB_HALVES the SH rows go through LDS 32 at a time at the end of the kernel
 // (lanes 0-31, then 32-63): 6.6 KiB of LDS per wave instead of 13, twice the waves per CU.
 constexpr int kGbShRows = GSR_GB_HALVES ? 32 : 64;
-// GSR_GB_ONEPASS (live list, combined SH layout): the deferred SH pass takes all 64 rows at once --
-// one gather latency instead of two in a row.  Its 13 KiB of LDS per wave costs no occupancy there:
-// the kernel's ~150 VGPRs already hold it to three waves per SIMD.  (The split layout keeps the halves:
-// one lane per 45-float rest row would hold 45 loads in registers.)
-#ifndef GSR_GB_ONEPASS
-#define GSR_GB_ONEPASS 1
-#endif
-template <int SH_MODE, bool LIST>
-constexpr int gb_sh_rows() { return (LIST && SH_MODE == kShLdsCombined && GSR_GB_ONEPASS) ? 64 : kGbShRows; }
 // Occupancy target (A/B: GSR_GB_WAVES).  Unconstrained, the body takes 134 VGPRs: 3 waves per
 // SIMD, too few loads in flight for an HBM-bound kernel.
 #ifdef GSR_GB_WAVES
@@ -588,8 +579,7 @@ constexpr int gb_sh_rows() { return (LIST && SH_MODE == kShLdsCombined && GSR_GB
 // row is touched.  At 1M@1080p that is ~2000 waves instead of 15625.
 template <int SH_MODE, bool LIST = false>
 __global__ void __launch_bounds__(64) GSR_GB_OCCUPANCY gauss_bwd_kernel(GaussBwdArgs a) {
-    constexpr int kRows = gb_sh_rows<SH_MODE, LIST>();  // SH rows per pass of the deferred SH backward
-    __shared__ __attribute__((aligned(16))) float s_sh[SH_MODE != kShGlobal ? kRows * kShStride : 4];
+    __shared__ __attribute__((aligned(16))) float s_sh[SH_MODE != kShGlobal ? kGbShRows * kShStride : 4];
     const int lane = threadIdx.x;
     const int g0 = blockIdx.x * 64;
     int idx = g0 + lane;
@@ -728,18 +718,18 @@ __global__ void __launch_bounds__(64) GSR_GB_OCCUPANCY gauss_bwd_kernel(GaussBwd
         // SH backward, half a wave at a time through LDS: coalesced stage-in of 32 rows,
         // their lanes evaluate it in place, coalesced write-back of the 32 dL/dSH rows
         const unsigned long long need = __ballot(sh_late);  // rows whose SH is read at all
-        for (int half = 0; half < 64 / kRows; half++) {
-            const int rows = LIST ? kRows : min(kRows, nvalid - half * kRows);
+        for (int half = 0; half < 2; half++) {
+            const int rows = LIST ? kGbShRows : min(kGbShRows, nvalid - half * kGbShRows);
             if (rows <= 0) break;  // wave-uniform
             if constexpr (LIST)  // the lanes' rows, wherever they are
-                sh_gather_in<kRows, 64, SH_MODE == kShLdsSplit>(sh_src, sh_late ? idx : -1, half * kRows, s_sh,
+                sh_gather_in<kGbShRows, 64, SH_MODE == kShLdsSplit>(sh_src, sh_late ? idx : -1, half * kGbShRows, s_sh,
                                                                    kShStride, lane);
             else
-                sh_stage_in<kRows, 64, SH_MODE == kShLdsSplit>(sh_src, g0 + half * kRows, rows, s_sh,
-                                                              kShStride, lane, need >> (half * kRows));
+                sh_stage_in<kGbShRows, 64, SH_MODE == kShLdsSplit>(sh_src, g0 + half * kGbShRows, rows, s_sh,
+                                                                  kShStride, lane, need >> (half * kGbShRows));
             __syncthreads();
-            if (lane / kRows == half && idx < a.P) {
-                float* row = &s_sh[(lane % kRows) * kShStride];
+            if ((lane >> 5) == half && idx < a.P) {
+                float* row = &s_sh[(lane & 31) * kShStride];
                 if (sh_late) {
                     // split layout: pin the view vector here -- otherwise the compiler evaluates the SH
                     // basis ahead of the row gather and the barrier, and the values held across it push
@@ -759,12 +749,12 @@ __global__ void __launch_bounds__(64) GSR_GB_OCCUPANCY gauss_bwd_kernel(GaussBwd
             __syncthreads();
             if constexpr (LIST) {
                 if (a.dL_dsh || a.dL_ddc)
-                    sh_gather_out<kRows, 64, SH_MODE == kShLdsSplit>(sh_dst, sh_late ? idx : -1, half * kRows,
+                    sh_gather_out<kGbShRows, 64, SH_MODE == kShLdsSplit>(sh_dst, sh_late ? idx : -1, half * kGbShRows,
                                                                         s_sh, kShStride, lane);
             } else if (a.dL_dsh || a.dL_ddc) {
-                sh_stage_out<kRows, 64, SH_MODE == kShLdsSplit>(sh_dst, g0 + half * kRows, rows, s_sh,
-                                                               kShStride, lane,
-                                                               a.sparse ? need >> (half * kRows) : ~0ull);
+                sh_stage_out<kGbShRows, 64, SH_MODE == kShLdsSplit>(sh_dst, g0 + half * kGbShRows, rows, s_sh,
+                                                                   kShStride, lane,
+                                                                   a.sparse ? need >> (half * kGbShRows) : ~0ull);
             }
             __syncthreads();
         }
