@@ -196,6 +196,139 @@ __device__ __forceinline__ void reduce_records(int P, int g0, const uint32_t* __
     }
 }
 
+// Compacted variant (GSR_REDUCE_COMPACT, the default): per window of 1024 content bytes the
+// positions of the records are compacted into an LDS list (per-lane popcounts of the set bytes, a
+// wave prefix sum, each lane writing its own positions), and the list is reduced 64 RECORDS at a
+// time instead of 64 positions at a time -- at 1M@1080p a wave's ~508 instance positions hold ~80
+// records: two groups instead of a chain of ~8 chunks, each a dependent load + scan + hand-off.
+// A Gaussian's records are its slots [r0, r1) of the list (counted from the bytes below its range
+// start and end); the owner search, segmented scan and hand-off are the chunked variant's, in slot
+// space.  Deterministic (fixed order), though grouped differently from the chunked variant.
+#ifndef GSR_REDUCE_COMPACT
+#define GSR_REDUCE_COMPACT 1
+#endif
+__device__ __forceinline__ uint64_t byte_flags(uint64_t x) {  // each nonzero byte -> 0x01, zero -> 0x00
+    x |= x >> 4;
+    x |= x >> 2;
+    x |= x >> 1;
+    return x & 0x0101010101010101ull;
+}
+__device__ __forceinline__ void reduce_records_compact(int P, int g0, const uint32_t* __restrict__ rec_start,
+                                                       const uint32_t* __restrict__ tiles_touched,
+                                                       const GradRecs& recs, float* s_rec, float4& sa, float4& sb,
+                                                       float2& sc) {
+    const int lane = threadIdx.x;
+    const int g = g0 + lane;
+    const bool valid = g < P;
+    const int g_last = min(g0 + 63, P - 1);
+    const uint32_t E0 = rec_start[g0];
+    const uint32_t E1 = rec_start[g_last] + tiles_touched[g_last];
+    const uint32_t n = valid ? tiles_touched[g] : 0u;
+    const uint32_t my0 = valid ? rec_start[g] : E1;
+    const uint32_t my1 = my0 + n;
+    sa = make_float4(0.f, 0.f, 0.f, 0.f);
+    sb = sa;
+    sc = make_float2(0.f, 0.f);
+    __shared__ uint16_t s_list[1024];  // the window's record positions, as offsets from its first byte
+    __shared__ uint32_t s_mark[64];
+    float4* part = reinterpret_cast<float4*>(s_rec);  // [64][3] float4: a Gaussian's group total
+    for (uint32_t wa = E0 & ~15u; wa < E1; wa += 1024u) {  // uniform
+        // content bytes [wa, wa + 1024): lane l holds wa + 16 l .. + 15, masked to [E0, E1)
+        const uint32_t p = wa + 16u * (uint32_t)lane;
+        uint64_t lo = 0, hi = 0;
+        if (p < E1) {
+            const uint4 f = *reinterpret_cast<const uint4*>(recs.flag + p);
+            lo = byte_flags((uint64_t)f.x | ((uint64_t)f.y << 32));
+            hi = byte_flags((uint64_t)f.z | ((uint64_t)f.w << 32));
+            const uint32_t k = E1 - p;  // bytes of this lane below E1
+            if (k < 8) { lo &= (1ull << (8 * k)) - 1ull; hi = 0; }
+            else if (k < 16) hi &= (1ull << (8 * (k - 8))) - 1ull;
+            if (p < E0) {  // (first window, lane 0 only) bytes below E0 are the previous wave's
+                const uint32_t d = E0 - p;
+                if (d >= 8) { lo = 0; hi &= ~0ull << (8 * (d - 8)); }
+                else lo &= ~0ull << (8 * d);
+            }
+        }
+        const uint32_t c = (uint32_t)(__popcll(lo) + __popcll(hi));
+        const uint32_t incl = wave_incl_sum(c), off = incl - c;
+        const uint32_t R = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);  // records in the window
+        if (R == 0) continue;  // uniform
+        __builtin_amdgcn_wave_barrier();  // the previous window's readers are done (in-order LDS)
+        {
+            uint32_t k = off;
+            for (uint64_t t = lo; t; t &= t - 1) s_list[k++] = (uint16_t)(16 * lane + (__builtin_ctzll(t) >> 3));
+            for (uint64_t t = hi; t; t &= t - 1) s_list[k++] = (uint16_t)(16 * lane + 8 + (__builtin_ctzll(t) >> 3));
+        }
+        __builtin_amdgcn_wave_barrier();
+        // this lane's Gaussian: its record slots [r0, r1) of the list (records at positions below q)
+        auto slots_below = [&](uint32_t q) -> uint32_t {
+            const uint32_t d = q <= wa ? 0u : min(q - wa, 1024u);
+            const int L = (int)min(d >> 4, 63u);
+            const uint32_t offL = (uint32_t)__shfl((int)off, L);
+            const uint64_t loL = __shfl(lo, L), hiL = __shfl(hi, L);
+            const uint32_t b = d - 16u * (uint32_t)L;  // bytes of lane L below q (16: all of them)
+            const uint64_t mlo = b >= 8 ? ~0ull : (1ull << (8 * b)) - 1ull;
+            const uint64_t mhi = b >= 16 ? ~0ull : b <= 8 ? 0ull : (1ull << (8 * (b - 8))) - 1ull;
+            return offL + (uint32_t)(__popcll(loL & mlo) + __popcll(hiL & mhi));
+        };
+        const uint32_t r0 = slots_below(my0), r1 = n ? slots_below(my1) : r0;
+        const bool mine = r1 > r0;
+        for (uint32_t k0 = 0; k0 < R; k0 += 64) {  // uniform: 64 records at a time
+            const uint32_t k = k0 + (uint32_t)lane;
+            const bool has = k < R;
+            // owner of slot k: the largest lane with records whose first slot is <= k
+            const unsigned long long st = __ballot(mine && r0 < k0);
+            const uint32_t carry = st ? 64u - (uint32_t)__clzll((long long)st) : 0u;
+            s_mark[lane] = 0u;
+            __builtin_amdgcn_wave_barrier();
+            if (mine && r0 >= k0 && r0 < k0 + 64) s_mark[r0 - k0] = (uint32_t)lane + 1u;
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t m = max(wave_incl_max(s_mark[lane]), carry);
+            __builtin_amdgcn_wave_barrier();
+            const int owner = has && m ? (int)m - 1 : -1;
+            const uint32_t o0 = (uint32_t)__shfl((int)r0, owner < 0 ? 0 : owner);
+            const int seg0 = has ? (o0 > k0 ? (int)(o0 - k0) : 0) : lane;
+            float4 x = make_float4(0.f, 0.f, 0.f, 0.f), y = x;
+            float2 z = make_float2(0.f, 0.f);
+            if (has) {
+                const uint32_t e = wa + (uint32_t)s_list[k];
+                x = GSR_LD_REC(recs.a + (size_t)kRecAB * e);
+                y = GSR_LD_REC(recs.b + (size_t)kRecAB * e);
+                z = GSR_LD_REC(recs.c + (size_t)kRecC * e);
+            }
+            const int r = lane & 15, row = lane >> 4;
+            const float m1 = lane - 1 >= seg0 && r >= 1 ? 1.f : 0.f, m2 = lane - 2 >= seg0 && r >= 2 ? 1.f : 0.f,
+                        m4 = lane - 4 >= seg0 && r >= 4 ? 1.f : 0.f, m8 = lane - 8 >= seg0 && r >= 8 ? 1.f : 0.f,
+                        mb15 = (row & 1) && row * 16 - 1 >= seg0 ? 1.f : 0.f,
+                        mb31 = row >= 2 && 31 >= seg0 ? 1.f : 0.f;
+            float v[10] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w, z.x, z.y};
+#pragma unroll
+            for (int i = 0; i < 10; i++) {
+                v[i] = fmaf(dpp_f32<0x111, 0xf, true>(v[i]), m1, v[i]);
+                v[i] = fmaf(dpp_f32<0x112, 0xf, true>(v[i]), m2, v[i]);
+                v[i] = fmaf(dpp_f32<0x114, 0xf, true>(v[i]), m4, v[i]);
+                v[i] = fmaf(dpp_f32<0x118, 0xf, true>(v[i]), m8, v[i]);
+                v[i] = fmaf(dpp_f32<0x142, 0xa, false>(v[i]), mb15, v[i]);
+                v[i] = fmaf(dpp_f32<0x143, 0xc, false>(v[i]), mb31, v[i]);
+            }
+            const int next_owner = __shfl_down(owner, 1);
+            if (owner >= 0 && (lane == 63 || next_owner != owner)) {  // the run's last lane hands it over
+                part[owner * 3 + 0] = make_float4(v[0], v[1], v[2], v[3]);
+                part[owner * 3 + 1] = make_float4(v[4], v[5], v[6], v[7]);
+                part[owner * 3 + 2] = make_float4(v[8], v[9], 0.f, 0.f);
+            }
+            __syncthreads();
+            if (max(r0, k0) < min(r1, k0 + 64)) {  // this Gaussian has records in the group
+                const float4 pp = part[lane * 3 + 0], q = part[lane * 3 + 1], ww = part[lane * 3 + 2];
+                sa.x += pp.x; sa.y += pp.y; sa.z += pp.z; sa.w += pp.w;
+                sb.x += q.x; sb.y += q.y; sb.z += q.z; sb.w += q.w;
+                sc.x += ww.x; sc.y += ww.y;
+            }
+            __syncthreads();
+        }
+    }
+}
+
 __global__ void __launch_bounds__(64) gauss_reduce_kernel(int P, const uint32_t* __restrict__ rec_start,
                                                           const uint32_t* __restrict__ tiles_touched,
                                                           GradRecs recs, GradRecs sums, uint32_t* __restrict__ flags,
@@ -207,7 +340,10 @@ __global__ void __launch_bounds__(64) gauss_reduce_kernel(int P, const uint32_t*
     const int g = blockIdx.x * 64 + (int)threadIdx.x;
     float4 sa, sb;
     float2 sc;
-    reduce_records(P, blockIdx.x * 64, rec_start, tiles_touched, recs, s_rec, sa, sb, sc);
+    if (GSR_REDUCE_COMPACT)
+        reduce_records_compact(P, blockIdx.x * 64, rec_start, tiles_touched, recs, s_rec, sa, sb, sc);
+    else
+        reduce_records(P, blockIdx.x * 64, rec_start, tiles_touched, recs, s_rec, sa, sb, sc);
     // a Gaussian with a gradient (gauss_bwd's condition)
     const bool lv = g < P && radii[g] > 0 &&
                     ((sa.x != 0.f) | (sa.y != 0.f) | (sa.z != 0.f) | (sa.w != 0.f) | (sb.x != 0.f) |
