@@ -271,7 +271,8 @@ __device__ __forceinline__ void reduce_records_compact(int P, int g0, const uint
             const uint64_t mhi = b >= 16 ? ~0ull : b <= 8 ? 0ull : (1ull << (8 * (b - 8))) - 1ull;
             return offL + (uint32_t)(__popcll(loL & mlo) + __popcll(hiL & mhi));
         };
-        const uint32_t r0 = slots_below(my0), r1 = n ? slots_below(my1) : r0;
+        // (both calls on every lane: slots_below shuffles across lanes, so it must not sit in a branch)
+        const uint32_t r0 = slots_below(my0), r1e = slots_below(my1), r1 = n ? r1e : r0;
         const bool mine = r1 > r0;
         for (uint32_t k0 = 0; k0 < R; k0 += 64) {  // uniform: 64 records at a time
             const uint32_t k = k0 + (uint32_t)lane;
