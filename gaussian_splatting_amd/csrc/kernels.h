@@ -49,6 +49,7 @@ struct RenderFwdArgs {
     int seg_ck;
     uint32_t* seg_ck_out;           // GeomState::fwd_seg_ck: seg_ck recorded for the backward
     uint32_t* fault;                // GeomState::status + 1: bit 0 = a shared-staging wait gave up (never expected)
+    uint32_t half_tiles;            // hybrid grid (render.hip GSR_FWD_TAIL_QUADS): tiles done as half-tile units
     unsigned long long* census;     // diagnostic pair counts (gsr_census_set) or null
     // reachable-prefix sort (GeomState): entries in order per tile, and the redo filing
     const uint32_t* sorted_len;

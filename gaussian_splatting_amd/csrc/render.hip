@@ -181,6 +181,17 @@ __device__ __forceinline__ void lds_store_rel(int* p, int v) {
     __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+template <int NB>
+struct FwdLds {
+    float4 xy[NB][kBatch], cq[NB][kBatch], col[NB][kBatch];
+    int tag[NB], claim[NB], done[2];
+};
+template <int NB>
+__device__ __forceinline__ FwdLds<NB>& fwd_lds() {
+    __shared__ FwdLds<NB> s;
+    return s;
+}
+
 template <int NQ, bool CENSUS, bool SHARED = false>
 __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const uint32_t tile, const int part) {
   {
@@ -200,8 +211,14 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const ui
         GSR_STAMP_RT(g_st_rfwd, tile, 4);
     }
 
-    __shared__ float4 s_xy[NB][kBatch], s_cq[NB][kBatch], s_col[NB][kBatch];  // (x, y, o, 1/z), (A, B, C, quads), rgb
-    __shared__ int s_tag[NB], s_claim[NB], s_done[2];  // SHARED: slot k % NB holds batch s_tag; batches walked
+    // (one LDS block per NB, whatever NQ: the hybrid launch's half-tile and quadrant units share it)
+    FwdLds<NB>& L = fwd_lds<NB>();
+    auto& s_xy = L.xy;  // (x, y, o, 1/z)
+    auto& s_cq = L.cq;  // (A, B, C, quads)
+    auto& s_col = L.col;  // rgb
+    auto& s_tag = L.tag;  // SHARED: slot k % NB holds batch s_tag
+    auto& s_claim = L.claim;
+    auto& s_done = L.done;  // SHARED: batches walked per part
     if (SHARED) {
         if (threadIdx.x < NB) s_tag[threadIdx.x] = s_claim[threadIdx.x] = (int)threadIdx.x - NB;
         if (threadIdx.x < 2) s_done[threadIdx.x] = 0;
@@ -430,6 +447,20 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const ui
         old = __shfl(old, 0);
         if ((old >> 62) == 0) return;  // the other part finishes the tile
         lm = max(lm, (uint32_t)((old >> (31 * (part ^ 1))) & 0x7fffffffull));
+    } else if (NPART == 4) {
+        // quadrant units: the join word's low half is the max of the limits, its high half the count
+        // of parts done.  Each part's max returns before it counts itself, so the part that counts 3
+        // finds every other part's limit in the max (one L2, atomics in arrival order).
+        uint32_t* jw = reinterpret_cast<uint32_t*>(&a.tile_join[tile]);
+        uint32_t done = 0;
+        if (lane == 0) {
+            const uint32_t prev = atomicMax(&jw[0], lm);
+            done = atomicAdd(&jw[1], 1u + 0u * prev);  // (prev: issued after the max has returned)
+            if (done == 3u) lm = max(lm, atomicMax(&jw[0], 0u));
+        }
+        done = (uint32_t)__shfl((int)done, 0);
+        if (done != 3u) return;  // another part finishes the tile
+        lm = (uint32_t)__shfl((int)lm, 0);
     }
     // The backward's work list: units (tile, k * seg_ck) for the full segments of S entries below
     // the limit, then the last partial segment into one of four lists by length quarter.
@@ -460,6 +491,29 @@ __global__ void __launch_bounds__(64) GSR_FWD_OCCUPANCY render_fwd_kernel(Render
     if (blockIdx.x == 0 && threadIdx.x == 0) *a.seg_ck_out = (uint32_t)a.seg_ck;  // for the backward
     if (tile >= a.gx * a.gy) return;
     render_fwd_tile<NQ, CENSUS>(a, tile, part);
+}
+
+// Hybrid grid (GSR_FWD_TAIL_QUADS): half-tile units for the first tiles in dispatch order, quadrant
+// units (one wave per 8x8 quadrant, four per tile) for the last `quad_tiles` tiles.  A launch ends about
+// one unit's duration after its last units start, and a half tile's cost (set by how soon its pixels
+// saturate) is not known in advance, so the units dispatched last are made short instead: the tail
+// shrinks, for ~2x the staging work on those tiles only.
+#ifndef GSR_FWD_TAIL_QUADS
+#define GSR_FWD_TAIL_QUADS 0
+#endif
+__global__ void __launch_bounds__(64) GSR_FWD_OCCUPANCY render_fwd_hybrid_kernel(RenderFwdArgs a) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *a.seg_ck_out = (uint32_t)a.seg_ck;  // for the backward
+    const uint32_t half_tiles = a.half_tiles;
+    const uint32_t hb = 2 * half_tiles;  // blocks of the half-tile region (half_tiles: a multiple of 8)
+    if (blockIdx.x < hb) {
+        const uint32_t tile = (blockIdx.x / 16) * 8 + blockIdx.x % 8;
+        render_fwd_tile<2, false>(a, tile, (int)((blockIdx.x / 8) % 2));
+    } else {
+        const uint32_t b = blockIdx.x - hb;
+        const uint32_t tile = half_tiles + (b / 32) * 8 + b % 8;
+        if (tile >= a.gx * a.gy) return;
+        render_fwd_tile<1, false>(a, tile, (int)((b / 8) % 4));
+    }
 }
 
 // Shared staging (GSR_FWD_SHARED): one 128-thread workgroup per tile, its two waves the halves.
@@ -518,7 +572,14 @@ hipError_t launch_render_fwd(const RenderFwdArgs& a, hipStream_t stream, int qua
     const uint32_t tiles = a.gx * a.gy;
     if (tiles == 0) return hipSuccess;
     const uint32_t groups = (tiles + 7) / 8;
-    if (GSR_FWD_SHARED && quads == 2) {
+    if (GSR_FWD_TAIL_QUADS && quads == 2 && !a.census && tiles >= 16) {
+        // the last ~GSR_FWD_TAIL_QUADS percent of the tiles (whole groups of 8) as quadrant units
+        const uint32_t qgroups = max(1u, groups * (uint32_t)GSR_FWD_TAIL_QUADS / 100u);
+        const uint32_t hgroups = groups - qgroups;
+        RenderFwdArgs h = a;
+        h.half_tiles = hgroups * 8;
+        hipLaunchKernelGGL(render_fwd_hybrid_kernel, dim3(hgroups * 16 + qgroups * 32), dim3(kWave), 0, stream, h);
+    } else if (GSR_FWD_SHARED && quads == 2) {
         if (a.census)
             hipLaunchKernelGGL((render_fwd_shared_kernel<true>), dim3(tiles), dim3(2 * kWave), 0, stream, a);
         else
