@@ -454,8 +454,9 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const ui
         uint32_t* jw = reinterpret_cast<uint32_t*>(&a.tile_join[tile]);
         uint32_t done = 0;
         if (lane == 0) {
-            const uint32_t prev = atomicMax(&jw[0], lm);
-            done = atomicAdd(&jw[1], 1u + 0u * prev);  // (prev: issued after the max has returned)
+            (void)atomicMax(&jw[0], lm);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the max has been performed before the count
+            done = atomicAdd(&jw[1], 1u);
             if (done == 3u) lm = max(lm, atomicMax(&jw[0], 0u));
         }
         done = (uint32_t)__shfl((int)done, 0);
