@@ -500,7 +500,7 @@ __global__ void __launch_bounds__(64) GSR_FWD_OCCUPANCY render_fwd_kernel(Render
 // saturate) is not known in advance, so the units dispatched last are made short instead: the tail
 // shrinks, for ~2x the staging work on those tiles only.
 #ifndef GSR_FWD_TAIL_QUADS
-#define GSR_FWD_TAIL_QUADS 0
+#define GSR_FWD_TAIL_QUADS 10
 #endif
 __global__ void __launch_bounds__(64) GSR_FWD_OCCUPANCY render_fwd_hybrid_kernel(RenderFwdArgs a) {
     if (blockIdx.x == 0 && threadIdx.x == 0) *a.seg_ck_out = (uint32_t)a.seg_ck;  // for the backward
@@ -573,9 +573,18 @@ hipError_t launch_render_fwd(const RenderFwdArgs& a, hipStream_t stream, int qua
     const uint32_t tiles = a.gx * a.gy;
     if (tiles == 0) return hipSuccess;
     const uint32_t groups = (tiles + 7) / 8;
-    if (GSR_FWD_TAIL_QUADS && quads == 2 && !a.census && tiles >= 16) {
-        // the last ~GSR_FWD_TAIL_QUADS percent of the tiles (whole groups of 8) as quadrant units
-        const uint32_t qgroups = max(1u, groups * (uint32_t)GSR_FWD_TAIL_QUADS / 100u);
+    // the device's CU count, read once (the hybrid grid below is sized by it)
+    static const uint32_t cus = [] {
+        int dev = 0, n = 256;
+        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+        return (uint32_t)max(1, n);
+    }();
+    if (GSR_FWD_TAIL_QUADS && quads == 2 && !a.census && tiles >= 16 && tiles <= 64 * cus) {
+        // the last tiles (whole groups of 8) as quadrant units: GSR_FWD_TAIL_QUADS percent of them, at most
+        // ~0.4 groups per CU.  Measured (profiles/r04/r4k, r4l): 1M@1080p render_fwd 194 -> 188 us, 500k@1080p
+        // 217 -> 212 us; at 5M@4K (32400 tiles, ~8 rounds of half tiles per wave slot) the tail is a smaller
+        // share and the quadrants' extra staging cost more than it saves (+3..8 us), hence the tile bound.
+        const uint32_t qgroups = min((cus * 2) / 5 + 1, max(1u, groups * (uint32_t)GSR_FWD_TAIL_QUADS / 100u));
         const uint32_t hgroups = groups - qgroups;
         RenderFwdArgs h = a;
         h.half_tiles = hgroups * 8;
