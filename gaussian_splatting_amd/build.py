@@ -74,13 +74,18 @@ def _stamp_path(lib: str) -> str:
     return lib + ".inputs"
 
 
-def _compile(src: str, objdir: str = OBJ, extra=(), build_id: str = "") -> str:
+def _compile(src: str, objdir: str = OBJ, extra=(), build_id: str = "", verbose: bool = False) -> str:
+    import time
+
     obj = os.path.join(objdir, os.path.splitext(src)[0] + ".o")
     ident = [f'-DGSR_BUILD_ID="{build_id}"'] if build_id and src == "api.hip" else []
     cmd = [HIPCC, *CXXFLAGS, *FILE_FLAGS.get(src, []), *extra, *ident, "-c", os.path.join(CSRC, src), "-o", obj]
+    t0 = time.perf_counter()
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    if verbose:  # one line per compiled file: the build log shows that hipcc ran, and for how long
+        print(f"[gsr] hipcc {src} -> {os.path.basename(obj)} {time.perf_counter() - t0:.1f}s", flush=True)
     return obj
 
 
@@ -107,7 +112,7 @@ def build(force: bool = False, jobs: int = 5, verbose: bool = True, variant: str
     if os.path.exists(stamp):
         os.remove(stamp)
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-        objs = list(ex.map(lambda f: _compile(f, objdir, extra, ident), SOURCES))
+        objs = list(ex.map(lambda f: _compile(f, objdir, extra, ident, verbose), SOURCES))
     LIB_OUT = lib
     tmp = os.path.join(os.path.dirname(LIB_OUT), "tmp_" + os.path.basename(LIB_OUT))
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs]

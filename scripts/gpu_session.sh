@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU-box session: parity tests, bench, rocprofv3 kernel trace.  Stops at the
 # first crash / timeout (exit codes other than 0 = pass and 1 = test failures).
-# Usage: scripts/gpu_session.sh TAG [tests] [bench] [prof] [pmc] [full]
+# Usage: scripts/gpu_session.sh TAG [forcebuild] [tests] [smoke] [full] [bench] [prof] [pmc] [cfg:C] ...
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
@@ -57,6 +57,12 @@ for stage in "$@"; do
     stamps)  # per-workgroup timelines of the binning and render kernels (needs libgsr_stamps.so, built beforehand)
       GSR_LIBRARY=$ROOT/gaussian_splatting_amd/lib/libgsr_stamps.so timeout -k 10 300 python tools/stamps.py > "$OUT/stamps.json" 2> "$OUT/stamps.err"; rc=$?
       echo "stamps rc=$rc"; tail -c 3000 "$OUT/stamps.json"; [ $rc -eq 0 ] || exit $rc ;;
+    forcebuild)  # rebuild libgsr.so from the sources on this box (ignoring the pushed library) and check its id
+      { sha256sum gaussian_splatting_amd/lib/libgsr.so; cat gaussian_splatting_amd/lib/libgsr.so.inputs; } > "$OUT/build_force.log" 2>&1
+      timeout -k 10 900 python -m gaussian_splatting_amd.build --force --jobs 16 >> "$OUT/build_force.log" 2>&1; rc=$?
+      { sha256sum gaussian_splatting_amd/lib/libgsr.so; python -c "from gaussian_splatting_amd import _lib, build; \
+print('gsr_build_id', _lib.build_id(), 'tree', build.input_hash())"; } >> "$OUT/build_force.log" 2>&1
+      echo "forcebuild rc=$rc"; cat "$OUT/build_force.log"; [ $rc -eq 0 ] || exit $rc ;;
     cpus)  # the CPU set the baselines run on
       python -c "import os; print('affinity', len(os.sched_getaffinity(0)), 'cpu_count', os.cpu_count(), 'OMP', os.environ.get('OMP_NUM_THREADS'))" | tee "$OUT/cpus.txt" ;;
     rehearse2)  # N=2 on one GPU (gloo collectives): the multi-rank bench path, both exchanges
