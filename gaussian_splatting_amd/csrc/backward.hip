@@ -714,6 +714,18 @@ constexpr int kGbShRows = GSR_GB_HALVES ? 32 : 64;
 // LIST: lane i of the grid takes entry i of the live list (the Gaussians with a gradient,
 // gauss_reduce), with per-lane SH access (kShGlobal); the outputs were zero-filled, so no other
 // row is touched.  At 1M@1080p that is ~2000 waves instead of 15625.
+// The workgroup is one wave: the SH pass's LDS hand-offs need only the wave's own in-order LDS
+// (GSR_GB_WAVESYNC), not __syncthreads, whose fence also waits for every store the wave has issued.
+#ifndef GSR_GB_WAVESYNC
+#define GSR_GB_WAVESYNC 1
+#endif
+__device__ __forceinline__ void gb_sync() {
+#if GSR_GB_WAVESYNC
+    __builtin_amdgcn_wave_barrier();
+#else
+    __syncthreads();
+#endif
+}
 template <int SH_MODE, bool LIST = false>
 __global__ void __launch_bounds__(64) GSR_GB_OCCUPANCY gauss_bwd_kernel(GaussBwdArgs a) {
     __shared__ __attribute__((aligned(16))) float s_sh[SH_MODE != kShGlobal ? kGbShRows * kShStride : 4];
@@ -864,7 +876,7 @@ __global__ void __launch_bounds__(64) GSR_GB_OCCUPANCY gauss_bwd_kernel(GaussBwd
             else
                 sh_stage_in<kGbShRows, 64, SH_MODE == kShLdsSplit>(sh_src, g0 + half * kGbShRows, rows, s_sh,
                                                                   kShStride, lane, need >> (half * kGbShRows));
-            __syncthreads();
+            gb_sync();
             if ((lane >> 5) == half && idx < a.P) {
                 float* row = &s_sh[(lane & 31) * kShStride];
                 if (sh_late) {
@@ -883,7 +895,7 @@ __global__ void __launch_bounds__(64) GSR_GB_OCCUPANCY gauss_bwd_kernel(GaussBwd
                         *reinterpret_cast<float4*>(&row[k]) = make_float4(0.f, 0.f, 0.f, 0.f);
                 }
             }
-            __syncthreads();
+            gb_sync();
             if constexpr (LIST) {
                 if (a.dL_dsh || a.dL_ddc)
                     sh_gather_out<kGbShRows, 64, SH_MODE == kShLdsSplit>(sh_dst, sh_late ? idx : -1, half * kGbShRows,
@@ -893,7 +905,7 @@ __global__ void __launch_bounds__(64) GSR_GB_OCCUPANCY gauss_bwd_kernel(GaussBwd
                                                                    kShStride, lane,
                                                                    a.sparse ? need >> (half * kGbShRows) : ~0ull);
             }
-            __syncthreads();
+            gb_sync();
         }
     } else if constexpr (SH_MODE != kShGlobal) {
         // coalesced write-back of the wave's dL/dSH rows

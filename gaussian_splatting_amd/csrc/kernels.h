@@ -291,12 +291,37 @@ __device__ __forceinline__ void sh_stage_out(const ShGradAddr& ga, int r0, int r
 // fully unrolled loop kept ~23 iterations' addresses live across the kernel: 308 VGPRs, one wave
 // per SIMD; one iteration at a time serialised the loads.)
 #define GSR_PRAGMA(x) _Pragma(#x)
+#ifndef GSR_GATHER_BATCH
+#define GSR_GATHER_BATCH 1
+#endif
 #ifndef GSR_GATHER_UNROLL_COMB
 #define GSR_GATHER_UNROLL_COMB 12
 #endif
 template <int ROWS, int THREADS, bool SPLIT>
 __device__ __forceinline__ void sh_gather_in(const ShAddr& sa, int g, int row0, float* lds, int stride, int tid) {
     if constexpr (!SPLIT) {
+#if GSR_GATHER_BATCH
+        // every piece loaded before any is stored (a row not wanted loads row 0's piece, which the
+        // caller's tensor always has): one memory latency for the block, where a load inside the
+        // per-lane branch made each piece wait for its own (six dependent round trips per 32 rows)
+        typedef float v4f __attribute__((ext_vector_type(4)));
+        constexpr int K = ROWS * (kShRowF / 4) / THREADS;
+        static_assert(K <= 12, "pieces per lane held in registers");
+        v4f v[K];
+        int gk[K];
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const int i4 = k * THREADS + tid, row = i4 / (kShRowF / 4), c4 = i4 - row * (kShRowF / 4);
+            gk[k] = __shfl(g, row0 + row);
+            v[k] = reinterpret_cast<const v4f*>(sa.shs + (size_t)max(gk[k], 0) * kShRowF)[c4];
+        }
+        __builtin_amdgcn_sched_barrier(0);  // (left alone, the scheduler sinks each load to its store)
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const int i4 = k * THREADS + tid, row = i4 / (kShRowF / 4), c4 = i4 - row * (kShRowF / 4);
+            if (gk[k] >= 0) *reinterpret_cast<v4f*>(&lds[row * stride + 4 * c4]) = v[k];
+        }
+#else
 GSR_PRAGMA(unroll GSR_GATHER_UNROLL_COMB)
         for (int k = 0; k < ROWS * (kShRowF / 4) / THREADS; k++) {
             const int i4 = k * THREADS + tid, row = i4 / (kShRowF / 4), c4 = i4 - row * (kShRowF / 4);
@@ -305,6 +330,7 @@ GSR_PRAGMA(unroll GSR_GATHER_UNROLL_COMB)
                 *reinterpret_cast<float4*>(&lds[row * stride + 4 * c4]) =
                     reinterpret_cast<const float4*>(sa.shs + (size_t)gr * kShRowF)[c4];
         }
+#endif
     } else {
         // THREADS / ROWS lanes per row, each copying its share of the row's 45 rest floats (one base
         // address, immediate offsets, every load independent) and the last of them the dc triple
