@@ -114,12 +114,20 @@ __device__ __forceinline__ void load_sh(const ShAddr& sa, int idx, int K, float3
 //  * the 64-byte splat records are assembled in LDS and written as one 4 KiB block.
 // A culled Gaussian gets the reference's zero radius / tiles_touched, a 0xffffffff depth
 // key and an all-zero record (never read).
+#ifndef GSR_PRE_PREFETCH
+#define GSR_PRE_PREFETCH 2
+#endif
 constexpr int kPreThreads = 64;
 constexpr int kShHalfRows = 32;
 constexpr int kShRowStride = 52;   // padded LDS row stride (16-byte aligned, conflict-free b128)
 
+#ifdef GSR_PRE_WAVES
+#define GSR_PRE_OCCUPANCY __attribute__((amdgpu_waves_per_eu(GSR_PRE_WAVES)))
+#else
+#define GSR_PRE_OCCUPANCY
+#endif
 template <int SH_MODE>
-__global__ void __launch_bounds__(kPreThreads) preprocess_kernel(PreprocessArgs a) {
+__global__ void __launch_bounds__(kPreThreads) GSR_PRE_OCCUPANCY preprocess_kernel(PreprocessArgs a) {
     __shared__ __attribute__((aligned(16))) float s_buf[SH_MODE != kShGlobal ? kShHalfRows * kShRowStride : 64 * 16];
     static_assert(kShHalfRows * kShRowStride >= 64 * 16, "the record block reuses the SH buffer");
     static_assert(kShHalfRows * kShRowStride >= kShHalfRows * (kShRestF + 3), "the split staging fits the buffer");
@@ -129,6 +137,37 @@ __global__ void __launch_bounds__(kPreThreads) preprocess_kernel(PreprocessArgs 
     const bool valid = idx < a.P;
     const int nvalid = min(kPreThreads, a.P - g0);
     for (uint32_t i = blockIdx.x * kPreThreads + lane; i < a.zero_n; i += gridDim.x * kPreThreads) a.zero[i] = 0u;
+#if GSR_PRE_PREFETCH
+    // Every input of the wave requested up front (GSR_PRE_PREFETCH): the scale, rotation and opacity of
+    // each lane's Gaussian, and both halves of the wave's SH block in registers (6 x 16 B per lane and
+    // half) -- one memory latency for the wave, where the geometry's loads waited for the view
+    // transform and each SH half for the previous half's colours.
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    constexpr bool kPf = SH_MODE == kShLdsCombined;
+    constexpr int kPieces = kShHalfRows * (kShRowF / 4) / kPreThreads;  // 16-byte pieces per lane and half
+    v4f shp[2][kPieces];
+    if constexpr (kPf) {
+        const v4f* src = reinterpret_cast<const v4f*>(a.shs + (size_t)g0 * kShRowF);
+        const int n4 = nvalid * (kShRowF / 4);
+#pragma unroll
+        for (int h = 0; h < (GSR_PRE_PREFETCH == 2 ? 1 : 2); h++)
+#pragma unroll
+            for (int k = 0; k < kPieces; k++) {
+                const int i4 = h * kShHalfRows * (kShRowF / 4) + k * kPreThreads + lane;
+                shp[h][k] = i4 < n4 ? __builtin_nontemporal_load(src + i4) : (v4f){0.f, 0.f, 0.f, 0.f};
+            }
+    }
+    float3 pf_sc = make_float3(0.f, 0.f, 0.f);
+    float4 pf_q = make_float4(1.f, 0.f, 0.f, 0.f);
+    float pf_op = 0.f;
+    if (valid) {
+        if (a.scales && !a.cov3D_precomp) {
+            pf_sc = make_float3(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]);
+            pf_q = reinterpret_cast<const float4*>(a.rotations)[idx];
+        }
+        pf_op = a.opacities[idx];
+    }
+#endif
 
     // ---- geometry (CR/forward.cu:255-326): `ok` replaces the reference's early returns
     bool ok = valid;
@@ -155,9 +194,13 @@ __global__ void __launch_bounds__(kPreThreads) preprocess_kernel(PreprocessArgs 
 #pragma unroll
             for (int i = 0; i < 6; i++) cov3[i] = a.cov3D_precomp[6 * idx + i];
         } else {
+#if GSR_PRE_PREFETCH
+            cov3d_from_scale_rot(pf_sc, a.scale_modifier, pf_q, cov3);
+#else
             const float3 sc = make_float3(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]);
             const float4 q = reinterpret_cast<const float4*>(a.rotations)[idx];
             cov3d_from_scale_rot(sc, a.scale_modifier, q, cov3);
+#endif
         }
         cov = cov2d_project(p_view, a.focal_x, a.focal_y, a.tan_fovx, a.tan_fovy, a.viewmatrix, cov3);
         constexpr float h_var = 0.3f;
@@ -202,8 +245,27 @@ __global__ void __launch_bounds__(kPreThreads) preprocess_kernel(PreprocessArgs 
         for (int half = 0; half < 2; half++) {
             const int rows = min(kShHalfRows, nvalid - half * kShHalfRows);
             if (rows > 0) {  // wave-uniform
+#if GSR_PRE_PREFETCH
+                (void)sa;
+#pragma unroll
+                for (int k = 0; k < kPieces; k++) {
+                    const int i4 = k * kPreThreads + lane, row = i4 / (kShRowF / 4), c4 = i4 - row * (kShRowF / 4);
+                    *reinterpret_cast<v4f*>(&s_buf[row * kShRowStride + 4 * c4]) = shp[half][k];
+                }
+                if (GSR_PRE_PREFETCH == 2 && half == 0) {  // the second half requested now, read after this one
+                    const v4f* src = reinterpret_cast<const v4f*>(a.shs + (size_t)g0 * kShRowF);
+                    const int n4 = nvalid * (kShRowF / 4);
+#pragma unroll
+                    for (int k = 0; k < kPieces; k++) {
+                        const int i4 = kShHalfRows * (kShRowF / 4) + k * kPreThreads + lane;
+                        shp[1][k] = i4 < n4 ? __builtin_nontemporal_load(src + i4) : (v4f){0.f, 0.f, 0.f, 0.f};
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();  // (one wave: its LDS accesses complete in order)
+#else
                 sh_stage_in<kShHalfRows, kPreThreads, false>(sa, g0 + half * kShHalfRows, rows, s_buf, kShRowStride, lane);
                 __syncthreads();
+#endif
                 if ((lane >> 5) == half && ok) {
                     const float* row = &s_buf[(lane & 31) * kShRowStride];
                     float3 sh[16];
@@ -211,7 +273,11 @@ __global__ void __launch_bounds__(kPreThreads) preprocess_kernel(PreprocessArgs 
                     for (int k = 0; k < 16; k++) sh[k] = make_float3(row[3 * k], row[3 * k + 1], row[3 * k + 2]);
                     rgb = sh_to_rgb(a.D, sh, dir.x, dir.y, dir.z);
                 }
+#if GSR_PRE_PREFETCH
+                __builtin_amdgcn_wave_barrier();
+#else
                 __syncthreads();
+#endif
             }
         }
     } else if constexpr (SH_MODE == kShLdsSplit) {
@@ -266,7 +332,11 @@ __global__ void __launch_bounds__(kPreThreads) preprocess_kernel(PreprocessArgs 
     // ---- footprint box and outputs
     float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, r2 = r0, r3 = r0;
     if (ok) {
+#if GSR_PRE_PREFETCH
+        const float o_eff = pf_op * h_scale;
+#else
         const float o_eff = a.opacities[idx] * h_scale;
+#endif
         // Conservative box of the alpha >= 1/255 footprint: o*exp(-q/2) >= 1/255 <=> q <= 2 ln(255 o).
         uint32_t bbx = pack_i16x2(-32768, 32767), bby = pack_i16x2(-32768, 32767);
         if (a.footprint_cull) {
@@ -300,7 +370,11 @@ __global__ void __launch_bounds__(kPreThreads) preprocess_kernel(PreprocessArgs 
     s_rec[lane * kRecRows + 1] = r1;
     s_rec[lane * kRecRows + 2] = r2;
     s_rec[lane * kRecRows + 3] = r3;
+#if GSR_PRE_PREFETCH
+    __builtin_amdgcn_wave_barrier();  // (not __syncthreads: its fence would wait for the stores above)
+#else
     __syncthreads();
+#endif
     float4* dst = a.geom.rec + (size_t)kRecRows * g0;
 #pragma unroll
     for (int k = 0; k < kRecRows; k++) {
