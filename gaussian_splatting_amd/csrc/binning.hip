@@ -1392,6 +1392,9 @@ hipError_t launch_bin_scatter(int P, const GeomState& g, uint32_t gx, uint32_t g
     return hipGetLastError();
 }
 
+#ifndef GSR_C1_GRID_SMALL
+#define GSR_C1_GRID_SMALL 64
+#endif
 hipError_t launch_tile_sort(uint32_t tiles, const uint2* ranges, const GeomState& g, const BinningState& b,
                             size_t cap, hipStream_t stream, bool zero_counts, uint32_t cells, uint32_t prefix) {
     if (tiles == 0 || cap == 0) return hipSuccess;
@@ -1418,7 +1421,7 @@ hipError_t launch_tile_sort(uint32_t tiles, const uint2* ranges, const GeomState
     // class 1 (lists > kClass0Max) is empty or nearly so while the mean list is short (1M@1080p: mean
     // 973 keys): then a small persistent grid -- 512 workgroups of 82 KiB LDS cost 4.6 us to dispatch
     // and retire with nothing to do (r4a trace)
-    const uint32_t c1_grid = cap / tiles <= kClass0Max / 2 ? 64u : 512u;
+    const uint32_t c1_grid = cap / tiles <= kClass0Max / 2 ? (uint32_t)GSR_C1_GRID_SMALL : 512u;
     hipLaunchKernelGGL(tile_sort_class_kernel<1>, grid(c1_grid), dim3(class_threads<1>()), 0, stream, ranges, b.keys, c,
                        b.gid_sorted, g.cls_list + tiles, g.cls_count + 1, lim, g.sorted_len);
     return hipGetLastError();
