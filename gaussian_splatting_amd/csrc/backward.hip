@@ -207,6 +207,18 @@ __device__ __forceinline__ void reduce_records(int P, int g0, const uint32_t* __
 #ifndef GSR_REDUCE_COMPACT
 #define GSR_REDUCE_COMPACT 1
 #endif
+// GSR_REDUCE_PIPE: the records of a window's next group requested before its current group is
+// reduced, the radius read at the start, and wave-local LDS hand-offs (the workgroup is one wave).
+#ifndef GSR_REDUCE_PIPE
+#define GSR_REDUCE_PIPE 1
+#endif
+__device__ __forceinline__ void reduce_sync() {
+#if GSR_REDUCE_PIPE
+    __builtin_amdgcn_wave_barrier();
+#else
+    __syncthreads();
+#endif
+}
 __device__ __forceinline__ uint64_t byte_flags(uint64_t x) {  // each nonzero byte -> 0x01, zero -> 0x00
     x |= x >> 4;
     x |= x >> 2;
@@ -274,9 +286,34 @@ __device__ __forceinline__ void reduce_records_compact(int P, int g0, const uint
         // (both calls on every lane: slots_below shuffles across lanes, so it must not sit in a branch)
         const uint32_t r0 = slots_below(my0), r1e = slots_below(my1), r1 = n ? r1e : r0;
         const bool mine = r1 > r0;
+#if GSR_REDUCE_PIPE
+        // the next group's records are requested before this group is reduced (one latency per window
+        // instead of one per group)
+        float4 xn = make_float4(0.f, 0.f, 0.f, 0.f), yn = xn;
+        float2 zn = make_float2(0.f, 0.f);
+        if ((uint32_t)lane < R) {
+            const uint32_t e = wa + (uint32_t)s_list[lane];
+            xn = GSR_LD_REC(recs.a + (size_t)kRecAB * e);
+            yn = GSR_LD_REC(recs.b + (size_t)kRecAB * e);
+            zn = GSR_LD_REC(recs.c + (size_t)kRecC * e);
+        }
+#endif
         for (uint32_t k0 = 0; k0 < R; k0 += 64) {  // uniform: 64 records at a time
             const uint32_t k = k0 + (uint32_t)lane;
             const bool has = k < R;
+#if GSR_REDUCE_PIPE
+            const float4 x = xn, y = yn;
+            const float2 z = zn;
+            if (k + 64 < R) {
+                const uint32_t e = wa + (uint32_t)s_list[k + 64];
+                xn = GSR_LD_REC(recs.a + (size_t)kRecAB * e);
+                yn = GSR_LD_REC(recs.b + (size_t)kRecAB * e);
+                zn = GSR_LD_REC(recs.c + (size_t)kRecC * e);
+            } else {  // (lanes past the window's records: zeros, as unloaded lanes always held)
+                xn = yn = make_float4(0.f, 0.f, 0.f, 0.f);
+                zn = make_float2(0.f, 0.f);
+            }
+#endif
             // owner of slot k: the largest lane with records whose first slot is <= k
             const unsigned long long st = __ballot(mine && r0 < k0);
             const uint32_t carry = st ? 64u - (uint32_t)__clzll((long long)st) : 0u;
@@ -289,6 +326,7 @@ __device__ __forceinline__ void reduce_records_compact(int P, int g0, const uint
             const int owner = has && m ? (int)m - 1 : -1;
             const uint32_t o0 = (uint32_t)__shfl((int)r0, owner < 0 ? 0 : owner);
             const int seg0 = has ? (o0 > k0 ? (int)(o0 - k0) : 0) : lane;
+#if !GSR_REDUCE_PIPE
             float4 x = make_float4(0.f, 0.f, 0.f, 0.f), y = x;
             float2 z = make_float2(0.f, 0.f);
             if (has) {
@@ -297,6 +335,7 @@ __device__ __forceinline__ void reduce_records_compact(int P, int g0, const uint
                 y = GSR_LD_REC(recs.b + (size_t)kRecAB * e);
                 z = GSR_LD_REC(recs.c + (size_t)kRecC * e);
             }
+#endif
             const int r = lane & 15, row = lane >> 4;
             const float m1 = lane - 1 >= seg0 && r >= 1 ? 1.f : 0.f, m2 = lane - 2 >= seg0 && r >= 2 ? 1.f : 0.f,
                         m4 = lane - 4 >= seg0 && r >= 4 ? 1.f : 0.f, m8 = lane - 8 >= seg0 && r >= 8 ? 1.f : 0.f,
@@ -318,14 +357,14 @@ __device__ __forceinline__ void reduce_records_compact(int P, int g0, const uint
                 part[owner * 3 + 1] = make_float4(v[4], v[5], v[6], v[7]);
                 part[owner * 3 + 2] = make_float4(v[8], v[9], 0.f, 0.f);
             }
-            __syncthreads();
+            reduce_sync();
             if (max(r0, k0) < min(r1, k0 + 64)) {  // this Gaussian has records in the group
                 const float4 pp = part[lane * 3 + 0], q = part[lane * 3 + 1], ww = part[lane * 3 + 2];
                 sa.x += pp.x; sa.y += pp.y; sa.z += pp.z; sa.w += pp.w;
                 sb.x += q.x; sb.y += q.y; sb.z += q.z; sb.w += q.w;
                 sc.x += ww.x; sc.y += ww.y;
             }
-            __syncthreads();
+            reduce_sync();
         }
     }
 }
@@ -339,6 +378,9 @@ __global__ void __launch_bounds__(64) gauss_reduce_kernel(int P, const uint32_t*
                                                           uint32_t* __restrict__ live_count, uint32_t live_cap) {
     __shared__ __attribute__((aligned(16))) float s_rec[64 * kRecStride];
     const int g = blockIdx.x * 64 + (int)threadIdx.x;
+#if GSR_REDUCE_PIPE
+    const int rad = g < P ? radii[g] : 0;  // requested with the range loads, not after the reduction
+#endif
     float4 sa, sb;
     float2 sc;
     if (GSR_REDUCE_COMPACT)
@@ -346,7 +388,10 @@ __global__ void __launch_bounds__(64) gauss_reduce_kernel(int P, const uint32_t*
     else
         reduce_records(P, blockIdx.x * 64, rec_start, tiles_touched, recs, s_rec, sa, sb, sc);
     // a Gaussian with a gradient (gauss_bwd's condition)
-    const bool lv = g < P && radii[g] > 0 &&
+#if !GSR_REDUCE_PIPE
+    const int rad = g < P ? radii[g] : 0;
+#endif
+    const bool lv = g < P && rad > 0 &&
                     ((sa.x != 0.f) | (sa.y != 0.f) | (sa.z != 0.f) | (sa.w != 0.f) | (sb.x != 0.f) |
                      (sb.y != 0.f) | (sb.z != 0.f) | (sb.w != 0.f) | (sc.x != 0.f) | (sc.y != 0.f));
     // With a live list (single view) gauss_bwd reads the sums of the listed Gaussians only, so the
@@ -357,7 +402,7 @@ __global__ void __launch_bounds__(64) gauss_reduce_kernel(int P, const uint32_t*
         sums.c[g] = sc;
     }
     // view-block flag word (gauss_bwd_views_kernel): bit 0 visible, bits 1-3 the SH clamp mask
-    if (g < P && flags) flags[g] = (radii[g] > 0 ? 1u : 0u) | ((uint32_t)(clamped[g] & 7u) << 1);
+    if (g < P && flags) flags[g] = (rad > 0 ? 1u : 0u) | ((uint32_t)(clamped[g] & 7u) << 1);
     if (live) {
         // append them to the live list: one atomic per wave; the list order varies from run to run,
         // each entry's result does not
