@@ -76,24 +76,39 @@ __device__ __forceinline__ uint32_t rect_tiles(uint2 r) {
     return ((r.y & 0xffffu) - (r.x & 0xffffu)) * ((r.y >> 16) - (r.x >> 16));
 }
 
+// A workgroup barrier that orders LDS only: unlike __syncthreads, whose workgroup fence also waits for
+// every global store the wave has in flight, it leaves the wave's stores draining.
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+template <bool LDS_ONLY>
+__device__ __forceinline__ void wg_barrier() {
+    if constexpr (LDS_ONLY)
+        lds_barrier();
+    else
+        __syncthreads();
+}
+
 // Sum over the workgroup (a multiple of 64 threads); result valid in every thread.
-template <typename T>
+template <typename T, bool LDS_ONLY = false>
 __device__ T block_sum(T v, T* s_tmp) {
     if constexpr (sizeof(T) == 4)
         v = (T)wave_incl_sum((uint32_t)v);  // DPP: the wave's sum lands in lane 63
     else
         v = (T)wave_incl_sum_u64((unsigned long long)v);
     const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    __syncthreads();
+    wg_barrier<LDS_ONLY>();
     if ((threadIdx.x & 63) == 63) s_tmp[w] = v;
-    __syncthreads();
+    wg_barrier<LDS_ONLY>();
     T t = 0;
     for (int i = 0; i < nw; i++) t += s_tmp[i];
     return t;
 }
 
 // Exclusive scan over the workgroup of one value per thread (thread order).
-template <typename T>
+template <typename T, bool LDS_ONLY = false>
 __device__ T block_exclusive_scan(T v, T* s_tmp, T* total) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
     T incl = v;
@@ -101,9 +116,9 @@ __device__ T block_exclusive_scan(T v, T* s_tmp, T* total) {
         incl = (T)wave_incl_sum((uint32_t)v);  // DPP, no ds_bpermute chain
     else
         incl = (T)wave_incl_sum_u64((unsigned long long)v);
-    __syncthreads();
+    wg_barrier<LDS_ONLY>();
     if (lane == 63) s_tmp[w] = incl;
-    __syncthreads();
+    wg_barrier<LDS_ONLY>();
     T base = 0, all = 0;
     for (int i = 0; i < nw; i++) {
         if (i < w) base += s_tmp[i];
@@ -550,6 +565,10 @@ struct FusedScan {
 __device__ u64* g_k3_scratch;
 #endif
 
+#ifndef GSR_K3_PRO
+#define GSR_K3_PRO 1
+#endif
+
 template <bool LDS>
 __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
     int P, int chunk, const uint2* __restrict__ rect, const uint32_t* __restrict__ tiles_touched,
@@ -635,6 +654,41 @@ __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
         for (uint32_t i = threadIdx.x; i < tiles; i += blockDim.x) s_cur[i] = tile_base[i] + off[i];
     }
     // first record index of every Gaussian: chunk base + in-order scan of tiles_touched
+#if GSR_K3_PRO
+    // (GSR_K3_PRO: the counts of up to four rounds requested before the first scan, the scans' barriers
+    // LDS-only, and the content-byte zeroing issued last -- the memory counter is in order, so a load
+    // issued after a store waits for that store too: each round had waited for the previous round's
+    // stores, and the scans' __syncthreads for all of them)
+    u64 carry = block_sum<u64, true>(before, s_tmp);
+    const u64 chunk_base = carry;
+    for (int gq = g0; gq < g1; gq += 4 * kBinThreads) {
+        uint32_t nr[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int g = gq + u * kBinThreads + (int)threadIdx.x;
+            nr[u] = g < g1 ? tiles_touched[g] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int gb = gq + u * kBinThreads;
+            if (gb >= g1) break;  // uniform
+            const int g = gb + (int)threadIdx.x;
+            u64 all = 0;
+            const u64 at = carry + block_exclusive_scan<u64, true>((u64)nr[u], s_tmp, &all);
+            if (g < g1) {
+                rec_start[g] = (uint32_t)at;
+                if (nr[u]) reinterpret_cast<uint32_t*>(rec + (size_t)kRecRows * g + 3)[3] = (uint32_t)at;
+            }
+            carry += all;
+        }
+    }
+    if (rec_flag) {
+        const u64 e1 = min(chunk_base + chunk_total[blockIdx.x], cap);
+        uint4* w = reinterpret_cast<uint4*>(rec_flag);
+        for (u64 i = chunk_base / 16 + threadIdx.x; i < (e1 + 15) / 16; i += blockDim.x) w[i] = make_uint4(0u, 0u, 0u, 0u);
+    }
+    if (LDS) lds_barrier();
+#else
     u64 carry = block_sum(before, s_tmp);
     if (rec_flag) {
         // the gradient records' content bytes of this chunk's emission range [carry, carry + total),
@@ -657,6 +711,7 @@ __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
         carry += all;
     }
     if (LDS) __syncthreads();
+#endif
     GSR_STAMP(g_st_scatter, blockIdx.x, 1);
     // the keys: chunk positions [q0, q1) of the spatial order (K0), as K1 counted them
     const int V = (int)n_visible[0];
