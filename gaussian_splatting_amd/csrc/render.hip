@@ -181,6 +181,22 @@ __device__ __forceinline__ void lds_store_rel(int* p, int v) {
     __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// The render kernels' per-batch LDS hand-offs (staged entries, the backward's reduced sums).  A
+// non-shared render unit is one wave, whose LDS accesses complete in order, so the hand-off needs only
+// the compiler kept from moving LDS accesses across it (GSR_RENDER_WAVESYNC) -- __syncthreads'
+// workgroup fence also makes the wave wait for every store it has in flight (the backward's gradient
+// records, the forward's entry masks and checkpoints) before the next batch's loads.
+#ifndef GSR_RENDER_WAVESYNC
+#define GSR_RENDER_WAVESYNC 1
+#endif
+__device__ __forceinline__ void unit_sync() {
+#if GSR_RENDER_WAVESYNC
+    __builtin_amdgcn_wave_barrier();
+#else
+    __syncthreads();
+#endif
+}
+
 template <int NB>
 struct FwdLds {
     float4 xy[NB][kBatch], cq[NB][kBatch], col[NB][kBatch];
@@ -319,7 +335,7 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const ui
 #endif
         }
         if (kPf && b0 + kBatch + lane < ns) ent_next = a.gid_sorted[range.x + b0 + kBatch + lane];
-        if (!SHARED) __syncthreads();
+        if (!SHARED) unit_sync();
         // Blend checkpoint (gsr_common.h): the state before entry b0, stored after this batch's
         // loads have landed.  vmcnt counts stores too, so stores issued ahead of the loads would
         // make the staging wait for them; here they drain while the batch blends.  A part writes
@@ -380,7 +396,7 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const ui
         if (SHARED) {
             if (lane == 0) lds_store_rel(&s_done[part], bk + 1);  // slot sl may be restaged for bk + NB
         } else {
-            __syncthreads();
+            unit_sync();
         }
 #ifdef GSR_STAMPS
         if (lane == 0 && part == 0) g_st_rfwd[(size_t)tile * kStampSlots + 3] = (unsigned long long)(b0 + kBatch);
@@ -765,7 +781,7 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
             s_cq[lane] = stage_conic(v0, v1, qm);
         }
         if (GSR_PF_ENTRY && b0 + kBatch + lane < end) ent_next = a.gid_sorted[range.x + b0 + kBatch + lane];
-        __syncthreads();
+        unit_sync();
         unsigned long long todo = __ballot(qm != 0);
         unsigned long long written = 0;
         while (todo) {
@@ -844,7 +860,7 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
                 if (CENSUS) c_red++;
             }
         }
-        __syncthreads();
+        unit_sync();
         const bool content = (written >> lane) & 1ull;
         if (has && content && !(GSR_ATTR & 1)) {
             a.recs.flag[e] = 1;  // (the bytes were zeroed by the forward's K3, binning.hip)
@@ -872,7 +888,7 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
                 a.recs.c[e] = rc;
             }
         }
-        __syncthreads();
+        unit_sync();
     }
     if (CENSUS && lane == 0) {
         atomicAdd(&a.census[4], c_staged);
