@@ -118,6 +118,7 @@ __device__ __forceinline__ void load_sh(const ShAddr& sa, int idx, int K, float3
 #define GSR_PRE_PREFETCH 2
 #endif
 constexpr int kPreThreads = 64;
+static_assert(!GSR_PRE_PREFETCH || kPreThreads == 64, "the prefetching path's LDS hand-offs are wave-local: one wave");
 constexpr int kShHalfRows = 32;
 constexpr int kShRowStride = 52;   // padded LDS row stride (16-byte aligned, conflict-free b128)
 
