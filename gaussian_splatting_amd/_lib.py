@@ -187,7 +187,7 @@ def build_id() -> str:
 
 # ---- runtime options (include/gsr.h gsr_option_set) ---------------------------------
 OPTIONS = ("fused_bin", "fwd_quads", "bwd_seg_ck", "host_total", "zero_fill", "live_list", "sort_prefix",
-           "count_wait")
+           "count_wait", "bwd_grid")
 
 
 def option_get(name: str) -> int:

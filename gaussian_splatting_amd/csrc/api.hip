@@ -287,7 +287,7 @@ void carve_recs(char* base, size_t R, size_t P, gsr::GradRecs* recs, gsr::GradRe
 #endif
 enum Opt {
     OPT_FUSED_BIN = 0, OPT_FWD_QUADS, OPT_BWD_SEG_CK, OPT_HOST_TOTAL, OPT_ZERO_FILL, OPT_LIVE_LIST, OPT_SORT_PREFIX,
-    OPT_COUNT_WAIT, OPT_COUNT
+    OPT_COUNT_WAIT, OPT_BWD_GRID, OPT_COUNT
 };
 struct OptionSpec {
     const char* name;
@@ -303,6 +303,7 @@ const OptionSpec kOptions[OPT_COUNT] = {
     {"live_list", "GSR_LIVE_LIST", GSR_LIVE_LIST_DEFAULT, 0, 1},
     {"sort_prefix", "GSR_SORT_PREFIX", GSR_SORT_PREFIX_DEFAULT, 0, (int)gsr::kSortPrefixMax},
     {"count_wait", "GSR_COUNT_WAIT", GSR_COUNT_WAIT_DEFAULT, 0, 2},
+    {"bwd_grid", "GSR_BWD_GRID", 0, 0, 2},
 };
 std::atomic<int> g_opt[OPT_COUNT];
 std::once_flag g_opt_once;
@@ -1179,6 +1180,7 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
     // dense outputs to zero-fill (gauss_bwd then writes only the non-zero rows)
     FillArgs fill{};
     const int zmode = screen ? 0 : zero_fill_mode();
+    const int grid_mode = option(OPT_BWD_GRID);  // (read once, as every option)
     const int m_rest = dc ? M - 1 : M;
     auto seg = [&](float* ptr, size_t n) {
         if (ptr && n) {
@@ -1255,7 +1257,7 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
             ra.fill = fill;
             ra.fill_blocks = GSR_FUSED_FILL_BLOCKS;
         }
-        HIP_TRY(launch_render_bwd(ra, max_units, stream), "render_bwd");
+        HIP_TRY(launch_render_bwd(ra, max_units, stream, grid_mode), "render_bwd");
     }
     if (int rc = check_debug(debug, stream, "render_bwd")) return rc;
     {

@@ -499,7 +499,9 @@ hipError_t launch_render_fwd(const RenderFwdArgs& a, hipStream_t stream, int qua
 hipError_t launch_render_fwd_redo(const RenderFwdArgs& a, hipStream_t stream, int quads = 2);
 // a tile-major pixel plane (tile_px) -> image order [H][W], 4-byte elements (inspection only)
 hipError_t launch_untile(const uint32_t* src, uint32_t* dst, int W, int H, uint32_t gx, hipStream_t stream);
-hipError_t launch_render_bwd(const RenderBwdArgs& a, size_t max_units, hipStream_t stream);
+// grid_mode ("bwd_grid" option): 0 = strided when the worst-case grid is far larger than the tiles,
+// 1 = one block per possible unit, 2 = strided
+hipError_t launch_render_bwd(const RenderBwdArgs& a, size_t max_units, hipStream_t stream, int grid_mode = 0);
 // backward work list: one unit per (tile, segment of seg_ck * kCkStride entries below the tile's limit),
 // written by the forward render; at most R / (seg_ck kCkStride) + tiles of them
 size_t bwd_max_units(size_t R, uint32_t tiles, int seg_ck);

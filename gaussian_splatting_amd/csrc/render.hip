@@ -38,6 +38,8 @@
 #include "footprint.h"
 #include "kernels.h"
 
+#include <algorithm>
+
 namespace gsr {
 
 constexpr int kBatch = 64;  // list entries staged per round (one per lane)
@@ -620,7 +622,7 @@ hipError_t launch_render_fwd(const RenderFwdArgs& a, hipStream_t stream, int qua
 }
 
 // ---------------------------------------------------------------------------
-template <bool CENSUS>
+template <bool CENSUS, bool STRIDED>
 __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(RenderBwdArgs a) {
   {
     // One wave per unit = (tile, segment): the entries [start, end) of the tile's list, start a
@@ -634,16 +636,19 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
                        (unsigned long long)a.fill_blocks * kWave);
         return;
     }
+    static_assert(kUnitLists * kUnitShards <= kWave, "one lane per list counter");
+    constexpr int nl = kUnitLists * kUnitShards;
+    // All 40 list counters in one vector load and an inclusive DPP scan (once per block)
+    const uint32_t incl = wave_incl_sum(threadIdx.x < nl ? a.unit_cnt[threadIdx.x * kUnitCntStride] : 0u);
+    // STRIDED (launch_render_bwd picks it when the worst-case grid is far larger than the tile count):
+    // kBwdGridTiles blocks per tile, each taking units i, i + G, ... -- the grid sized for the shortest
+    // segments launches ~10x more blocks than there are units at 5M@4K, each a counter load before it
+    // can exit (render_bwd 882 -> 803-833 us, r4ad); at 1080p (~2.5x) the one-unit grid stays.
+    for (uint32_t i = blockIdx.x - a.fill_blocks;; i += gridDim.x - a.fill_blocks) {
     uint2 unit;
-    {  // full segments first, then the partial ones, longest quarter first; shards in order.
-        // All 40 list counters in one vector load, an inclusive DPP scan, and a ballot find the
-        // list holding this block's unit (a chain of dependent scalar loads before, r2).
-        static_assert(kUnitLists * kUnitShards <= kWave, "one lane per list counter");
-        constexpr int nl = kUnitLists * kUnitShards;
+    {  // full segments first, then the partial ones, longest quarter first; shards in order:
+        // a ballot over the scanned counters finds the list holding unit i
         const int lane = threadIdx.x;
-        const uint32_t c = lane < nl ? a.unit_cnt[lane * kUnitCntStride] : 0u;
-        const uint32_t incl = wave_incl_sum(c);
-        const uint32_t i = blockIdx.x - a.fill_blocks;
         const int l = __popcll(__ballot(lane < nl && incl <= i));  // lists wholly before unit i
         if (l >= nl) return;  // past the lists (the grid is sized for the worst case)
         const uint32_t before = l ? (uint32_t)__builtin_amdgcn_readlane((int)incl, l - 1) : 0u;
@@ -656,7 +661,11 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
     const uint32_t tile = unit.x;
     const int start = (int)unit.y * kCkStride;
     const int tile_x0 = (int)(tile % a.gx) * kTile, tile_y0 = (int)(tile / a.gx) * kTile;
-    const int lane = threadIdx.x;
+    // (STRIDED: opaque to the compiler, so that lane-derived constants are formed per unit rather than
+    // hoisted out of the unit loop and held in registers across it: 86 VGPRs instead of 98)
+    int lane_o = threadIdx.x;
+    if (STRIDED) asm volatile("" : "+v"(lane_o));
+    const int lane = lane_o;
     const int lx = lane & 7, ly = lane >> 3;
     const float pxf0 = (float)(tile_x0 + lx), pyf0 = (float)(tile_y0 + ly);  // this lane's pixel in quadrant 0
 
@@ -901,6 +910,8 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
     GSR_STAMP_RT(g_st_rbwd, blockIdx.x, 5);
     GSR_STAMP_VAL(g_st_rbwd, blockIdx.x, 2, tile);
     GSR_STAMP_VAL(g_st_rbwd, blockIdx.x, 3, end - start);
+    if (!STRIDED) break;  // one unit per block
+    }
   }
 }
 
@@ -908,13 +919,20 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
 // own seg_ck is on the device only; surplus blocks exit at the unit lookup)
 size_t bwd_max_units(size_t R, uint32_t tiles, int seg_ck) { return R / ((size_t)seg_ck * kCkStride) + tiles; }
 
-hipError_t launch_render_bwd(const RenderBwdArgs& a, size_t max_units, hipStream_t stream) {
+// The strided grid: kBwdGridTiles unit blocks per tile, used when the worst-case grid (max_units) is
+// more than kBwdStrideRatio times that.
+constexpr uint32_t kBwdGridTiles = 2, kBwdStrideRatio = 4;
+hipError_t launch_render_bwd(const RenderBwdArgs& a, size_t max_units, hipStream_t stream, int grid_mode) {
     if (max_units == 0) return hipSuccess;
-    const uint32_t grid = (uint32_t)max_units + a.fill_blocks;  // fill blocks first, then the units
+    const size_t strided_units = std::min(max_units, (size_t)kBwdGridTiles * a.gx * a.gy);
+    const bool strided = !a.census && (grid_mode == 2 || (grid_mode == 0 && max_units > kBwdStrideRatio * strided_units));
+    const uint32_t grid = (uint32_t)(strided ? strided_units : max_units) + a.fill_blocks;  // fill blocks first
     if (a.census)
-        hipLaunchKernelGGL(render_bwd_kernel<true>, dim3(grid), dim3(kWave), 0, stream, a);
+        hipLaunchKernelGGL((render_bwd_kernel<true, false>), dim3(grid), dim3(kWave), 0, stream, a);
+    else if (strided)
+        hipLaunchKernelGGL((render_bwd_kernel<false, true>), dim3(grid), dim3(kWave), 0, stream, a);
     else
-        hipLaunchKernelGGL(render_bwd_kernel<false>, dim3(grid), dim3(kWave), 0, stream, a);
+        hipLaunchKernelGGL((render_bwd_kernel<false, false>), dim3(grid), dim3(kWave), 0, stream, a);
     return hipGetLastError();
 }
 

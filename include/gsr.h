@@ -309,6 +309,9 @@ int gsr_host_stats(double* values, int n, int reset);
  *                        mapped count slot the binning kernel stores into (spins 100 us, then yields the
  *                        core between polls) | polls the event recorded behind the count (20 ms at most,
  *                        then blocks) | blocks in hipEventSynchronize (woken by the completion interrupt)
+ *   "bwd_grid"   0|1|2  render_bwd's grid: 2 blocks per tile, each walking units i, i + G, ... when the
+ *                        grid sized for the shortest segments would be over 4x that (5M@4K) | that worst-case
+ *                        grid, one unit per block | always the strided grid
  * Every option is read once per forward / backward call, so a concurrent gsr_option_set never splits
  * one call's launches between two values.
  * gsr_option_get returns -1 for an unknown name; gsr_option_set returns GSR_ERR_ARGUMENT for an

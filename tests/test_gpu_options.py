@@ -36,6 +36,8 @@ VARIANTS = {
     "sort_prefix=64": dict(sort_prefix=64),   # long lists sorted to 64 entries: most of their tiles redone
     "count_wait=0": dict(count_wait=0),       # the blocking wait for the instance count
     "count_wait=1": dict(count_wait=1),       # the host polls an event behind the count (default 2: the slot)
+    "bwd_grid=1": dict(bwd_grid=1),           # render_bwd: one block per possible unit
+    "bwd_grid=2": dict(bwd_grid=2),           # render_bwd: two blocks per tile walking units i, i + G, ...
 }
 CASES = ["sh3_scalerot", "antialiasing", "dense_opaque", "lists_1k_2k", "lists_4k_8k", "lists_over_8k"]
 

@@ -210,6 +210,9 @@ def test_option_errors_and_restore():
         _lib.option_set("fwd_quads", 3)
     with pytest.raises(_lib.GsrError, match="out of range"):
         _lib.option_set("zero_fill", 4)
+    with pytest.raises(_lib.GsrError, match="out of range"):
+        _lib.option_set("bwd_grid", 3)
+    assert before["bwd_grid"] == 0  # auto: the strided grid only where the worst case is far larger
     # the reachable prefix is bounded by the prefix sort's LDS buffer: 1024 at most
     _lib.option_set("sort_prefix", 1024)
     with pytest.raises(_lib.GsrError, match="out of range"):
