@@ -207,6 +207,7 @@ __device__ __forceinline__ void reduce_records(int P, int g0, const uint32_t* __
 #ifndef GSR_REDUCE_COMPACT
 #define GSR_REDUCE_COMPACT 1
 #endif
+static_assert(GSR_REDUCE_COMPACT || !GSR_FLAG_BITS, "the flag bits are read by the compacted reduction only");
 // GSR_REDUCE_PIPE: the records of a window's next group requested before its current group is
 // reduced, the radius read at the start, and wave-local LDS hand-offs (the workgroup is one wave).
 #ifndef GSR_REDUCE_PIPE
@@ -247,6 +248,33 @@ __device__ __forceinline__ void reduce_records_compact(int P, int g0, const uint
     for (uint32_t wa = E0 & ~15u; wa < E1; wa += 1024u) {  // uniform
         // content bytes [wa, wa + 1024): lane l holds wa + 16 l .. + 15, masked to [E0, E1)
         const uint32_t p = wa + 16u * (uint32_t)lane;
+#if GSR_FLAG_BITS
+        // (flag bits: this lane's 16 positions are half of one 32-bit word, wa being a multiple of 16)
+        uint32_t m16 = 0;
+        if (p < E1) {
+            m16 = (reinterpret_cast<const uint32_t*>(recs.flag)[p >> 5] >> (p & 16u)) & 0xffffu;
+            const uint32_t k = E1 - p;  // positions of this lane below E1
+            if (k < 16) m16 &= (1u << k) - 1u;
+            if (p < E0) m16 &= 0xffffu << (E0 - p);  // (first window, lane 0 only) the previous wave's
+        }
+        const uint32_t c = (uint32_t)__popc(m16);
+        const uint32_t incl = wave_incl_sum(c), off = incl - c;
+        const uint32_t R = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);  // records in the window
+        if (R == 0) continue;  // uniform
+        __builtin_amdgcn_wave_barrier();  // the previous window's readers are done (in-order LDS)
+        {
+            uint32_t k = off;
+            for (uint32_t t = m16; t; t &= t - 1) s_list[k++] = (uint16_t)(16 * lane + __builtin_ctz(t));
+        }
+        __builtin_amdgcn_wave_barrier();
+        auto slots_below = [&](uint32_t q) -> uint32_t {
+            const uint32_t d = q <= wa ? 0u : min(q - wa, 1024u);
+            const int L = (int)min(d >> 4, 63u);
+            const uint32_t offL = (uint32_t)__shfl((int)off, L), mL = (uint32_t)__shfl((int)m16, L);
+            const uint32_t b = d - 16u * (uint32_t)L;  // positions of lane L below q (16: all of them)
+            return offL + (uint32_t)__popc(mL & (b >= 16 ? 0xffffu : (1u << b) - 1u));
+        };
+#else
         uint64_t lo = 0, hi = 0;
         if (p < E1) {
             const uint4 f = *reinterpret_cast<const uint4*>(recs.flag + p);
@@ -283,6 +311,7 @@ __device__ __forceinline__ void reduce_records_compact(int P, int g0, const uint
             const uint64_t mhi = b >= 16 ? ~0ull : b <= 8 ? 0ull : (1ull << (8 * (b - 8))) - 1ull;
             return offL + (uint32_t)(__popcll(loL & mlo) + __popcll(hiL & mhi));
         };
+#endif
         // (both calls on every lane: slots_below shuffles across lanes, so it must not sit in a branch)
         const uint32_t r0 = slots_below(my0), r1e = slots_below(my1), r1 = n ? r1e : r0;
         const bool mine = r1 > r0;

@@ -682,10 +682,12 @@ __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
             carry += all;
         }
     }
-    if (rec_flag) {
+    if (rec_flag) {  // (GSR_FLAG_BITS: 128 flags per 16-byte word)
+        constexpr u64 kPer = GSR_FLAG_BITS ? 128 : 16;
         const u64 e1 = min(chunk_base + chunk_total[blockIdx.x], cap);
         uint4* w = reinterpret_cast<uint4*>(rec_flag);
-        for (u64 i = chunk_base / 16 + threadIdx.x; i < (e1 + 15) / 16; i += blockDim.x) w[i] = make_uint4(0u, 0u, 0u, 0u);
+        for (u64 i = chunk_base / kPer + threadIdx.x; i < (e1 + kPer - 1) / kPer; i += blockDim.x)
+            w[i] = make_uint4(0u, 0u, 0u, 0u);
     }
     if (LDS) lds_barrier();
 #else
@@ -695,9 +697,11 @@ __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
         // zeroed for the backward (render_bwd sets them): 16-byte words, rounded outward -- a word
         // shared with the next chunk gets zeros from both.  Clamped to the capacity (a truncated pass
         // is rebuilt).
+        constexpr u64 kPer = GSR_FLAG_BITS ? 128 : 16;  // flags per 16-byte word
         const u64 e1 = min(carry + chunk_total[blockIdx.x], cap);
         uint4* w = reinterpret_cast<uint4*>(rec_flag);
-        for (u64 i = carry / 16 + threadIdx.x; i < (e1 + 15) / 16; i += blockDim.x) w[i] = make_uint4(0u, 0u, 0u, 0u);
+        for (u64 i = carry / kPer + threadIdx.x; i < (e1 + kPer - 1) / kPer; i += blockDim.x)
+            w[i] = make_uint4(0u, 0u, 0u, 0u);
     }
     for (int gb = g0; gb < g1; gb += kBinThreads) {
         const int g = gb + (int)threadIdx.x;

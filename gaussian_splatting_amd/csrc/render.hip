@@ -872,7 +872,11 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
         unit_sync();
         const bool content = (written >> lane) & 1ull;
         if (has && content && !(GSR_ATTR & 1)) {
+#if GSR_FLAG_BITS  // (the bits were zeroed by the forward's K3, binning.hip; OR is order-free: deterministic)
+            (void)atomicOr(reinterpret_cast<uint32_t*>(a.recs.flag) + (e >> 5), 1u << (e & 31u));
+#else
             a.recs.flag[e] = 1;  // (the bytes were zeroed by the forward's K3, binning.hip)
+#endif
             float4 ra = make_float4(0.f, 0.f, 0.f, 0.f), rb = ra;
             float2 rc = make_float2(0.f, 0.f);
             if (content) {
