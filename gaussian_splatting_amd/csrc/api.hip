@@ -1248,7 +1248,7 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
         ra.W = width; ra.H = height; ra.gx = gx; ra.gy = gy; ra.ranges = img.ranges; ra.gid_sorted = bin.gid_sorted;
         ra.rec = geom.rec;
         ra.bg = background; ra.dL_dpix = dL_dpix; ra.dL_dinvdepth = dL_dinvdepths; ra.img = img; ra.recs = recs;
-        ra.ckpt = bin.ckpt; ra.seg_ck = geom.fwd_seg_ck;
+        ra.ckpt = bin.ckpt; ra.seg_ck = geom.fwd_seg_ck; ra.rec_start = geom.rec_start;
         ra.unit_cnt = geom.unit_cnt; ra.unit_part = geom.unit_part; ra.unit_full = bin.unit_full;
         ra.full_cap = (uint32_t)unit_full_cap(C);
         ra.census = g_census;

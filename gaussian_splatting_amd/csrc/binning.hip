@@ -677,7 +677,7 @@ __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
             const u64 at = carry + block_exclusive_scan<u64, true>((u64)nr[u], s_tmp, &all);
             if (g < g1) {
                 rec_start[g] = (uint32_t)at;
-                if (nr[u]) reinterpret_cast<uint32_t*>(rec + (size_t)kRecRows * g + 3)[3] = (uint32_t)at;
+                if (!GSR_REC_START_GATHER && nr[u]) reinterpret_cast<uint32_t*>(rec + (size_t)kRecRows * g + 3)[3] = (uint32_t)at;
             }
             carry += all;
         }
@@ -710,7 +710,7 @@ __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
         const u64 at = carry + block_exclusive_scan((u64)n, s_tmp, &all);
         if (g < g1) {
             rec_start[g] = (uint32_t)at;
-            if (n) reinterpret_cast<uint32_t*>(rec + (size_t)kRecRows * g + 3)[3] = (uint32_t)at;
+            if (!GSR_REC_START_GATHER && n) reinterpret_cast<uint32_t*>(rec + (size_t)kRecRows * g + 3)[3] = (uint32_t)at;
         }
         carry += all;
     }

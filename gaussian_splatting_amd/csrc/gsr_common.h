@@ -190,6 +190,12 @@ __host__ __device__ inline size_t view_pack_floats(size_t entries) {
 // GSR_FLAG_BITS: the records' content flags as one BIT per emission index (render_bwd ORs it in with a
 // global atomic, order-free) instead of one byte: 8x less for K3 to zero and gauss_reduce to scan
 // (5M@4K: 14 MB instead of 115 MB each way).
+// GSR_REC_START_GATHER: render_bwd reads each entry's first emission index from rec_start[] instead of
+// the splat record's row 3, so K3 no longer patches every visible Gaussian's record (one 4-byte store
+// into a 64-byte record each: a partial 32-byte write per Gaussian, 160 MB at 5M@4K).
+#ifndef GSR_REC_START_GATHER
+#define GSR_REC_START_GATHER 1
+#endif
 #ifndef GSR_FLAG_BITS
 #define GSR_FLAG_BITS 1
 #endif

@@ -84,6 +84,7 @@ struct RenderBwdArgs {
     const uint2* unit_part;
     const uint2* unit_full;
     uint32_t full_cap;
+    const uint32_t* rec_start;          // GeomState::rec_start (GSR_REC_START_GATHER)
     const uint32_t* seg_ck;             // GeomState::fwd_seg_ck: checkpoints per backward segment as the
                                         // forward that built the work list used it (segment = seg_ck * kCkStride)
     unsigned long long* census;         // diagnostic pair counts (gsr_census_set) or null

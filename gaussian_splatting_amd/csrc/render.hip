@@ -777,9 +777,9 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
             const uint32_t ent = GSR_PF_ENTRY ? ent_next : a.gid_sorted[range.x + b0 + lane];
             const float4* rec = a.rec + (size_t)kRecRows * (ent >> kEntryMaskBits);
             const float4 v0 = rec[0], v1 = rec[1], v2 = rec[2], v3 = rec[3];
-            // this instance's emission index (row 3: tile rectangle and first emission)
-            e = __float_as_uint(v3.w) + (tty - __float_as_uint(v3.y)) * __float_as_uint(v3.z) +
-                (ttx - __float_as_uint(v3.x));
+            // this instance's emission index (row 3: tile rectangle [and first emission])
+            const uint32_t first = GSR_REC_START_GATHER ? a.rec_start[ent >> kEntryMaskBits] : __float_as_uint(v3.w);
+            e = first + (tty - __float_as_uint(v3.y)) * __float_as_uint(v3.z) + (ttx - __float_as_uint(v3.x));
             s_xy[lane] = make_float4(v0.x, v0.y, v1.y, v1.z);
             s_col[lane] = v2;
             ca = v0.z;
