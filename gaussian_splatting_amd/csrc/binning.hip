@@ -223,7 +223,10 @@ __device__ __forceinline__ void for_each_instance(uint32_t n, uint2 r, uint32_t 
 // Gaussians in this order, so a chunk covers a compact screen region: it touches
 // few tiles, with long runs per tile, and K3's key stores land in long contiguous
 // runs instead of a few bytes per (chunk, tile) across the whole image.
-constexpr uint32_t kCell = 4;
+#ifndef GSR_CELL
+#define GSR_CELL 4
+#endif
+constexpr uint32_t kCell = GSR_CELL;
 
 // GSR_CELL_MORTON: cells in Z order (Morton code of the cell column and row, over the power-of-two
 // square that holds the grid), so a chunk of the order covers a square-ish block of cells rather than
