@@ -80,7 +80,8 @@ def test_backward_without_invdepth_grad():
 
 
 def test_deterministic_bitwise():
-    """No atomics anywhere: two runs give bit-identical images and gradients."""
+    """No float atomics anywhere (the one atomic, an OR of a record's content bit, is order-free): two runs
+    give bit-identical images and gradients."""
     case = C.SMALL_CASES[-1]
     inp = C.build(case)
     gc, gd = C.unit_grads(case.H, case.W)
