@@ -87,7 +87,12 @@ def cpu_threads():
     omp = os.environ.get("OMP_NUM_THREADS")
     share = int(omp) if omp and omp.isdigit() and int(omp) > 0 else None
     threads = max(1, min(aff, share) if share else aff)
-    return threads, {"affinity_cpus": aff, "omp_num_threads": share, "host_cpus": os.cpu_count()}
+    policy = ("the lease's OMP_NUM_THREADS share: the GPU pool gives one GPU's job a 16-CPU share of the host and "
+              "asks worker pools to stay within it (the affinity mask still lists the whole machine), so the "
+              "whole affinity set is not used (DESIGN.md section 8)" if share and share < aff else
+              "the process's whole CPU set (os.sched_getaffinity)")
+    return threads, {"affinity_cpus": aff, "omp_num_threads": share, "host_cpus": os.cpu_count(),
+                     "threads_policy": policy}
 
 
 def cpu_baseline(cfg_name: str, P: int, W: int, H: int, forward_only: bool = False):
@@ -507,13 +512,14 @@ def main():
         ms_per_step = elapsed / args.steps * 1e3
         value = world * P * args.steps / elapsed
         dom_ms = dom_total / dom_calls if dom_calls else 0.0  # HIP events on the launch stream, timed region
+        # SURVEY.md 8d's algorithmic bytes of the kernel's own work (render_bwd: 44 I + 24 W H + 40 P); the
+        # contract excludes zero-init memsets, so the fill that rides in the launch is reported beside it
         alg = algorithmic_bytes(dom, P, nr, W, H, K)
         # zero_fill = 3 (the default): the zero fill of the backward's dense outputs rides in render_bwd's
-        # launch (api.hip), so its bytes are that launch's too: 4 B x (means2D 3, opacity 1, colour 3,
-        # inverse depth 1, means3D 3, cov3D 6, SH 3K, scale 3, rotation 4) per Gaussian
+        # launch (api.hip): 4 B x (means2D 3, opacity 1, colour 3, inverse depth 1, means3D 3, cov3D 6, SH 3K,
+        # scale 3, rotation 4) per Gaussian -- NOT algorithmic bytes, its own field and rate
         fill_bytes = 4.0 * P * (24 + 3 * K) if dom == "render_bwd" and _lib.option_get("zero_fill") == 3 else 0.0
-        alg += fill_bytes
-        traffic, traffic_src, kk = None, None, {}
+        traffic, traffic_src, kk, traffic_detail = None, None, {}, None
         if os.path.exists(PMC_PROFILE):
             prof = json.load(open(PMC_PROFILE))
             entry = prof.get("configs", {}).get(args.config) or (prof if args.config == "1m_1080p_sh3" else {})
@@ -521,7 +527,21 @@ def main():
             if kk:
                 traffic = kk["hbm_read_bytes"] + kk["hbm_write_bytes"]
                 traffic_src = entry.get("source")
+                # the raw counters beside the corrected figure: FETCH_SIZE x 1024 B and WRITE_SIZE x 1024 B per
+                # launch, and the read factor applied (tools/pmc_summary.py; calibrated per access shape by
+                # tools/fetch_calib.hip where the kernel's reads are not wide coalesced streams)
+                rf = kk.get("read_factor", 2.0)
+                traffic_detail = {"fetch_size_bytes_raw": kk.get("fetch_size_bytes", kk["hbm_read_bytes"] / rf),
+                                  "write_size_bytes_raw": kk.get("write_size_bytes", kk["hbm_write_bytes"]),
+                                  "read_factor": rf, "read_factor_basis": kk.get("read_factor_basis",
+                                                                                 "x2: MI355X_MICROARCH.md 'HBM'"),
+                                  "read_bytes": kk["hbm_read_bytes"], "write_bytes": kk["hbm_write_bytes"],
+                                  "write_bytes_less_fill": kk["hbm_write_bytes"] - fill_bytes}
         achieved = alg / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
+        traffic_frac = traffic / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if traffic is not None and dom_ms > 0 else None
+        # 5M@4K: the 8d byte model bills 44 B for every instance, but the render walks ~7% of each 3,540-entry
+        # list, so there the counter-based fraction is the headline and the model's beside it
+        counter_headline = args.config == "5m_4k_sh3" and traffic_frac is not None
         valu_frac = None
         if traffic is not None and kk.get("valu_insts"):
             # wave64 VALU issues in 2 cycles on a 32-wide SIMD; 1024 SIMDs at 2.4 GHz (MI355X_MICROARCH.md)
@@ -557,12 +577,21 @@ def main():
             "config": {"workload": args.config, "gaussians": P, "width": W, "height": H, "sh_degree": Kdeg,
                        "num_rendered": nr, "views": "one per GPU, yaw 5 deg x rank", "parallelism": par,
                        "sh_layout": "dc + rest (separate_sh)" if args.separate_sh else "one [P,M,3] tensor"},
-            "roofline": {"kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+            "roofline": {"kernel": dom, "bound": "hbm",
+                         "achieved": traffic / (dom_ms * 1e-3) / 1e9 if counter_headline else achieved,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": traffic_frac if counter_headline else achieved / HBM_PEAK_GBS,
+                         "frac_basis": ("PMC counter bytes per launch (the 8d model overstates this frame)"
+                                        if counter_headline else "SURVEY.md 8d algorithmic bytes per launch"),
+                         "model_frac": achieved / HBM_PEAK_GBS, "model_GBs": achieved,
+                         "traffic": traffic, "traffic_source": traffic_src, "traffic_counters": traffic_detail,
                          # counter bytes per launch over the launch time: the HBM rate the kernel really moves
-                         "traffic_frac": (traffic / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
-                                          if traffic is not None and dom_ms > 0 else None),
-                         "algorithmic_bytes_per_launch": alg, "fused_zero_fill_bytes": fill_bytes,
+                         "traffic_frac": traffic_frac,
+                         "algorithmic_bytes_per_launch": alg,
+                         # the zero fill riding in the launch: its bytes and their rate over the launch time,
+                         # excluded from frac (SURVEY.md 8d "zero-init memsets")
+                         "fused_zero_fill_bytes": fill_bytes,
+                         "fused_zero_fill_GBs": fill_bytes / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0,
                          "mean_launch_ms": dom_ms, "timed_launches": int(dom_calls), "timed_every": every,
                          # what actually limits the render kernels: "hbm" above is the
                          # contract's roofline axis, not the limiter

@@ -162,7 +162,14 @@ def load():
             # the in-tree library must be the build of THIS tree's sources (build.py input_hash)
             from gaussian_splatting_amd import build as _build
 
-            want, got = _build.input_hash(), lib.gsr_build_id().decode()
+            got = lib.gsr_build_id().decode()
+            try:
+                want = _build.input_hash()
+            except OSError as e:  # an install without the csrc sources: nothing to compare with
+                import warnings
+
+                warnings.warn(f"libgsr build-id check skipped: the sources are not readable ({e})")
+                want = got
             if got != want:
                 raise GsrError(f"{LIB_PATH} was built from other sources (build id {got[:16]}, this tree "
                                f"{want[:16]}); rebuild it with `python -m gaussian_splatting_amd.build`")

@@ -66,7 +66,9 @@ def input_hash(extra=()) -> str:
         with open(path, "rb") as f:
             data = f.read()
         h.update(os.path.basename(path).encode() + b"\0" + str(len(data)).encode() + b"\0" + data)
-    h.update(json.dumps([CXXFLAGS[:-4], FILE_FLAGS, list(extra), ARCH, HIPCC], sort_keys=True).encode())
+    # (the compiler's path is not part of the identity: a library built with HIPCC=/custom/hipcc must load in a
+    # shell without that variable; the target is)
+    h.update(json.dumps([CXXFLAGS[:-4], FILE_FLAGS, list(extra), ARCH], sort_keys=True).encode())
     return h.hexdigest()
 
 

@@ -861,6 +861,12 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
     if (gx > 65535u || gy > 65535u)
         return fail(GSR_ERR_ARGUMENT, "rasterize_forward: image of %dx%d has more than 65535 tile columns/rows",
                     width, height);
+    // the binning's instance walk divides tile offsets inside a rectangle in fp32 (exact below 2^21,
+    // binning.hip GSR_FEI_FDIV): a 536-Mpx frame, far beyond any camera
+    constexpr size_t kMaxTiles = size_t(1) << 21;
+    if ((size_t)gx * gy >= kMaxTiles)
+        return fail(GSR_ERR_ARGUMENT, "rasterize_forward: image of %dx%d has %zu tiles (the limit is %zu)", width,
+                    height, (size_t)gx * gy, kMaxTiles - 1);
 
     size_t geom_bytes = 0, img_bytes = 0;
     carve_geom(nullptr, P, gx, gy, &geom_bytes);

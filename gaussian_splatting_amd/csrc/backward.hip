@@ -99,11 +99,11 @@ __device__ __forceinline__ void reduce_records(int P, int g0, const uint32_t* __
         const unsigned long long st = __ballot(n && my0 < base);
         const uint32_t carry = st ? 64u - (uint32_t)__clzll((long long)st) : 0u;
         s_mark[lane] = 0u;
-        __builtin_amdgcn_wave_barrier();
+        wave_lds_sync();
         if (n && my0 >= base && my0 < base + 64) s_mark[my0 - base] = (uint32_t)lane + 1u;
-        __builtin_amdgcn_wave_barrier();
+        wave_lds_sync();
         const uint32_t m = max(wave_incl_max(s_mark[lane]), carry);
-        __builtin_amdgcn_wave_barrier();
+        wave_lds_sync();
         const int owner = m ? (int)m - 1 : 0;
         const uint32_t o0 = __shfl(my0, owner);
         if (e >= E1) return Slot{false, -1, lane};
@@ -169,10 +169,10 @@ __device__ __forceinline__ void reduce_records(int P, int g0, const uint32_t* __
             else if (k < 16) hi &= (1ull << (8 * (k - 8))) - 1ull;  // k == 8 clears hi
         }
 #if GSR_REDUCE_WIN_LDS
-        __builtin_amdgcn_wave_barrier();  // the previous window's readers are done (in-order LDS)
+        wave_lds_sync();  // the previous window's readers are done (in-order LDS)
         reinterpret_cast<uint4*>(s_win)[lane] =
             make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
-        __builtin_amdgcn_wave_barrier();
+        wave_lds_sync();
 #endif
         while (true) {
             // drop the bytes below base (already reduced or before the range)
@@ -215,7 +215,7 @@ static_assert(GSR_REDUCE_COMPACT || !GSR_FLAG_BITS, "the flag bits are read by t
 #endif
 __device__ __forceinline__ void reduce_sync() {
 #if GSR_REDUCE_PIPE
-    __builtin_amdgcn_wave_barrier();
+    wave_lds_sync();
 #else
     __syncthreads();
 #endif
@@ -261,12 +261,12 @@ __device__ __forceinline__ void reduce_records_compact(int P, int g0, const uint
         const uint32_t incl = wave_incl_sum(c), off = incl - c;
         const uint32_t R = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);  // records in the window
         if (R == 0) continue;  // uniform
-        __builtin_amdgcn_wave_barrier();  // the previous window's readers are done (in-order LDS)
+        wave_lds_sync();  // the previous window's readers are done (in-order LDS)
         {
             uint32_t k = off;
             for (uint32_t t = m16; t; t &= t - 1) s_list[k++] = (uint16_t)(16 * lane + __builtin_ctz(t));
         }
-        __builtin_amdgcn_wave_barrier();
+        wave_lds_sync();
         auto slots_below = [&](uint32_t q) -> uint32_t {
             const uint32_t d = q <= wa ? 0u : min(q - wa, 1024u);
             const int L = (int)min(d >> 4, 63u);
@@ -293,13 +293,13 @@ __device__ __forceinline__ void reduce_records_compact(int P, int g0, const uint
         const uint32_t incl = wave_incl_sum(c), off = incl - c;
         const uint32_t R = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);  // records in the window
         if (R == 0) continue;  // uniform
-        __builtin_amdgcn_wave_barrier();  // the previous window's readers are done (in-order LDS)
+        wave_lds_sync();  // the previous window's readers are done (in-order LDS)
         {
             uint32_t k = off;
             for (uint64_t t = lo; t; t &= t - 1) s_list[k++] = (uint16_t)(16 * lane + (__builtin_ctzll(t) >> 3));
             for (uint64_t t = hi; t; t &= t - 1) s_list[k++] = (uint16_t)(16 * lane + 8 + (__builtin_ctzll(t) >> 3));
         }
-        __builtin_amdgcn_wave_barrier();
+        wave_lds_sync();
         // this lane's Gaussian: its record slots [r0, r1) of the list (records at positions below q)
         auto slots_below = [&](uint32_t q) -> uint32_t {
             const uint32_t d = q <= wa ? 0u : min(q - wa, 1024u);
@@ -347,11 +347,11 @@ __device__ __forceinline__ void reduce_records_compact(int P, int g0, const uint
             const unsigned long long st = __ballot(mine && r0 < k0);
             const uint32_t carry = st ? 64u - (uint32_t)__clzll((long long)st) : 0u;
             s_mark[lane] = 0u;
-            __builtin_amdgcn_wave_barrier();
+            wave_lds_sync();
             if (mine && r0 >= k0 && r0 < k0 + 64) s_mark[r0 - k0] = (uint32_t)lane + 1u;
-            __builtin_amdgcn_wave_barrier();
+            wave_lds_sync();
             const uint32_t m = max(wave_incl_max(s_mark[lane]), carry);
-            __builtin_amdgcn_wave_barrier();
+            wave_lds_sync();
             const int owner = has && m ? (int)m - 1 : -1;
             const uint32_t o0 = (uint32_t)__shfl((int)r0, owner < 0 ? 0 : owner);
             const int seg0 = has ? (o0 > k0 ? (int)(o0 - k0) : 0) : lane;
@@ -795,7 +795,7 @@ constexpr int kGbShRows = GSR_GB_HALVES ? 32 : 64;
 #endif
 __device__ __forceinline__ void gb_sync() {
 #if GSR_GB_WAVESYNC
-    __builtin_amdgcn_wave_barrier();
+    wave_lds_sync();
 #else
     __syncthreads();
 #endif

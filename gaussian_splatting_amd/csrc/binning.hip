@@ -160,11 +160,11 @@ __device__ __forceinline__ void for_each_instance(uint32_t n, uint2 r, uint32_t 
     for (uint32_t base = 0; base < total; base += 64) {
         const uint32_t s = base + lane;
         mark[lane] = 0u;
-        __builtin_amdgcn_wave_barrier();
+        wave_lds_sync();
         if (n && excl >= base && excl < base + 64) mark[excl - base] = (uint32_t)lane + 1u;
-        __builtin_amdgcn_wave_barrier();
+        wave_lds_sync();
         const uint32_t m = max(wave_incl_max(mark[lane]), carry);
-        __builtin_amdgcn_wave_barrier();
+        wave_lds_sync();
         carry = (uint32_t)__builtin_amdgcn_readlane((int)m, 63);
         const int owner = (int)m - 1;
 #else
@@ -193,7 +193,7 @@ __device__ __forceinline__ void for_each_instance(uint32_t n, uint2 r, uint32_t 
         // k / ow in fp32, branch-free (so the caller's shuffles from `owner` issue with these):
         // (k + 1/2) / ow is at least 1/(2 ow) from an integer, and rcp + mul err by < 2^-22
         // relative, so the floor is exact while k < 2^21 (a Gaussian touches < 2^21 tiles:
-        // launch_bin_count rejects grids of more than kLdsTilesMax cells, 589824 tiles).  Invalid lanes compute garbage that f ignores.
+        // the forward rejects grids of 2^21 tiles or more, api.hip kMaxTiles).  Invalid lanes compute garbage that f ignores.
         const uint32_t dy = (uint32_t)(((float)k + 0.5f) * __builtin_amdgcn_rcpf((float)max(ow, 1u)));
         // 24-bit multiplies (full rate; v_mul_lo_u32 / v_mad_u64_u32 are quarter rate): every
         // operand is < 2^16 (tile coordinates and widths, gx)
@@ -227,6 +227,8 @@ __device__ __forceinline__ void for_each_instance(uint32_t n, uint2 r, uint32_t 
 #define GSR_CELL 4
 #endif
 constexpr uint32_t kCell = GSR_CELL;
+static_assert(kCell >= 1 && kCell <= 64 && (kCell & (kCell - 1)) == 0,
+              "GSR_CELL: a power of two in [1, 64] (cells are formed by shifts; bin_cells coarsens them by powers of two)");
 
 // GSR_CELL_MORTON: cells in Z order (Morton code of the cell column and row, over the power-of-two
 // square that holds the grid), so a chunk of the order covers a square-ish block of cells rather than
@@ -241,10 +243,20 @@ __host__ __device__ inline uint32_t spread_bits16(uint32_t x) {
     x = (x | (x << 2)) & 0x33333333u;
     return (x | (x << 1)) & 0x55555555u;
 }
-__device__ __forceinline__ uint32_t cell_of(uint2 r, uint32_t cgx) {
-    const uint32_t cx = ((r.x & 0xffffu) + (r.y & 0xffffu)) >> 1, cy = ((r.x >> 16) + (r.y >> 16)) >> 1;
-    if (GSR_CELL_MORTON) return spread_bits16(cx / kCell) | (spread_bits16(cy / kCell) << 1);
-    return (cy / kCell) * cgx + cx / kCell;
+// The cell grid K0 sorts by (bin_cells): cells of (1 << shift) tiles a side, numbered in Z order when the
+// power-of-two square around the grid fits K0's LDS table (kLdsTilesMax words), row-major otherwise (a wide
+// or tall frame: 10000 x 1000 px is 157 x 16 cells, whose Z square would be 65536); and coarser than
+// kCell when even the row-major grid would not fit (> 589,824 tiles), so no image size is refused.
+struct CellGrid {
+    uint32_t cgx;     // cells per row (row-major numbering)
+    uint32_t shift;   // log2 of the cell side in tiles
+    uint32_t morton;  // 1: Z-order numbering
+};
+__device__ __forceinline__ uint32_t cell_of(uint2 r, CellGrid g) {
+    const uint32_t cx = (((r.x & 0xffffu) + (r.y & 0xffffu)) >> 1) >> g.shift,
+                   cy = (((r.x >> 16) + (r.y >> 16)) >> 1) >> g.shift;
+    if (g.morton) return spread_bits16(cx) | (spread_bits16(cy) << 1);  // (uniform branch: a kernel argument)
+    return cy * g.cgx + cx;
 }
 
 // K0a: per-chunk cell histogram in LDS; one returning atomic per (chunk, cell) gives the
@@ -252,7 +264,7 @@ __device__ __forceinline__ uint32_t cell_of(uint2 r, uint32_t cgx) {
 // chunk's instance total (index order), for the record starts.
 __global__ void __launch_bounds__(kBinThreads) cell_count_kernel(int P, int chunk, const uint2* __restrict__ rect,
                                                                  const uint32_t* __restrict__ tiles_touched,
-                                                                 uint32_t cells, uint32_t cgx,
+                                                                 uint32_t cells, CellGrid cgx,
                                                                  uint32_t* __restrict__ cell_cnt,
                                                                  uint32_t* __restrict__ cell_off,
                                                                  u64* __restrict__ chunk_total) {
@@ -293,7 +305,7 @@ __global__ void __launch_bounds__(kBinThreads) cell_count_kernel(int P, int chun
 // instead of gathering them.  Block 0 publishes V.
 __global__ void __launch_bounds__(kBinThreads) cell_scatter_kernel(int P, int chunk, const uint2* __restrict__ rect,
                                                                    const uint32_t* __restrict__ tiles_touched,
-                                                                   uint32_t cells, uint32_t cgx,
+                                                                   uint32_t cells, CellGrid cgx,
                                                                    const uint32_t* __restrict__ cell_cnt,
                                                                    const uint32_t* __restrict__ cell_off,
                                                                    const uint32_t* __restrict__ depth_key,
@@ -1368,22 +1380,32 @@ size_t bin_chunk_count(int P) {
     return (size_t)bin_chunks(P, &chunk);
 }
 
-uint32_t bin_cells(uint32_t gx, uint32_t gy, uint32_t* cgx) {
-    *cgx = (gx + kCell - 1) / kCell;
-    const uint32_t cgy = (gy + kCell - 1) / kCell;
-    if (GSR_CELL_MORTON) {  // Morton codes of the cells: the power-of-two square around the grid
-        uint32_t side = 1;
-        while (side < *cgx || side < cgy) side <<= 1;
-        return side * side;
+// The cell grid of a gx x gy tile grid (CellGrid above) and its cell count, always <= kLdsTilesMax.
+uint32_t bin_cells(uint32_t gx, uint32_t gy, CellGrid* cg) {
+    uint32_t shift = 0;
+    while ((1u << shift) < kCell) shift++;
+    for (;; shift++) {
+        const uint32_t cgx = (gx + (1u << shift) - 1) >> shift, cgy = (gy + (1u << shift) - 1) >> shift;
+        if (GSR_CELL_MORTON) {  // Morton codes of the cells: the power-of-two square around the grid
+            uint32_t side = 1;
+            while (side < cgx || side < cgy) side <<= 1;
+            if ((size_t)side * side <= kLdsTilesMax) {
+                *cg = CellGrid{cgx, shift, 1u};
+                return side * side;
+            }
+        }
+        if ((size_t)cgx * cgy <= kLdsTilesMax) {
+            *cg = CellGrid{cgx, shift, 0u};
+            return cgx * cgy;
+        }
     }
-    return *cgx * cgy;
 }
 
 bool bin_fused_ok(uint32_t tiles) { return tiles <= kLdsTilesMax; }
 
 size_t bin_cell_count(uint32_t gx, uint32_t gy) {
-    uint32_t cgx = 0;
-    return bin_cells(gx, gy, &cgx);
+    CellGrid cg{};
+    return bin_cells(gx, gy, &cg);
 }
 
 // K0 + K1 + K2: spatial order, chunk instance totals, tile counts, ranges, tile starts,
@@ -1393,11 +1415,10 @@ hipError_t launch_bin_count(int P, const GeomState& g, uint32_t gx, uint32_t gy,
     const uint32_t tiles = gx * gy;
     int chunk = 0;
     const int nchunks = bin_chunks(P, &chunk);
-    uint32_t cgx = 0;
-    const uint32_t cells = bin_cells(gx, gy, &cgx);
+    CellGrid cgx{};
+    const uint32_t cells = bin_cells(gx, gy, &cgx);  // (<= kLdsTilesMax for any grid)
     const bool lds = tiles <= kLdsTilesMax;
     const dim3 grid(nchunks), block(kBinThreads);
-    if (cells > kLdsTilesMax) return hipErrorInvalidValue;  // > 589k tiles: far beyond any image size
     // g.tile_cnt / g.cell_cnt are zero here: preprocess zeroes them, tile_scan_kernel re-zeroes them
     const size_t cell_bytes = cells * sizeof(uint32_t);
     hipLaunchKernelGGL(cell_count_kernel, grid, block, cell_bytes, stream, P, chunk, g.rect, g.tiles_touched, cells,

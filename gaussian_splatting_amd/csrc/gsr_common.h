@@ -33,14 +33,15 @@ constexpr float SH_C3_0 = -0.5900435899266435f, SH_C3_1 = 2.890611442640554f, SH
 //   row 0 = (x_pix, y_pix, conic.a, conic.b)
 //   row 1 = (conic.c, opacity_eff, 1/depth, bbox_x packed)
 //   row 2 = (r, g, b, bbox_y packed)
-//   row 3 = (rect_min.x, rect_min.y, rect width, e0) as u32 bits
+//   row 3 = (rect_min.x, rect_min.y, rect width, unused) as u32 bits
 // bbox_* are the conservative pixel bounds of the alpha >= 1/255 footprint
 // (int16 lo | int16 hi << 16), used to skip whole waves (DESIGN.md "footprint
 // culling"); lo > hi means "never contributes".  Row 3 is the tile rectangle of
-// getRect and the Gaussian's first emission index (written by the duplicate
-// pass): the instance of this Gaussian in tile (tx, ty) has emission index
-// e0 + (ty - min.y) * width + (tx - min.x), the row-major order of
-// duplicateWithKeys (CR/rasterizer_impl.cu:108-124).
+// getRect.  The Gaussian's first emission index e0 is in the record-start array
+// (GeomState::rec_start, written by K3; GSR_REC_START_GATHER, the default) -- only a
+// GSR_REC_START_GATHER=0 build patches it into row 3's .w: the instance of this
+// Gaussian in tile (tx, ty) has emission index e0 + (ty - min.y) * width + (tx - min.x),
+// the row-major order of duplicateWithKeys (CR/rasterizer_impl.cu:108-124).
 // ---------------------------------------------------------------------------
 constexpr int kRecRows = 4;
 
@@ -54,6 +55,26 @@ constexpr uint32_t kEntryMask = 0xfu;
 constexpr int kMaxGaussians = 1 << (32 - kEntryMaskBits);
 
 __host__ __device__ inline size_t align_up(size_t x, size_t a = kAlign) { return (x + a - 1) / a * a; }
+
+// LDS hand-off between the lanes of ONE wave (a one-wave workgroup, or the lanes of one wave of a
+// larger one): a wave's LDS accesses complete in order, so no s_barrier and no wait for the wave's
+// outstanding global stores (which __syncthreads' workgroup fence adds) is needed.  The wavefront-scope
+// release / acquire fences emit no instructions; they give the IR the ordering of one lane's LDS store
+// before another lane's load, which wave_barrier alone (IntrNoMem: a scheduling barrier only) does not
+// (the form rocPRIM's wave_barrier uses).
+// (GSR_WAVE_FENCE=0: the bare wave_barrier, for A/B of the schedule the fences leave the compiler)
+#ifndef GSR_WAVE_FENCE
+#define GSR_WAVE_FENCE 1
+#endif
+__device__ __forceinline__ void wave_lds_sync() {
+#if GSR_WAVE_FENCE
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#endif
+    __builtin_amdgcn_wave_barrier();
+#if GSR_WAVE_FENCE
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#endif
+}
 
 // Bump allocator over a caller-provided chunk (the three opaque uint8 tensors of
 // the reference, CR/rasterizer_impl.h:26-90; contents are private to us).

@@ -262,7 +262,7 @@ __global__ void __launch_bounds__(kPreThreads) GSR_PRE_OCCUPANCY preprocess_kern
                         shp[1][k] = i4 < n4 ? __builtin_nontemporal_load(src + i4) : (v4f){0.f, 0.f, 0.f, 0.f};
                     }
                 }
-                __builtin_amdgcn_wave_barrier();  // (one wave: its LDS accesses complete in order)
+                wave_lds_sync();  // (one wave: its LDS accesses complete in order)
 #else
                 sh_stage_in<kShHalfRows, kPreThreads, false>(sa, g0 + half * kShHalfRows, rows, s_buf, kShRowStride, lane);
                 __syncthreads();
@@ -275,7 +275,7 @@ __global__ void __launch_bounds__(kPreThreads) GSR_PRE_OCCUPANCY preprocess_kern
                     rgb = sh_to_rgb(a.D, sh, dir.x, dir.y, dir.z);
                 }
 #if GSR_PRE_PREFETCH
-                __builtin_amdgcn_wave_barrier();
+                wave_lds_sync();
 #else
                 __syncthreads();
 #endif
@@ -372,7 +372,7 @@ __global__ void __launch_bounds__(kPreThreads) GSR_PRE_OCCUPANCY preprocess_kern
     s_rec[lane * kRecRows + 2] = r2;
     s_rec[lane * kRecRows + 3] = r3;
 #if GSR_PRE_PREFETCH
-    __builtin_amdgcn_wave_barrier();  // (not __syncthreads: its fence would wait for the stores above)
+    wave_lds_sync();  // (not __syncthreads: its fence would wait for the stores above)
 #else
     __syncthreads();
 #endif

@@ -39,6 +39,7 @@
 #include "kernels.h"
 
 #include <algorithm>
+#include <atomic>
 
 namespace gsr {
 
@@ -193,7 +194,7 @@ __device__ __forceinline__ void lds_store_rel(int* p, int v) {
 #endif
 __device__ __forceinline__ void unit_sync() {
 #if GSR_RENDER_WAVESYNC
-    __builtin_amdgcn_wave_barrier();
+    wave_lds_sync();
 #else
     __syncthreads();
 #endif
@@ -591,12 +592,19 @@ hipError_t launch_render_fwd(const RenderFwdArgs& a, hipStream_t stream, int qua
     const uint32_t tiles = a.gx * a.gy;
     if (tiles == 0) return hipSuccess;
     const uint32_t groups = (tiles + 7) / 8;
-    // the device's CU count, read once (the hybrid grid below is sized by it)
-    static const uint32_t cus = [] {
-        int dev = 0, n = 256;
-        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-        return (uint32_t)max(1, n);
-    }();
+    // the current device's CU count, read once per device (the hybrid grid below is sized by it)
+    static std::atomic<uint32_t> cu_count[64];
+    uint32_t cus = 256;
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
+        cus = cu_count[dev].load(std::memory_order_relaxed);
+        if (cus == 0) {
+            int n = 256;
+            (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+            cus = (uint32_t)max(1, n);
+            cu_count[dev].store(cus, std::memory_order_relaxed);
+        }
+    }
     if (GSR_FWD_TAIL_QUADS && quads == 2 && !a.census && tiles >= 16 && tiles <= 64 * cus) {
         // the last tiles (whole groups of 8) as quadrant units: GSR_FWD_TAIL_QUADS percent of them, at most
         // ~0.4 groups per CU.  Measured (profiles/r04/r4k, r4l): 1M@1080p render_fwd 194 -> 188 us, 500k@1080p

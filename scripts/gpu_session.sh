@@ -63,6 +63,18 @@ for stage in "$@"; do
       { sha256sum gaussian_splatting_amd/lib/libgsr.so; python -c "from gaussian_splatting_amd import _lib, build; \
 print('gsr_build_id', _lib.build_id(), 'tree', build.input_hash())"; } >> "$OUT/build_force.log" 2>&1
       echo "forcebuild rc=$rc"; cat "$OUT/build_force.log"; [ $rc -eq 0 ] || exit $rc ;;
+    calib)  # FETCH_SIZE / WRITE_SIZE against known byte counts per access shape (tools/fetch_calib.hip), one pass each
+      for ctr in FETCH_SIZE WRITE_SIZE; do
+        (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $ctr --output-format csv -d "$OUT/calib_$ctr" -o run -- \
+          "$ROOT/tools/fetch_calib" > "$OUT/calib_$ctr.log" 2>&1); rc=$?
+        echo "calib $ctr rc=$rc"; [ $rc -eq 0 ] || exit $rc
+      done
+      python tools/fetch_calib.py "$OUT/calib_FETCH_SIZE" "$OUT/calib_WRITE_SIZE" "$OUT/calib_FETCH_SIZE.log" \
+        --json "$OUT/fetch_calib.json" | tee "$OUT/fetch_calib.md" ;;
+    abn:*)  # interleaved A/B of the side libraries: abn:<rounds>[:<config>]
+      spec=${stage#abn:}; r=${spec%%:*}; c=1m_1080p_sh3; [ "$spec" != "$r" ] && c=${spec#*:}
+      bash scripts/abn.sh "$TAG/abn_$c" $r $c > "$OUT/abn_$c.txt" 2>&1; rc=$?
+      echo "abn $c rc=$rc"; cat "$OUT/abn_$c.txt"; [ $rc -eq 0 ] || exit $rc ;;
     cpus)  # the CPU set the baselines run on
       python -c "import os; print('affinity', len(os.sched_getaffinity(0)), 'cpu_count', os.cpu_count(), 'OMP', os.environ.get('OMP_NUM_THREADS'))" | tee "$OUT/cpus.txt" ;;
     rehearse2)  # N=2 on one GPU (gloo collectives): the multi-rank bench path, both exchanges

@@ -409,14 +409,18 @@ def test_sort_prefix_and_redo(name, prefix):
         np.testing.assert_array_equal(a, b)
 
 
-@pytest.mark.parametrize("P,W,H", [(3000, 2304, 2048), (40000, 2304, 2048), (6000, 5120, 2048)],
-                         ids=["2304x2048_sparse", "2304x2048_dense", "5120x2048_global_cursors"])
+@pytest.mark.parametrize("P,W,H", [(3000, 2304, 2048), (40000, 2304, 2048), (6000, 5120, 2048), (4000, 8400, 64),
+                                   (4000, 64, 8400)],
+                         ids=["2304x2048_sparse", "2304x2048_dense", "5120x2048_global_cursors", "8400x64_wide",
+                              "64x8400_tall"])
 def test_large_image(P, W, H):
     """A 2304x2048 frame (18432 tiles: K3's LDS cursors hold 74 KiB), sparse (3000 Gaussians, every
-    binning chunk spanning most of the screen) and denser (40000); and a 5120x2048 frame (40960 tiles,
+    binning chunk spanning most of the screen) and denser (40000); a 5120x2048 frame (40960 tiles,
     more than K1 / K3 keep in LDS: the binning falls back to global-memory counters and cursors and the
-    unfused tile scan).  Lists identical, the image by the full-size threshold-flip rule, L1-gradient
-    parity 1e-5."""
+    unfused tile scan); and a frame wider / taller than 8192 px, whose Z-ordered cell square (256 x 256
+    cells) exceeds K0's LDS table, so the cells are numbered row-major (binning.hip bin_cells; round 4
+    refused it).  Lists identical, the image by the full-size threshold-flip rule, L1-gradient parity
+    1e-5."""
     case = C.Case("large_image", P=P, W=W, H=H, focal=1400.0, scale_range=(0.01, 0.08))
     inp = C.build(case)
     ref = C.run_oracle(inp, nthreads=8)

@@ -235,3 +235,28 @@ def test_library_is_the_build_of_this_tree():
     with open(_lib.DEFAULT_LIB + ".inputs") as f:
         assert f.read().strip() == want
     assert build.input_hash(extra=("-DX=1",)) != want  # flags are part of the identity
+
+
+def test_build_identity_ignores_the_compiler_path(monkeypatch):
+    """the identity is the sources, flags and target, not the compiler's path -- a library
+    built with HIPCC=/custom/hipcc loads in a shell without that variable."""
+    from gaussian_splatting_amd import build
+
+    want = build.input_hash()
+    monkeypatch.setattr(build, "HIPCC", "/somewhere/else/hipcc")
+    assert build.input_hash() == want
+    monkeypatch.setattr(build, "ARCH", "gfx942")
+    assert build.input_hash() != want  # the target is part of it
+
+
+def test_build_id_check_without_sources(monkeypatch):
+    """an install without the csrc sources skips the build-id check with a warning instead
+    of raising FileNotFoundError from load()."""
+    from gaussian_splatting_amd import _lib, build
+
+    if _lib.LIB_PATH != _lib.DEFAULT_LIB:
+        pytest.skip("GSR_LIBRARY selects a variant build")
+    monkeypatch.setattr(build, "CSRC", "/nonexistent/csrc")
+    monkeypatch.setattr(_lib, "_lib", None)
+    with pytest.warns(UserWarning, match="build-id check skipped"):
+        _lib.load()

@@ -3,8 +3,13 @@ dispatch, plus derived figures.  Development tool.
 
     python tools/pmc_summary.py gpurun_out/<tag> [--out profiles/r01/pmc_<tag>.md]
 
-HBM bytes follow MI355X_MICROARCH.md: FETCH_SIZE / WRITE_SIZE are in KiB, and FETCH_SIZE
-under-reports by 2x on gfx950 (the guide's correction), so bytes = 2 * FETCH_SIZE * 1024.
+HBM bytes: FETCH_SIZE / WRITE_SIZE are in KiB.  MI355X_MICROARCH.md measured FETCH_SIZE at half the
+bytes of a wide coalesced streaming read (16 B per lane); tools/fetch_calib.hip calibrated the other shapes
+on the MI355X (profiles/r05/r5a/fetch_calib.md): a per-lane gather of a 64-byte record, of 48 bytes of one
+or of 4 bytes of one is counted as one whole 64-byte line, exactly (known / FETCH = 1.03 for whole
+records, the 0.03 being the coalesced index stream at half), and WRITE_SIZE counts a 48-byte scattered
+record as its 64-byte line.  So the read factor is per kernel (READ_FACTOR): 1 where the reads are
+record / line gathers (the render kernels), 2 where they are wide streams.
 """
 from __future__ import annotations
 
@@ -26,6 +31,16 @@ def short(name: str) -> str:
         if k in name:
             return v
     return name[:40]
+
+
+# read factor per kernel (bytes = factor x FETCH_SIZE x 1024) and why
+_GATHER = "x1: per-lane 64-B record / line gathers dominate, counted exactly (tools/fetch_calib.hip, profiles/r05/r5a)"
+_STREAM = "x2: wide coalesced streams dominate (MI355X_MICROARCH.md 'HBM'; tools/fetch_calib.hip stream16: 2.000)"
+READ_FACTOR = {"render_bwd": (1.0, _GATHER), "render_fwd": (1.0, _GATHER)}
+
+
+def read_factor(kernel: str):
+    return READ_FACTOR.get(kernel, (2.0, _STREAM))
 
 
 def load(d):
@@ -60,10 +75,13 @@ def main():
             return sum(x) / len(x) if x else float("nan")
 
         vg, lds, grid, wg = meta[k]
-        rd = 2 * m("FETCH_SIZE") * 1024 / 1e6
+        rf, basis = read_factor(k)
+        rd = rf * m("FETCH_SIZE") * 1024 / 1e6
         wr = m("WRITE_SIZE") * 1024 / 1e6
         table[k] = {"hbm_read_bytes": rd * 1e6, "hbm_write_bytes": wr * 1e6, "valu_insts": m("SQ_INSTS_VALU"),
-                    "salu_insts": m("SQ_INSTS_SALU"), "wave_cycles": m("SQ_WAVE_CYCLES")}
+                    "salu_insts": m("SQ_INSTS_SALU"), "wave_cycles": m("SQ_WAVE_CYCLES"),
+                    "fetch_size_bytes": m("FETCH_SIZE") * 1024, "write_size_bytes": m("WRITE_SIZE") * 1024,
+                    "read_factor": rf, "read_factor_basis": basis}
         lines.append(f"| {k} | {vg} | {lds} | {grid} | {m('SQ_INSTS_VALU'):.3g} | {m('SQ_INSTS_SALU'):.3g} | "
                      f"{m('SQ_INSTS_LDS'):.3g} | {m('SQ_INSTS_VMEM_RD'):.3g} | {m('SQ_WAVE_CYCLES'):.3g} | "
                      f"{m('SQ_ACTIVE_INST_ANY'):.3g} | {m('SQ_WAIT_INST_ANY'):.3g} | {m('SQ_WAIT_ANY'):.3g} | "
@@ -73,7 +91,8 @@ def main():
     if a.json:
         import json
 
-        entry = {"source": a.out or a.dir, "correction": "read = 2 x FETCH_SIZE KiB (gfx950), write = WRITE_SIZE KiB",
+        entry = {"source": a.out or a.dir, "correction": "read = read_factor x FETCH_SIZE KiB (per kernel), write = "
+                                                       "WRITE_SIZE KiB",
                  "kernels": table}
         if a.config:
             doc = json.load(open(a.json)) if os.path.exists(a.json) else {}
@@ -86,7 +105,8 @@ def main():
     if a.out:
         with open(a.out, "w") as f:
             f.write(f"# PMC summary ({a.dir}): mean per dispatch\n\n"
-                    "HBM rd = 2 x FETCH_SIZE (gfx950 correction, MI355X_MICROARCH.md), KiB -> MB; "
+                    "HBM rd = read factor x FETCH_SIZE (x1 render kernels: 64-B gathers, x2 streams; tools/fetch_calib.hip), "
+                    "KiB -> MB; "
                     "SQ cycle counters as reported (aggregated over SEs).\n\n" + text + "\n")
 
 
