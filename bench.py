@@ -171,25 +171,33 @@ def multi_rank_diagnostics(args, world, exchange, ex, arena, per_rank, cand_ms, 
     dist.barrier()
     t0 = time.perf_counter()
     for _ in range(reps):
-        if exchange == "views":
+        if exchange in ("views", "chunked"):
             ex.exchange()
+            if exchange == "chunked":  # the chunks' gathers are waited for by the backward; here by hand
+                for w in ex._cworks or []:
+                    if w is not None:
+                        w.wait()
+                ex._cworks = None
             ex.finish()
         else:
             arena.all_reduce()
     torch.cuda.synchronize()
     ms = torch.tensor([(time.perf_counter() - t0) / reps * 1e3], dtype=torch.float64, device=dev)
     dist.all_reduce(ms, op=dist.ReduceOp.MAX)
-    if exchange == "views":
+    if exchange in ("views", "chunked"):
         recv = ex.received_bytes()
         what = ("all-gather of sparse view blocks (48 B per Gaussian with a non-zero render gradient; "
                 f"{ex.last_entries} entries gathered per rank at the capacity hint; "
                 f"{ex.resyncs} re-gathers after a hint below the count)" if ex.sparse and ex.last_entries else
                 "all-gather of dense 44-B/Gaussian view blocks") + " + the multi-view backward on every rank"
+        if exchange == "chunked":
+            what = (f"{ex.chunks} Gaussian-range chunks, each an async " + what +
+                    "; chunk k+1's all-gather runs during chunk k's backward")
     else:
         recv = int(2 * (world - 1) / world * arena.flat.numel() * 4)
         what = "RCCL all-reduce of the 59-float/Gaussian parameter-gradient arena"
     if args.exchange == "auto":
-        why = ("--exchange auto: both exchanges timed in the warm-up on this fabric (whole steps, max over "
+        why = ("--exchange auto: the candidate exchanges timed in the warm-up on this fabric (whole steps, max over "
                f"ranks, {args.auto_steps} steps each): " + ", ".join(f"{k} {v:.4f} ms/step" for k, v in cand_ms.items())
                + f"; the faster is {exchange}")
     else:
@@ -289,10 +297,12 @@ def parse_args(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-census", action="store_true",
                     help="skip the census pass (profiler runs: keeps its kernel instantiations out of the trace)")
-    ap.add_argument("--exchange", choices=("auto", "views", "dense", "allreduce"), default="auto",
-                    help="N > 1: all-gather the sparse view blocks (views), the dense view blocks (dense), or "
-                         "all-reduce the parameter gradients (allreduce); auto times views and allreduce in the "
-                         "warm-up and keeps the faster (DESIGN.md section 7)")
+    ap.add_argument("--exchange", choices=("auto", "views", "chunked", "dense", "allreduce"), default="auto",
+                    help="N > 1: all-gather the sparse view blocks (views), the same in Gaussian-range chunks whose "
+                         "all-gathers overlap the multi-view backward of the earlier chunks (chunked), the dense "
+                         "view blocks (dense), or all-reduce the parameter gradients (allreduce); auto times views, "
+                         "chunked and allreduce in the warm-up and keeps the fastest (DESIGN.md section 7)")
+    ap.add_argument("--exchange-chunks", type=int, default=4, help="Gaussian-range chunks of --exchange chunked")
     ap.add_argument("--auto-steps", type=int, default=5, help="timed warm-up steps per candidate of --exchange auto")
     ap.add_argument("--separate-sh", action="store_true",
                     help="SH as train.py's separate_sh path passes it: dc [P,1,3] + rest [P,M-1,3] (3DGS-accel surface)")
@@ -377,9 +387,11 @@ def main():
     arena = GradArena(P, scene.shs.shape[1], dev, separate_sh=args.separate_sh)
     uses_views = world > 1 and args.exchange in ("auto", "views", "dense")
     ex = ViewExchange(P, dev, sparse=args.exchange != "dense") if uses_views else None
+    exc = (ViewExchange(P, dev, chunks=args.exchange_chunks)
+           if world > 1 and args.exchange in ("auto", "chunked") else None)
     # the exchange the steps run: fixed by --exchange, or (auto) picked by timing in the warm-up below
     exchange = "none" if world == 1 else ("allreduce" if args.exchange == "allreduce" else
-                                          "views" if args.exchange in ("views", "dense") else "views")
+                                          "chunked" if args.exchange == "chunked" else "views")
     clock = HostClock()
     pc = time.perf_counter
 
@@ -394,12 +406,13 @@ def main():
                cam.viewmatrix, cam.projmatrix, cam.tanfovx, cam.tanfovy, gc, gd, *sh_in, Kdeg, cam.campos, geom, nr,
                binning, img, False, False)
         t2 = pc()
-        if exchange == "views" and collective:  # sparse view blocks, every rank sums all views' gradients
-            _C.rasterize_gaussians_backward_screen(*bwd, view_block=ex.local_block())
+        if exchange in ("views", "chunked") and collective:  # view blocks, every rank sums all views' gradients
+            E = exc if exchange == "chunked" else ex
+            _C.rasterize_gaussians_backward_screen(*bwd, view_block=E.local_block())
             t3 = pc()
-            ex.exchange(zero=arena.flat)  # the outputs zeroed beside the exchange; a live-list backward
-            ex.views_backward(scene.means3D, sh_dc, sh_rest, Kdeg, scene.opacities, scene.scales, scene.rotations,
-                              1.0, out=arena.views())
+            E.exchange(zero=arena.flat)  # the outputs zeroed beside the exchange; a live-list backward
+            E.views_backward(scene.means3D, sh_dc, sh_rest, Kdeg, scene.opacities, scene.scales, scene.rotations,
+                             1.0, out=arena.views())
         else:
             _C.rasterize_gaussians_backward(*bwd, out=arena.views())
             t3 = pc()
@@ -430,7 +443,7 @@ def main():
     # steps and collectives on every rank, the max over ranks), keep the faster
     cand_ms = {}
     if world > 1 and args.exchange == "auto":
-        for cand in ("views", "allreduce"):
+        for cand in ("views", "chunked", "allreduce"):
             exchange = cand
             for _ in range(2):
                 step()
@@ -503,7 +516,8 @@ def main():
         per_rank = [float(g.item()) for g in gathered]
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
-    multi = multi_rank_diagnostics(args, world, exchange, ex, arena, per_rank, cand_ms, dev) if world > 1 else None
+    multi = (multi_rank_diagnostics(args, world, exchange, exc if exchange == "chunked" else ex, arena, per_rank,
+                                    cand_ms, dev) if world > 1 else None)
     if multi is not None:
         multi.update({"ranks_seen_by_backend": ranks_seen, "rank_devices": rank_devices,
                       "visible_devices_per_rank": ndev, "shared_gpu_rehearsal": rehearse})
@@ -558,8 +572,13 @@ def main():
                   f"Gaussian-splats/sec fwd+bwd @{W}x{H}, {P} Gaussians ({args.config}; not the headline metric)")
         par = f"view-sharded x{world}"
         if world > 1:
-            par += {"views": " + RCCL all-gather of " + ("sparse " if ex is not None and ex.sparse else "dense ")
-                    + "view blocks", "allreduce": " + RCCL all-reduce of the gradient arena"}[exchange]
+            # the backend that really ran (gloo in the one-GPU rehearsal, nccl = RCCL on ROCm)
+            be = "RCCL" if multi["backend"] == "nccl" else multi["backend"]
+            par += {"views": f" + {be} all-gather of " + ("sparse " if ex is not None and ex.sparse else "dense ")
+                    + "view blocks",
+                    "chunked": f" + {be} all-gathers of sparse view blocks in {args.exchange_chunks} Gaussian-range "
+                               "chunks, overlapped with the multi-view backward",
+                    "allreduce": f" + {be} all-reduce of the gradient arena"}[exchange]
         line = {
             "metric": metric,
             "value": value,

@@ -365,11 +365,20 @@ def view_pack_floats(entries: int) -> int:
     return int(_lib.load().gsr_view_pack_floats(int(entries)))
 
 
+def _range(P, rng):
+    g0, g1 = (0, P) if rng is None else (int(rng[0]), int(rng[1]))
+    if not 0 <= g0 <= g1 <= P:
+        raise RuntimeError(f"Gaussian range [{g0}, {g1}) outside [0, {P})")
+    return g0, g1
+
+
 def view_block_pack(view_block: torch.Tensor, packed: torch.Tensor, scratch: torch.Tensor, count: torch.Tensor,
-                    P: int) -> None:
+                    P: int, rng=None) -> None:
     """Pack a dense view block into ``packed`` (capacity from its size); the entry count lands in
     ``count`` (an int32 device tensor of one element) and in the packed header (include/gsr.h
-    gsr_view_block_pack).  Only Gaussians with a non-zero render gradient are kept."""
+    gsr_view_block_pack).  Only Gaussians with a non-zero render gradient are kept; with ``rng`` =
+    (g0, g1) only those of Gaussians [g0, g1) (one chunk of a chunked exchange)."""
+    g0, g1 = _range(P, rng)
     _require_device(view_block, "view_block")
     nb = view_block_floats(P)
     if view_block.numel() != nb or view_block.dtype != torch.float32 or not view_block.is_contiguous():
@@ -382,8 +391,8 @@ def view_block_pack(view_block: torch.Tensor, packed: torch.Tensor, scratch: tor
         raise RuntimeError("view_block_pack: scratch too small or count not an int32 scalar tensor")
     lib = _lib.load()
     with torch.cuda.device(view_block.device):
-        rc = lib.gsr_view_block_pack(int(P), view_block.data_ptr(), packed.data_ptr(), int(cap), scratch.data_ptr(),
-                                     count.data_ptr(), _stream_handle(view_block.device))
+        rc = lib.gsr_view_block_pack_range(int(P), g0, g1, view_block.data_ptr(), packed.data_ptr(), int(cap),
+                                           scratch.data_ptr(), count.data_ptr(), _stream_handle(view_block.device))
     _lib.check(rc, "view_block_pack")
 
 
@@ -404,10 +413,12 @@ def view_block_unpack(packed: torch.Tensor, blocks: torch.Tensor, P: int) -> Non
     _lib.check(rc, "view_block_unpack")
 
 
-def view_block_index(packed: torch.Tensor, flags: torch.Tensor, P: int) -> None:
+def view_block_index(packed: torch.Tensor, flags: torch.Tensor, P: int, rng=None) -> None:
     """Index ``packed`` ([n_views, packed_floats]) for ``gauss_backward_views(..., flags=flags)``:
     ``flags`` ([n_views, P] int32) is cleared and, for each packed entry i of view v, flags[v, g] =
-    i << 4 | its flag bits (include/gsr.h gsr_view_block_index)."""
+    i << 4 | its flag bits (include/gsr.h gsr_view_block_index); with ``rng`` = (g0, g1) only the
+    flags of Gaussians [g0, g1) (the packed blocks of one chunk)."""
+    g0, g1 = _range(P, rng)
     _require_device(packed, "packed")
     if packed.dim() != 2 or flags.dim() != 2 or tuple(flags.shape) != (packed.size(0), P):
         raise RuntimeError(f"packed [n_views, k] and flags [n_views, {P}] expected")
@@ -416,8 +427,9 @@ def view_block_index(packed: torch.Tensor, flags: torch.Tensor, P: int) -> None:
     cap = (packed.size(1) - 64) // 12
     lib = _lib.load()
     with torch.cuda.device(packed.device):
-        rc = lib.gsr_view_block_index(int(P), int(packed.size(0)), packed.data_ptr(), int(packed.size(1)),
-                                      flags.data_ptr(), int(cap), _stream_handle(packed.device))
+        rc = lib.gsr_view_block_index_range(int(P), g0, g1, int(packed.size(0)), packed.data_ptr(),
+                                            int(packed.size(1)), flags.data_ptr(), int(cap),
+                                            _stream_handle(packed.device))
     _lib.check(rc, "view_block_index")
 
 
@@ -426,9 +438,11 @@ def views_live_floats(P: int) -> int:
     return int(_lib.load().gsr_views_live_floats(int(P)))
 
 
-def views_live_list(flags: torch.Tensor, live: torch.Tensor, P: int) -> None:
+def views_live_list(flags: torch.Tensor, live: torch.Tensor, P: int, rng=None) -> None:
     """The Gaussians some view flags (``flags`` from ``view_block_index``) into ``live``
-    (int32, ``views_live_floats(P)`` words), for ``gauss_backward_views(..., live=live)``."""
+    (int32, ``views_live_floats(P)`` words), for ``gauss_backward_views(..., live=live)``; with
+    ``rng`` = (g0, g1) only Gaussians [g0, g1)."""
+    g0, g1 = _range(P, rng)
     _require_device(flags, "flags")
     if flags.dim() != 2 or flags.size(1) != P or flags.dtype != torch.int32 or not flags.is_contiguous():
         raise RuntimeError(f"flags must be a contiguous int32 [n_views, {P}] tensor")
@@ -436,8 +450,8 @@ def views_live_list(flags: torch.Tensor, live: torch.Tensor, P: int) -> None:
         raise RuntimeError(f"live must be a contiguous int32 tensor of {views_live_floats(P)} words")
     lib = _lib.load()
     with torch.cuda.device(flags.device):
-        rc = lib.gsr_views_live_list(int(P), int(flags.size(0)), flags.data_ptr(), live.data_ptr(),
-                                     _stream_handle(flags.device))
+        rc = lib.gsr_views_live_list_range(int(P), g0, g1, int(flags.size(0)), flags.data_ptr(), live.data_ptr(),
+                                           _stream_handle(flags.device))
     _lib.check(rc, "views_live_list")
 
 

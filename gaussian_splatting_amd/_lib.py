@@ -73,6 +73,9 @@ SIGNATURES = {
     "gsr_view_pack_floats": (ctypes.c_ulonglong, [ctypes.c_longlong]),
     "gsr_view_pack_scratch_bytes": (ctypes.c_ulonglong, [_i]),
     "gsr_view_block_pack": (_i, [_i, _vp, _vp, ctypes.c_longlong, _vp, _vp, _vp]),
+    "gsr_view_block_pack_range": (_i, [_i, _i, _i, _vp, _vp, ctypes.c_longlong, _vp, _vp, _vp]),
+    "gsr_view_block_index_range": (_i, [_i, _i, _i, _i, _vp, ctypes.c_longlong, _vp, ctypes.c_longlong, _vp]),
+    "gsr_views_live_list_range": (_i, [_i, _i, _i, _i, _vp, _vp, _vp]),
     "gsr_view_block_unpack": (_i, [_i, _i, _vp, ctypes.c_longlong, _vp, ctypes.c_longlong, _vp]),
     "gsr_view_block_index": (_i, [_i, _i, _vp, ctypes.c_longlong, _vp, ctypes.c_longlong, _vp]),
     "gsr_views_live_floats": (ctypes.c_ulonglong, [_i]),
@@ -194,7 +197,7 @@ def build_id() -> str:
 
 # ---- runtime options (include/gsr.h gsr_option_set) ---------------------------------
 OPTIONS = ("fused_bin", "fwd_quads", "bwd_seg_ck", "host_total", "zero_fill", "live_list", "sort_prefix",
-           "count_wait", "bwd_grid")
+           "count_wait", "bwd_grid", "bwd_atomic")
 
 
 def option_get(name: str) -> int:

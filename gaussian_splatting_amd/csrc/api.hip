@@ -163,6 +163,8 @@ gsr::GeomState carve_geom(char* base, int P, uint32_t gx, uint32_t gy, size_t* t
     g.redo_flag = c.take<uint32_t>(tiles);
     g.redo_list = c.take<uint32_t>(tiles);
     g.redo_cnt = c.take<uint32_t>(1);
+    g.acc = c.take<float4>((size_t)kAccRow4 * P);
+    g.touched = c.take<uint32_t>(touched_words((size_t)P));
     *total = align_up(c.off);
     return g;
 }
@@ -285,9 +287,20 @@ void carve_recs(char* base, size_t R, size_t P, gsr::GradRecs* recs, gsr::GradRe
 #ifndef GSR_COUNT_WAIT_DEFAULT
 #define GSR_COUNT_WAIT_DEFAULT 2
 #endif
+// "bwd_atomic": the render backward adds each instance's sums into per-Gaussian rows with float atomics
+// (render.hip ATOMIC) and gauss_live lists the touched Gaussians, instead of per-instance records summed
+// by gauss_reduce (deterministic).  The forward zeroes the rows when the option is on at forward time,
+// so a forward and its backwards must see the same value (an A/B switch: set it once).
+#ifndef GSR_BWD_ATOMIC_DEFAULT
+#define GSR_BWD_ATOMIC_DEFAULT 0
+#endif
+#ifndef GSR_FWD_FILL_BLOCKS
+#define GSR_FWD_FILL_BLOCKS 256  // one-wave blocks zeroing the accumulators in render_fwd's launch (a multiple of 8)
+#endif
+static_assert(GSR_FWD_FILL_BLOCKS % 8 == 0, "the forward's fill blocks keep the tiles' XCD mapping");
 enum Opt {
     OPT_FUSED_BIN = 0, OPT_FWD_QUADS, OPT_BWD_SEG_CK, OPT_HOST_TOTAL, OPT_ZERO_FILL, OPT_LIVE_LIST, OPT_SORT_PREFIX,
-    OPT_COUNT_WAIT, OPT_BWD_GRID, OPT_COUNT
+    OPT_COUNT_WAIT, OPT_BWD_GRID, OPT_BWD_ATOMIC, OPT_COUNT
 };
 struct OptionSpec {
     const char* name;
@@ -304,6 +317,7 @@ const OptionSpec kOptions[OPT_COUNT] = {
     {"sort_prefix", "GSR_SORT_PREFIX", GSR_SORT_PREFIX_DEFAULT, 0, (int)gsr::kSortPrefixMax},
     {"count_wait", "GSR_COUNT_WAIT", GSR_COUNT_WAIT_DEFAULT, 0, 2},
     {"bwd_grid", "GSR_BWD_GRID", 0, 0, 2},
+    {"bwd_atomic", "GSR_BWD_ATOMIC", GSR_BWD_ATOMIC_DEFAULT, 0, 1},
 };
 std::atomic<int> g_opt[OPT_COUNT];
 std::once_flag g_opt_once;
@@ -827,6 +841,7 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
     const uint32_t opt_prefix = (uint32_t)option(OPT_SORT_PREFIX);
     const bool opt_fused = fused_binning_mode(), opt_host_total = host_total_store();
     const int opt_count_wait = option(OPT_COUNT_WAIT);
+    const bool opt_atomic = option(OPT_BWD_ATOMIC) != 0;
     // _ex / _dc forwards lay the binning buffer out for a multiple of kCapQuantum (the backward
     // recovers it from the buffer's size); gsr_rasterize_forward keeps the exact C = R layout
     const auto capacity_for = [quantized](size_t c) {
@@ -1005,6 +1020,14 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
             ra.redo_cnt = geom.redo_cnt;
             // (C == 0: no lists and no K4, so nothing is prefix-sorted and no redo state was reset)
             if (C == 0) ra.sorted_len = nullptr;
+            if (opt_atomic) {  // the atomic backward's accumulator rows and touched bits, zeroed beside the render
+                ra.fill.ptr[0] = reinterpret_cast<float*>(geom.acc);
+                ra.fill.n[0] = (unsigned long long)kAccRow4 * 4 * P;
+                ra.fill.ptr[1] = reinterpret_cast<float*>(geom.touched);
+                ra.fill.n[1] = touched_words((size_t)P);
+                ra.fill.count = 2;
+                ra.fill_blocks = GSR_FWD_FILL_BLOCKS;
+            }
             HIP_TRY(launch_render_fwd(ra, stream, opt_quads), "render_fwd");
             if (prefix && C > 0) {  // the tiles whose walk passed their sorted prefix (usually none)
                 HIP_TRY(launch_tile_sort_redo(tiles, img.ranges, geom, bin, C, stream), "render_fwd redo sort");
@@ -1170,10 +1193,21 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
     // sized for the shortest segments (seg_ck = 1), so it covers whatever the forward used
     const size_t max_units = R > 0 ? bwd_max_units((size_t)R, tiles, 1) : 0;
     uint32_t *live = nullptr, *live_count = nullptr;
-    carve_recs(nullptr, (size_t)R, (size_t)P, &recs, &sums, &live, &live_count, &rec_bytes);
+    // the options, each read once
+    const int zmode = screen ? 0 : zero_fill_mode();
+    const int grid_mode = option(OPT_BWD_GRID);
+    // With the outputs zero-filled, gauss_bwd walks a list of the Gaussians with a gradient
+    // (~13% of a 1M@1080p view) that gauss_reduce appends to, instead of a lane per Gaussian.
+    const bool use_list = zmode != 0 && live_list_mode();
+    // atomic backward: per-Gaussian rows (zeroed by the forward) instead of records + gauss_reduce; it
+    // needs the live list (the record path serves every other mode, and the view blocks)
+    const bool atomic = !screen && use_list && R > 0 && option(OPT_BWD_ATOMIC) != 0;
+    // (the atomic backward writes no per-instance records: no record scratch)
+    const size_t R_recs = atomic ? 0 : (size_t)R;
+    carve_recs(nullptr, R_recs, (size_t)P, &recs, &sums, &live, &live_count, &rec_bytes);
     char* rbase = (char*)call_alloc(scratch_alloc, scratch_ctx, rec_bytes);
     if (!rbase) return fail(GSR_ERR_ALLOC, "rasterize_backward: scratch allocation failed");
-    carve_recs(rbase, (size_t)R, (size_t)P, &recs, &sums, &live, &live_count, &rec_bytes);
+    carve_recs(rbase, R_recs, (size_t)P, &recs, &sums, &live, &live_count, &rec_bytes);
     uint32_t* flags = nullptr;
     if (screen) {  // the sums and flags go to the view block (gsr_common.h "View block")
         float* body = view_block + kViewBlockHeader;
@@ -1185,8 +1219,6 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
 
     // dense outputs to zero-fill (gauss_bwd then writes only the non-zero rows)
     FillArgs fill{};
-    const int zmode = screen ? 0 : zero_fill_mode();
-    const int grid_mode = option(OPT_BWD_GRID);  // (read once, as every option)
     const int m_rest = dc ? M - 1 : M;
     auto seg = [&](float* ptr, size_t n) {
         if (ptr && n) {
@@ -1208,9 +1240,6 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
         seg(dL_dscale, 3 * (size_t)P);
         seg(dL_drot, 4 * (size_t)P);
     }
-    // With the outputs zero-filled, gauss_bwd walks a list of the Gaussians with a gradient
-    // (~13% of a 1M@1080p view) that gauss_reduce appends to, instead of a lane per Gaussian.
-    const bool use_list = zmode != 0 && live_list_mode();
     if (!use_list) live = live_count = nullptr;
     if (use_list && R == 0)
         HIP_TRY(hipMemsetAsync(live_count, 0, sizeof(uint32_t) * kLiveShards * kLiveCntStride, stream), "live count");
@@ -1263,10 +1292,17 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
             ra.fill = fill;
             ra.fill_blocks = GSR_FUSED_FILL_BLOCKS;
         }
+        if (atomic) {
+            ra.acc = reinterpret_cast<float*>(geom.acc);
+            ra.touched = geom.touched;
+        }
         HIP_TRY(launch_render_bwd(ra, max_units, stream, grid_mode), "render_bwd");
     }
     if (int rc = check_debug(debug, stream, "render_bwd")) return rc;
-    {
+    if (atomic) {  // (stage "gauss_reduce": the step between render_bwd and gauss_bwd)
+        StageScope sc(ST_GAUSS_REDUCE, stream);
+        HIP_TRY(launch_gauss_live(P, geom.touched, live, live_count, stream), "gauss_live");
+    } else {
         StageScope sc(ST_GAUSS_REDUCE, stream);
         HIP_TRY(launch_gauss_reduce(P, geom, recs, sums, flags, radii, live, live_count, stream),
                 "gauss_reduce");
@@ -1288,6 +1324,16 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
         ga.viewmatrix = viewmatrix; ga.projmatrix = projmatrix; ga.campos = campos;
         ga.tan_fovx = tan_fovx; ga.tan_fovy = tan_fovy; ga.focal_x = focal_x; ga.focal_y = focal_y;
         ga.antialiasing = antialiasing; ga.radii = radii; ga.geom = geom; ga.sums = sums;
+        ga.sum_stride4 = 1;
+        ga.sum_stride2 = 1;
+        if (atomic) {  // the accumulator rows: a at +0, b at +1 float4, c at +2 float4 of each 64-B row
+            ga.sums.a = geom.acc;
+            ga.sums.b = geom.acc + 1;
+            ga.sums.c = reinterpret_cast<float2*>(geom.acc + 2);
+            ga.sum_stride4 = kAccRow4;
+            ga.sum_stride2 = 2 * kAccRow4;
+            ga.acc_restore = geom.acc;
+        }
         ga.have_invdepth = dL_dinvdepths != nullptr;
         ga.dL_dmean2D = dL_dmean2D; ga.dL_dconic = dL_dconic; ga.dL_dopacity = dL_dopacity; ga.dL_dcolor = dL_dcolor;
         ga.dL_dinvdepth = dL_dinvdepth; ga.dL_dmean3D = dL_dmean3D; ga.dL_dcov3D = dL_dcov3D;
@@ -1395,17 +1441,23 @@ unsigned long long gsr_view_pack_floats(long long entries) {
 
 unsigned long long gsr_view_pack_scratch_bytes(int P) { return P > 0 ? 4ull * ((P + 255) / 256) : 4ull; }
 
-int gsr_view_block_pack(int P, const float* view_block, float* packed, long long cap, void* scratch,
-                        unsigned int* count, void* stream) {
+int gsr_view_block_pack_range(int P, int g0, int g1, const float* view_block, float* packed, long long cap,
+                              void* scratch, unsigned int* count, void* stream) {
     g_err[0] = 0;
     if (P <= 0 || cap < 0) return fail(GSR_ERR_ARGUMENT, "view_block_pack: P=%d cap=%lld", P, cap);
+    if (g0 < 0 || g1 < g0 || g1 > P) return fail(GSR_ERR_ARGUMENT, "view_block_pack: range [%d, %d) of P=%d", g0, g1, P);
     if (!view_block || !packed || !scratch) return fail(GSR_ERR_ARGUMENT, "view_block_pack: null pointer");
     if ((reinterpret_cast<uintptr_t>(view_block) & 15) || (reinterpret_cast<uintptr_t>(packed) & 15))
         return fail(GSR_ERR_ARGUMENT, "view_block_pack: blocks must be 16-byte aligned");
-    HIP_TRY(gsr::launch_view_pack((uint32_t)P, view_block, packed, (unsigned long long)cap,
+    HIP_TRY(gsr::launch_view_pack((uint32_t)P, (uint32_t)g0, (uint32_t)g1, view_block, packed, (unsigned long long)cap,
                                   reinterpret_cast<uint32_t*>(scratch), count, (hipStream_t)stream),
             "view_block_pack");
     return GSR_OK;
+}
+
+int gsr_view_block_pack(int P, const float* view_block, float* packed, long long cap, void* scratch,
+                        unsigned int* count, void* stream) {
+    return gsr_view_block_pack_range(P, 0, P, view_block, packed, cap, scratch, count, stream);
 }
 
 int gsr_view_block_unpack(int P, int n_views, const float* packed, long long packed_floats, float* blocks,
@@ -1428,7 +1480,13 @@ int gsr_view_block_unpack(int P, int n_views, const float* packed, long long pac
 
 int gsr_view_block_index(int P, int n_views, const float* packed, long long packed_floats, unsigned int* flags,
                          long long cap, void* stream) {
+    return gsr_view_block_index_range(P, 0, P, n_views, packed, packed_floats, flags, cap, stream);
+}
+
+int gsr_view_block_index_range(int P, int g0, int g1, int n_views, const float* packed, long long packed_floats,
+                               unsigned int* flags, long long cap, void* stream) {
     g_err[0] = 0;
+    if (g0 < 0 || g1 < g0 || g1 > P) return fail(GSR_ERR_ARGUMENT, "view_block_index: range [%d, %d) of P=%d", g0, g1, P);
     if (P <= 0 || n_views < 0 || cap < 0 || packed_floats < (long long)gsr::view_pack_floats(0))
         return fail(GSR_ERR_ARGUMENT, "view_block_index: P=%d views=%d packed_floats=%lld cap=%lld", P, n_views,
                     packed_floats, cap);
@@ -1439,8 +1497,8 @@ int gsr_view_block_index(int P, int n_views, const float* packed, long long pack
     if (n_views > 0 && (!packed || !flags)) return fail(GSR_ERR_ARGUMENT, "view_block_index: null pointer");
     if ((reinterpret_cast<uintptr_t>(packed) & 15) || (packed_floats & 3))
         return fail(GSR_ERR_ARGUMENT, "view_block_index: packed blocks must be 16-byte aligned");
-    HIP_TRY(gsr::launch_view_index((uint32_t)P, n_views, packed, (unsigned long long)packed_floats, flags,
-                                   (unsigned long long)cap, (hipStream_t)stream),
+    HIP_TRY(gsr::launch_view_index((uint32_t)P, (uint32_t)g0, (uint32_t)g1, n_views, packed,
+                                   (unsigned long long)packed_floats, flags, (unsigned long long)cap, (hipStream_t)stream),
             "view_block_index");
     return GSR_OK;
 }
@@ -1595,14 +1653,22 @@ unsigned long long gsr_views_live_floats(int P) {
                  : 0ull;
 }
 
-int gsr_views_live_list(int P, int n_views, const unsigned int* flags, unsigned int* live, void* stream) {
+int gsr_views_live_list_range(int P, int g0, int g1, int n_views, const unsigned int* flags, unsigned int* live,
+                              void* stream) {
     g_err[0] = 0;
     if (P < 0 || n_views < 0) return fail(GSR_ERR_ARGUMENT, "views_live_list: P=%d views=%d", P, n_views);
+    if (g0 < 0 || g1 < g0 || g1 > P) return fail(GSR_ERR_ARGUMENT, "views_live_list: range [%d, %d) of P=%d", g0, g1, P);
     if (P == 0) return GSR_OK;
     if (!live || (n_views > 0 && !flags)) return fail(GSR_ERR_ARGUMENT, "views_live_list: null pointer");
     unsigned int* count = live + (size_t)gsr::kLiveShards * gsr::live_list_cap((uint32_t)P);
-    HIP_TRY(gsr::launch_views_live((uint32_t)P, n_views, flags, live, count, (hipStream_t)stream), "views_live_list");
+    HIP_TRY(gsr::launch_views_live((uint32_t)P, (uint32_t)g0, (uint32_t)g1, n_views, flags, live, count,
+                                   (hipStream_t)stream),
+            "views_live_list");
     return GSR_OK;
+}
+
+int gsr_views_live_list(int P, int n_views, const unsigned int* flags, unsigned int* live, void* stream) {
+    return gsr_views_live_list_range(P, 0, P, n_views, flags, live, stream);
 }
 
 int gsr_gauss_backward_views_live(int P, int D, int M, const float* means3D, const float* dc, const float* shs,

@@ -456,6 +456,38 @@ hipError_t launch_gauss_reduce(int P, const GeomState& g, const GradRecs& recs, 
     return hipGetLastError();
 }
 
+// ---- 1b. atomic backward: the live list from the touched bits ----------------------
+// render_bwd ("bwd_atomic") added every instance's sums into its Gaussian's accumulator row and set
+// the Gaussian's bit; this lists the Gaussians with a bit (gauss_bwd's live list) and clears the words
+// it read, so the next backward of the same forward starts from zero bits (gauss_bwd clears the rows).
+// One lane per 32-bit word; the shard of Gaussian g is (g / 64) % kLiveShards, as in gauss_reduce, so
+// live_list_cap bounds every shard: lanes 2k and 2k + 1 (one 64-Gaussian group) share one append.
+__global__ void __launch_bounds__(64) gauss_live_kernel(int P, uint32_t* __restrict__ touched,
+                                                        uint32_t* __restrict__ live,
+                                                        uint32_t* __restrict__ live_count, uint32_t live_cap) {
+    const int lane = threadIdx.x;
+    const size_t wi = (size_t)blockIdx.x * 64 + lane, nwords = touched_words((size_t)P);
+    const uint32_t w = wi < nwords ? touched[wi] : 0u;
+    if (w) touched[wi] = 0u;
+    const uint32_t n = (uint32_t)__popc(w);
+    const uint32_t pair = n + (uint32_t)__shfl_xor((int)n, 1);
+    const uint32_t shard = (uint32_t)((wi >> 1) % kLiveShards);
+    uint32_t base = 0;
+    if (!(lane & 1) && pair) base = atomicAdd(&live_count[shard * kLiveCntStride], pair);
+    const uint32_t even_n = (uint32_t)__shfl((int)n, lane & ~1);
+    base = (uint32_t)__shfl((int)base, lane & ~1) + ((lane & 1) ? even_n : 0u);
+    uint32_t* dst = live + (size_t)shard * live_cap + base;
+    for (uint32_t m = w; m; m &= m - 1u) *dst++ = (uint32_t)(wi * 32 + (size_t)__builtin_ctz(m));
+}
+
+hipError_t launch_gauss_live(int P, uint32_t* touched, uint32_t* live, uint32_t* live_count, hipStream_t stream) {
+    if (P <= 0) return hipSuccess;
+    const size_t blocks = (touched_words((size_t)P) + 63) / 64;
+    hipLaunchKernelGGL(gauss_live_kernel, dim3((uint32_t)blocks), dim3(64), 0, stream, P, touched, live, live_count,
+                       live_list_cap((uint32_t)P));
+    return hipGetLastError();
+}
+
 // ---- 2. SH colour backward, one coefficient at a time ---------------------------
 // Row accessors: coefficient k of this thread's Gaussian (3 floats).
 struct ShLds {
@@ -838,9 +870,13 @@ __global__ void __launch_bounds__(64) GSR_GB_OCCUPANCY gauss_bwd_kernel(GaussBwd
     int rad = 0;
     if (valid) {
         rad = a.radii[idx];
-        sa = a.sums.a[idx];
-        sb = a.sums.b[idx];
-        sc = a.sums.c[idx];
+        sa = a.sums.a[(size_t)idx * a.sum_stride4];
+        sb = a.sums.b[(size_t)idx * a.sum_stride4];
+        sc = a.sums.c[(size_t)idx * a.sum_stride2];
+        if (a.acc_restore) {  // atomic backward: the row back to zero for the next backward of this forward
+            float4* row = a.acc_restore + (size_t)idx * kAccRow4;
+            row[0] = row[1] = row[2] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
     }
     const bool any_grad = (sa.x != 0.f) | (sa.y != 0.f) | (sa.z != 0.f) | (sa.w != 0.f) | (sb.x != 0.f) |
                           (sb.y != 0.f) | (sb.z != 0.f) | (sb.w != 0.f) | (sc.x != 0.f) | (sc.y != 0.f);
@@ -1313,11 +1349,14 @@ __device__ __forceinline__ uint32_t block_live_rank(bool live, uint32_t* s_w, ui
     return before + in_wave;
 }
 
-__global__ void __launch_bounds__(kPackThreads) view_pack_count_kernel(uint32_t P, const float* __restrict__ block,
+// (range forms: only Gaussians [g0, g1) are packed, indexed, listed -- one chunk of a chunked exchange,
+// distributed.py ViewExchange(chunks=K); entries keep their absolute Gaussian index)
+__global__ void __launch_bounds__(kPackThreads) view_pack_count_kernel(uint32_t P, uint32_t g0, uint32_t g1,
+                                                                       const float* __restrict__ block,
                                                                        uint32_t* __restrict__ wg_cnt) {
     __shared__ uint32_t s_w[kPackThreads / 64];
-    const uint32_t g = blockIdx.x * kPackThreads + threadIdx.x;
-    const bool live = g < P && view_entry_live(block + kViewBlockHeader, P, g);
+    const uint32_t g = g0 + blockIdx.x * kPackThreads + threadIdx.x;
+    const bool live = g < g1 && view_entry_live(block + kViewBlockHeader, P, g);
     uint32_t total = 0;
     block_live_rank(live, s_w, &total);
     if (threadIdx.x == 0) wg_cnt[blockIdx.x] = total;
@@ -1350,7 +1389,8 @@ __global__ void __launch_bounds__(1024) view_pack_scan_kernel(uint32_t nb, uint3
     }
 }
 
-__global__ void __launch_bounds__(kPackThreads) view_pack_scatter_kernel(uint32_t P, const float* __restrict__ block,
+__global__ void __launch_bounds__(kPackThreads) view_pack_scatter_kernel(uint32_t P, uint32_t g0, uint32_t g1,
+                                                                         const float* __restrict__ block,
                                                                          const uint32_t* __restrict__ wg_off,
                                                                          float* __restrict__ packed,
                                                                          unsigned long long cap) {
@@ -1358,8 +1398,8 @@ __global__ void __launch_bounds__(kPackThreads) view_pack_scatter_kernel(uint32_
     if (blockIdx.x == 0 && threadIdx.x < kViewBlockHeader && threadIdx.x != kViewPackCount)
         packed[threadIdx.x] = block[threadIdx.x];
     const float* body = block + kViewBlockHeader;
-    const uint32_t g = blockIdx.x * kPackThreads + threadIdx.x;
-    const bool live = g < P && view_entry_live(body, P, g);
+    const uint32_t g = g0 + blockIdx.x * kPackThreads + threadIdx.x;
+    const bool live = g < g1 && view_entry_live(body, P, g);
     uint32_t total = 0;
     const uint32_t pos = wg_off[blockIdx.x] + block_live_rank(live, s_w, &total);
     if (live && pos < cap) {
@@ -1374,13 +1414,19 @@ __global__ void __launch_bounds__(kPackThreads) view_pack_scatter_kernel(uint32_
     }
 }
 
-hipError_t launch_view_pack(uint32_t P, const float* block, float* packed, unsigned long long cap, uint32_t* scratch,
-                            uint32_t* count, hipStream_t stream) {
-    const uint32_t nb = (P + kPackThreads - 1) / kPackThreads;
-    hipLaunchKernelGGL(view_pack_count_kernel, dim3(nb), dim3(kPackThreads), 0, stream, P, block, scratch);
+hipError_t launch_view_pack(uint32_t P, uint32_t g0, uint32_t g1, const float* block, float* packed,
+                            unsigned long long cap, uint32_t* scratch, uint32_t* count, hipStream_t stream) {
+    const uint32_t nb = (g1 - g0 + kPackThreads - 1) / kPackThreads;
+    if (nb == 0) {  // an empty range: a header with no entries
+        hipLaunchKernelGGL(view_pack_scan_kernel, dim3(1), dim3(1024), 0, stream, 0u, scratch, packed, count);
+        hipLaunchKernelGGL(view_pack_scatter_kernel, dim3(1), dim3(kPackThreads), 0, stream, P, g0, g0, block, scratch,
+                           packed, cap);
+        return hipGetLastError();
+    }
+    hipLaunchKernelGGL(view_pack_count_kernel, dim3(nb), dim3(kPackThreads), 0, stream, P, g0, g1, block, scratch);
     hipLaunchKernelGGL(view_pack_scan_kernel, dim3(1), dim3(1024), 0, stream, nb, scratch, packed, count);
-    hipLaunchKernelGGL(view_pack_scatter_kernel, dim3(nb), dim3(kPackThreads), 0, stream, P, block, scratch, packed,
-                       cap);
+    hipLaunchKernelGGL(view_pack_scatter_kernel, dim3(nb), dim3(kPackThreads), 0, stream, P, g0, g1, block, scratch,
+                       packed, cap);
     return hipGetLastError();
 }
 
@@ -1453,17 +1499,19 @@ __global__ void __launch_bounds__(kPackThreads) view_index_kernel(uint32_t P, co
     }
 }
 
-__global__ void __launch_bounds__(kPackThreads) flags_zero_kernel(uint32_t P, uint32_t* __restrict__ flags) {
+__global__ void __launch_bounds__(kPackThreads) flags_zero_kernel(uint32_t P, uint32_t g0, uint32_t g1,
+                                                                  uint32_t* __restrict__ flags) {
     uint32_t* f = flags + (size_t)blockIdx.y * P;
-    for (uint32_t g = blockIdx.x * kPackThreads + threadIdx.x; g < P; g += gridDim.x * kPackThreads) f[g] = 0u;
+    for (uint32_t g = g0 + blockIdx.x * kPackThreads + threadIdx.x; g < g1; g += gridDim.x * kPackThreads) f[g] = 0u;
 }
 
-hipError_t launch_view_index(uint32_t P, int n_views, const float* packed, unsigned long long packed_floats,
-                             uint32_t* flags, unsigned long long cap, hipStream_t stream) {
+hipError_t launch_view_index(uint32_t P, uint32_t g0, uint32_t g1, int n_views, const float* packed,
+                             unsigned long long packed_floats, uint32_t* flags, unsigned long long cap,
+                             hipStream_t stream) {
     if (n_views <= 0) return hipSuccess;
-    const uint32_t gz = (P + kPackThreads - 1) / kPackThreads;
+    const uint32_t gz = (g1 - g0 + kPackThreads - 1) / kPackThreads;
     hipLaunchKernelGGL(flags_zero_kernel, dim3(gz < 1024 ? (gz ? gz : 1) : 1024, n_views), dim3(kPackThreads), 0,
-                       stream, P, flags);
+                       stream, P, g0, g1, flags);
     const uint32_t gx = (uint32_t)((cap + kPackThreads - 1) / kPackThreads);
     hipLaunchKernelGGL(view_index_kernel, dim3(gx < 1024 ? (gx ? gx : 1) : 1024, n_views), dim3(kPackThreads), 0,
                        stream, P, packed, packed_floats, flags, cap);
@@ -1472,12 +1520,13 @@ hipError_t launch_view_index(uint32_t P, int n_views, const float* packed, unsig
 
 // The Gaussians some view flags (visible with a gradient in a packed block), appended to the
 // sharded live list (one atomic per wave, kLiveShards counters the caller zeroed).
-__global__ void __launch_bounds__(64) views_live_kernel(uint32_t P, int n_views, const uint32_t* __restrict__ flags,
+__global__ void __launch_bounds__(64) views_live_kernel(uint32_t P, uint32_t g0, uint32_t g1, int n_views,
+                                                        const uint32_t* __restrict__ flags,
                                                         uint32_t* __restrict__ live, uint32_t* __restrict__ live_count,
                                                         uint32_t live_cap) {
-    const uint32_t g = blockIdx.x * 64 + threadIdx.x;
+    const uint32_t g = g0 + blockIdx.x * 64 + threadIdx.x;
     bool lv = false;
-    if (g < P)
+    if (g < g1)
         for (int v = 0; v < n_views; v++) lv |= (flags[(size_t)v * P + g] & 1u) != 0;
     const unsigned long long m = __ballot(lv);
     if (!m) return;
@@ -1488,12 +1537,13 @@ __global__ void __launch_bounds__(64) views_live_kernel(uint32_t P, int n_views,
     if (lv) live[(size_t)shard * live_cap + base + (uint32_t)__popcll(m & ((1ull << threadIdx.x) - 1ull))] = g;
 }
 
-hipError_t launch_views_live(uint32_t P, int n_views, const uint32_t* flags, uint32_t* live, uint32_t* live_count,
-                             hipStream_t stream) {
+hipError_t launch_views_live(uint32_t P, uint32_t g0, uint32_t g1, int n_views, const uint32_t* flags, uint32_t* live,
+                             uint32_t* live_count, hipStream_t stream) {
     const hipError_t e = hipMemsetAsync(live_count, 0, sizeof(uint32_t) * kLiveShards * kLiveCntStride, stream);
-    if (e != hipSuccess || P == 0) return e;
-    hipLaunchKernelGGL(views_live_kernel, dim3((P + 63) / 64), dim3(64), 0, stream, P, n_views, flags, live,
-                       live_count, live_list_cap(P));
+    if (e != hipSuccess || g1 <= g0) return e;
+    // (a range's blocks are at most P's, so live_list_cap(P) bounds every shard)
+    hipLaunchKernelGGL(views_live_kernel, dim3((g1 - g0 + 63) / 64), dim3(64), 0, stream, P, g0, g1, n_views, flags,
+                       live, live_count, live_list_cap(P));
     return hipGetLastError();
 }
 

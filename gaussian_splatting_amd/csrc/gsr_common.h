@@ -126,7 +126,16 @@ struct GeomState {
     uint32_t* redo_flag;        // [tiles]
     uint32_t* redo_list;        // [tiles]
     uint32_t* redo_cnt;         // [1]
+    // Atomic backward ("bwd_atomic" option, gsr_common.h "Per-Gaussian accumulators"): the render
+    // backward adds each (tile, Gaussian) instance's ten reduced sums straight into the Gaussian's row
+    // and sets its bit in `touched`.  Both are zeroed by the forward (fill blocks in render_fwd's launch)
+    // and restored to zero by the backward that consumed them (gauss_live: the bits; gauss_bwd: the
+    // rows), so any number of backwards of one forward start from zero.
+    float4* acc;                // [P][kAccRow4]: (dcolour, dinvdepth), (dmean2D, dopacity, dconic.b), (dconic.a, .c, 0, 0), pad
+    uint32_t* touched;          // [touched_words(P)] bit g: Gaussian g has a gradient term
 };
+constexpr int kAccRow4 = 4;     // float4 per accumulator row: 64 bytes, one line (one memory-side atomic request)
+__host__ __device__ inline size_t touched_words(size_t P) { return (P + 31) / 32; }
 
 // Image state: per pixel and per tile.  The per-pixel planes are tile-major: pixel (x, y) of
 // tile t, in 8x8 quadrant q at lane l = (y & 7) * 8 + (x & 7), is element t * 256 + q * 64 + l

@@ -29,6 +29,16 @@ struct PreprocessArgs {
     uint32_t zero_n;
 };
 
+// Zero-fill of up to kFillSegs float ranges (the backward's dense outputs), zeroed beside render_bwd
+// (VALU-bound, it leaves HBM bandwidth idle): "zero_fill" option, api.hip; and the atomic backward's
+// accumulators, zeroed beside render_fwd.
+constexpr int kFillSegs = 12;
+struct FillArgs {
+    float* ptr[kFillSegs];
+    unsigned long long n[kFillSegs];  // floats
+    int count;
+};
+
 struct RenderFwdArgs {
     int W, H;
     uint32_t gx, gy;
@@ -56,15 +66,10 @@ struct RenderFwdArgs {
     uint32_t* redo_flag;
     uint32_t* redo_list;
     uint32_t* redo_cnt;
-};
-
-// Zero-fill of up to kFillSegs float ranges (the backward's dense outputs), zeroed beside render_bwd
-// (VALU-bound, it leaves HBM bandwidth idle): "zero_fill" option, api.hip.
-constexpr int kFillSegs = 12;
-struct FillArgs {
-    float* ptr[kFillSegs];
-    unsigned long long n[kFillSegs];  // floats
-    int count;
+    // the first fill_blocks blocks of the launch zero `fill` (the atomic backward's accumulators,
+    // GeomState::acc / touched) beside the VALU-bound render waves, which leave HBM mostly idle
+    uint32_t fill_blocks;
+    FillArgs fill;
 };
 
 struct RenderBwdArgs {
@@ -94,6 +99,10 @@ struct RenderBwdArgs {
     // events -- each event left the GPU idle for 6-7 us (r4a trace)
     uint32_t fill_blocks;
     FillArgs fill;
+    // atomic backward ("bwd_atomic"): the per-Gaussian accumulator rows and touched bits (GeomState),
+    // or null for the per-instance gradient records + gauss_reduce
+    float* acc;
+    uint32_t* touched;
 };
 
 struct GaussBwdArgs {
@@ -113,7 +122,11 @@ struct GaussBwdArgs {
     int antialiasing;
     const int* radii;
     GeomState geom;
-    GradRecs sums;  // per Gaussian: summed render gradients (gauss_reduce_kernel)
+    GradRecs sums;  // per Gaussian: summed render gradients (gauss_reduce_kernel, or the atomic rows)
+    // element strides of sums.a / .b (float4 units) and sums.c (float2 units): 1 / 1 for gauss_reduce's
+    // arrays, kAccRow4 / 2 kAccRow4 for the atomic backward's rows (GeomState::acc)
+    int sum_stride4, sum_stride2;
+    float4* acc_restore;  // atomic backward: zero each listed Gaussian's row after reading it, or null
     int have_invdepth;
     float* dL_dmean2D;    // [P,3]
     float* dL_dconic;     // [P,4] or null
@@ -521,6 +534,8 @@ hipError_t launch_ssim_bwd(int planes, int H, int W, const float* img1, const fl
 hipError_t launch_gauss_reduce(int P, const GeomState& g, const GradRecs& recs, const GradRecs& sums,
                                uint32_t* flags, const int* radii, uint32_t* live, uint32_t* live_count,
                                hipStream_t stream);
+// atomic backward: the live list from the touched bits (which it re-zeroes), instead of gauss_reduce
+hipError_t launch_gauss_live(int P, uint32_t* touched, uint32_t* live, uint32_t* live_count, hipStream_t stream);
 // multi-view backward over gathered view blocks (backward.hip section 4)
 struct ViewsBwdArgs {
     int P, D, M;
@@ -551,12 +566,14 @@ struct ViewsBwdArgs {
     float* dL_drot;
 };
 hipError_t launch_gauss_bwd_views(const ViewsBwdArgs& a, hipStream_t stream);
-hipError_t launch_view_pack(uint32_t P, const float* block, float* packed, unsigned long long cap, uint32_t* scratch,
-                            uint32_t* count, hipStream_t stream);
-hipError_t launch_views_live(uint32_t P, int n_views, const uint32_t* flags, uint32_t* live, uint32_t* live_count,
+// (g0, g1): the Gaussian range of one chunk of a chunked exchange; (0, P) for the whole block
+hipError_t launch_view_pack(uint32_t P, uint32_t g0, uint32_t g1, const float* block, float* packed,
+                            unsigned long long cap, uint32_t* scratch, uint32_t* count, hipStream_t stream);
+hipError_t launch_views_live(uint32_t P, uint32_t g0, uint32_t g1, int n_views, const uint32_t* flags, uint32_t* live,
+                             uint32_t* live_count, hipStream_t stream);
+hipError_t launch_view_index(uint32_t P, uint32_t g0, uint32_t g1, int n_views, const float* packed,
+                             unsigned long long packed_floats, uint32_t* flags, unsigned long long cap,
                              hipStream_t stream);
-hipError_t launch_view_index(uint32_t P, int n_views, const float* packed, unsigned long long packed_floats,
-                             uint32_t* flags, unsigned long long cap, hipStream_t stream);
 hipError_t launch_view_unpack(uint32_t P, int n_views, const float* packed, unsigned long long packed_floats,
                               float* blocks, unsigned long long cap, hipStream_t stream);
 hipError_t launch_view_header(float* blk, const float* view, const float* proj, const float* campos, float tan_fovx,

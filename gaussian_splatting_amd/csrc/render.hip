@@ -503,12 +503,27 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const ui
   }
 }
 
+// The forward launch's first fill_blocks blocks zero RenderFwdArgs::fill (the atomic backward's
+// accumulator rows and touched bits) beside the render waves and exit; the render blocks count from
+// there (fill_blocks is a multiple of 8, so a tile's blocks keep their XCD).
+__device__ __forceinline__ bool fwd_fill_block(const RenderFwdArgs& a, uint32_t& bid) {
+    if (blockIdx.x < a.fill_blocks) {  // uniform
+        zero_fill_part(a.fill, (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x,
+                       (unsigned long long)a.fill_blocks * blockDim.x);
+        return true;
+    }
+    bid = blockIdx.x - a.fill_blocks;
+    return false;
+}
+
 template <int NQ, bool CENSUS>
 __global__ void __launch_bounds__(64) GSR_FWD_OCCUPANCY render_fwd_kernel(RenderFwdArgs a) {
     constexpr int NPART = 4 / NQ;
-    const uint32_t tile = (blockIdx.x / (8 * NPART)) * 8 + blockIdx.x % 8;
-    const int part = NPART == 1 ? 0 : (int)((blockIdx.x / 8) % NPART);
-    if (blockIdx.x == 0 && threadIdx.x == 0) *a.seg_ck_out = (uint32_t)a.seg_ck;  // for the backward
+    uint32_t bid = 0;
+    if (fwd_fill_block(a, bid)) return;
+    const uint32_t tile = (bid / (8 * NPART)) * 8 + bid % 8;
+    const int part = NPART == 1 ? 0 : (int)((bid / 8) % NPART);
+    if (bid == 0 && threadIdx.x == 0) *a.seg_ck_out = (uint32_t)a.seg_ck;  // for the backward
     if (tile >= a.gx * a.gy) return;
     render_fwd_tile<NQ, CENSUS>(a, tile, part);
 }
@@ -522,14 +537,16 @@ __global__ void __launch_bounds__(64) GSR_FWD_OCCUPANCY render_fwd_kernel(Render
 #define GSR_FWD_TAIL_QUADS 10
 #endif
 __global__ void __launch_bounds__(64) GSR_FWD_OCCUPANCY render_fwd_hybrid_kernel(RenderFwdArgs a) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) *a.seg_ck_out = (uint32_t)a.seg_ck;  // for the backward
+    uint32_t bid = 0;
+    if (fwd_fill_block(a, bid)) return;
+    if (bid == 0 && threadIdx.x == 0) *a.seg_ck_out = (uint32_t)a.seg_ck;  // for the backward
     const uint32_t half_tiles = a.half_tiles;
     const uint32_t hb = 2 * half_tiles;  // blocks of the half-tile region (half_tiles: a multiple of 8)
-    if (blockIdx.x < hb) {
-        const uint32_t tile = (blockIdx.x / 16) * 8 + blockIdx.x % 8;
-        render_fwd_tile<2, false>(a, tile, (int)((blockIdx.x / 8) % 2));
+    if (bid < hb) {
+        const uint32_t tile = (bid / 16) * 8 + bid % 8;
+        render_fwd_tile<2, false>(a, tile, (int)((bid / 8) % 2));
     } else {
-        const uint32_t b = blockIdx.x - hb;
+        const uint32_t b = bid - hb;
         const uint32_t tile = half_tiles + (b / 32) * 8 + b % 8;
         if (tile >= a.gx * a.gy) return;
         render_fwd_tile<1, false>(a, tile, (int)((b / 8) % 4));
@@ -545,9 +562,11 @@ __global__ void __launch_bounds__(64) GSR_FWD_OCCUPANCY render_fwd_hybrid_kernel
 template <bool CENSUS>
 __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(GSR_FWD_SHARED_WAVES, GSR_FWD_SHARED_WAVES)))
 GSR_FWD_SGPR_ATTR render_fwd_shared_kernel(RenderFwdArgs a) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) *a.seg_ck_out = (uint32_t)a.seg_ck;  // for the backward
-    if (blockIdx.x >= a.gx * a.gy) return;  // (uniform over the workgroup)
-    render_fwd_tile<2, CENSUS, true>(a, blockIdx.x, (int)(threadIdx.x >> 6));
+    uint32_t bid = 0;
+    if (fwd_fill_block(a, bid)) return;
+    if (bid == 0 && threadIdx.x == 0) *a.seg_ck_out = (uint32_t)a.seg_ck;  // for the backward
+    if (bid >= a.gx * a.gy) return;  // (uniform over the workgroup)
+    render_fwd_tile<2, CENSUS, true>(a, bid, (int)(threadIdx.x >> 6));
 }
 
 // The redo of the tiles render_fwd_kernel filed (their whole lists sorted since, by
@@ -605,6 +624,7 @@ hipError_t launch_render_fwd(const RenderFwdArgs& a, hipStream_t stream, int qua
             cu_count[dev].store(cus, std::memory_order_relaxed);
         }
     }
+    const uint32_t fb = a.fill_blocks;  // (fill blocks first: a multiple of 8)
     if (GSR_FWD_TAIL_QUADS && quads == 2 && !a.census && tiles >= 16 && tiles <= 64 * cus) {
         // the last tiles (whole groups of 8) as quadrant units: GSR_FWD_TAIL_QUADS percent of them, at most
         // ~0.4 groups per CU.  Measured (profiles/r04/r4k, r4l): 1M@1080p render_fwd 194 -> 188 us, 500k@1080p
@@ -614,23 +634,32 @@ hipError_t launch_render_fwd(const RenderFwdArgs& a, hipStream_t stream, int qua
         const uint32_t hgroups = groups - qgroups;
         RenderFwdArgs h = a;
         h.half_tiles = hgroups * 8;
-        hipLaunchKernelGGL(render_fwd_hybrid_kernel, dim3(hgroups * 16 + qgroups * 32), dim3(kWave), 0, stream, h);
+        hipLaunchKernelGGL(render_fwd_hybrid_kernel, dim3(fb + hgroups * 16 + qgroups * 32), dim3(kWave), 0, stream, h);
     } else if (GSR_FWD_SHARED && quads == 2) {
         if (a.census)
-            hipLaunchKernelGGL((render_fwd_shared_kernel<true>), dim3(tiles), dim3(2 * kWave), 0, stream, a);
+            hipLaunchKernelGGL((render_fwd_shared_kernel<true>), dim3(fb + tiles), dim3(2 * kWave), 0, stream, a);
         else
-            hipLaunchKernelGGL((render_fwd_shared_kernel<false>), dim3(tiles), dim3(2 * kWave), 0, stream, a);
+            hipLaunchKernelGGL((render_fwd_shared_kernel<false>), dim3(fb + tiles), dim3(2 * kWave), 0, stream, a);
     } else if (a.census)
-        hipLaunchKernelGGL((render_fwd_kernel<2, true>), dim3(groups * 16), dim3(kWave), 0, stream, a);
+        hipLaunchKernelGGL((render_fwd_kernel<2, true>), dim3(fb + groups * 16), dim3(kWave), 0, stream, a);
     else if (quads == 4)
-        hipLaunchKernelGGL((render_fwd_kernel<4, false>), dim3(groups * 8), dim3(kWave), 0, stream, a);
+        hipLaunchKernelGGL((render_fwd_kernel<4, false>), dim3(fb + groups * 8), dim3(kWave), 0, stream, a);
     else
-        hipLaunchKernelGGL((render_fwd_kernel<2, false>), dim3(groups * 16), dim3(kWave), 0, stream, a);
+        hipLaunchKernelGGL((render_fwd_kernel<2, false>), dim3(fb + groups * 16), dim3(kWave), 0, stream, a);
     return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
-template <bool CENSUS, bool STRIDED>
+// ATOMIC ("bwd_atomic" option): each entry's ten reduced sums are added straight into its Gaussian's
+// accumulator row (GeomState::acc, 64 B) with float atomics and the Gaussian's touched bit is set,
+// instead of a 48-byte record at the instance's emission index for gauss_reduce to sum: no record
+// writes, no record-start gathers, no gauss_reduce.  The flush compacts the batch's written entries
+// into an LDS list and issues one wave instruction per FOUR entries -- lane 16k + v adds value v
+// (< 10) of listed entry k -- so an instruction touches four 64-byte rows, the shape the memory-side
+// atomic units take at full rate (MI355X_MICROARCH.md "Global float atomics": 64 lanes in 64 rows
+// run ~17x slower).  The summation order over a Gaussian's instances then follows the hardware, so
+// the result is not bitwise reproducible; the record path (the default) is.
+template <bool CENSUS, bool STRIDED, bool ATOMIC>
 __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(RenderBwdArgs a) {
   {
     // One wave per unit = (tile, segment): the entries [start, end) of the tile's list, start a
@@ -682,6 +711,7 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
     // staged rows, so a reduction's store address is the entry's row offset (already scalar for the
     // row reads) plus a per-lane constant (an [entry][3] layout cost a quarter-rate v_mad_u64_u32)
     __shared__ float4 s_acc[3][kBatch];
+    __shared__ uint32_t s_wgid[ATOMIC ? kBatch : 1], s_wj[ATOMIC ? kBatch : 1];  // ATOMIC: written entries' Gaussian, slot
     GSR_STAMP(g_st_rbwd, blockIdx.x, 0);
     GSR_STAMP_HWID(g_st_rbwd, blockIdx.x);
     GSR_STAMP_RT(g_st_rbwd, blockIdx.x, 4);
@@ -784,10 +814,15 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
             // Gaussian << 4 | quadrant mask (GSR_PF_ENTRY: loaded during the previous batch)
             const uint32_t ent = GSR_PF_ENTRY ? ent_next : a.gid_sorted[range.x + b0 + lane];
             const float4* rec = a.rec + (size_t)kRecRows * (ent >> kEntryMaskBits);
-            const float4 v0 = rec[0], v1 = rec[1], v2 = rec[2], v3 = rec[3];
-            // this instance's emission index (row 3: tile rectangle [and first emission])
-            const uint32_t first = GSR_REC_START_GATHER ? a.rec_start[ent >> kEntryMaskBits] : __float_as_uint(v3.w);
-            e = first + (tty - __float_as_uint(v3.y)) * __float_as_uint(v3.z) + (ttx - __float_as_uint(v3.x));
+            const float4 v0 = rec[0], v1 = rec[1], v2 = rec[2];
+            if (ATOMIC) {
+                e = ent >> kEntryMaskBits;  // (the Gaussian: its accumulator row)
+            } else {
+                const float4 v3 = rec[3];
+                // this instance's emission index (row 3: tile rectangle [and first emission])
+                const uint32_t first = GSR_REC_START_GATHER ? a.rec_start[ent >> kEntryMaskBits] : __float_as_uint(v3.w);
+                e = first + (tty - __float_as_uint(v3.y)) * __float_as_uint(v3.z) + (ttx - __float_as_uint(v3.x));
+            }
             s_xy[lane] = make_float4(v0.x, v0.y, v1.y, v1.z);
             s_col[lane] = v2;
             ca = v0.z;
@@ -879,7 +914,33 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
         }
         unit_sync();
         const bool content = (written >> lane) & 1ull;
-        if (has && content && !(GSR_ATTR & 1)) {
+        if (ATOMIC) {
+            // this entry's sums in their final form, over its own LDS slots, and its place in the list
+            if (has && content) {
+                const float4 A = s_acc[0][lane], B = s_acc[1][lane], Cc = s_acc[2][lane];
+                const float s8 = Cc.x + Cc.y, s9 = Cc.z + Cc.w;
+                s_acc[1][lane] = make_float4(-0.5f * (float)a.W * o * (ca * B.x + cb * B.y),
+                                             -0.5f * (float)a.H * o * (cc * B.y + cb * B.x), s9, -0.5f * o * B.w);
+                s_acc[2][lane] = make_float4(-0.5f * o * B.z, -0.5f * o * s8, 0.f, 0.f);
+                (void)A;  // (row a is stored as reduced)
+                const int slot = __popcll(written & ((1ull << lane) - 1ull));
+                s_wgid[slot] = e;
+                s_wj[slot] = (uint32_t)lane;
+                // the Gaussian has a gradient (gauss_live lists it); OR is order-free
+                (void)atomicOr(a.touched + (e >> 5), 1u << (e & 31u));
+            }
+            unit_sync();
+            // one wave instruction per four listed entries: lane 16 k + v adds value v of entry k
+            const int nw = __popcll(written), sub = lane >> 4, v = lane & 15;
+            for (int k0 = 0; k0 < nw; k0 += 4) {  // uniform
+                const int k = k0 + sub;
+                if (k < nw && v < 10) {
+                    const int j = (int)s_wj[k];
+                    const float val = reinterpret_cast<const float*>(s_acc)[(v >> 2) * (4 * kBatch) + j * 4 + (v & 3)];
+                    (void)atomicAdd(a.acc + (size_t)s_wgid[k] * (4 * kAccRow4) + v, val);  // (no return: fire and forget)
+                }
+            }
+        } else if (has && content && !(GSR_ATTR & 1)) {
 #if GSR_FLAG_BITS  // (the bits were zeroed by the forward's K3, binning.hip; OR is order-free: deterministic)
             (void)atomicOr(reinterpret_cast<uint32_t*>(a.recs.flag) + (e >> 5), 1u << (e & 31u));
 #else
@@ -931,6 +992,16 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
 // own seg_ck is on the device only; surplus blocks exit at the unit lookup)
 size_t bwd_max_units(size_t R, uint32_t tiles, int seg_ck) { return R / ((size_t)seg_ck * kCkStride) + tiles; }
 
+template <bool ATOMIC>
+static void launch_render_bwd_t(const RenderBwdArgs& a, uint32_t grid, bool strided, hipStream_t stream) {
+    if (a.census)
+        hipLaunchKernelGGL((render_bwd_kernel<true, false, ATOMIC>), dim3(grid), dim3(kWave), 0, stream, a);
+    else if (strided)
+        hipLaunchKernelGGL((render_bwd_kernel<false, true, ATOMIC>), dim3(grid), dim3(kWave), 0, stream, a);
+    else
+        hipLaunchKernelGGL((render_bwd_kernel<false, false, ATOMIC>), dim3(grid), dim3(kWave), 0, stream, a);
+}
+
 // The strided grid: kBwdGridTiles unit blocks per tile, used when the worst-case grid (max_units) is
 // more than kBwdStrideRatio times that.
 constexpr uint32_t kBwdGridTiles = 2, kBwdStrideRatio = 4;
@@ -939,12 +1010,10 @@ hipError_t launch_render_bwd(const RenderBwdArgs& a, size_t max_units, hipStream
     const size_t strided_units = std::min(max_units, (size_t)kBwdGridTiles * a.gx * a.gy);
     const bool strided = !a.census && (grid_mode == 2 || (grid_mode == 0 && max_units > kBwdStrideRatio * strided_units));
     const uint32_t grid = (uint32_t)(strided ? strided_units : max_units) + a.fill_blocks;  // fill blocks first
-    if (a.census)
-        hipLaunchKernelGGL((render_bwd_kernel<true, false>), dim3(grid), dim3(kWave), 0, stream, a);
-    else if (strided)
-        hipLaunchKernelGGL((render_bwd_kernel<false, true>), dim3(grid), dim3(kWave), 0, stream, a);
+    if (a.acc)
+        launch_render_bwd_t<true>(a, grid, strided, stream);
     else
-        hipLaunchKernelGGL((render_bwd_kernel<false, false>), dim3(grid), dim3(kWave), 0, stream, a);
+        launch_render_bwd_t<false>(a, grid, strided, stream);
     return hipGetLastError();
 }
 

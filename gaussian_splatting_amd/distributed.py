@@ -148,10 +148,15 @@ class ViewExchange:
     CAP_MARGIN = 1.05
     CAP_DECAY = 0.98
 
-    def __init__(self, P: int, device, group: Optional[dist.ProcessGroup] = None, sparse: bool = True):
+    def __init__(self, P: int, device, group: Optional[dist.ProcessGroup] = None, sparse: bool = True,
+                 chunks: int = 1):
         from . import _C
 
         self.P, self.group, self.sparse, self.device = P, group, sparse and P > 0, torch.device(device)
+        # chunks > 1 (sparse only): the Gaussians in `chunks` index ranges, each packed and gathered on its
+        # own (async all-gathers, all queued at once on the collective stream), so chunk k+1's all-gather
+        # runs while the multi-view backward works on chunk k ("Chunked exchange")
+        self.chunks = max(1, int(chunks)) if self.sparse else 1
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.block_floats = _C.view_block_floats(P) if P > 0 else 0
@@ -174,6 +179,20 @@ class ViewExchange:
             self._count_ev = torch.cuda.Event()
             self._flags = torch.empty(self.world, P, dtype=torch.int32, device=device)  # view_block_index
             self._live = torch.empty(_C.views_live_floats(P), dtype=torch.int32, device=device)
+        if self.chunks > 1:
+            K = self.chunks
+            self.bounds = [P * k // K for k in range(K + 1)]
+            sizes = [self.bounds[k + 1] - self.bounds[k] for k in range(K)]
+            self._cpacked = [torch.empty(_C.view_pack_floats(n), dtype=torch.float32, device=device) for n in sizes]
+            self._crecv = [torch.empty(self.world * _C.view_pack_floats(n), dtype=torch.float32, device=device)
+                           for n in sizes]
+            self._ccount = torch.zeros(K, dtype=torch.int32, device=device)
+            self._ccount64 = torch.zeros(K, dtype=torch.int64, device=device)
+            self._ccount_host = torch.zeros(K, dtype=torch.int64, pin_memory=True)
+            self._ccap_last = [0] * K
+            self._cworks = None   # the chunks' async all-gathers, waited for one at a time
+            self._chint = None    # entries gathered per chunk
+            self._crecv_views = [None] * K
         self._view_blocks, self._view_flags, self._view_live = None, None, None  # views_backward reads
         self._side = None      # the stream zeroing the outputs during the exchange
         self._zeroed = None    # the flat output buffer it zeroes
@@ -198,6 +217,88 @@ class ViewExchange:
 
     def _note_count(self, n: int) -> None:
         self._cap_last = max(int(n), int(self._cap_last * self.CAP_DECAY))
+
+    def chunk_hint(self, k: int) -> int:
+        """Entries the next chunked exchange gathers per rank for chunk k (0: none yet)."""
+        if self._ccap_last[k] <= 0:
+            return 0
+        n = self.bounds[k + 1] - self.bounds[k]
+        return min(n, int(self._ccap_last[k] * self.CAP_MARGIN) + 256)
+
+    def _exchange_chunked(self) -> None:
+        """Chunked sparse exchange: pack every chunk, one MAX all-reduce of the K counts, then the K
+        all-gathers queued at once (async); views_backward waits for chunk k's gather just before its
+        part of the multi-view backward, so the later gathers overlap the earlier chunks' backward."""
+        from . import _C
+
+        K = self.chunks
+        for k in range(K):
+            _C.view_block_pack(self._local, self._cpacked[k], self._scratch, self._ccount[k:k + 1], self.P,
+                               rng=(self.bounds[k], self.bounds[k + 1]))
+        self._ccount64.copy_(self._ccount)
+        if self.world > 1:
+            if dist.get_backend(self.group) == "nccl":
+                dist.all_reduce(self._ccount64, op=dist.ReduceOp.MAX, group=self.group)
+                self._ccount_host.copy_(self._ccount64, non_blocking=True)
+            else:  # gloo (CPU rehearsals): the collective needs a host tensor
+                host = self._ccount64.cpu()
+                dist.all_reduce(host, op=dist.ReduceOp.MAX, group=self.group)
+                self._ccount_host.copy_(host)
+        else:
+            self._ccount_host.copy_(self._ccount64, non_blocking=True)
+        self._count_ev.record()
+        hints = [self.chunk_hint(k) for k in range(K)]
+        if min(hints) == 0:  # no history: wait for this step's counts
+            self._count_ev.synchronize()
+            hints = [min(int(self._ccount_host[k]), self.bounds[k + 1] - self.bounds[k]) for k in range(K)]
+        self._chint = hints
+        self._cworks = [self._gather_chunk(k, hints[k], async_op=True) for k in range(K)]
+        self.last_entries = sum(hints)
+        self._pending = (hints, True)
+
+    def _gather_chunk(self, k: int, n: int, async_op: bool):
+        from . import _C
+
+        size = _C.view_pack_floats(n)
+        recv = self._crecv[k][: self.world * size].view(self.world, size)
+        self._crecv_views[k] = recv
+        if self.world > 1:
+            return dist.all_gather_into_tensor(recv.view(-1), self._cpacked[k][:size], group=self.group,
+                                               async_op=async_op)
+        recv[0].copy_(self._cpacked[k][:size])
+        return None
+
+    def _chunk_backward(self, k: int, bwd_args) -> None:
+        """Index, list and run the multi-view backward over chunk k's gathered blocks (after its gather)."""
+        from . import _C
+
+        means3D, dc, sh, degree, opacities, scales, rotations, scale_modifier, out = bwd_args
+        rng = (self.bounds[k], self.bounds[k + 1])
+        recv = self._crecv_views[k]
+        _C.view_block_index(recv, self._flags, self.P, rng=rng)
+        live = None
+        if self._zeroed is not None:
+            _C.views_live_list(self._flags, self._live, self.P, rng=rng)
+            live = self._live
+        _C.gauss_backward_views(means3D, dc, sh, degree, opacities, scales, rotations, scale_modifier, recv, out,
+                                flags=self._flags, live=live)
+
+    def _finish_chunked(self) -> bool:
+        hints, _ = self._pending
+        self._pending = None
+        self._count_ev.synchronize()
+        redone = False
+        for k in range(self.chunks):
+            n = min(int(self._ccount_host[k]), self.bounds[k + 1] - self.bounds[k])
+            self._ccap_last[k] = max(n, int(self._ccap_last[k] * self.CAP_DECAY))
+            if n > hints[k]:  # this chunk's hint was too small: gather it again at its exact size, rerun its part
+                redone = True
+                self._gather_chunk(k, n, async_op=False)
+                if self._last_bwd is not None:
+                    self._chunk_backward(k, self._last_bwd)
+        if redone:
+            self.resyncs += 1
+        return redone
 
     def exchange(self, zero: Optional[torch.Tensor] = None) -> None:
         """Give every rank all N view blocks.
@@ -235,6 +336,9 @@ class ViewExchange:
             if self.world > 1:
                 dist.all_gather_into_tensor(self.gathered.view(-1), self.local_block(), group=self.group)
             self._view_blocks = self.gathered
+            return
+        if self.chunks > 1:
+            self._exchange_chunked()
             return
         _C.view_block_pack(self._local, self._packed, self._scratch, self._count, self.P)
         self._count64.copy_(self._count)
@@ -288,6 +392,8 @@ class ViewExchange:
         True if the exchange was redone.  Called by ``views_backward``; idempotent."""
         if self._pending is None:
             return False
+        if self.chunks > 1:
+            return self._finish_chunked()
         hint, _ = self._pending
         self._pending = None
         self._count_ev.synchronize()
@@ -314,6 +420,15 @@ class ViewExchange:
 
         if self._zeroed is not None:  # the outputs' zero fill (exchange(zero=...)) must be done
             torch.cuda.current_stream(self._zeroed.device).wait_stream(self._side)
+        if self.chunks > 1:
+            args = (means3D, dc, sh, degree, opacities, scales, rotations, scale_modifier, out)
+            for k in range(self.chunks):
+                w = self._cworks[k] if self._cworks is not None else None
+                if w is not None:
+                    w.wait()  # (RCCL: the compute stream waits for the gather, not the host)
+                self._chunk_backward(k, args)
+            self._cworks = None
+            return
         _C.gauss_backward_views(means3D, dc, sh, degree, opacities, scales, rotations, scale_modifier,
                                 self._view_blocks, out, flags=self._view_flags, live=self._view_live)
 
@@ -323,6 +438,8 @@ class ViewExchange:
 
         if not self.sparse:
             return (self.world - 1) * self.block_floats * 4
+        if self.chunks > 1:
+            return (self.world - 1) * sum(_C.view_pack_floats(n) for n in (self._chint or [0])) * 4
         if self.last_entries is None:  # the last exchange fell back to the dense blocks
             return (self.world - 1) * self.block_floats * 4
         return (self.world - 1) * _C.view_pack_floats(self.last_entries) * 4
@@ -335,6 +452,14 @@ class ViewExchange:
         r = self.rank if rank is None else rank
         if self.sparse and r == self.rank:
             return self._local[64 + 4 * self.P: 64 + 8 * self.P].view(self.P, 4)[:, :2]
+        if self.chunks > 1:  # packed chunks: scatter each chunk's entries of view r
+            g = torch.zeros(self.P, 2, dtype=torch.float32, device=self.device)
+            for k in range(self.chunks):
+                pk = self._crecv_views[k][r]
+                n = int(pk[63].view(torch.int32).item())
+                ent = pk[64: 64 + 12 * n].view(n, 12)
+                g[ent[:, 0].view(torch.int32).long()] = ent[:, 5:7]
+            return g
         if self._view_flags is None:  # dense blocks
             return self.gathered[r][64 + 4 * self.P: 64 + 8 * self.P].view(self.P, 4)[:, :2]
         pk = self._view_blocks[r]  # packed: scatter its entries' (b.x, b.y) -- entry layout, include/gsr.h

@@ -216,6 +216,12 @@ unsigned long long gsr_view_pack_floats(long long entries);
 unsigned long long gsr_view_pack_scratch_bytes(int P);
 int gsr_view_block_pack(int P, const float* view_block, float* packed, long long cap, void* scratch,
                         unsigned int* count, void* stream);
+/* Chunked exchange (distributed.py ViewExchange(chunks=K), no reference counterpart): the same over the
+ * Gaussians [g0, g1) only -- one chunk's packed block (entries keep their absolute index), so chunk k+1's
+ * all-gather can run while the multi-view backward works on chunk k.  gsr_view_block_pack(...) is
+ * gsr_view_block_pack_range(P, 0, P, ...). */
+int gsr_view_block_pack_range(int P, int g0, int g1, const float* view_block, float* packed, long long cap,
+                              void* scratch, unsigned int* count, void* stream);
 int gsr_view_block_unpack(int P, int n_views, const float* packed, long long packed_floats, float* blocks,
                           long long cap, void* stream);
 
@@ -228,6 +234,9 @@ int gsr_view_block_unpack(int P, int n_views, const float* packed, long long pac
  *   as over the unpacked blocks. */
 int gsr_view_block_index(int P, int n_views, const float* packed, long long packed_floats, unsigned int* flags,
                          long long cap, void* stream);
+/* Chunk form: clears and sets the flags of Gaussians [g0, g1) only (the packed blocks hold that chunk). */
+int gsr_view_block_index_range(int P, int g0, int g1, int n_views, const float* packed, long long packed_floats,
+                               unsigned int* flags, long long cap, void* stream);
 int gsr_gauss_backward_views_packed(int P, int D, int M, const float* means3D, const float* dc, const float* shs,
                                     const float* opacities, const float* scales, const float* rotations,
                                     float scale_modifier, int n_views, const float* packed, long long packed_floats,
@@ -242,6 +251,9 @@ int gsr_gauss_backward_views_packed(int P, int D, int M, const float* means3D, c
  *   outputs beforehand (ViewExchange does it on a second stream while the all-gather runs). */
 unsigned long long gsr_views_live_floats(int P);
 int gsr_views_live_list(int P, int n_views, const unsigned int* flags, unsigned int* live, void* stream);
+/* Chunk form: only Gaussians [g0, g1) are listed. */
+int gsr_views_live_list_range(int P, int g0, int g1, int n_views, const unsigned int* flags, unsigned int* live,
+                              void* stream);
 int gsr_gauss_backward_views_live(int P, int D, int M, const float* means3D, const float* dc, const float* shs,
                                   const float* opacities, const float* scales, const float* rotations,
                                   float scale_modifier, int n_views, const float* packed, long long packed_floats,
@@ -312,6 +324,12 @@ int gsr_host_stats(double* values, int n, int reset);
  *   "bwd_grid"   0|1|2  render_bwd's grid: 2 blocks per tile, each walking units i, i + G, ... when the
  *                        grid sized for the shortest segments would be over 4x that (5M@4K) | that worst-case
  *                        grid, one unit per block | always the strided grid
+ *   "bwd_atomic" 0|1    the render backward writes one gradient record per (tile, Gaussian) instance, summed
+ *                        per Gaussian by gauss_reduce in a fixed order: bitwise deterministic (default) | adds
+ *                        each instance's ten sums into per-Gaussian rows with float atomics (no records, no
+ *                        gauss_reduce; the order of the adds follows the hardware).  Read by the forward too,
+ *                        which zeroes the rows when it is 1: a forward and its backwards must see one value.
+ *                        The screen-space backward (view blocks) always takes the record path
  * Every option is read once per forward / backward call, so a concurrent gsr_option_set never splits
  * one call's launches between two values.
  * gsr_option_get returns -1 for an unknown name; gsr_option_set returns GSR_ERR_ARGUMENT for an

@@ -6,9 +6,11 @@ two exchanges run for real:
   * GradArena.all_reduce -- the backward writes the 59-float parameter gradients into the flat arena,
     one all-reduce sums them;
   * ViewExchange -- each rank writes its view block (gsr_rasterize_backward_screen), one all-gather of the
-    packed (sparse) blocks -- and of the dense ones -- and every rank runs gsr_gauss_backward_views over
-    both views; the sparse exchange again at its capacity hint (no wait for the count), and with a hint
-    forced below the count (the exchange is redone at the exact size).
+    packed (sparse) blocks -- and of the dense ones, and of the packed blocks in three Gaussian-range chunks
+    gathered asynchronously (chunks=3) -- and every rank runs gsr_gauss_backward_views over both views; the
+    sparse exchanges again at their capacity hints (no wait for the count), and with a hint forced below
+    the count (the exchange is redone at the exact size).  The chunked exchange equals the unchunked one
+    bit for bit.
 
 Both must equal the oracle's sum of the per-view gradients (unit-scale upstream gradient, the small-case
 bar max |diff| / max |ref| <= 2e-4), and the replicas must be bitwise identical after each exchange.
@@ -71,8 +73,10 @@ def _worker(rank, port, outdir):
         bwd = (d("bg"), d("means3D"), radii, torch.Tensor([]), d("opacities"), d("scales"), d("rotations"), 1.0,
                torch.Tensor([]), d("viewmatrix"), d("projmatrix"), inp["tanfovx"], inp["tanfovy"], gc.to(dev),
                gd.to(dev), d("shs"), inp["sh_degree"], d("campos"), geom, nr, binning, img, False, False)
-        for mode, sparse in (("views", True), ("dense", False)):  # sparse (default) and dense view blocks
-            ex = ViewExchange(CASE.P, dev, sparse=sparse)
+        # sparse (default) and dense view blocks, and the sparse blocks in 3 Gaussian-range chunks whose
+        # async all-gathers overlap the earlier chunks' multi-view backward
+        for mode, sparse, chunks in (("views", True, 1), ("dense", False, 1), ("chunked", True, 3)):
+            ex = ViewExchange(CASE.P, dev, sparse=sparse, chunks=chunks)
             _C.rasterize_gaussians_backward_screen(*bwd, view_block=ex.local_block())
             arena2 = GradArena(CASE.P, M, dev)
             arena2.flat.fill_(float("nan"))  # the sparse exchange's zero fill must cover every row
@@ -85,10 +89,12 @@ def _worker(rank, port, outdir):
                 # later steps gather at the capacity hint without waiting for the count; a hint below
                 # the count (forced here) is detected after the backward is queued and the exchange
                 # is redone at the exact size -- the same gradients bit for bit every time
-                assert ex.capacity_hint() > 0 and ex.resyncs == 0
+                assert (ex.capacity_hint() > 0 if chunks == 1 else min(ex.chunk_hint(k) for k in range(3)) > 0)
+                assert ex.resyncs == 0
                 for forced in (None, 8):
                     if forced is not None:
                         ex.capacity_hint = lambda: forced  # noqa: E731
+                        ex.chunk_hint = lambda k: forced  # noqa: E731
                     arena2.flat.fill_(float("nan"))
                     ex.exchange(zero=arena2.flat)
                     ex.views_backward(d("means3D"), None, d("shs"), inp["sh_degree"], d("opacities"), d("scales"),
@@ -96,7 +102,7 @@ def _worker(rank, port, outdir):
                     torch.cuda.synchronize()
                     assert torch.equal(arena2.flat, first), forced
                 assert ex.resyncs == 1, ex.resyncs
-                del ex.capacity_hint
+                del ex.capacity_hint, ex.chunk_hint
             np.save(os.path.join(outdir, f"{mode}{rank}.npy"), arena2.flat.cpu().numpy())
             m2d = np.stack([ex.means2D_grad(r).cpu().numpy() for r in range(WORLD)])  # densification input
             np.save(os.path.join(outdir, f"m2d_{mode}{rank}.npy"), m2d)
@@ -114,14 +120,18 @@ def test_two_ranks_on_gpu_equal_oracle_sum_of_views():
     with tempfile.TemporaryDirectory() as d:
         mp.start_processes(_worker, args=(_free_port(), d), nprocs=WORLD, join=True, start_method="spawn")
         got = {m: [np.load(os.path.join(d, f"{m}{r}.npy")) for r in range(WORLD)]
-               for m in ("allreduce", "views", "dense")}
-        m2d = {m: [np.load(os.path.join(d, f"m2d_{m}{r}.npy")) for r in range(WORLD)] for m in ("views", "dense")}
-    # every rank sees every view's dL/dmeans2D, the same through either exchange
+               for m in ("allreduce", "views", "dense", "chunked")}
+        m2d = {m: [np.load(os.path.join(d, f"m2d_{m}{r}.npy")) for r in range(WORLD)]
+               for m in ("views", "dense", "chunked")}
+    # every rank sees every view's dL/dmeans2D, the same through any exchange
     for r in range(WORLD):
         np.testing.assert_array_equal(m2d["views"][r], m2d["dense"][r])
+        np.testing.assert_array_equal(m2d["chunked"][r], m2d["dense"][r])
         np.testing.assert_array_equal(m2d["dense"][r], m2d["dense"][0])
-    # the sparse exchange gives the dense one's gradients
+    # the sparse exchange gives the dense one's gradients, and the chunked exchange the sparse one's, bit for bit
     np.testing.assert_array_equal(got["views"][0], got["dense"][0])
+    np.testing.assert_array_equal(got["chunked"][0], got["views"][0])
+    np.testing.assert_array_equal(got["chunked"][1], got["views"][1])
     for m, (a, b) in got.items():
         np.testing.assert_array_equal(a, b, err_msg=f"{m}: replicas differ")
     ref = GradArena(CASE.P, 16, "cpu")

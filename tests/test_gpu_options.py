@@ -10,7 +10,9 @@ synchronising and the capacity-hint forward:
   * colour / inverse depth within 1e-5; gradients within 1e-5 absolute with the L1 upstream
     gradient and 2e-4 of max |ref| with a unit one;
   * and against the default path itself: bitwise equal, except the backward of "bwd_seg_ck",
-    whose work units start from other blend checkpoints (the same sums in another rounding), and
+    whose work units start from other blend checkpoints (the same sums in another rounding), the
+    backward of "bwd_atomic", whose per-Gaussian sums are added in the hardware's order (and whose
+    second backward of one forward checks that the first restored its accumulators to zero), and
     "fwd_quads=4", a separate instantiation of the forward kernel in which the compiler contracts
     other multiply-adds into FMAs (the oracle bars above still hold it).
 """
@@ -38,6 +40,7 @@ VARIANTS = {
     "count_wait=1": dict(count_wait=1),       # the host polls an event behind the count (default 2: the slot)
     "bwd_grid=1": dict(bwd_grid=1),           # render_bwd: one block per possible unit
     "bwd_grid=2": dict(bwd_grid=2),           # render_bwd: two blocks per tile walking units i, i + G, ...
+    "bwd_atomic=1": dict(bwd_atomic=1),       # per-Gaussian float-atomic rows instead of records + gauss_reduce
 }
 CASES = ["sh3_scalerot", "antialiasing", "dense_opaque", "lists_1k_2k", "lists_4k_8k", "lists_over_8k"]
 
@@ -96,7 +99,7 @@ def test_option_path_matches_oracle(variant, case_name, hint):
         assert float((fwd[1] - base_fwd[1]).abs().max()) <= 1e-6
         return
     assert torch.equal(fwd[1], base_fwd[1]) and torch.equal(fwd[6], base_fwd[6])
-    if not variant.startswith("bwd_seg_ck"):
+    if not variant.startswith(("bwd_seg_ck", "bwd_atomic")):
         for out, base in zip(outs, base_outs):
             for a, b in zip(out, base):
                 assert torch.equal(a, b), variant
@@ -131,3 +134,28 @@ def test_seg_ck_set_around_forward_only(seg_ck, case_name):
         assert torch.equal(a, b)
     for k, got in zip(C.GRAD_NAMES, split_k):
         np.testing.assert_allclose(_np(got), r[k], atol=1e-5, rtol=0, err_msg=k)
+
+
+@pytest.mark.parametrize("case_name", ["sh3_scalerot", "lists_4k_8k"])
+def test_atomic_backward_repeats(case_name):
+    """bwd_atomic: the forward zeroes the accumulator rows and touched bits, and each backward restores
+    what it used to zero (gauss_live the bits, gauss_bwd the rows), so three backwards of one forward
+    agree to float rounding of the add order (a row left over would double a Gaussian's gradient);
+    and a record-path backward of a forward run with the option on equals the default path bitwise."""
+    from gaussian_splatting_amd import _lib
+
+    case = next(c for c in C.SMALL_CASES if c.name == case_name)
+    inp = C.build(case)
+    gc, gd = C.l1_grads(case.H, case.W)
+    with _lib.options(bwd_atomic=1):
+        fwd = C.run_gpu_forward(inp)
+        outs = [C.run_gpu_backward(inp, fwd, gc, gd) for _ in range(3)]
+    rec = C.run_gpu_backward(inp, fwd, gc, gd)  # the record path on the same buffers
+    base = C.run_gpu_backward(inp, C.run_gpu_forward(inp), gc, gd)
+    torch.cuda.synchronize()
+    for a, b in zip(rec, base):
+        assert torch.equal(a, b)
+    for o in outs:
+        for k, a, b in zip(C.GRAD_NAMES, o, base):
+            scale = float(b.abs().max()) or 1.0
+            assert float((a - b).abs().max()) <= 1e-5 * scale, (k, float((a - b).abs().max()), scale)

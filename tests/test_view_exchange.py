@@ -63,23 +63,27 @@ def _single_and_block(inp, case, dev, split):
     return dict(zip(names, out)), block, t
 
 
-def _views_backward(t, blocks, split, dev, flags=None, live=None):
+def _views_backward(t, blocks, split, dev, flags=None, live=None, out=None):
     from gaussian_splatting_amd import _C
 
     P = t["means3D"].shape[0]
     sh = t["shs"]
     M = sh.shape[1]
     new = torch.zeros if live is not None else torch.empty  # the live-list form leaves unlisted rows as they are
-    out = {"dL_dmeans3D": new(P, 3, device=dev), "dL_dopacity": new(P, 1, device=dev),
-           "dL_dscales": new(P, 3, device=dev), "dL_drotations": new(P, 4, device=dev)}
+    given = out is not None  # (the caller's outputs: chunk by chunk into one set)
+    if not given:
+        out = {"dL_dmeans3D": new(P, 3, device=dev), "dL_dopacity": new(P, 1, device=dev),
+               "dL_dscales": new(P, 3, device=dev), "dL_drotations": new(P, 4, device=dev)}
     if split:
         dc, rest = sh[:, :1].contiguous(), sh[:, 1:].contiguous()
-        out["dL_ddc"] = new(P, 1, 3, device=dev)
-        out["dL_dsh"] = new(P, M - 1, 3, device=dev)
+        if not given:
+            out["dL_ddc"] = new(P, 1, 3, device=dev)
+            out["dL_dsh"] = new(P, M - 1, 3, device=dev)
         _C.gauss_backward_views(t["means3D"], dc, rest, t["sh_degree"], t["opacities"], t["scales"], t["rotations"],
                                 t["scale_modifier"], blocks, out, flags=flags, live=live)
     else:
-        out["dL_dsh"] = new(P, M, 3, device=dev)
+        if not given:
+            out["dL_dsh"] = new(P, M, 3, device=dev)
         _C.gauss_backward_views(t["means3D"], None, sh, t["sh_degree"], t["opacities"], t["scales"], t["rotations"],
                                 t["scale_modifier"], blocks, out, flags=flags, live=live)
     return out
@@ -211,6 +215,29 @@ def test_sparse_blocks_pack_unpack(split):
     small = torch.zeros(_C.view_pack_floats(5), device=dev)
     _C.view_block_pack(blocks[0], small, scratch, count, P)
     assert int(count.item()) == counts[0]
+    # chunked exchange (ViewExchange(chunks=K)): each Gaussian range packs exactly the whole block's entries
+    # of its Gaussians (absolute indices), and index + live list + backward run chunk by chunk over the
+    # ranges' blocks write the whole-block result bit for bit (an empty range included)
+    bounds = [0, 777, 777, 2100, P]
+    out = {k: torch.zeros_like(v) for k, v in ref.items()}
+    flags_c = torch.full((len(blocks), P), -1, dtype=torch.int32, device=dev)
+    for g0, g1 in zip(bounds[:-1], bounds[1:]):
+        pk = torch.zeros(len(blocks), _C.view_pack_floats(max(g1 - g0, 1)), device=dev)
+        for v, b in enumerate(blocks):
+            _C.view_block_pack(b, pk[v], scratch, count, P, rng=(g0, g1))
+            n = int(count.item())
+            full = packed[v, 64:64 + 12 * counts[v]].view(-1, 12)
+            gi = full[:, 0].view(torch.int32)
+            want = full[(gi >= g0) & (gi < g1)]
+            assert n == want.shape[0]
+            assert torch.equal(pk[v, 64:64 + 12 * n].view(-1, 12), want)
+            assert torch.equal(pk[v, :41], packed[v, :41])
+        _C.view_block_index(pk, flags_c, P, rng=(g0, g1))
+        _C.views_live_list(flags_c, live, P, rng=(g0, g1))
+        _views_backward(t, pk, split, dev, flags=flags_c, live=live, out=out)
+    assert bool((flags_c != -1).all())  # every range's flags written
+    for k in ref:
+        assert torch.equal(out[k], ref[k]), k
 
 
 def _free_port():
