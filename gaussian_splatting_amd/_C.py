@@ -355,6 +355,29 @@ def debug_sort_state(fwd, P: int) -> dict:
     return {"sorted_len": sl.cpu().long(), "redo_count": int(rc.item())}
 
 
+def debug_near_state(fwd, P: int) -> dict:
+    """The forward's near-first binning state (include/gsr.h gsr_debug_near_state): ``zcut`` (the depth bin
+    of its cut, None when there was none) and ``near_len`` [tiles] (entries keyed and sorted per tile;
+    the whole list lengths when there was no cut); int / int64 CPU tensor."""
+    num_rendered, color, _radii, geom, binning, img, _inv = fwd
+    H, W = int(color.size(1)), int(color.size(2))
+    device = color.device
+    tiles = ((W + 15) // 16) * ((H + 15) // 16)
+    zc = torch.zeros(1, dtype=torch.int32, device=device)
+    nr = torch.zeros((tiles, 2), dtype=torch.int32, device=device)
+    with torch.cuda.device(device):
+        r = _lib.load().gsr_debug_near_state(int(P), W, H, geom.data_ptr(), zc.data_ptr(), nr.data_ptr(),
+                                             _stream_handle(device))
+    _lib.check(r, "debug_near_state")
+    cut = int(zc.item()) & 0xFFFFFFFF
+    st = debug_forward_state(fwd, P)
+    rg = st["ranges"]
+    if cut == 0xFFFFFFFF:
+        return {"zcut": None, "near_len": rg[:, 1] - rg[:, 0]}
+    n = nr.cpu().numpy().view("uint32").astype("int64")
+    return {"zcut": cut, "near_len": torch.from_numpy(n[:, 1] - n[:, 0])}
+
+
 def view_block_floats(P: int) -> int:
     """Floats in one view block (include/gsr.h, multi-GPU view exchange)."""
     return int(_lib.load().gsr_view_block_floats(int(P)))

@@ -92,6 +92,7 @@ SIGNATURES = {
     "gsr_debug_forward_state": (_i, [_i, _i, _i, _i, _i, ctypes.c_size_t, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "gsr_forward_rebuilds": (ctypes.c_longlong, []),
     "gsr_debug_sort_state": (_i, [_i, _i, _i, _vp, _vp, _vp, _vp]),
+    "gsr_debug_near_state": (_i, [_i, _i, _i, _vp, _vp, _vp, _vp]),
     "gsr_option_set": (_i, [ctypes.c_char_p, _i]),
     "gsr_host_stats": (_i, [ctypes.POINTER(ctypes.c_double), _i, _i]),
     "gsr_option_get": (_i, [ctypes.c_char_p]),
@@ -197,7 +198,7 @@ def build_id() -> str:
 
 # ---- runtime options (include/gsr.h gsr_option_set) ---------------------------------
 OPTIONS = ("fused_bin", "fwd_quads", "bwd_seg_ck", "host_total", "zero_fill", "live_list", "sort_prefix",
-           "count_wait", "bwd_grid", "bwd_atomic")
+           "count_wait", "bwd_grid", "bwd_atomic", "near_mass")
 
 
 def option_get(name: str) -> int:

@@ -143,8 +143,12 @@ gsr::GeomState carve_geom(char* base, int P, uint32_t gx, uint32_t gy, size_t* t
     g.fwd_seg_ck = g.status + 2;
     const uint32_t tiles = gx * gy;
     const size_t cells = bin_cell_count(gx, gy);
-    g.tile_cnt = c.take<uint32_t>(tiles + cells);
+    // the counters preprocess zeroes in one range (bin_zero_words): tile counts, cell counts, near counts,
+    // the depth-mass histogram (8-byte aligned)
+    g.tile_cnt = c.take<uint32_t>(bin_zero_words(tiles, cells));
     g.cell_cnt = g.tile_cnt + tiles;
+    g.near_cnt = g.cell_cnt + cells;
+    g.zhist = reinterpret_cast<unsigned long long*>(g.tile_cnt + ((2 * (size_t)tiles + cells + 1) & ~(size_t)1));
     g.tile_base = c.take<uint32_t>(tiles);
     const size_t chunks = bin_chunk_count(P);
     g.cell_off = c.take<uint32_t>(chunks * cells);
@@ -165,6 +169,10 @@ gsr::GeomState carve_geom(char* base, int P, uint32_t gx, uint32_t gy, size_t* t
     g.redo_cnt = c.take<uint32_t>(1);
     g.acc = c.take<float4>((size_t)kAccRow4 * P);
     g.touched = c.take<uint32_t>(touched_words((size_t)P));
+    g.mass = c.take<uint32_t>(P);
+    g.zcut = g.status + 3;
+    g.sranges = c.take<uint2>(tiles);
+    g.far_cur = c.take<uint32_t>(tiles);
     *total = align_up(c.off);
     return g;
 }
@@ -287,6 +295,12 @@ void carve_recs(char* base, size_t R, size_t P, gsr::GradRecs* recs, gsr::GradRe
 #ifndef GSR_COUNT_WAIT_DEFAULT
 #define GSR_COUNT_WAIT_DEFAULT 2
 #endif
+// "near_mass": near-first binning (binning.hip) -- only the Gaussians in front of the depth at which the
+// screen-averaged opacity mass reaches this value get keys and are sorted; 0 = off.  Capacity-hinted
+// forwards with the fused scan only.
+#ifndef GSR_NEAR_MASS_DEFAULT
+#define GSR_NEAR_MASS_DEFAULT 30
+#endif
 // "bwd_atomic": the render backward adds each instance's sums into per-Gaussian rows with float atomics
 // (render.hip ATOMIC) and gauss_live lists the touched Gaussians, instead of per-instance records summed
 // by gauss_reduce (deterministic).  The forward zeroes the rows when the option is on at forward time,
@@ -300,7 +314,7 @@ void carve_recs(char* base, size_t R, size_t P, gsr::GradRecs* recs, gsr::GradRe
 static_assert(GSR_FWD_FILL_BLOCKS % 8 == 0, "the forward's fill blocks keep the tiles' XCD mapping");
 enum Opt {
     OPT_FUSED_BIN = 0, OPT_FWD_QUADS, OPT_BWD_SEG_CK, OPT_HOST_TOTAL, OPT_ZERO_FILL, OPT_LIVE_LIST, OPT_SORT_PREFIX,
-    OPT_COUNT_WAIT, OPT_BWD_GRID, OPT_BWD_ATOMIC, OPT_COUNT
+    OPT_COUNT_WAIT, OPT_BWD_GRID, OPT_BWD_ATOMIC, OPT_NEAR_MASS, OPT_COUNT
 };
 struct OptionSpec {
     const char* name;
@@ -318,6 +332,7 @@ const OptionSpec kOptions[OPT_COUNT] = {
     {"count_wait", "GSR_COUNT_WAIT", GSR_COUNT_WAIT_DEFAULT, 0, 2},
     {"bwd_grid", "GSR_BWD_GRID", 0, 0, 2},
     {"bwd_atomic", "GSR_BWD_ATOMIC", GSR_BWD_ATOMIC_DEFAULT, 0, 1},
+    {"near_mass", "GSR_NEAR_MASS", GSR_NEAR_MASS_DEFAULT, 0, 1 << 20},
 };
 std::atomic<int> g_opt[OPT_COUNT];
 std::once_flag g_opt_once;
@@ -842,6 +857,7 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
     const bool opt_fused = fused_binning_mode(), opt_host_total = host_total_store();
     const int opt_count_wait = option(OPT_COUNT_WAIT);
     const bool opt_atomic = option(OPT_BWD_ATOMIC) != 0;
+    const int opt_near_mass = option(OPT_NEAR_MASS);
     // _ex / _dc forwards lay the binning buffer out for a multiple of kCapQuantum (the backward
     // recovers it from the buffer's size); gsr_rasterize_forward keeps the exact C = R layout
     const auto capacity_for = [quantized](size_t c) {
@@ -906,8 +922,8 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
         pa.focal_y = focal_y; pa.gx = gx; pa.gy = gy; pa.prefiltered = prefiltered; pa.antialiasing = antialiasing;
         pa.footprint_cull = (width < 32000 && height < 32000) ? 1 : 0;
         pa.radii = radii; pa.geom = geom;
-        pa.zero = geom.tile_cnt;  // tile and cell counters (binning.hip K0/K1), contiguous
-        pa.zero_n = tiles + (uint32_t)bin_cell_count(gx, gy);
+        pa.zero = geom.tile_cnt;  // tile, cell and near counters and the depth-mass histogram (binning.hip), contiguous
+        pa.zero_n = (uint32_t)bin_zero_words(tiles, bin_cell_count(gx, gy));
         HIP_TRY(launch_preprocess(pa, stream), "preprocess");
     }
     if (int rc = check_debug(debug, stream, "preprocess")) return rc;
@@ -927,6 +943,12 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
     const size_t C_hint = capacity_hint > 0 ? capacity_for((size_t)capacity_hint) : 0;
     // capacity mode with LDS cursors: K2 folded into K3 (binning.hip FusedScan)
     const bool fused = capacity_hint > 0 && bin_fused_ok(tiles) && opt_fused;
+    // near-first binning (binning.hip): the depth cut's target, mass x kMassScale over the image
+    const unsigned long long near_target =
+        fused && opt_near_mass > 0 && bin_near_ok(tiles)
+            ? (unsigned long long)opt_near_mass * (unsigned long long)kMassScale * (unsigned long long)width * height
+            : 0ull;
+    const bool near_first = near_target > 0;
     // "count_wait" 2 (capacity mode, the kernels storing the count into the mapped slot): no event
     // behind the count -- the host polls the slot itself, reset to a sentinel before the launch that
     // stores it, so the stream carries no marker (an event's marker left the GPU idle ~6 us between
@@ -937,7 +959,7 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
     {
         StageScope sc(ST_BIN_COUNT, stream);
         HIP_TRY(launch_bin_count(P, geom, gx, gy, img.ranges, capacity_hint > 0 ? C_hint : kNoCap,
-                                 fused ? nullptr : rb->dev, stream, fused),
+                                 fused ? nullptr : rb->dev, stream, fused, near_target),
                 "bin_count");
     }
     if (int rc = check_debug(debug, stream, "bin_count")) return rc;
@@ -986,7 +1008,7 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
             // was rendered (fused: also the ranges, classes and the count)
             StageScope sc(ST_BIN_SCATTER, stream);
             HIP_TRY(launch_bin_scatter(P, geom, gx, gy, bin, C, stream, img.ranges, fused_now ? rb->dev : nullptr,
-                                       fused_now),
+                                       fused_now, fused_now && near_first),
                     "bin_scatter");
         }
         if (fused_now)
@@ -995,7 +1017,9 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
         if (C > 0) {
             {
                 StageScope sc(ST_TILE_SORT, stream);
-                HIP_TRY(launch_tile_sort(tiles, img.ranges, geom, bin, C, stream, fused_now,
+                // (near-first binning: K4 sorts each tile's near entries, GeomState::sranges)
+                HIP_TRY(launch_tile_sort(tiles, fused_now && near_first ? geom.sranges : img.ranges, geom, bin, C,
+                                         stream, fused_now,
                                          (uint32_t)bin_cell_count(gx, gy), prefix),
                         "tile_sort");
             }
@@ -1029,7 +1053,10 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
                 ra.fill_blocks = GSR_FWD_FILL_BLOCKS;
             }
             HIP_TRY(launch_render_fwd(ra, stream, opt_quads), "render_fwd");
-            if (prefix && C > 0) {  // the tiles whose walk passed their sorted prefix (usually none)
+            const bool near_now = fused_now && near_first;
+            if ((prefix || near_now) && C > 0) {  // the tiles whose walk passed their sorted prefix (usually none)
+                if (near_now)  // their far instances first (none emitted by K3)
+                    HIP_TRY(launch_far_fill(P, geom, gx, tiles, img.ranges, bin, C, true, stream), "render_fwd far fill");
                 HIP_TRY(launch_tile_sort_redo(tiles, img.ranges, geom, bin, C, stream), "render_fwd redo sort");
                 HIP_TRY(launch_render_fwd_redo(ra, stream, opt_quads), "render_fwd redo");
             }
@@ -1054,7 +1081,8 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
             g_rebuilds.fetch_add(1, std::memory_order_relaxed);
             C = capacity_for((size_t)total);
             if (fused)  // (the fused sort re-zeroes the counters only when it ran: C > 0)
-                HIP_TRY(hipMemsetAsync(geom.tile_cnt, 0, sizeof(uint32_t) * (tiles + bin_cell_count(gx, gy)), stream),
+                HIP_TRY(hipMemsetAsync(geom.tile_cnt, 0, sizeof(uint32_t) * bin_zero_words(tiles, bin_cell_count(gx, gy)),
+                                       stream),
                         "bin counters");
             HIP_TRY(launch_bin_count(P, geom, gx, gy, img.ranges, C, nullptr, stream), "bin_count");
             if (int rc = bin_and_render(C, false)) return rc;
@@ -1555,7 +1583,7 @@ int gsr_debug_forward_state(int P, int width, int height, int R, int binning_cap
         if (!geom_buffer) return fail(GSR_ERR_ARGUMENT, "debug_forward_state: point_list needs the geometry buffer");
         BinningState bin = carve_binning((char*)binning_buffer, C, &tmp);
         GeomState geom = carve_geom((char*)const_cast<void*>(geom_buffer), P, gx, gy, &tmp);
-        HIP_TRY(launch_sorted_lists_copy(gx * gy, img.ranges, geom, bin, C, point_list, stream),
+        HIP_TRY(launch_sorted_lists_copy(gx * gy, img.ranges, geom, bin, C, point_list, stream, P, gx, true),
                 "debug_forward_state point_list");
     }
     return GSR_OK;
@@ -1577,6 +1605,24 @@ int gsr_debug_sort_state(int P, int width, int height, const void* geom_buffer, 
     if (redo_count)
         HIP_TRY(hipMemcpyAsync(redo_count, geom.redo_cnt, sizeof(uint32_t), hipMemcpyDeviceToDevice, stream),
                 "debug_sort_state redo_count");
+    return GSR_OK;
+}
+
+int gsr_debug_near_state(int P, int width, int height, const void* geom_buffer, unsigned int* zcut,
+                         unsigned int* near_ranges, void* stream_) {
+    using namespace gsr;
+    g_err[0] = 0;
+    hipStream_t stream = (hipStream_t)stream_;
+    if (P <= 0 || width <= 0 || height <= 0 || !geom_buffer)
+        return fail(GSR_ERR_ARGUMENT, "debug_near_state: invalid sizes or no geometry buffer");
+    const uint32_t gx = (width + kTile - 1) / kTile, gy = (height + kTile - 1) / kTile;
+    size_t tmp = 0;
+    GeomState geom = carve_geom((char*)const_cast<void*>(geom_buffer), P, gx, gy, &tmp);
+    if (zcut)
+        HIP_TRY(hipMemcpyAsync(zcut, geom.zcut, sizeof(uint32_t), hipMemcpyDeviceToDevice, stream), "debug_near_state zcut");
+    if (near_ranges)
+        HIP_TRY(hipMemcpyAsync(near_ranges, geom.sranges, sizeof(uint2) * gx * gy, hipMemcpyDeviceToDevice, stream),
+                "debug_near_state sranges");
     return GSR_OK;
 }
 

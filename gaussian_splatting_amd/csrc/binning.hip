@@ -262,42 +262,103 @@ __device__ __forceinline__ uint32_t cell_of(uint2 r, CellGrid g) {
 // K0a: per-chunk cell histogram in LDS; one returning atomic per (chunk, cell) gives the
 // chunk's offset inside the cell's block (kept in cell_off[chunk][cell]).  Also the
 // chunk's instance total (index order), for the record starts.
+// zhist (near-first binning, null otherwise): each visible Gaussian's opacity mass (GeomState::mass) is
+// added to its depth bin (LDS, then one global add per bin and chunk) -- the profile K1 cuts at.
 __global__ void __launch_bounds__(kBinThreads) cell_count_kernel(int P, int chunk, const uint2* __restrict__ rect,
                                                                  const uint32_t* __restrict__ tiles_touched,
                                                                  uint32_t cells, CellGrid cgx,
                                                                  uint32_t* __restrict__ cell_cnt,
                                                                  uint32_t* __restrict__ cell_off,
-                                                                 u64* __restrict__ chunk_total) {
+                                                                 u64* __restrict__ chunk_total,
+                                                                 const uint32_t* __restrict__ depth_key,
+                                                                 const uint32_t* __restrict__ mass,
+                                                                 u64* __restrict__ zhist) {
     extern __shared__ uint32_t s_c[];  // cells words
     __shared__ u64 s_tmp[kBinWaves];
+    __shared__ u64 s_zh[kZBins];
     const int g0 = blockIdx.x * chunk, g1 = min(P, g0 + chunk);
     for (uint32_t i = threadIdx.x; i < cells; i += blockDim.x) s_c[i] = 0;
+    if (zhist && threadIdx.x < kZBins) s_zh[threadIdx.x] = 0ull;
     __syncthreads();
     u64 mine = 0;
     // kBinUnroll Gaussians per thread per round, their loads all issued before the LDS atomics
     for (int gb = g0 + (int)threadIdx.x; gb < g1; gb += kBinUnroll * kBinThreads) {
-        uint32_t n[kBinUnroll];
+        uint32_t n[kBinUnroll], dk[kBinUnroll], ms[kBinUnroll];
         uint2 r[kBinUnroll];
 #pragma unroll
         for (int u = 0; u < kBinUnroll; u++) {
             const int g = gb + u * kBinThreads;
             n[u] = g < g1 ? tiles_touched[g] : 0u;
             r[u] = g < g1 ? rect[g] : make_uint2(0u, 0u);
+            dk[u] = zhist && g < g1 ? depth_key[g] : 0u;
+            ms[u] = zhist && g < g1 ? mass[g] : 0u;
         }
 #pragma unroll
         for (int u = 0; u < kBinUnroll; u++) {
             mine += n[u];
-            if (n[u]) atomicAdd(&s_c[cell_of(r[u], cgx)], 1u);
+            if (n[u]) {
+                atomicAdd(&s_c[cell_of(r[u], cgx)], 1u);
+                if (zhist && ms[u]) atomicAdd(&s_zh[zbin(dk[u])], (u64)ms[u]);
+            }
         }
     }
-    const u64 total = block_sum(mine, s_tmp);  // ends with a barrier: the histogram is complete
+    const u64 total = block_sum(mine, s_tmp);  // ends with a barrier: the histograms are complete
     if (threadIdx.x == 0) chunk_total[blockIdx.x] = total;
+    if (zhist && threadIdx.x < kZBins && s_zh[threadIdx.x]) atomicAdd(&zhist[threadIdx.x], s_zh[threadIdx.x]);
     uint32_t* off = cell_off + (size_t)blockIdx.x * cells;
     for (uint32_t i = threadIdx.x; i < cells; i += blockDim.x) {
         const uint32_t c = s_c[i];
         if (c) off[i] = atomicAdd(&cell_cnt[i], c);
     }
 }
+
+// ---- Near-first binning ----------------------------------------------------------
+// ("near_mass" option, api.hip.)  A pixel stops blending once T < 1e-4, after an opacity mass of
+// -ln 1e-4 = 9.2 in front of it, so the back of a dense frame is never reached: at 5M@4K the walk reads
+// 6.7% of the 114.7M instances and no tile reads past z = 2.29 of the scene's [2, 12]
+// (tools/cutoff_estimate.py, profiles/r05/cutoff_estimate_5m_4k.json).  The cut: the depth bin at which
+// the screen-averaged mass of the Gaussians in front (K0a's histogram over the image area) reaches the
+// option's target (30 by default: 3.3x what one pixel needs -- 2.52 at 5M@4K).  Only the Gaussians at or
+// in front of it get keys (K3) and are sorted (K4, over GeomState::sranges); each tile's range keeps its
+// full length, the near entries at its start, so num_rendered, the ranges and the emission indices are
+// the full list's.  A tile whose forward walk passes its near entries with pixels still blending is filed
+// for the redo (render.hip, as for the reachable-prefix sort): tile_far_fill_kernel emits its far
+// instances behind the near ones, the whole list is sorted and the tile rendered again -- so images and
+// gradients are those of the full lists whatever the cut.
+// The cut bin (in each K1 workgroup, one wave): the first bin whose cumulative mass reaches `target`
+// (fixed point, kMassScale x pixels x mean mass), or kZCutNone.
+__device__ uint32_t zcut_from_hist(const u64* __restrict__ zhist, u64 target) {
+    const int lane = threadIdx.x & 63;
+    constexpr int kPer = kZBins / 64;
+    u64 v[kPer], run = 0;
+#pragma unroll
+    for (int i = 0; i < kPer; i++) {
+        v[i] = zhist[lane * kPer + i];
+        run += v[i];
+    }
+    const u64 incl = wave_incl_sum_u64(run);
+    u64 at = incl - run;
+    uint32_t found = kZCutNone;
+#pragma unroll
+    for (int i = 0; i < kPer; i++) {
+        at += v[i];
+        if (at >= target && found == kZCutNone) found = (uint32_t)(lane * kPer + i);
+    }
+    // the first lane with a crossing holds the smallest bin
+    const unsigned long long m = __ballot(found != kZCutNone);
+    return m ? (uint32_t)__builtin_amdgcn_readlane((int)found, __builtin_ctzll(m)) : kZCutNone;
+}
+__device__ __forceinline__ bool is_near(uint32_t depth_bits, uint32_t cut) {
+    return cut == kZCutNone || zbin(depth_bits) <= cut;
+}
+// K1 / K3 arguments of the near-first binning (zhist null: off)
+struct NearArgs {
+    const u64* zhist;
+    u64 target;
+    uint32_t* zcut;      // written by K1 workgroup 0, read by K3 and the far fill
+    uint32_t* near_cnt;  // per tile: near instances (K1's returning adds give each chunk its near offset)
+    uint2* sranges;      // per tile: [start, start + near) (K3)
+};
 
 // K0c: every chunk scans the cell counts (redundantly, cells are few), then scatters its
 // visible Gaussians into their cells' blocks as 16-byte binning records (index, rect,
@@ -366,30 +427,36 @@ struct FusedZero {
 #endif
 constexpr int kColBlock = 8;  // rows per register block of the column pass
 
+// cut != kZCutNone (near-first binning): each Gaussian counts 1 in the low 16 bits (all instances) and,
+// when near, also 1 in the high 16 (near instances) -- both fields exact after the prefix sums, since a
+// chunk holds < 65536 Gaussians (bin_chunks) and the sums are exact integers modulo 2^32.
 __device__ __forceinline__ void count_by_rectangles(int g0, int g1, const uint4* __restrict__ order, uint32_t tiles,
-                                                    uint32_t gx, uint32_t* s_d) {
+                                                    uint32_t gx, uint32_t* s_d, uint32_t cut = kZCutNone) {
     const uint32_t gy = tiles / gx;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (uint32_t i = threadIdx.x; i < tiles; i += blockDim.x) s_d[i] = 0u;
     __syncthreads();
     for (int pb = g0 + (int)threadIdx.x; pb < g1; pb += kBinUnroll * kBinThreads) {
         uint2 rr[kBinUnroll];
+        uint32_t wt[kBinUnroll];
 #pragma unroll
         for (int u = 0; u < kBinUnroll; u++) {
             const int p = pb + u * kBinThreads;
             const uint4 o = p < g1 ? order[p] : make_uint4(0u, 0u, 0u, 0u);
             rr[u] = make_uint2(o.y, o.z);
+            wt[u] = cut == kZCutNone ? 1u : (is_near(o.w, cut) ? 0x10001u : 1u);
         }
 #pragma unroll
         for (int u = 0; u < kBinUnroll; u++) {
             uint32_t x0, y0, x1, y1;
             unpack_rect(rr[u], x0, y0, x1, y1);
             if (x0 < x1 && y0 < y1) {  // (K0 orders only Gaussians with tiles; padding lanes are empty)
-                atomicAdd(&s_d[y0 * gx + x0], 1u);
-                if (x1 < gx) atomicAdd(&s_d[y0 * gx + x1], ~0u);
+                const uint32_t w = wt[u], nw = 0u - wt[u];
+                atomicAdd(&s_d[y0 * gx + x0], w);
+                if (x1 < gx) atomicAdd(&s_d[y0 * gx + x1], nw);
                 if (y1 < gy) {
-                    atomicAdd(&s_d[y1 * gx + x0], ~0u);
-                    if (x1 < gx) atomicAdd(&s_d[y1 * gx + x1], 1u);
+                    atomicAdd(&s_d[y1 * gx + x0], nw);
+                    if (x1 < gx) atomicAdd(&s_d[y1 * gx + x1], w);
                 }
             }
         }
@@ -431,7 +498,8 @@ __global__ void __launch_bounds__(kBinThreads) tile_count_kernel(int P, int chun
                                                                  const uint4* __restrict__ order,
                                                                  const uint32_t* __restrict__ n_visible,
                                                                  uint32_t tiles, uint32_t gx, uint32_t* __restrict__ cnt,
-                                                                 uint32_t* __restrict__ chunk_off, FusedZero fz) {
+                                                                 uint32_t* __restrict__ chunk_off, FusedZero fz,
+                                                                 NearArgs na) {
     extern __shared__ uint32_t s_hist[];  // by rectangles: tiles words; walk: (tiles + 1) / 2 words of 16-bit counters (a chunk has < 65536 Gaussians)
     if (fz.unit_cnt) {
         if (blockIdx.x == 0 && threadIdx.x < kUnitLists * kUnitShards) fz.unit_cnt[threadIdx.x * kUnitCntStride] = 0u;
@@ -439,18 +507,42 @@ __global__ void __launch_bounds__(kBinThreads) tile_count_kernel(int P, int chun
         for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < tiles; i += gridDim.x * blockDim.x)
             fz.tile_join[i] = 0ull;
     }
+    if (!na.zhist && na.zcut && blockIdx.x == 0 && threadIdx.x == 0) *na.zcut = kZCutNone;  // (inspection, far fill)
     const int V = (int)n_visible[0];
     const int g0 = blockIdx.x * chunk, g1 = min(V, g0 + chunk);  // positions in order[]
     const uint32_t words = (tiles + 1) / 2;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     GSR_STAMP(g_st_count, blockIdx.x, 0);
     if (LDS && GSR_K1_RECT) {
-        count_by_rectangles(g0, g1, order, tiles, gx, s_hist);
+        uint32_t cut = kZCutNone;
+        if (na.zhist) {  // near-first binning: the cut, from K0a's depth-mass histogram (each workgroup alike)
+            __shared__ uint32_t s_cut;
+            if (wave == 0) {
+                const uint32_t c = zcut_from_hist(na.zhist, na.target);
+                if (lane == 0) {
+                    s_cut = c;
+                    if (blockIdx.x == 0) *na.zcut = c;
+                }
+            }
+            __syncthreads();
+            cut = s_cut;
+        }
+        count_by_rectangles(g0, g1, order, tiles, gx, s_hist, cut);
         GSR_STAMP(g_st_count, blockIdx.x, 2);
         uint32_t* off = chunk_off + (size_t)blockIdx.x * tiles;
-        for (uint32_t i = threadIdx.x; i < tiles; i += blockDim.x) {
-            const uint32_t c = s_hist[i];
-            if (c) off[i] = atomicAdd(&cnt[i], c);
+        if (cut != kZCutNone) {
+            // all instances into the tile counts (the ranges keep the full lists); the near ones into the
+            // near counts, whose returning adds give this chunk's near offsets (K3 places only those)
+            for (uint32_t i = threadIdx.x; i < tiles; i += blockDim.x) {
+                const uint32_t v = s_hist[i], full = v & 0xffffu, nr = v >> 16;
+                if (full) atomicAdd(&cnt[i], full);
+                if (nr) off[i] = atomicAdd(&na.near_cnt[i], nr);
+            }
+        } else {
+            for (uint32_t i = threadIdx.x; i < tiles; i += blockDim.x) {
+                const uint32_t c = s_hist[i];
+                if (c) off[i] = atomicAdd(&cnt[i], c);
+            }
         }
         GSR_STAMP(g_st_count, blockIdx.x, 3);
         return;
@@ -590,9 +682,13 @@ __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
     const uint32_t* __restrict__ depth_key, const uint4* __restrict__ order, const uint32_t* __restrict__ n_visible,
     uint32_t tiles, uint32_t gx, uint32_t* __restrict__ tile_base,
     const uint32_t* __restrict__ chunk_off, const u64* __restrict__ chunk_total, u64* __restrict__ keys, u64 cap,
-    uint32_t* __restrict__ rec_start, float4* __restrict__ rec, uint8_t* __restrict__ rec_flag, FusedScan fs) {
+    uint32_t* __restrict__ rec_start, float4* __restrict__ rec, uint8_t* __restrict__ rec_flag, FusedScan fs,
+    NearArgs na) {
     extern __shared__ uint32_t s_cur[];  // tiles words
     __shared__ u64 s_tmp[kBinWaves];
+    // near-first binning (fused only): the cut K1 chose; kZCutNone when off or when the frame's mass never
+    // reached the target (then K1 counted as usual and the near lists are the whole lists)
+    const uint32_t cut = na.zhist && fs.cnt ? *na.zcut : kZCutNone;
     const int g0 = blockIdx.x * chunk, g1 = min(P, g0 + chunk);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     GSR_STAMP(g_st_scatter, blockIdx.x, 0);
@@ -623,6 +719,11 @@ __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
                     if (publish) {
                         const u64 lo = at < cap ? at : cap, hi = at + v[i] < cap ? at + v[i] : cap;
                         fs.ranges[b + i] = make_uint2((uint32_t)lo, (uint32_t)hi);
+                        if (na.zhist) {  // K4's list: the near entries at the range's start
+                            const uint32_t nr = cut == kZCutNone ? v[i] : na.near_cnt[b + i];
+                            const u64 nh = at + nr < cap ? at + nr : cap;
+                            na.sranges[b + i] = make_uint2((uint32_t)lo, (uint32_t)nh);
+                        }
                     }
                 }
                 at += v[i];
@@ -642,9 +743,11 @@ __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
         const uint32_t my_groups = groups > blockIdx.x ? (groups - blockIdx.x + gridDim.x - 1) / gridDim.x : 0u;
         if (threadIdx.x < kSortClasses) s_cls[threadIdx.x] = 0u;
         __syncthreads();
+        // (the sort's list length: the near count under a cut)
+        const uint32_t* scnt = cut != kZCutNone ? na.near_cnt : fs.cnt;
         for (uint32_t j = threadIdx.x; j < my_groups * kScanV; j += blockDim.x) {
             const uint32_t t = (blockIdx.x + (j / kScanV) * gridDim.x) * kScanV + j % kScanV;
-            const uint32_t v = t < tiles ? fs.cnt[t] : 0u;
+            const uint32_t v = t < tiles ? scnt[t] : 0u;
             if (v > kSortWaveMax) atomicAdd(&s_cls[v <= kClass0Max ? 0 : 1], 1u);
         }
         __syncthreads();
@@ -656,7 +759,7 @@ __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
         __syncthreads();
         for (uint32_t j = threadIdx.x; j < my_groups * kScanV; j += blockDim.x) {
             const uint32_t t = (blockIdx.x + (j / kScanV) * gridDim.x) * kScanV + j % kScanV;
-            const uint32_t v = t < tiles ? fs.cnt[t] : 0u;
+            const uint32_t v = t < tiles ? scnt[t] : 0u;
             if (v > kSortWaveMax) {
                 const int c = v <= kClass0Max ? 0 : 1;
                 fs.cls_list[(size_t)c * tiles + s_cbase[c] + atomicAdd(&s_cls[c], 1u)] = t;
@@ -743,7 +846,7 @@ __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
         const uint4 o = p < q1 ? order[p] : make_uint4(0u, 0u, 0u, 0u);
         const uint32_t g = o.x, dk = o.w;
         const uint2 r = make_uint2(o.y, o.z);
-        const uint32_t n = rect_tiles(r);
+        const uint32_t n = is_near(dk, cut) ? rect_tiles(r) : 0u;  // (a cut: the far Gaussians get no keys)
         for_each_instance(n, r, gx, [&](bool valid, int owner, uint32_t t, uint32_t, uint32_t) {
             const uint32_t kh = __shfl(dk, owner), kg = __shfl(g, owner);
             if (!valid) return;
@@ -1125,15 +1228,19 @@ static_assert(kSortT == 64 || kSortT == 128 || kSortT == 256, "tile_sort_kernel:
 __global__ void __launch_bounds__(kSortT) tile_sort_kernel(const uint2* __restrict__ ranges,
                                                        const u64* __restrict__ keys, u64 cap,
                                                        uint32_t* __restrict__ gid_sorted,
-                                                       uint32_t* __restrict__ zero_cnt, uint32_t n_cells,
+                                                       uint32_t* __restrict__ zero_cnt, uint32_t n_zero,
                                                        uint32_t* __restrict__ sorted_len,
                                                        uint32_t* __restrict__ redo_flag,
-                                                       uint32_t* __restrict__ redo_cnt) {
+                                                       uint32_t* __restrict__ redo_cnt,
+                                                       uint32_t* __restrict__ far_cur) {
     __shared__ BucketLds<kSortT, kSortWaveMax, kSortWaveMax / 2> s;
-    if (zero_cnt && threadIdx.x == 0) {  // fused binning: K2's re-zeroing of the tile / cell counters
-        zero_cnt[blockIdx.x] = 0u;
-        if (blockIdx.x < n_cells) zero_cnt[gridDim.x + blockIdx.x] = 0u;
+    // fused binning: K2's re-zeroing of the counters (tile, cell and near counts, the depth-mass
+    // histogram: bin_zero_words), word blockIdx.x + k gridDim.x by thread k
+    if (zero_cnt) {
+        const uint32_t i = blockIdx.x + threadIdx.x * gridDim.x;
+        if (i < n_zero) zero_cnt[i] = 0u;
     }
+    if (far_cur && threadIdx.x == 0) far_cur[blockIdx.x] = 0u;  // (near-first binning: the redo's far fill)
     const uint2 r = ranges[blockIdx.x];
     const uint32_t n = tile_len(r, cap);
     if (threadIdx.x == 0) {  // the forward's redo state (render.hip), and this kernel's lists' lengths
@@ -1402,6 +1509,7 @@ uint32_t bin_cells(uint32_t gx, uint32_t gy, CellGrid* cg) {
 }
 
 bool bin_fused_ok(uint32_t tiles) { return tiles <= kLdsTilesMax; }
+bool bin_near_ok(uint32_t tiles) { return tiles <= kLdsTilesMax && GSR_K1_RECT; }
 
 size_t bin_cell_count(uint32_t gx, uint32_t gy) {
     CellGrid cg{};
@@ -1411,7 +1519,7 @@ size_t bin_cell_count(uint32_t gx, uint32_t gy) {
 // K0 + K1 + K2: spatial order, chunk instance totals, tile counts, ranges, tile starts,
 // chunk offsets, the long-list class lists and the instance count (g.total).
 hipError_t launch_bin_count(int P, const GeomState& g, uint32_t gx, uint32_t gy, uint2* ranges, size_t cap,
-                            unsigned long long* host_total, hipStream_t stream, bool fused) {
+                            unsigned long long* host_total, hipStream_t stream, bool fused, unsigned long long near_target) {
     const uint32_t tiles = gx * gy;
     int chunk = 0;
     const int nchunks = bin_chunks(P, &chunk);
@@ -1421,8 +1529,12 @@ hipError_t launch_bin_count(int P, const GeomState& g, uint32_t gx, uint32_t gy,
     const dim3 grid(nchunks), block(kBinThreads);
     // g.tile_cnt / g.cell_cnt are zero here: preprocess zeroes them, tile_scan_kernel re-zeroes them
     const size_t cell_bytes = cells * sizeof(uint32_t);
+    // near-first binning (near_target > 0; fused, K1 by rectangles only): K0a's depth-mass histogram, K1's cut
+    const bool near = near_target > 0 && fused && lds && GSR_K1_RECT;
+    const NearArgs na = near ? NearArgs{g.zhist, near_target, g.zcut, g.near_cnt, g.sranges}
+                             : NearArgs{nullptr, 0ull, g.zcut, nullptr, nullptr};  // (K1 records "no cut")
     hipLaunchKernelGGL(cell_count_kernel, grid, block, cell_bytes, stream, P, chunk, g.rect, g.tiles_touched, cells,
-                       cgx, g.cell_cnt, g.cell_off, g.chunk_total);
+                       cgx, g.cell_cnt, g.cell_off, g.chunk_total, g.depth_key, g.mass, near ? g.zhist : nullptr);
     hipLaunchKernelGGL(cell_scatter_kernel, grid, block, cell_bytes, stream, P, chunk, g.rect, g.tiles_touched,
                        cells, cgx, g.cell_cnt, g.cell_off, g.depth_key, g.order, g.n_visible);
     // K1's LDS: one u32 per tile (by rectangles) or two 16-bit walk counters per word
@@ -1431,10 +1543,10 @@ hipError_t launch_bin_count(int P, const GeomState& g, uint32_t gx, uint32_t gy,
     const FusedZero fz = fused ? FusedZero{g.unit_cnt, g.tile_join, g.cls_count} : FusedZero{nullptr, nullptr, nullptr};
     if (lds)
         hipLaunchKernelGGL(tile_count_kernel<true>, grid, block, hist_bytes, stream, P, chunk, g.rect, g.tiles_touched,
-                           g.order, g.n_visible, tiles, gx, g.tile_cnt, g.chunk_off, fz);
+                           g.order, g.n_visible, tiles, gx, g.tile_cnt, g.chunk_off, fz, na);
     else
         hipLaunchKernelGGL(tile_count_kernel<false>, grid, block, 0, stream, P, chunk, g.rect, g.tiles_touched,
-                           g.order, g.n_visible, tiles, gx, g.tile_cnt, g.chunk_off, fz);
+                           g.order, g.n_visible, tiles, gx, g.tile_cnt, g.chunk_off, fz, na);
     if (!fused)  // (fused: K3 scans the counts itself)
         hipLaunchKernelGGL(tile_scan_kernel, dim3(1), block, 0, stream, tiles, g.tile_cnt, tiles + cells, g.unit_cnt,
                            g.tile_join, ranges, g.tile_base, g.total, (u64*)host_total, (u64)cap, g.cls_list,
@@ -1444,7 +1556,8 @@ hipError_t launch_bin_count(int P, const GeomState& g, uint32_t gx, uint32_t gy,
 
 // K3: scatter the keys into a binning buffer of capacity `cap` (after launch_bin_count).
 hipError_t launch_bin_scatter(int P, const GeomState& g, uint32_t gx, uint32_t gy, const BinningState& b, size_t cap,
-                              hipStream_t stream, uint2* ranges, unsigned long long* host_total, bool fused) {
+                              hipStream_t stream, uint2* ranges, unsigned long long* host_total, bool fused,
+                              bool near_first) {
     const uint32_t tiles = gx * gy;
     int chunk = 0;
     const int nchunks = bin_chunks(P, &chunk);
@@ -1454,6 +1567,10 @@ hipError_t launch_bin_scatter(int P, const GeomState& g, uint32_t gx, uint32_t g
     if (fused && !lds) return hipErrorInvalidValue;
     const FusedScan fs = fused ? FusedScan{g.tile_cnt, ranges, g.total, (u64*)host_total, g.cls_list, g.cls_count}
                                : FusedScan{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    // (as launch_bin_count decided it: the target is K1's business, K3 reads the cut)
+    const NearArgs na = near_first && fused && lds && GSR_K1_RECT
+                            ? NearArgs{g.zhist, 1ull, g.zcut, g.near_cnt, g.sranges}
+                            : NearArgs{nullptr, 0ull, nullptr, nullptr, nullptr};
 #if GSR_K3_ATTR
     static u64* scratch = nullptr;
     static size_t scratch_cap = 0;
@@ -1467,11 +1584,11 @@ hipError_t launch_bin_scatter(int P, const GeomState& g, uint32_t gx, uint32_t g
     if (lds)
         hipLaunchKernelGGL(tile_scatter_kernel<true>, grid, block, cur_bytes, stream, P, chunk, g.rect,
                            g.tiles_touched, g.depth_key, g.order, g.n_visible, tiles, gx, g.tile_base, g.chunk_off,
-                           g.chunk_total, b.keys, (u64)cap, g.rec_start, g.rec, b.rec_flag, fs);
+                           g.chunk_total, b.keys, (u64)cap, g.rec_start, g.rec, b.rec_flag, fs, na);
     else
         hipLaunchKernelGGL(tile_scatter_kernel<false>, grid, block, 0, stream, P, chunk, g.rect, g.tiles_touched,
                            g.depth_key, g.order, g.n_visible, tiles, gx, g.tile_base, g.chunk_off, g.chunk_total,
-                           b.keys, (u64)cap, g.rec_start, g.rec, b.rec_flag, fs);
+                           b.keys, (u64)cap, g.rec_start, g.rec, b.rec_flag, fs, na);
     return hipGetLastError();
 }
 
@@ -1483,8 +1600,10 @@ hipError_t launch_tile_sort(uint32_t tiles, const uint2* ranges, const GeomState
     if (tiles == 0 || cap == 0) return hipSuccess;
     const u64 c = cap;
     const uint32_t lim = prefix ? prefix : ~0u;
+    const uint32_t n_zero = (uint32_t)bin_zero_words(tiles, cells);
+    if (zero_counts && n_zero > (uint64_t)tiles * kSortT) return hipErrorInvalidValue;  // (never: ~2 words per tile)
     hipLaunchKernelGGL(tile_sort_kernel, dim3(tiles), dim3(kSortT), 0, stream, ranges, b.keys, c, b.gid_sorted,
-                       zero_counts ? g.tile_cnt : nullptr, cells, g.sorted_len, g.redo_flag, g.redo_cnt);
+                       zero_counts ? g.tile_cnt : nullptr, n_zero, g.sorted_len, g.redo_flag, g.redo_cnt, g.far_cur);
     // persistent class kernels: grids sized to fill the chip when their lists are long
     const auto grid = [&](uint32_t want) { return dim3(tiles < want ? tiles : want); };
     if (GSR_PREFIX_KERNEL && prefix) {
@@ -1518,9 +1637,78 @@ hipError_t launch_tile_sort_redo(uint32_t tiles, const uint2* ranges, const Geom
     return hipGetLastError();
 }
 
+// Near-first binning's far fill: the far instances (depth bin past the cut) of the selected tiles, keyed
+// as K3 keys them, behind each tile's near entries [start + near, start + full) -- in any order (the
+// whole-list sort follows).  Selected: the tiles the forward filed for a redo (redo mode; exits at once
+// when none, the usual case), or every tile whose sorted entries fall short of its whole list
+// (inspection, gsr_debug_forward_state).  The walk is K3's, over the spatial order, with the selected
+// tiles as a bitmap in LDS; its cost is an instance walk of the far Gaussians, paid only by a frame
+// with a filed tile.
+__global__ void __launch_bounds__(kBinThreads) tile_far_fill_kernel(int chunk, const uint4* __restrict__ order,
+                                                                    const uint32_t* __restrict__ n_visible,
+                                                                    const uint32_t* __restrict__ zcut, uint32_t tiles,
+                                                                    uint32_t gx, const uint2* __restrict__ ranges,
+                                                                    const uint2* __restrict__ sranges,
+                                                                    const uint32_t* __restrict__ redo_list,
+                                                                    const uint32_t* __restrict__ redo_cnt,
+                                                                    const uint32_t* __restrict__ sorted_len,
+                                                                    uint32_t* __restrict__ far_cur, u64* __restrict__ keys,
+                                                                    u64 cap) {
+    extern __shared__ uint32_t s_sel[];  // (tiles + 31) / 32 words: selected tiles
+    const uint32_t cut = *zcut;
+    const uint32_t nred = redo_cnt ? redo_cnt[0] : 0u;
+    if (cut == kZCutNone || (redo_cnt && nred == 0)) return;  // uniform
+    const uint32_t words = (tiles + 31) / 32;
+    for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) s_sel[i] = 0u;
+    __syncthreads();
+    if (redo_cnt) {
+        for (uint32_t i = threadIdx.x; i < nred; i += blockDim.x) {
+            const uint32_t t = redo_list[i];
+            atomicOr(&s_sel[t >> 5], 1u << (t & 31u));
+        }
+    } else {
+        for (uint32_t t = threadIdx.x; t < tiles; t += blockDim.x)
+            if (sorted_len[t] < tile_len(ranges[t], cap)) atomicOr(&s_sel[t >> 5], 1u << (t & 31u));
+    }
+    __syncthreads();
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int V = (int)n_visible[0];
+    const int q0 = blockIdx.x * chunk, q1 = min(V, q0 + chunk);
+    for (int pb = q0 + wave * 64; pb < q1; pb += kBinThreads) {
+        const int p = pb + lane;
+        const uint4 o = p < q1 ? order[p] : make_uint4(0u, 0u, 0u, 0u);
+        const uint32_t g = o.x, dk = o.w;
+        const uint2 r = make_uint2(o.y, o.z);
+        const uint32_t n = p < q1 && !is_near(dk, cut) ? rect_tiles(r) : 0u;
+        for_each_instance(n, r, gx, [&](bool valid, int owner, uint32_t t, uint32_t, uint32_t) {
+            const uint32_t kh = __shfl(dk, owner), kg = __shfl(g, owner);
+            if (!valid || !((s_sel[t >> 5] >> (t & 31u)) & 1u)) return;
+            const uint2 rr = ranges[t];
+            const uint32_t at = sranges[t].y + atomicAdd(&far_cur[t], 1u);
+            if (at < rr.y && at < cap) keys[at] = ((u64)kh << 32) | (kg << kEntryMaskBits);
+        });
+    }
+}
+
+hipError_t launch_far_fill(int P, const GeomState& g, uint32_t gx, uint32_t tiles, const uint2* ranges,
+                           const BinningState& b, size_t cap, bool redo, hipStream_t stream) {
+    if (tiles == 0 || cap == 0 || P == 0) return hipSuccess;
+    int chunk = 0;
+    const int nchunks = bin_chunks(P, &chunk);
+    hipLaunchKernelGGL(tile_far_fill_kernel, dim3(nchunks), dim3(kBinThreads), ((tiles + 31) / 32) * sizeof(uint32_t),
+                       stream, chunk, g.order, g.n_visible, g.zcut, tiles, gx, ranges, g.sranges,
+                       redo ? g.redo_list : nullptr, redo ? g.redo_cnt : nullptr, g.sorted_len, g.far_cur, b.keys,
+                       (u64)cap);
+    return hipGetLastError();
+}
+
 hipError_t launch_sorted_lists_copy(uint32_t tiles, const uint2* ranges, const GeomState& g, const BinningState& b,
-                                    size_t cap, uint32_t* out, hipStream_t stream) {
+                                    size_t cap, uint32_t* out, hipStream_t stream, int P, uint32_t gx, bool near_first) {
     if (tiles == 0 || cap == 0) return hipSuccess;
+    if (near_first) {  // the far entries of every tile not rendered from its whole list, then their cursors reset
+        if (hipError_t e = launch_far_fill(P, g, gx, tiles, ranges, b, cap, false, stream)) return e;
+        if (hipError_t e = hipMemsetAsync(g.far_cur, 0, sizeof(uint32_t) * tiles, stream)) return e;
+    }
     hipLaunchKernelGGL(tile_sort_full_kernel, dim3(tiles < 2048 ? tiles : 2048), dim3(kClassThreads), 0, stream,
                        ranges, b.keys, (u64)cap, out, nullptr, nullptr, tiles, g.sorted_len, nullptr);
     hipLaunchKernelGGL(copy_sorted_prefix_kernel, dim3(tiles), dim3(64), 0, stream, ranges, (u64)cap, b.gid_sorted,

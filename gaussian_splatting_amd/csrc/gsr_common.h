@@ -133,9 +133,28 @@ struct GeomState {
     // rows), so any number of backwards of one forward start from zero.
     float4* acc;                // [P][kAccRow4]: (dcolour, dinvdepth), (dmean2D, dopacity, dconic.b), (dconic.a, .c, 0, 0), pad
     uint32_t* touched;          // [touched_words(P)] bit g: Gaussian g has a gradient term
+    // Near-first binning ("near_mass" option, binning.hip "Near-first binning"): only the Gaussians in
+    // front of a frame-wide depth cut enter the keys and the sort; the rest are emitted for a tile only
+    // if its forward walk passes its near entries (the redo).
+    uint32_t* mass;             // [P] opacity mass of each Gaussian's footprint, x kMassScale (preprocess)
+    uint32_t* near_cnt;         // [tiles] near instances per tile (K1; zeroed with tile_cnt)
+    unsigned long long* zhist;  // [kZBins] opacity mass by depth bin (K0a; zeroed with tile_cnt)
+    uint32_t* zcut;             // [1] the depth bin of the cut (K1 block 0): near iff zbin(depth) <= zcut
+    uint2* sranges;             // [tiles] each tile's near entries [start, start + near) (K3): K4's lists
+    uint32_t* far_cur;          // [tiles] far-fill cursors (zeroed by K4)
 };
 constexpr int kAccRow4 = 4;     // float4 per accumulator row: 64 bytes, one line (one memory-side atomic request)
 __host__ __device__ inline size_t touched_words(size_t P) { return (P + 31) / 32; }
+// Depth bins of the near-first cut: 16 per octave of view-space z from the near plane (0.2) on, by the
+// float bits (monotonic for z > 0): bin = (bits >> 19) - (bits(0.2f) >> 19), clamped to [0, kZBins).
+constexpr int kZBins = 256;
+constexpr uint32_t kZBinBase = 0x3E4CCCCDu >> 19;  // bits of 0.2f
+__host__ __device__ inline uint32_t zbin(uint32_t depth_bits) {
+    const uint32_t b = depth_bits >> 19;
+    return b <= kZBinBase ? 0u : (b - kZBinBase >= (uint32_t)kZBins ? (uint32_t)kZBins - 1u : b - kZBinBase);
+}
+constexpr float kMassScale = 16.f;  // fixed point of GeomState::mass (per pixel of footprint)
+constexpr uint32_t kZCutNone = 0xffffffffu;  // no cut: every Gaussian is near
 
 // Image state: per pixel and per tile.  The per-pixel planes are tile-major: pixel (x, y) of
 // tile t, in 8x8 quadrant q at lane l = (y & 7) * 8 + (x & 7), is element t * 256 + q * 64 + l

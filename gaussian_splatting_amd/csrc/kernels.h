@@ -483,15 +483,25 @@ hipError_t launch_mark_visible(int P, const float* means3D, const float* view, b
 // binning.hip
 size_t bin_chunk_count(int P);
 size_t bin_cell_count(uint32_t gx, uint32_t gy);
+// u32 words of the counters preprocess zeroes (GeomState::tile_cnt on): tile, cell and near counts, the
+// depth-mass histogram
+inline size_t bin_zero_words(size_t tiles, size_t cells) { return ((2 * tiles + cells + 1) & ~(size_t)1) + 2 * kZBins; }
 // host_total: mapped coherent host memory K2 (or the fused K3) also writes the instance count to, or
 // null.  fused (capacity mode, LDS cursors): K2 is folded into K3 -- launch_bin_count runs K0 + K1
 // only, launch_bin_scatter scans the counts and publishes ranges / classes / the count, and
 // launch_tile_sort re-zeroes the tile and cell counters.
+// near_target > 0 (fused only): near-first binning (binning.hip) with that depth-cut target (fixed-point
+// mass over the image: kMassScale x W x H x mean mass); launch_bin_scatter's near_first must agree.
 hipError_t launch_bin_count(int P, const GeomState& g, uint32_t gx, uint32_t gy, uint2* ranges, size_t cap,
-                            unsigned long long* host_total, hipStream_t stream, bool fused = false);
+                            unsigned long long* host_total, hipStream_t stream, bool fused = false,
+                            unsigned long long near_target = 0);
 hipError_t launch_bin_scatter(int P, const GeomState& g, uint32_t gx, uint32_t gy, const BinningState& b, size_t cap,
                               hipStream_t stream, uint2* ranges = nullptr, unsigned long long* host_total = nullptr,
-                              bool fused = false);
+                              bool fused = false, bool near_first = false);
+// the far instances of the tiles the forward filed for a redo (redo), behind their near entries
+hipError_t launch_far_fill(int P, const GeomState& g, uint32_t gx, uint32_t tiles, const uint2* ranges,
+                           const BinningState& b, size_t cap, bool redo, hipStream_t stream);
+bool bin_near_ok(uint32_t tiles);  // near-first binning applies (fused scan, K1 by rectangles)
 // prefix: sort only the first `prefix` (+ the rest of an LDS bin) entries of the lists longer than
 // one wave's sort (0: whole lists); GeomState::sorted_len records each list's sorted length.
 hipError_t launch_tile_sort(uint32_t tiles, const uint2* ranges, const GeomState& g, const BinningState& b,
@@ -504,7 +514,8 @@ hipError_t launch_tile_sort_redo(uint32_t tiles, const uint2* ranges, const Geom
 // Inspection: every tile's whole sorted list into `out` (the product's sorted entries, the rest
 // sorted here), without writing the forward's buffers.
 hipError_t launch_sorted_lists_copy(uint32_t tiles, const uint2* ranges, const GeomState& g, const BinningState& b,
-                                    size_t cap, uint32_t* out, hipStream_t stream);
+                                    size_t cap, uint32_t* out, hipStream_t stream, int P = 0, uint32_t gx = 0,
+                                    bool near_first = false);
 bool bin_fused_ok(uint32_t tiles);  // the fused form applies (LDS cursors)
 // render.hip
 // quads: 8x8 quadrants per wave, 2 (half tiles) or 4 (whole tiles; the "fwd_quads" option)

@@ -364,6 +364,17 @@ __global__ void __launch_bounds__(kPreThreads) GSR_PRE_OCCUPANCY preprocess_kern
         a.geom.tiles_touched[idx] = ok ? touched : 0u;
         a.geom.depth_key[idx] = ok ? __float_as_uint(p_view.z) : 0xffffffffu;
         a.geom.rect[idx] = make_uint2(rmin.x | (rmin.y << 16), rmax.x | (rmax.y << 16));
+        // the footprint's opacity mass, the integral of alpha over the plane (o 2 pi sqrt(det cov2D)), for
+        // the near-first binning's depth cut (binning.hip); fixed point, saturating
+        float mass = 0.f;
+        if (ok) {
+#if GSR_PRE_PREFETCH
+            mass = pf_op * h_scale * 6.2831853f * sqrtf(fmaxf(det, 0.f)) * kMassScale;
+#else
+            mass = a.opacities[idx] * h_scale * 6.2831853f * sqrtf(fmaxf(det, 0.f)) * kMassScale;
+#endif
+        }
+        a.geom.mass[idx] = (uint32_t)fminf(mass, 4.0e9f);
     }
     // the wave's 64 records as one contiguous 4 KiB store
     float4* s_rec = reinterpret_cast<float4*>(s_buf);

@@ -287,6 +287,11 @@ int gsr_debug_forward_state(int P, int width, int height, int R, int binning_cap
  * passed the sorted prefix (redo_count [1]).  Either pointer may be NULL. */
 int gsr_debug_sort_state(int P, int width, int height, const void* geom_buffer, unsigned int* sorted_len,
                          unsigned int* redo_count, void* stream);
+/* Near-first binning state of a forward (the "near_mass" option; tests): the depth bin of its cut
+ * (0xffffffff: none -- off, or the frame's opacity mass never reached the target) and, when there was a
+ * cut, each tile's near entries [start, start + near) as K4 sorted them ([tiles][2] uint32). */
+int gsr_debug_near_state(int P, int width, int height, const void* geom_buffer, unsigned int* zcut,
+                         unsigned int* near_ranges, void* stream);
 
 /* Number of forwards (process-wide) whose capacity hint was too small, so the binning stage
  * was redone with the exact count (gsr_rasterize_forward_ex). */
@@ -330,6 +335,12 @@ int gsr_host_stats(double* values, int n, int reset);
  *                        gauss_reduce; the order of the adds follows the hardware).  Read by the forward too,
  *                        which zeroes the rows when it is 1: a forward and its backwards must see one value.
  *                        The screen-space backward (view blocks) always takes the record path
+ *   "near_mass"  M|0    near-first binning (capacity-hinted forwards with the fused scan): only the Gaussians
+ *                        in front of the depth at which the screen-averaged opacity mass (the integral of
+ *                        alpha over the plane, summed front to back, over the image area) reaches M get keys
+ *                        and are sorted; a tile whose forward walk passes its near entries is redone with its
+ *                        whole list, so every output is the whole lists' (default M = 30; a pixel saturates
+ *                        at 9.2) | every instance keyed and sorted
  * Every option is read once per forward / backward call, so a concurrent gsr_option_set never splits
  * one call's launches between two values.
  * gsr_option_get returns -1 for an unknown name; gsr_option_set returns GSR_ERR_ARGUMENT for an

@@ -283,3 +283,34 @@ def _sh_eval(sh, dirs, deg):
                        + C3[4] * x * (4 * zz - xx - yy) * sh[:, 13] + C3[5] * z * (xx - yy) * sh[:, 14]
                        + C3[6] * x * (xx - 3 * yy) * sh[:, 15])
     return res
+
+
+def test_fullsize_near_first_bitwise(fullsize):
+    """Near-first binning at full size (binning.hip, the "near_mass" default): the capacity-hinted forward
+    keys and sorts only the Gaussians in front of the frame's depth cut; its images, radii, num_rendered
+    and gradients are bitwise those of the synchronising forward without a cut (the fixture's), and its
+    lists (near entries sorted by the product, the rest filled for inspection) equal the oracle's."""
+    from gaussian_splatting_amd import _C
+
+    inp, fwd = fullsize["inp"], fullsize["fwd"]
+    P = inp["means3D"].shape[0]
+    key = (torch.cuda.current_device(), inp["W"], inp["H"])
+    _C._capacity[key] = (P, int(fwd[0]))
+    fwd2 = C.run_gpu_forward(inp)
+    out2 = C.run_gpu_backward(inp, fwd2, *fullsize["unit"])
+    torch.cuda.synchronize()
+    nst = _C.debug_near_state(fwd2, P)
+    ss = _C.debug_sort_state(fwd2, P)
+    st = _C.debug_forward_state(fwd2, P)
+    _C._capacity.pop(key, None)
+    rg = st["ranges"].numpy()
+    n = rg[:, 1] - rg[:, 0]
+    near = nst["near_len"].numpy()
+    print(f"[{fullsize['name']}] near-first: cut bin {nst['zcut']}, keyed and sorted {int(near.sum())} of "
+          f"{int(n.sum())} instances ({near.sum() / max(1, n.sum()):.3f}), redone tiles {ss['redo_count']}")
+    assert (near <= n).all()
+    assert fwd2[0] == fwd[0]
+    assert torch.equal(fwd2[1], fwd[1]) and torch.equal(fwd2[2], fwd[2]) and torch.equal(fwd2[6], fwd[6])
+    for a, b in zip(out2, fullsize["out_unit"]):
+        assert torch.equal(a, b)
+    np.testing.assert_array_equal(st["point_list"].numpy(), fullsize["ref"].handle.binning()["point_list"].astype(np.int64))

@@ -41,6 +41,8 @@ VARIANTS = {
     "bwd_grid=1": dict(bwd_grid=1),           # render_bwd: one block per possible unit
     "bwd_grid=2": dict(bwd_grid=2),           # render_bwd: two blocks per tile walking units i, i + G, ...
     "bwd_atomic=1": dict(bwd_atomic=1),       # per-Gaussian float-atomic rows instead of records + gauss_reduce
+    "near_mass=0": dict(near_mass=0),         # no near-first binning: every instance keyed and sorted
+    "near_mass=1": dict(near_mass=1),         # a very early depth cut: far fills and redos in dense tiles
 }
 CASES = ["sh3_scalerot", "antialiasing", "dense_opaque", "lists_1k_2k", "lists_4k_8k", "lists_over_8k"]
 

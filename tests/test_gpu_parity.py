@@ -381,9 +381,11 @@ def test_sort_prefix_and_redo(name, prefix):
     inp = C.build(case)
     ref = C.run_oracle(inp)
     gc, gd = C.unit_grads(case.H, case.W)
-    with _lib.options(sort_prefix=0):
+    # (near-first binning off: every list is keyed whole, so sorted_len measures the prefix sort alone;
+    # test_near_first_binning covers the two together)
+    with _lib.options(sort_prefix=0, near_mass=0):
         whole = _run_pair(inp, gc, gd)
-    with _lib.options(sort_prefix=prefix):
+    with _lib.options(sort_prefix=prefix, near_mass=0):
         fwd = C.run_gpu_forward(inp)
         out = C.run_gpu_backward(inp, fwd, gc, gd)
         torch.cuda.synchronize()
@@ -444,3 +446,55 @@ def test_large_image(P, W, H):
     for k, got in zip(C.GRAD_NAMES, out):
         np.testing.assert_allclose(_to_np(got), r[k], atol=1e-5, rtol=0, err_msg=k)
     print(f"[large_image P={P} {W}x{H}] pixels over 1e-5: {int((d > ATOL_FWD).sum())}, all at threshold flips")
+
+
+@pytest.mark.parametrize("name,mass", [("dense_opaque", 1), ("dense_opaque", 4), ("lists_1k_2k", 2),
+                                       ("lists_4k_8k", 8), ("lists_over_8k", 30), ("sh3_scalerot", 1)])
+def test_near_first_binning(name, mass):
+    """Near-first binning (binning.hip, "near_mass"): with a capacity hint, only the Gaussians in front of
+    the depth at which the frame's screen-averaged opacity mass reaches `mass` get keys and are sorted; a
+    tile whose forward walk passes its near entries is filed, its far instances emitted behind them, its
+    whole list sorted and rendered again.  Small targets cut early, so many tiles are redone.  Checked:
+    a cut was made where the frame's mass reaches the target, each tile's near entries are a prefix of
+    its list and never longer, every list (near entries as the product sorted them, the far ones filled
+    and sorted for inspection) equals the oracle's, num_rendered / radii are the whole lists', and images
+    and gradients are bitwise those of the binning without a cut."""
+    from gaussian_splatting_amd import _C as CM
+    from gaussian_splatting_amd import _lib
+
+    case = next(c for c in C.SMALL_CASES if c.name == name)
+    inp = C.build(case)
+    ref = C.run_oracle(inp)
+    gc, gd = C.unit_grads(case.H, case.W)
+    key = (torch.cuda.current_device(), case.W, case.H)
+    with _lib.options(near_mass=0):
+        whole = _run_pair(inp, gc, gd)
+    CM._capacity[key] = (case.P, ref.num_rendered)  # the capacity-hinted (fused) forward takes the cut
+    with _lib.options(near_mass=mass):
+        fwd = C.run_gpu_forward(inp)
+        out = C.run_gpu_backward(inp, fwd, gc, gd)
+        torch.cuda.synchronize()
+        nst = CM.debug_near_state(fwd, case.P)
+        st = CM.debug_sort_state(fwd, case.P)
+        lists = CM.debug_forward_state(fwd, case.P)
+    CM._capacity.pop(key, None)
+    rng = lists["ranges"].numpy()
+    n = rng[:, 1] - rng[:, 0]
+    near = nst["near_len"].numpy()
+    # the screen-averaged mass, as the library forms it (radius > 0: visible)
+    g = ref.handle.geom()
+    conic, op = g["conic_opacity"][:, :3].astype(np.float64), g["conic_opacity"][:, 3].astype(np.float64)
+    det_inv = conic[:, 0] * conic[:, 2] - conic[:, 1] ** 2
+    m = np.where((ref.radii > 0) & (det_inv > 0), op * 2 * np.pi / np.sqrt(np.maximum(det_inv, 1e-30)), 0.0)
+    total = m.sum() / (case.W * case.H)
+    print(f"[{name} near_mass {mass}] frame mass {total:.1f}, cut bin {nst['zcut']}, near entries "
+          f"{int(near.sum())} of {int(n.sum())}, redone tiles {st['redo_count']}")
+    if total > 1.1 * mass:
+        assert nst["zcut"] is not None and near.sum() < n.sum()
+    assert (near <= n).all()
+    np.testing.assert_array_equal(lists["point_list"].numpy(), ref.handle.binning()["point_list"].astype(np.int64))
+    np.testing.assert_array_equal(_to_np(fwd[2]).astype(np.int32), ref.radii)
+    got = [fwd[0]] + [_to_np(fwd[i]) for i in (1, 2, 6)] + [_to_np(o) for o in out]
+    assert got[0] == whole[0] == ref.num_rendered
+    for a, b in zip(got[1:], whole[1:]):
+        np.testing.assert_array_equal(a, b)

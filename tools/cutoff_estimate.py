@@ -136,6 +136,20 @@ def main():
         if k < len(ids):
             cut[i] = depth[ids[k]]
     score(cut, "covering_mass_bound")
+    # a frame-wide cutoff a kernel can form from preprocess's outputs alone: the depth at which the
+    # screen-averaged opacity mass of the Gaussians in front (each o * 2 pi sqrt(det cov2D) / (W H), the
+    # integral of its alpha over the plane) reaches `target` (saturation needs -ln 1e-4 = 9.2 per pixel)
+    vis = radii > 0
+    det_inv = conic[:, 0] * conic[:, 2] - conic[:, 1] ** 2  # det of the conic = 1 / det cov2D
+    mass = np.where(vis & (det_inv > 0), op * 2 * np.pi / np.sqrt(np.maximum(det_inv, 1e-30)), 0.0) / (W * H)
+    order = np.argsort(depth[vis], kind="stable")
+    dz, cm = depth[vis][order], np.cumsum(mass[vis][order])
+    out["mass_profile"] = {f"{q}": float(np.interp(q, cm, dz)) for q in (5, 9.2, 20, 40, 80) if q < cm[-1]}
+    for target in (20, 40, 80):
+        if target < cm[-1]:
+            d = float(np.interp(target, cm, dz))
+            score(np.full(len(tiles), d, np.float32), f"mass_target_{target}")
+            out[f"mass_target_{target}"]["depth"] = d
     out["covering_mass_bound"]["note"] = ("sure bound (no redo by construction); needs per-(tile, Gaussian) "
                                           "corner tests in depth order before K3")
     print(json.dumps(out, indent=1))
