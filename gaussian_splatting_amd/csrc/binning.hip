@@ -1235,11 +1235,9 @@ __global__ void __launch_bounds__(kSortT) tile_sort_kernel(const uint2* __restri
                                                        uint32_t* __restrict__ far_cur) {
     __shared__ BucketLds<kSortT, kSortWaveMax, kSortWaveMax / 2> s;
     // fused binning: K2's re-zeroing of the counters (tile, cell and near counts, the depth-mass
-    // histogram: bin_zero_words), word blockIdx.x + k gridDim.x by thread k
-    if (zero_cnt) {
-        const uint32_t i = blockIdx.x + threadIdx.x * gridDim.x;
-        if (i < n_zero) zero_cnt[i] = 0u;
-    }
+    // histogram: bin_zero_words), strided over the grid's threads (a tiny frame has fewer threads than words)
+    if (zero_cnt)
+        for (uint32_t i = blockIdx.x * kSortT + threadIdx.x; i < n_zero; i += gridDim.x * kSortT) zero_cnt[i] = 0u;
     if (far_cur && threadIdx.x == 0) far_cur[blockIdx.x] = 0u;  // (near-first binning: the redo's far fill)
     const uint2 r = ranges[blockIdx.x];
     const uint32_t n = tile_len(r, cap);
@@ -1601,7 +1599,6 @@ hipError_t launch_tile_sort(uint32_t tiles, const uint2* ranges, const GeomState
     const u64 c = cap;
     const uint32_t lim = prefix ? prefix : ~0u;
     const uint32_t n_zero = (uint32_t)bin_zero_words(tiles, cells);
-    if (zero_counts && n_zero > (uint64_t)tiles * kSortT) return hipErrorInvalidValue;  // (never: ~2 words per tile)
     hipLaunchKernelGGL(tile_sort_kernel, dim3(tiles), dim3(kSortT), 0, stream, ranges, b.keys, c, b.gid_sorted,
                        zero_counts ? g.tile_cnt : nullptr, n_zero, g.sorted_len, g.redo_flag, g.redo_cnt, g.far_cur);
     // persistent class kernels: grids sized to fill the chip when their lists are long
