@@ -263,9 +263,11 @@ void carve_recs(char* base, size_t R, size_t P, gsr::GradRecs* recs, gsr::GradRe
         recs->c = c.take<float2>(R);
     }
     recs->flag = nullptr;  // in the binning buffer (BinningState::rec_flag)
-    sums->a = c.take<float4>(P);
-    sums->b = c.take<float4>(P);
-    sums->c = c.take<float2>(P);
+    // (per Gaussian for gauss_reduce, per live-list position for the atomic backward's gauss_live)
+    const size_t ns = std::max(P, (size_t)kLiveShards * live_list_cap((uint32_t)P));
+    sums->a = c.take<float4>(ns);
+    sums->b = c.take<float4>(ns);
+    sums->c = c.take<float2>(ns);
     sums->flag = nullptr;
     // the Gaussians with a gradient (gauss_reduce appends, gauss_bwd walks), kLiveShards shards
     *live = c.take<uint32_t>((size_t)kLiveShards * live_list_cap((uint32_t)P));
@@ -943,9 +945,14 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
     const size_t C_hint = capacity_hint > 0 ? capacity_for((size_t)capacity_hint) : 0;
     // capacity mode with LDS cursors: K2 folded into K3 (binning.hip FusedScan)
     const bool fused = capacity_hint > 0 && bin_fused_ok(tiles) && opt_fused;
-    // near-first binning (binning.hip): the depth cut's target, mass x kMassScale over the image
+    // near-first binning (binning.hip): the depth cut's target, mass x kMassScale over the image.  Only for frames
+    // whose lists are long (a mean of kNearMinMeanList entries by the capacity hint, the reachable-prefix sort's
+    // regime): there the blend reaches a small part of each list and the cut pays; with short lists (1M@1080p:
+    // 973) the frame's mass stays under the target anyway, and the redo chain's launches (far fill, whole
+    // sort, redo render: ~6 us when empty) would only cost (r5d: 0.7305 -> 0.7372-0.7404 ms with no cut made)
+    constexpr size_t kNearMinMeanList = 2048;
     const unsigned long long near_target =
-        fused && opt_near_mass > 0 && bin_near_ok(tiles)
+        fused && opt_near_mass > 0 && bin_near_ok(tiles) && C_hint >= kNearMinMeanList * (size_t)tiles
             ? (unsigned long long)opt_near_mass * (unsigned long long)kMassScale * (unsigned long long)width * height
             : 0ull;
     const bool near_first = near_target > 0;
@@ -1045,18 +1052,20 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
             // (C == 0: no lists and no K4, so nothing is prefix-sorted and no redo state was reset)
             if (C == 0) ra.sorted_len = nullptr;
             if (opt_atomic) {  // the atomic backward's accumulator rows and touched bits, zeroed beside the render
-                ra.fill.ptr[0] = reinterpret_cast<float*>(geom.acc);
-                ra.fill.n[0] = (unsigned long long)kAccRow4 * 4 * P;
-                ra.fill.ptr[1] = reinterpret_cast<float*>(geom.touched);
-                ra.fill.n[1] = touched_words((size_t)P);
-                ra.fill.count = 2;
+                ra.acc = geom.acc;
+                ra.touched = geom.touched;
+                ra.depth_key = geom.depth_key;
+                ra.zcut = geom.zcut;
+                ra.n_gauss = (uint32_t)P;
                 ra.fill_blocks = GSR_FWD_FILL_BLOCKS;
             }
             HIP_TRY(launch_render_fwd(ra, stream, opt_quads), "render_fwd");
             const bool near_now = fused_now && near_first;
             if ((prefix || near_now) && C > 0) {  // the tiles whose walk passed their sorted prefix (usually none)
-                if (near_now)  // their far instances first (none emitted by K3)
-                    HIP_TRY(launch_far_fill(P, geom, gx, tiles, img.ranges, bin, C, true, stream), "render_fwd far fill");
+                if (near_now)  // their far instances first (none emitted by K3); their accumulator rows zeroed
+                    HIP_TRY(launch_far_fill(P, geom, gx, tiles, img.ranges, bin, C, true, stream,
+                                            opt_atomic ? geom.acc : nullptr),
+                            "render_fwd far fill");
                 HIP_TRY(launch_tile_sort_redo(tiles, img.ranges, geom, bin, C, stream), "render_fwd redo sort");
                 HIP_TRY(launch_render_fwd_redo(ra, stream, opt_quads), "render_fwd redo");
             }
@@ -1329,7 +1338,7 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
     if (int rc = check_debug(debug, stream, "render_bwd")) return rc;
     if (atomic) {  // (stage "gauss_reduce": the step between render_bwd and gauss_bwd)
         StageScope sc(ST_GAUSS_REDUCE, stream);
-        HIP_TRY(launch_gauss_live(P, geom.touched, live, live_count, stream), "gauss_live");
+        HIP_TRY(launch_gauss_live(P, geom.touched, geom.acc, sums, live, live_count, stream), "gauss_live");
     } else {
         StageScope sc(ST_GAUSS_REDUCE, stream);
         HIP_TRY(launch_gauss_reduce(P, geom, recs, sums, flags, radii, live, live_count, stream),
@@ -1352,16 +1361,7 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
         ga.viewmatrix = viewmatrix; ga.projmatrix = projmatrix; ga.campos = campos;
         ga.tan_fovx = tan_fovx; ga.tan_fovy = tan_fovy; ga.focal_x = focal_x; ga.focal_y = focal_y;
         ga.antialiasing = antialiasing; ga.radii = radii; ga.geom = geom; ga.sums = sums;
-        ga.sum_stride4 = 1;
-        ga.sum_stride2 = 1;
-        if (atomic) {  // the accumulator rows: a at +0, b at +1 float4, c at +2 float4 of each 64-B row
-            ga.sums.a = geom.acc;
-            ga.sums.b = geom.acc + 1;
-            ga.sums.c = reinterpret_cast<float2*>(geom.acc + 2);
-            ga.sum_stride4 = kAccRow4;
-            ga.sum_stride2 = 2 * kAccRow4;
-            ga.acc_restore = geom.acc;
-        }
+        ga.sums_by_list = atomic ? 1 : 0;  // (gauss_live moved the rows' sums to list order)
         ga.have_invdepth = dL_dinvdepths != nullptr;
         ga.dL_dmean2D = dL_dmean2D; ga.dL_dconic = dL_dconic; ga.dL_dopacity = dL_dopacity; ga.dL_dcolor = dL_dcolor;
         ga.dL_dinvdepth = dL_dinvdepth; ga.dL_dmean3D = dL_dmean3D; ga.dL_dcov3D = dL_dcov3D;

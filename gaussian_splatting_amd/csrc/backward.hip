@@ -462,8 +462,12 @@ hipError_t launch_gauss_reduce(int P, const GeomState& g, const GradRecs& recs, 
 // it read, so the next backward of the same forward starts from zero bits (gauss_bwd clears the rows).
 // One lane per 32-bit word; the shard of Gaussian g is (g / 64) % kLiveShards, as in gauss_reduce, so
 // live_list_cap bounds every shard: lanes 2k and 2k + 1 (one 64-Gaussian group) share one append.
-__global__ void __launch_bounds__(64) gauss_live_kernel(int P, uint32_t* __restrict__ touched,
-                                                        uint32_t* __restrict__ live,
+// It also moves each listed Gaussian's sums out of its accumulator row into list order (sums.a/b/c indexed
+// by list position: gauss_bwd then reads them coalesced, instead of a row per lane that the memory-side
+// atomics left in no cache -- gauss_bwd 44 -> 55 us at 1M@1080p when it read the rows itself, r5d) and
+// zeroes the row for the next backward of this forward.
+__global__ void __launch_bounds__(64) gauss_live_kernel(int P, uint32_t* __restrict__ touched, float4* __restrict__ acc,
+                                                        GradRecs sums, uint32_t* __restrict__ live,
                                                         uint32_t* __restrict__ live_count, uint32_t live_cap) {
     const int lane = threadIdx.x;
     const size_t wi = (size_t)blockIdx.x * 64 + lane, nwords = touched_words((size_t)P);
@@ -476,15 +480,26 @@ __global__ void __launch_bounds__(64) gauss_live_kernel(int P, uint32_t* __restr
     if (!(lane & 1) && pair) base = atomicAdd(&live_count[shard * kLiveCntStride], pair);
     const uint32_t even_n = (uint32_t)__shfl((int)n, lane & ~1);
     base = (uint32_t)__shfl((int)base, lane & ~1) + ((lane & 1) ? even_n : 0u);
-    uint32_t* dst = live + (size_t)shard * live_cap + base;
-    for (uint32_t m = w; m; m &= m - 1u) *dst++ = (uint32_t)(wi * 32 + (size_t)__builtin_ctz(m));
+    const size_t pos0 = (size_t)shard * live_cap + base;
+    uint32_t k = 0;
+    for (uint32_t m = w; m; m &= m - 1u, k++) {
+        const uint32_t g = (uint32_t)(wi * 32 + (size_t)__builtin_ctz(m));
+        live[pos0 + k] = g;
+        float4* row = acc + (size_t)g * kAccRow4;
+        const float4 a = row[0], b = row[1], c = row[2];
+        sums.a[pos0 + k] = a;
+        sums.b[pos0 + k] = b;
+        sums.c[pos0 + k] = make_float2(c.x, c.y);
+        row[0] = row[1] = row[2] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
 }
 
-hipError_t launch_gauss_live(int P, uint32_t* touched, uint32_t* live, uint32_t* live_count, hipStream_t stream) {
+hipError_t launch_gauss_live(int P, uint32_t* touched, float4* acc, const GradRecs& sums, uint32_t* live,
+                             uint32_t* live_count, hipStream_t stream) {
     if (P <= 0) return hipSuccess;
     const size_t blocks = (touched_words((size_t)P) + 63) / 64;
-    hipLaunchKernelGGL(gauss_live_kernel, dim3((uint32_t)blocks), dim3(64), 0, stream, P, touched, live, live_count,
-                       live_list_cap((uint32_t)P));
+    hipLaunchKernelGGL(gauss_live_kernel, dim3((uint32_t)blocks), dim3(64), 0, stream, P, touched, acc, sums, live,
+                       live_count, live_list_cap((uint32_t)P));
     return hipGetLastError();
 }
 
@@ -838,11 +853,13 @@ __global__ void __launch_bounds__(64) GSR_GB_OCCUPANCY gauss_bwd_kernel(GaussBwd
     const int lane = threadIdx.x;
     const int g0 = blockIdx.x * 64;
     int idx = g0 + lane;
+    size_t lpos = 0;  // LIST: this lane's position in the live list (sums_by_list: where its sums are)
     if constexpr (LIST) {  // block b: entries [64 (b / shards), +64) of shard b % shards
         const uint32_t shard = blockIdx.x % kLiveShards, k0 = (blockIdx.x / kLiveShards) * 64;
         const uint32_t n = a.live_count[shard * kLiveCntStride];
         if (k0 >= n) return;  // uniform: past the shard's list (the grid is sized for the worst case)
         idx = k0 + lane < n ? (int)a.live[(size_t)shard * a.live_cap + k0 + lane] : a.P;
+        lpos = (size_t)shard * a.live_cap + k0 + lane;
     }
     const int nvalid = min(64, a.P - g0);
     const int M = a.M;
@@ -870,13 +887,10 @@ __global__ void __launch_bounds__(64) GSR_GB_OCCUPANCY gauss_bwd_kernel(GaussBwd
     int rad = 0;
     if (valid) {
         rad = a.radii[idx];
-        sa = a.sums.a[(size_t)idx * a.sum_stride4];
-        sb = a.sums.b[(size_t)idx * a.sum_stride4];
-        sc = a.sums.c[(size_t)idx * a.sum_stride2];
-        if (a.acc_restore) {  // atomic backward: the row back to zero for the next backward of this forward
-            float4* row = a.acc_restore + (size_t)idx * kAccRow4;
-            row[0] = row[1] = row[2] = make_float4(0.f, 0.f, 0.f, 0.f);
-        }
+        const size_t si = LIST && a.sums_by_list ? lpos : (size_t)idx;  // (atomic backward: list order, gauss_live)
+        sa = a.sums.a[si];
+        sb = a.sums.b[si];
+        sc = a.sums.c[si];
     }
     const bool any_grad = (sa.x != 0.f) | (sa.y != 0.f) | (sa.z != 0.f) | (sa.w != 0.f) | (sb.x != 0.f) |
                           (sb.y != 0.f) | (sb.z != 0.f) | (sb.w != 0.f) | (sc.x != 0.f) | (sc.y != 0.f);

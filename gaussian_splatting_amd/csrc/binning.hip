@@ -1650,7 +1650,7 @@ __global__ void __launch_bounds__(kBinThreads) tile_far_fill_kernel(int chunk, c
                                                                     const uint32_t* __restrict__ redo_cnt,
                                                                     const uint32_t* __restrict__ sorted_len,
                                                                     uint32_t* __restrict__ far_cur, u64* __restrict__ keys,
-                                                                    u64 cap) {
+                                                                    u64 cap, float4* __restrict__ acc) {
     extern __shared__ uint32_t s_sel[];  // (tiles + 31) / 32 words: selected tiles
     const uint32_t cut = *zcut;
     const uint32_t nred = redo_cnt ? redo_cnt[0] : 0u;
@@ -1683,19 +1683,24 @@ __global__ void __launch_bounds__(kBinThreads) tile_far_fill_kernel(int chunk, c
             const uint2 rr = ranges[t];
             const uint32_t at = sranges[t].y + atomicAdd(&far_cur[t], 1u);
             if (at < rr.y && at < cap) keys[at] = ((u64)kh << 32) | (kg << kEntryMaskBits);
+            if (acc) {  // (atomic backward: this Gaussian's row, which the forward's fill left alone, zeroed)
+                float4* row = acc + (size_t)kg * kAccRow4;
+#pragma unroll
+                for (int k = 0; k < kAccRow4; k++) row[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
         });
     }
 }
 
 hipError_t launch_far_fill(int P, const GeomState& g, uint32_t gx, uint32_t tiles, const uint2* ranges,
-                           const BinningState& b, size_t cap, bool redo, hipStream_t stream) {
+                           const BinningState& b, size_t cap, bool redo, hipStream_t stream, float4* acc) {
     if (tiles == 0 || cap == 0 || P == 0) return hipSuccess;
     int chunk = 0;
     const int nchunks = bin_chunks(P, &chunk);
     hipLaunchKernelGGL(tile_far_fill_kernel, dim3(nchunks), dim3(kBinThreads), ((tiles + 31) / 32) * sizeof(uint32_t),
                        stream, chunk, g.order, g.n_visible, g.zcut, tiles, gx, ranges, g.sranges,
                        redo ? g.redo_list : nullptr, redo ? g.redo_cnt : nullptr, g.sorted_len, g.far_cur, b.keys,
-                       (u64)cap);
+                       (u64)cap, redo ? acc : nullptr);
     return hipGetLastError();
 }
 

@@ -66,10 +66,16 @@ struct RenderFwdArgs {
     uint32_t* redo_flag;
     uint32_t* redo_list;
     uint32_t* redo_cnt;
-    // the first fill_blocks blocks of the launch zero `fill` (the atomic backward's accumulators,
-    // GeomState::acc / touched) beside the VALU-bound render waves, which leave HBM mostly idle
+    // the first fill_blocks blocks of the launch zero the atomic backward's accumulators beside the VALU-bound
+    // render waves, which leave HBM mostly idle: every touched word, and the row of every Gaussian that can
+    // reach a list the render walks -- visible and (near-first binning) in front of the cut; the rows of far
+    // Gaussians in redone tiles are zeroed by the far fill
     uint32_t fill_blocks;
-    FillArgs fill;
+    float4* acc;
+    uint32_t* touched;
+    const uint32_t* depth_key;
+    const uint32_t* zcut;
+    uint32_t n_gauss;
 };
 
 struct RenderBwdArgs {
@@ -122,11 +128,8 @@ struct GaussBwdArgs {
     int antialiasing;
     const int* radii;
     GeomState geom;
-    GradRecs sums;  // per Gaussian: summed render gradients (gauss_reduce_kernel, or the atomic rows)
-    // element strides of sums.a / .b (float4 units) and sums.c (float2 units): 1 / 1 for gauss_reduce's
-    // arrays, kAccRow4 / 2 kAccRow4 for the atomic backward's rows (GeomState::acc)
-    int sum_stride4, sum_stride2;
-    float4* acc_restore;  // atomic backward: zero each listed Gaussian's row after reading it, or null
+    GradRecs sums;  // per Gaussian: summed render gradients (gauss_reduce_kernel), or per live-list position
+    int sums_by_list;  // 1: sums indexed by live-list position (the atomic backward's gauss_live_kernel)
     int have_invdepth;
     float* dL_dmean2D;    // [P,3]
     float* dL_dconic;     // [P,4] or null
@@ -499,8 +502,9 @@ hipError_t launch_bin_scatter(int P, const GeomState& g, uint32_t gx, uint32_t g
                               hipStream_t stream, uint2* ranges = nullptr, unsigned long long* host_total = nullptr,
                               bool fused = false, bool near_first = false);
 // the far instances of the tiles the forward filed for a redo (redo), behind their near entries
+// acc (atomic backward, redo only): the accumulator rows of the far Gaussians filled in are zeroed too
 hipError_t launch_far_fill(int P, const GeomState& g, uint32_t gx, uint32_t tiles, const uint2* ranges,
-                           const BinningState& b, size_t cap, bool redo, hipStream_t stream);
+                           const BinningState& b, size_t cap, bool redo, hipStream_t stream, float4* acc = nullptr);
 bool bin_near_ok(uint32_t tiles);  // near-first binning applies (fused scan, K1 by rectangles)
 // prefix: sort only the first `prefix` (+ the rest of an LDS bin) entries of the lists longer than
 // one wave's sort (0: whole lists); GeomState::sorted_len records each list's sorted length.
@@ -545,8 +549,10 @@ hipError_t launch_ssim_bwd(int planes, int H, int W, const float* img1, const fl
 hipError_t launch_gauss_reduce(int P, const GeomState& g, const GradRecs& recs, const GradRecs& sums,
                                uint32_t* flags, const int* radii, uint32_t* live, uint32_t* live_count,
                                hipStream_t stream);
-// atomic backward: the live list from the touched bits (which it re-zeroes), instead of gauss_reduce
-hipError_t launch_gauss_live(int P, uint32_t* touched, uint32_t* live, uint32_t* live_count, hipStream_t stream);
+// atomic backward: the live list from the touched bits (which it re-zeroes), each listed Gaussian's sums moved
+// from its accumulator row (zeroed) to `sums` at its list position -- instead of gauss_reduce
+hipError_t launch_gauss_live(int P, uint32_t* touched, float4* acc, const GradRecs& sums, uint32_t* live,
+                             uint32_t* live_count, hipStream_t stream);
 // multi-view backward over gathered view blocks (backward.hip section 4)
 struct ViewsBwdArgs {
     int P, D, M;

@@ -508,8 +508,18 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const ui
 // there (fill_blocks is a multiple of 8, so a tile's blocks keep their XCD).
 __device__ __forceinline__ bool fwd_fill_block(const RenderFwdArgs& a, uint32_t& bid) {
     if (blockIdx.x < a.fill_blocks) {  // uniform
-        zero_fill_part(a.fill, (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x,
-                       (unsigned long long)a.fill_blocks * blockDim.x);
+        const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, stride = a.fill_blocks * blockDim.x;
+        const uint32_t cut = *a.zcut, words = (uint32_t)touched_words(a.n_gauss);
+        for (uint32_t i = tid; i < words; i += stride) a.touched[i] = 0u;
+        typedef float v4f __attribute__((ext_vector_type(4)));
+        for (uint32_t g = tid; g < a.n_gauss; g += stride) {
+            const uint32_t dk = a.depth_key[g];
+            if (dk != 0xffffffffu && (cut == kZCutNone || zbin(dk) <= cut)) {  // visible, in front of the cut
+                v4f* row = reinterpret_cast<v4f*>(a.acc + (size_t)g * kAccRow4);
+#pragma unroll
+                for (int k = 0; k < kAccRow4; k++) __builtin_nontemporal_store((v4f){0.f, 0.f, 0.f, 0.f}, row + k);
+            }
+        }
         return true;
     }
     bid = blockIdx.x - a.fill_blocks;

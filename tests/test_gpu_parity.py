@@ -448,13 +448,14 @@ def test_large_image(P, W, H):
     print(f"[large_image P={P} {W}x{H}] pixels over 1e-5: {int((d > ATOL_FWD).sum())}, all at threshold flips")
 
 
-@pytest.mark.parametrize("name,mass", [("dense_opaque", 1), ("dense_opaque", 4), ("lists_1k_2k", 2),
-                                       ("lists_4k_8k", 8), ("lists_over_8k", 30), ("sh3_scalerot", 1)])
+@pytest.mark.parametrize("name,mass", [("lists_4k_8k", 1), ("lists_4k_8k", 8), ("lists_over_8k", 2),
+                                       ("lists_over_8k", 30), ("lists_2k_4k", 1), ("dense_opaque", 1)])
 def test_near_first_binning(name, mass):
     """Near-first binning (binning.hip, "near_mass"): with a capacity hint, only the Gaussians in front of
     the depth at which the frame's screen-averaged opacity mass reaches `mass` get keys and are sorted; a
     tile whose forward walk passes its near entries is filed, its far instances emitted behind them, its
-    whole list sorted and rendered again.  Small targets cut early, so many tiles are redone.  Checked:
+    whole list sorted and rendered again.  Small targets cut early, so many tiles are redone.  It applies
+    to frames whose mean list is at least 2048 entries (api.hip kNearMinMeanList).  Checked:
     a cut was made where the frame's mass reaches the target, each tile's near entries are a prefix of
     its list and never longer, every list (near entries as the product sorted them, the far ones filled
     and sorted for inspection) equals the oracle's, num_rendered / radii are the whole lists', and images
@@ -489,8 +490,10 @@ def test_near_first_binning(name, mass):
     total = m.sum() / (case.W * case.H)
     print(f"[{name} near_mass {mass}] frame mass {total:.1f}, cut bin {nst['zcut']}, near entries "
           f"{int(near.sum())} of {int(n.sum())}, redone tiles {st['redo_count']}")
-    if total > 1.1 * mass:
+    if total > 1.1 * mass and n.mean() >= 2048:
         assert nst["zcut"] is not None and near.sum() < n.sum()
+    if (name, mass) == ("lists_4k_8k", 1):
+        assert st["redo_count"] > 0  # a cut this early leaves tiles whose walk passes their near entries
     assert (near <= n).all()
     np.testing.assert_array_equal(lists["point_list"].numpy(), ref.handle.binning()["point_list"].astype(np.int64))
     np.testing.assert_array_equal(_to_np(fwd[2]).astype(np.int32), ref.radii)
