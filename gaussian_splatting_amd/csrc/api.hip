@@ -305,8 +305,8 @@ void carve_recs(char* base, size_t R, size_t P, gsr::GradRecs* recs, gsr::GradRe
 #endif
 // "bwd_atomic": the render backward adds each instance's sums into per-Gaussian rows with float atomics
 // (render.hip ATOMIC) and gauss_live lists the touched Gaussians, instead of per-instance records summed
-// by gauss_reduce (deterministic).  The forward zeroes the rows when the option is on at forward time,
-// so a forward and its backwards must see the same value (an A/B switch: set it once).
+// by gauss_reduce (deterministic).  The forward zeroes the rows when the option is on at forward time and
+// marks its buffer (acc_mark below); a backward adds atomically iff the option is on and its buffer is marked.
 #ifndef GSR_BWD_ATOMIC_DEFAULT
 #define GSR_BWD_ATOMIC_DEFAULT 0
 #endif
@@ -365,6 +365,34 @@ int option_index(const char* name) {
     for (int i = 0; i < OPT_COUNT; i++)
         if (strcmp(name, kOptions[i].name) == 0) return i;
     return -1;
+}
+
+// The geometry buffers whose last forward zeroed the atomic backward's accumulator rows ("bwd_atomic" on at
+// forward time).  The backward takes the atomic path only for them: a buffer from a forward without the
+// option (or one the library never saw, e.g. copied in) gets the record path, which reads no rows.  Every
+// forward re-marks its buffer, so an address the caching allocator hands out again carries its latest
+// forward's choice.  Bounded: past kAccMarksMax entries the table starts over (misses take the record path).
+std::mutex g_acc_mu;
+std::vector<std::pair<const void*, bool>> g_acc_marks;
+constexpr size_t kAccMarksMax = 4096;
+
+void acc_mark(const void* geom_buffer, bool zeroed) {
+    std::lock_guard<std::mutex> lk(g_acc_mu);
+    for (auto& m : g_acc_marks)
+        if (m.first == geom_buffer) {
+            m.second = zeroed;
+            return;
+        }
+    if (!zeroed) return;  // (absent = not zeroed)
+    if (g_acc_marks.size() >= kAccMarksMax) g_acc_marks.clear();
+    g_acc_marks.emplace_back(geom_buffer, true);
+}
+
+bool acc_marked(const void* geom_buffer) {
+    std::lock_guard<std::mutex> lk(g_acc_mu);
+    for (const auto& m : g_acc_marks)
+        if (m.first == geom_buffer) return m.second;
+    return false;
 }
 
 // K2 folded into K3 in capacity mode.
@@ -906,6 +934,7 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
     char* gbase = (char*)call_alloc(geom_alloc, geom_ctx, geom_bytes);
     if (!gbase) return fail(GSR_ERR_ALLOC, "rasterize_forward: geometry buffer allocation failed");
     GeomState geom = carve_geom(gbase, P, gx, gy, &geom_bytes);
+    acc_mark(gbase, false);  // (set below once the render's fill blocks are queued)
     carve_image(nullptr, width, height, tiles, &img_bytes);
     char* ibase = (char*)call_alloc(image_alloc, image_ctx, img_bytes);
     if (!ibase) return fail(GSR_ERR_ALLOC, "rasterize_forward: image buffer allocation failed");
@@ -1060,6 +1089,7 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
                 ra.fill_blocks = GSR_FWD_FILL_BLOCKS;
             }
             HIP_TRY(launch_render_fwd(ra, stream, opt_quads), "render_fwd");
+            if (opt_atomic) acc_mark(gbase, true);
             const bool near_now = fused_now && near_first;
             if ((prefix || near_now) && C > 0) {  // the tiles whose walk passed their sorted prefix (usually none)
                 if (near_now)  // their far instances first (none emitted by K3); their accumulator rows zeroed
@@ -1236,9 +1266,9 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
     // With the outputs zero-filled, gauss_bwd walks a list of the Gaussians with a gradient
     // (~13% of a 1M@1080p view) that gauss_reduce appends to, instead of a lane per Gaussian.
     const bool use_list = zmode != 0 && live_list_mode();
-    // atomic backward: per-Gaussian rows (zeroed by the forward) instead of records + gauss_reduce; it
-    // needs the live list (the record path serves every other mode, and the view blocks)
-    const bool atomic = !screen && use_list && R > 0 && option(OPT_BWD_ATOMIC) != 0;
+    // atomic backward: per-Gaussian rows (zeroed by the forward, which marked its buffer) instead of records +
+    // gauss_reduce; it needs the live list (the record path serves every other mode, and the view blocks)
+    const bool atomic = !screen && use_list && R > 0 && option(OPT_BWD_ATOMIC) != 0 && acc_marked(geom_buffer);
     // (the atomic backward writes no per-instance records: no record scratch)
     const size_t R_recs = atomic ? 0 : (size_t)R;
     carve_recs(nullptr, R_recs, (size_t)P, &recs, &sums, &live, &live_count, &rec_bytes);

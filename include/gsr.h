@@ -332,8 +332,10 @@ int gsr_host_stats(double* values, int n, int reset);
  *   "bwd_atomic" 0|1    the render backward writes one gradient record per (tile, Gaussian) instance, summed
  *                        per Gaussian by gauss_reduce in a fixed order: bitwise deterministic (default) | adds
  *                        each instance's ten sums into per-Gaussian rows with float atomics (no records, no
- *                        gauss_reduce; the order of the adds follows the hardware).  Read by the forward too,
- *                        which zeroes the rows when it is 1: a forward and its backwards must see one value.
+ *                        gauss_reduce; the order of the adds follows the hardware).  Read by the forward,
+ *                        which zeroes the rows when it is 1 and marks its geometry buffer; a backward takes
+ *                        the atomic path iff the option is 1 and its geometry buffer carries that mark (a
+ *                        buffer from a forward without the option, or one copied in, gets the record path).
  *                        The screen-space backward (view blocks) always takes the record path
  *   "near_mass"  M|0    near-first binning (capacity-hinted forwards with the fused scan): only the Gaussians
  *                        in front of the depth at which the screen-averaged opacity mass (the integral of

@@ -17,7 +17,9 @@ frame on the host.  What is checked:
     differs: a flip moves that pixel's whole term in or out of its gradient.  Those are counted,
     printed with their own error and held to max |diff| / max |ref| <= 2e-3; with the L1 upstream
     gradient every Gaussian, flips included, is within 1e-5 absolute (north_star's bar);
-  * bitwise determinism and the reference's colours-precomputed consistency switch.
+  * both backward paths ("bwd_atomic"): the record path and the atomic one each to the bars above, the
+    record path bitwise deterministic, the atomic one within float32 re-association of it;
+  * the reference's colours-precomputed consistency switch.
 """
 import os
 
@@ -48,7 +50,7 @@ def _np(t):
 
 @pytest.fixture(scope="module", params=["500k_1080p_sh3", "1m_1080p_sh3", "5m_4k_sh3"])
 def fullsize(request):
-    from gaussian_splatting_amd import _C
+    from gaussian_splatting_amd import _C, _lib
 
     scene, cam = syn.config_scene(request.param, seed=0)
     inp = dict(bg=torch.zeros(3), means3D=scene.means3D, opacities=scene.opacities, shs=scene.shs,
@@ -61,13 +63,21 @@ def fullsize(request):
     unit = C.unit_grads(cam.height, cam.width, seed=11)
     ref_l1 = ref.handle.backward(*l1, nthreads=THREADS)
     ref_unit = ref.handle.backward(*unit, nthreads=THREADS)
-    fwd = C.run_gpu_forward(inp)
-    state = _C.debug_forward_state(fwd, scene.means3D.shape[0])
-    out_l1 = C.run_gpu_backward(inp, fwd, *l1)
-    out_unit = C.run_gpu_backward(inp, fwd, *unit)
+    # both backward paths ("bwd_atomic", read by the forward): the deterministic record path, against which
+    # the bitwise tests compare, and the atomic one, each held to the oracle bars
+    with _lib.options(bwd_atomic=0):
+        fwd = C.run_gpu_forward(inp)
+        state = _C.debug_forward_state(fwd, scene.means3D.shape[0])
+        out_l1 = C.run_gpu_backward(inp, fwd, *l1)
+        out_unit = C.run_gpu_backward(inp, fwd, *unit)
+    with _lib.options(bwd_atomic=1):
+        fwd_a = C.run_gpu_forward(inp)
+        out_l1_a = C.run_gpu_backward(inp, fwd_a, *l1)
+        out_unit_a = C.run_gpu_backward(inp, fwd_a, *unit)
     torch.cuda.synchronize()
     return dict(name=request.param, inp=inp, ref=ref, ref_l1=ref_l1, ref_unit=ref_unit, fwd=fwd, state=state,
-                out_l1=out_l1, out_unit=out_unit, l1=l1, unit=unit)
+                out_l1=out_l1, out_unit=out_unit, l1=l1, unit=unit, fwd_atomic=fwd_a, out_l1_atomic=out_l1_a,
+                out_unit_atomic=out_unit_a)
 
 
 def test_fullsize_integers_identical(fullsize):
@@ -173,12 +183,13 @@ def _tile_members(fullsize, flipped):
     return mask
 
 
+@pytest.mark.parametrize("path", ["record", "atomic"])
 @pytest.mark.parametrize("upstream", ["unit", "l1"])
-def test_fullsize_backward(fullsize, upstream):
+def test_fullsize_backward(fullsize, upstream, path):
     d, over, nc_diff, near, _ = _flips(fullsize)
     taint = _tainted(fullsize, nc_diff)
     ref_g = fullsize["ref_unit" if upstream == "unit" else "ref_l1"]
-    out = fullsize["out_unit" if upstream == "unit" else "out_l1"]
+    out = fullsize[("out_unit" if upstream == "unit" else "out_l1") + ("_atomic" if path == "atomic" else "")]
     rows = []
     for k, got in zip(C.GRAD_NAMES, out):
         g, e = _np(got).astype(np.float64), ref_g[k]
@@ -188,11 +199,11 @@ def test_fullsize_backward(fullsize, upstream):
         clean = float(diff[~taint].max()) / scale if (~taint).any() else 0.0
         dirty = float(diff[taint].max()) / scale if taint.any() else 0.0
         rows.append((k, scale, clean, dirty))
-    print(f"[{fullsize['name']}/{upstream}] Gaussians at a threshold flip: {int(taint.sum())} "
+    print(f"[{fullsize['name']}/{upstream}/{path}] Gaussians at a threshold flip: {int(taint.sum())} "
           f"of {taint.size}; per tensor (max|ref|, max rel elsewhere, max rel at flips): "
           + "; ".join(f"{k} {s:.2e} {c:.2e} {t:.2e}" for k, s, c, t in rows))
     worst = max(rows, key=lambda r: r[3])
-    print(f"[{fullsize['name']}/{upstream}] worst Gaussian at a flip: {worst[0]} rel {worst[3]:.2e} "
+    print(f"[{fullsize['name']}/{upstream}/{path}] worst Gaussian at a flip: {worst[0]} rel {worst[3]:.2e} "
           f"(bar {RTOL_GRAD_FLIP:.0e})")
     for k, s, c, t in rows:
         assert c <= RTOL_GRAD, (k, c)
@@ -207,7 +218,9 @@ def test_fullsize_backward(fullsize, upstream):
     assert taint.mean() <= 0.05, taint.mean()
 
 
+@pytest.mark.record_path
 def test_fullsize_deterministic(fullsize):
+    """The record path (bwd_atomic=0) is bitwise deterministic; the forward is, whatever the backward path."""
     inp, fwd, out = fullsize["inp"], fullsize["fwd"], fullsize["out_unit"]
     fwd2 = C.run_gpu_forward(inp)
     out2 = C.run_gpu_backward(inp, fwd2, *fullsize["unit"])
@@ -215,6 +228,38 @@ def test_fullsize_deterministic(fullsize):
     assert torch.equal(fwd2[1], fwd[1]) and torch.equal(fwd2[6], fwd[6])
     for a, b in zip(out, out2):
         assert torch.equal(a, b)
+    fa = fullsize["fwd_atomic"]
+    assert fa[0] == fwd[0] and torch.equal(fa[1], fwd[1]) and torch.equal(fa[2], fwd[2]) and torch.equal(fa[6], fwd[6])
+
+
+def test_fullsize_atomic_matches_record(fullsize):
+    """The atomic backward sums the same instance terms as the record path in the hardware's order: per
+    tensor, max |atomic - record| / max |record| stays at float32 re-association size (bar 1e-5; a
+    threshold flip cannot differ between them, both walk the same forward), as close for a second atomic
+    backward of the same forward (the first restored its rows to zero) and for the capacity-hinted forward
+    with near-first binning (the far fill zeroes the rows of the far Gaussians it files)."""
+    from gaussian_splatting_amd import _C, _lib
+
+    inp = fullsize["inp"]
+    out_a, out_r = fullsize["out_unit_atomic"], fullsize["out_unit"]
+    with _lib.options(bwd_atomic=1):
+        again = C.run_gpu_backward(inp, fullsize["fwd_atomic"], *fullsize["unit"])
+    key = (torch.cuda.current_device(), inp["W"], inp["H"])
+    _C._capacity[key] = (inp["means3D"].shape[0], int(fullsize["fwd"][0]))
+    with _lib.options(bwd_atomic=1):
+        fwd_n = C.run_gpu_forward(inp)
+        near = C.run_gpu_backward(inp, fwd_n, *fullsize["unit"])
+    _C._capacity.pop(key, None)
+    torch.cuda.synchronize()
+    assert torch.equal(fwd_n[1], fullsize["fwd"][1])
+    rows = []
+    for k, a, r, b, n in zip(C.GRAD_NAMES, out_a, out_r, again, near):
+        scale = max(float(r.abs().max()), 1e-30)
+        rows.append((k, *(float((x - r).abs().max()) / scale for x in (a, b, n))))
+    print(f"[{fullsize['name']}] atomic vs record, max|d|/max|ref| (first, second backward, near-first forward): "
+          + "; ".join(f"{k} {x:.1e} {y:.1e} {z:.1e}" for k, x, y, z in rows))
+    for k, *v in rows:
+        assert max(v) <= 1e-5, (k, v)
 
 
 def test_fullsize_colors_precomp_matches_sh(fullsize):
@@ -232,6 +277,7 @@ def test_fullsize_colors_precomp_matches_sh(fullsize):
     assert float(d.mean()) <= 1e-6
 
 
+@pytest.mark.record_path
 def test_fullsize_separate_sh_bitwise(fullsize):
     """The SH layout train.py passes (separate_sh: dc [P,1,3] + rest [P,15,3], the 3DGS-accel entry points)
     gives the combined layout's image and gradients bit for bit at full size -- its own staging paths
@@ -285,6 +331,7 @@ def _sh_eval(sh, dirs, deg):
     return res
 
 
+@pytest.mark.record_path
 def test_fullsize_near_first_bitwise(fullsize):
     """Near-first binning at full size (binning.hip, the "near_mass" default): the capacity-hinted forward
     keys and sorts only the Gaussians in front of the frame's depth cut; its images, radii, num_rendered

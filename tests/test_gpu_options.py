@@ -9,7 +9,8 @@ synchronising and the capacity-hint forward:
   * integers identical to the f32 oracle: num_rendered, radii, the sorted tile lists;
   * colour / inverse depth within 1e-5; gradients within 1e-5 absolute with the L1 upstream
     gradient and 2e-4 of max |ref| with a unit one;
-  * and against the default path itself: bitwise equal, except the backward of "bwd_seg_ck",
+  * and against the record path with the other defaults (bwd_atomic=0 is the base here, whatever the
+    library's default, tests/conftest.py record_path): bitwise equal, except the backward of "bwd_seg_ck",
     whose work units start from other blend checkpoints (the same sums in another rounding), the
     backward of "bwd_atomic", whose per-Gaussian sums are added in the hardware's order (and whose
     second backward of one forward checks that the first restored its accumulators to zero), and
@@ -43,6 +44,7 @@ VARIANTS = {
     "bwd_atomic=1": dict(bwd_atomic=1),       # per-Gaussian float-atomic rows instead of records + gauss_reduce
     "near_mass=0": dict(near_mass=0),         # no near-first binning: every instance keyed and sorted
     "near_mass=1": dict(near_mass=1),         # a very early depth cut: far fills and redos in dense tiles
+    "bwd_atomic=1,near_mass=1": dict(bwd_atomic=1, near_mass=1),  # the far fill zeroes the far rows it files
 }
 CASES = ["sh3_scalerot", "antialiasing", "dense_opaque", "lists_1k_2k", "lists_4k_8k", "lists_over_8k"]
 
@@ -70,6 +72,7 @@ def _run(inp, case, grads, hint):
 @pytest.mark.parametrize("hint", [False, True], ids=["sync", "hint"])
 @pytest.mark.parametrize("case_name", CASES)
 @pytest.mark.parametrize("variant", sorted(VARIANTS))
+@pytest.mark.record_path
 def test_option_path_matches_oracle(variant, case_name, hint):
     from gaussian_splatting_amd import _C as CM
     from gaussian_splatting_amd import _lib
@@ -110,6 +113,7 @@ def test_option_path_matches_oracle(variant, case_name, hint):
 
 @pytest.mark.parametrize("seg_ck", [2, 1 << 20])
 @pytest.mark.parametrize("case_name", ["lists_1k_2k", "lists_over_8k"])
+@pytest.mark.record_path
 def test_seg_ck_set_around_forward_only(seg_ck, case_name):
     """the backward walks the work units its OWN forward wrote.  A forward run with
     bwd_seg_ck = k and a backward run after the option is restored (and the reverse) must give the
@@ -143,20 +147,26 @@ def test_atomic_backward_repeats(case_name):
     """bwd_atomic: the forward zeroes the accumulator rows and touched bits, and each backward restores
     what it used to zero (gauss_live the bits, gauss_bwd the rows), so three backwards of one forward
     agree to float rounding of the add order (a row left over would double a Gaussian's gradient);
-    and a record-path backward of a forward run with the option on equals the default path bitwise."""
+    a record-path backward of a forward run with the option on equals the record path bitwise, and so
+    does a backward with the option on of a forward without it (its buffer is not marked: no rows zeroed)."""
     from gaussian_splatting_amd import _lib
 
     case = next(c for c in C.SMALL_CASES if c.name == case_name)
     inp = C.build(case)
     gc, gd = C.l1_grads(case.H, case.W)
+    with _lib.options(bwd_atomic=0):
+        base_fwd = C.run_gpu_forward(inp)
     with _lib.options(bwd_atomic=1):
         fwd = C.run_gpu_forward(inp)
         outs = [C.run_gpu_backward(inp, fwd, gc, gd) for _ in range(3)]
-    rec = C.run_gpu_backward(inp, fwd, gc, gd)  # the record path on the same buffers
-    base = C.run_gpu_backward(inp, C.run_gpu_forward(inp), gc, gd)
+    with _lib.options(bwd_atomic=0):
+        rec = C.run_gpu_backward(inp, fwd, gc, gd)  # the record path on the same buffers
+        base = C.run_gpu_backward(inp, C.run_gpu_forward(inp), gc, gd)
+    with _lib.options(bwd_atomic=1):  # a forward without the option: its backward takes the record path
+        unmarked = C.run_gpu_backward(inp, base_fwd, gc, gd)
     torch.cuda.synchronize()
-    for a, b in zip(rec, base):
-        assert torch.equal(a, b)
+    for a, b, u in zip(rec, base, unmarked):
+        assert torch.equal(a, b) and torch.equal(u, b)
     for o in outs:
         for k, a, b in zip(C.GRAD_NAMES, o, base):
             scale = float(b.abs().max()) or 1.0

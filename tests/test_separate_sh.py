@@ -71,6 +71,7 @@ def test_dropin_exports_sparse_adam():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", CASES, ids=lambda c: c.name)
+@pytest.mark.record_path
 def test_split_equals_combined_bitwise(case):
     dev = "cuda"
     inp = C.build(case)
@@ -100,6 +101,7 @@ def test_split_equals_combined_bitwise(case):
 
 
 @pytest.mark.gpu
+@pytest.mark.record_path
 def test_rasterizer_module_separate_sh_autograd():
     """GaussianRasterizer(dc=..., shs=...) as gaussian_renderer/__init__.py:115-125 calls it: gradients land on
     dc and shs, equal to the combined path's split gradient."""

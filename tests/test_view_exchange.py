@@ -93,6 +93,7 @@ def _views_backward(t, blocks, split, dev, flags=None, live=None, out=None):
 @pytest.mark.parametrize("split", [False, True])
 @pytest.mark.parametrize("case_kw", [dict(P=300, W=64, H=48), dict(P=250, W=48, H=40, sh_degree=1),
                                      dict(P=300, W=64, H=48, antialiasing=True)])
+@pytest.mark.record_path
 def test_one_view_equals_single_view(case_kw, split):
     dev = torch.device("cuda", 0)
     inp, case = _view_inputs(case_kw, 0.0, dev)
@@ -109,6 +110,7 @@ def test_one_view_equals_single_view(case_kw, split):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("split", [False, True])
+@pytest.mark.record_path
 def test_views_sum_equals_sum_of_single_views(split):
     dev = torch.device("cuda", 0)
     blocks, sums = [], None
