@@ -308,7 +308,7 @@ void carve_recs(char* base, size_t R, size_t P, gsr::GradRecs* recs, gsr::GradRe
 // by gauss_reduce (deterministic).  The forward zeroes the rows when the option is on at forward time and
 // marks its buffer (acc_mark below); a backward adds atomically iff the option is on and its buffer is marked.
 #ifndef GSR_BWD_ATOMIC_DEFAULT
-#define GSR_BWD_ATOMIC_DEFAULT 0
+#define GSR_BWD_ATOMIC_DEFAULT 1
 #endif
 #ifndef GSR_FWD_FILL_BLOCKS
 #define GSR_FWD_FILL_BLOCKS 256  // one-wave blocks zeroing the accumulators in render_fwd's launch (a multiple of 8)

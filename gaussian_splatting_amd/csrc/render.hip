@@ -668,7 +668,8 @@ hipError_t launch_render_fwd(const RenderFwdArgs& a, hipStream_t stream, int qua
 // (< 10) of listed entry k -- so an instruction touches four 64-byte rows, the shape the memory-side
 // atomic units take at full rate (MI355X_MICROARCH.md "Global float atomics": 64 lanes in 64 rows
 // run ~17x slower).  The summation order over a Gaussian's instances then follows the hardware, so
-// the result is not bitwise reproducible; the record path (the default) is.
+// the result is not bitwise reproducible; the record path (bwd_atomic=0) is.  The default since r5f:
+// 1M@1080p 0.7335 -> 0.7320 ms, 5M@4K 2.328 -> 2.224 ms (gauss_reduce gone; profiles/r05/r5f).
 template <bool CENSUS, bool STRIDED, bool ATOMIC>
 __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(RenderBwdArgs a) {
   {

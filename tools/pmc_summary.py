@@ -20,7 +20,7 @@ import glob
 import os
 
 SHORT = [("render_bwd", "render_bwd"), ("render_fwd", "render_fwd"), ("gauss_bwd", "gauss_bwd"),
-         ("gauss_reduce", "gauss_reduce"), ("preprocess", "preprocess"), ("tile_count", "tile_count"),
+         ("gauss_reduce", "gauss_reduce"), ("gauss_live", "gauss_live"), ("preprocess", "preprocess"), ("tile_count", "tile_count"),
          ("tile_scan", "tile_scan"), ("tile_scatter", "tile_scatter"), ("tile_sort_class_kernel<128>", "tile_sort_c1"),
          ("tile_sort_class_kernel<512>", "tile_sort_c2"), ("tile_sort_global", "tile_sort_c3"),
          ("tile_sort_kernel", "tile_sort")]
