@@ -458,38 +458,41 @@ hipError_t launch_gauss_reduce(int P, const GeomState& g, const GradRecs& recs, 
 
 // ---- 1b. atomic backward: the live list from the touched bits ----------------------
 // render_bwd ("bwd_atomic") added every instance's sums into its Gaussian's accumulator row and set
-// the Gaussian's bit; this lists the Gaussians with a bit (gauss_bwd's live list) and clears the words
-// it read, so the next backward of the same forward starts from zero bits (gauss_bwd clears the rows).
-// One lane per 32-bit word; the shard of Gaussian g is (g / 64) % kLiveShards, as in gauss_reduce, so
-// live_list_cap bounds every shard: lanes 2k and 2k + 1 (one 64-Gaussian group) share one append.
-// It also moves each listed Gaussian's sums out of its accumulator row into list order (sums.a/b/c indexed
-// by list position: gauss_bwd then reads them coalesced, instead of a row per lane that the memory-side
-// atomics left in no cache -- gauss_bwd 44 -> 55 us at 1M@1080p when it read the rows itself, r5d) and
-// zeroes the row for the next backward of this forward.
+// the Gaussian's bit; this lists the Gaussians with a bit (gauss_bwd's live list), moves their sums to
+// list order and clears the rows and words it read, so the next backward of the same forward starts
+// from zero.
+// One lane per Gaussian, as gauss_reduce (so its live-list order and shards are gauss_reduce's): the wave
+// of Gaussians [64 b, 64 b + 64) reads its two touched words, appends its touched Gaussians to shard b %
+// kLiveShards with one atomic, and each touched lane moves its row's sums to its list position and zeroes
+// the row -- every row load of the wave in flight at once.  (One lane per 32-bit word walked a word's set
+// bits one dependent row load after another, 489 waves at 1M: 21.5 us, r5f.)
 __global__ void __launch_bounds__(64) gauss_live_kernel(int P, uint32_t* __restrict__ touched, float4* __restrict__ acc,
                                                         GradRecs sums, uint32_t* __restrict__ live,
                                                         uint32_t* __restrict__ live_count, uint32_t live_cap) {
     const int lane = threadIdx.x;
-    const size_t wi = (size_t)blockIdx.x * 64 + lane, nwords = touched_words((size_t)P);
-    const uint32_t w = wi < nwords ? touched[wi] : 0u;
-    if (w) touched[wi] = 0u;
-    const uint32_t n = (uint32_t)__popc(w);
-    const uint32_t pair = n + (uint32_t)__shfl_xor((int)n, 1);
-    const uint32_t shard = (uint32_t)((wi >> 1) % kLiveShards);
+    const uint32_t g = blockIdx.x * 64u + (uint32_t)lane;
+    const uint32_t w = g < (uint32_t)P ? touched[g >> 5] : 0u;  // (two words per wave, each read by 32 lanes)
+    const bool lv = (w >> (g & 31u)) & 1u;
+    const unsigned long long m = __ballot(lv);
+    if (!m) return;  // uniform
+    float4 ra, rb, rc;
+    float4* row = acc + (size_t)g * kAccRow4;
+    if (lv) {
+        ra = row[0];
+        rb = row[1];
+        rc = row[2];
+    }
     uint32_t base = 0;
-    if (!(lane & 1) && pair) base = atomicAdd(&live_count[shard * kLiveCntStride], pair);
-    const uint32_t even_n = (uint32_t)__shfl((int)n, lane & ~1);
-    base = (uint32_t)__shfl((int)base, lane & ~1) + ((lane & 1) ? even_n : 0u);
-    const size_t pos0 = (size_t)shard * live_cap + base;
-    uint32_t k = 0;
-    for (uint32_t m = w; m; m &= m - 1u, k++) {
-        const uint32_t g = (uint32_t)(wi * 32 + (size_t)__builtin_ctz(m));
-        live[pos0 + k] = g;
-        float4* row = acc + (size_t)g * kAccRow4;
-        const float4 a = row[0], b = row[1], c = row[2];
-        sums.a[pos0 + k] = a;
-        sums.b[pos0 + k] = b;
-        sums.c[pos0 + k] = make_float2(c.x, c.y);
+    const uint32_t shard = blockIdx.x % kLiveShards;
+    if (lane == 0) base = atomicAdd(&live_count[shard * kLiveCntStride], (uint32_t)__popcll(m));
+    if ((lane & 31) == 0 && w) touched[g >> 5] = 0u;  // (after every lane's read of the word: one instruction)
+    base = (uint32_t)__shfl((int)base, 0);
+    if (lv) {
+        const size_t pos = (size_t)shard * live_cap + base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        live[pos] = g;
+        sums.a[pos] = ra;
+        sums.b[pos] = rb;
+        sums.c[pos] = make_float2(rc.x, rc.y);
         row[0] = row[1] = row[2] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
 }
@@ -497,7 +500,7 @@ __global__ void __launch_bounds__(64) gauss_live_kernel(int P, uint32_t* __restr
 hipError_t launch_gauss_live(int P, uint32_t* touched, float4* acc, const GradRecs& sums, uint32_t* live,
                              uint32_t* live_count, hipStream_t stream) {
     if (P <= 0) return hipSuccess;
-    const size_t blocks = (touched_words((size_t)P) + 63) / 64;
+    const size_t blocks = ((size_t)P + 63) / 64;
     hipLaunchKernelGGL(gauss_live_kernel, dim3((uint32_t)blocks), dim3(64), 0, stream, P, touched, acc, sums, live,
                        live_count, live_list_cap((uint32_t)P));
     return hipGetLastError();
