@@ -461,46 +461,81 @@ hipError_t launch_gauss_reduce(int P, const GeomState& g, const GradRecs& recs, 
 // the Gaussian's bit; this lists the Gaussians with a bit (gauss_bwd's live list), moves their sums to
 // list order and clears the rows and words it read, so the next backward of the same forward starts
 // from zero.
-// One lane per Gaussian, as gauss_reduce (so its live-list order and shards are gauss_reduce's): the wave
-// of Gaussians [64 b, 64 b + 64) reads its two touched words, appends its touched Gaussians to shard b %
-// kLiveShards with one atomic, and each touched lane moves its row's sums to its list position and zeroes
-// the row -- every row load of the wave in flight at once.  (One lane per 32-bit word walked a word's set
-// bits one dependent row load after another, 489 waves at 1M: 21.5 us, r5f.)
+// One lane per Gaussian of kLiveGroups 64-Gaussian groups, each group as gauss_reduce's wave (so the
+// live-list order and shards are gauss_reduce's: group q appends to shard q % kLiveShards): the wave
+// reads its groups' touched words, appends each group's touched Gaussians with one atomic, and each
+// touched lane moves its rows' sums to their list positions and zeroes the rows -- every row load and
+// counter atomic of the wave in flight at once.  The kernel is a chain of dependent memory round
+// trips (word -> rows + counter -> stores), so it pays to have few waves each carrying several
+// groups: one lane per 32-bit word walked a word's bits one dependent row load after another (489
+// waves at 1M@1080p: 21.5 us, r5f); one group per wave, 15.6k waves, 15.4 us (r5h).
+#ifndef GSR_LIVE_GROUPS
+#define GSR_LIVE_GROUPS 4
+#endif
+constexpr int kLiveGroups = GSR_LIVE_GROUPS;
 __global__ void __launch_bounds__(64) gauss_live_kernel(int P, uint32_t* __restrict__ touched, float4* __restrict__ acc,
                                                         GradRecs sums, uint32_t* __restrict__ live,
                                                         uint32_t* __restrict__ live_count, uint32_t live_cap) {
     const int lane = threadIdx.x;
-    const uint32_t g = blockIdx.x * 64u + (uint32_t)lane;
-    const uint32_t w = g < (uint32_t)P ? touched[g >> 5] : 0u;  // (two words per wave, each read by 32 lanes)
-    const bool lv = (w >> (g & 31u)) & 1u;
-    const unsigned long long m = __ballot(lv);
-    if (!m) return;  // uniform
-    float4 ra, rb, rc;
-    float4* row = acc + (size_t)g * kAccRow4;
-    if (lv) {
-        ra = row[0];
-        rb = row[1];
-        rc = row[2];
+    const uint32_t q0 = blockIdx.x * kLiveGroups;  // this wave's first group
+    uint32_t w[kLiveGroups];
+    unsigned long long m[kLiveGroups];
+#pragma unroll
+    for (int j = 0; j < kLiveGroups; j++) {
+        const uint32_t g = (q0 + j) * 64u + (uint32_t)lane;
+        w[j] = g < (uint32_t)P ? touched[g >> 5] : 0u;  // (two words per group, each read by 32 lanes)
     }
-    uint32_t base = 0;
-    const uint32_t shard = blockIdx.x % kLiveShards;
-    if (lane == 0) base = atomicAdd(&live_count[shard * kLiveCntStride], (uint32_t)__popcll(m));
-    if ((lane & 31) == 0 && w) touched[g >> 5] = 0u;  // (after every lane's read of the word: one instruction)
-    base = (uint32_t)__shfl((int)base, 0);
-    if (lv) {
-        const size_t pos = (size_t)shard * live_cap + base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-        live[pos] = g;
-        sums.a[pos] = ra;
-        sums.b[pos] = rb;
-        sums.c[pos] = make_float2(rc.x, rc.y);
-        row[0] = row[1] = row[2] = make_float4(0.f, 0.f, 0.f, 0.f);
+    bool any = false;
+#pragma unroll
+    for (int j = 0; j < kLiveGroups; j++) {
+        m[j] = __ballot((w[j] >> (lane & 31)) & 1u);
+        any |= m[j] != 0ull;
+    }
+    if (!any) return;  // uniform
+    float4 ra[kLiveGroups], rb[kLiveGroups], rc[kLiveGroups];
+#pragma unroll
+    for (int j = 0; j < kLiveGroups; j++) {
+        const uint32_t g = (q0 + j) * 64u + (uint32_t)lane;
+        if ((m[j] >> lane) & 1ull) {
+            const float4* row = acc + (size_t)g * kAccRow4;
+            ra[j] = row[0];
+            rb[j] = row[1];
+            rc[j] = row[2];
+        }
+    }
+    uint32_t base[kLiveGroups];
+#pragma unroll
+    for (int j = 0; j < kLiveGroups; j++) {
+        base[j] = 0u;
+        if (lane == 0 && m[j]) base[j] = atomicAdd(&live_count[((q0 + j) % kLiveShards) * kLiveCntStride],
+                                                   (uint32_t)__popcll(m[j]));
+    }
+#pragma unroll
+    for (int j = 0; j < kLiveGroups; j++) {
+        // (the words are cleared after every lane's read of them: the ballots above depend on the loads)
+        if ((lane & 31) == 0 && w[j]) touched[((q0 + j) * 64u + (uint32_t)lane) >> 5] = 0u;
+        base[j] = (uint32_t)__shfl((int)base[j], 0);
+    }
+#pragma unroll
+    for (int j = 0; j < kLiveGroups; j++) {
+        if ((m[j] >> lane) & 1ull) {
+            const uint32_t g = (q0 + j) * 64u + (uint32_t)lane;
+            const size_t pos = (size_t)((q0 + j) % kLiveShards) * live_cap + base[j] +
+                               (uint32_t)__popcll(m[j] & ((1ull << lane) - 1ull));
+            live[pos] = g;
+            sums.a[pos] = ra[j];
+            sums.b[pos] = rb[j];
+            sums.c[pos] = make_float2(rc[j].x, rc[j].y);
+            float4* row = acc + (size_t)g * kAccRow4;
+            row[0] = row[1] = row[2] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
     }
 }
 
 hipError_t launch_gauss_live(int P, uint32_t* touched, float4* acc, const GradRecs& sums, uint32_t* live,
                              uint32_t* live_count, hipStream_t stream) {
     if (P <= 0) return hipSuccess;
-    const size_t blocks = ((size_t)P + 63) / 64;
+    const size_t blocks = (((size_t)P + 63) / 64 + kLiveGroups - 1) / kLiveGroups;
     hipLaunchKernelGGL(gauss_live_kernel, dim3((uint32_t)blocks), dim3(64), 0, stream, P, touched, acc, sums, live,
                        live_count, live_list_cap((uint32_t)P));
     return hipGetLastError();
