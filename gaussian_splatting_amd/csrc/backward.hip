@@ -461,67 +461,62 @@ hipError_t launch_gauss_reduce(int P, const GeomState& g, const GradRecs& recs, 
 // the Gaussian's bit; this lists the Gaussians with a bit (gauss_bwd's live list), moves their sums to
 // list order and clears the rows and words it read, so the next backward of the same forward starts
 // from zero.
-// One lane per Gaussian of kLiveGroups 64-Gaussian groups, each group as gauss_reduce's wave (so the
-// live-list order and shards are gauss_reduce's: group q appends to shard q % kLiveShards): the wave
-// reads its groups' touched words, appends each group's touched Gaussians with one atomic, and each
-// touched lane moves its rows' sums to their list positions and zeroes the rows -- every row load and
-// counter atomic of the wave in flight at once.  The kernel is a chain of dependent memory round
-// trips (word -> rows + counter -> stores), so it pays to have few waves each carrying several
-// groups: one lane per 32-bit word walked a word's bits one dependent row load after another (489
-// waves at 1M@1080p: 21.5 us, r5f); one group per wave, 15.6k waves, 15.4 us (r5h).
+// One wave per run of kLiveGroups x 64 consecutive Gaussians, one lane per Gaussian of each 64-group:
+// the wave reads its touched words, appends the run's touched Gaussians to shard (wave % kLiveShards)
+// with ONE atomic, and each touched lane moves its row's sums to its list position and zeroes the row.
+// What bounds it is the shard counters: one returning atomic per 64 Gaussians (15.6k at 1M@1080p, 244
+// on each counter, serialised where the counter lives) took 15.4 us (r5h); four atomics per wave, one
+// per group, 44 us (r5i).  A run of several groups per atomic divides that chain (live_list_cap bounds
+// a shard for runs up to kLiveGroupsMax groups).
 #ifndef GSR_LIVE_GROUPS
-#define GSR_LIVE_GROUPS 4
+#define GSR_LIVE_GROUPS 8
 #endif
 constexpr int kLiveGroups = GSR_LIVE_GROUPS;
+static_assert(kLiveGroups >= 1 && kLiveGroups <= (int)kLiveGroupsMax, "live_list_cap bounds runs of kLiveGroupsMax");
 __global__ void __launch_bounds__(64) gauss_live_kernel(int P, uint32_t* __restrict__ touched, float4* __restrict__ acc,
                                                         GradRecs sums, uint32_t* __restrict__ live,
                                                         uint32_t* __restrict__ live_count, uint32_t live_cap) {
     const int lane = threadIdx.x;
-    const uint32_t q0 = blockIdx.x * kLiveGroups;  // this wave's first group
+    const uint32_t g0 = blockIdx.x * (64u * kLiveGroups) + (uint32_t)lane;  // this lane's Gaussian in group 0
     uint32_t w[kLiveGroups];
-    unsigned long long m[kLiveGroups];
 #pragma unroll
     for (int j = 0; j < kLiveGroups; j++) {
-        const uint32_t g = (q0 + j) * 64u + (uint32_t)lane;
+        const uint32_t g = g0 + 64u * j;
         w[j] = g < (uint32_t)P ? touched[g >> 5] : 0u;  // (two words per group, each read by 32 lanes)
     }
-    bool any = false;
+    unsigned long long m[kLiveGroups];
+    uint32_t off[kLiveGroups], total = 0;
+    const unsigned long long below = (1ull << lane) - 1ull;
 #pragma unroll
     for (int j = 0; j < kLiveGroups; j++) {
         m[j] = __ballot((w[j] >> (lane & 31)) & 1u);
-        any |= m[j] != 0ull;
+        off[j] = total + (uint32_t)__popcll(m[j] & below);  // this lane's place in the run, if listed
+        total += (uint32_t)__popcll(m[j]);
     }
-    if (!any) return;  // uniform
+    if (total == 0) return;  // uniform
     float4 ra[kLiveGroups], rb[kLiveGroups], rc[kLiveGroups];
 #pragma unroll
     for (int j = 0; j < kLiveGroups; j++) {
-        const uint32_t g = (q0 + j) * 64u + (uint32_t)lane;
         if ((m[j] >> lane) & 1ull) {
-            const float4* row = acc + (size_t)g * kAccRow4;
+            const float4* row = acc + (size_t)(g0 + 64u * j) * kAccRow4;
             ra[j] = row[0];
             rb[j] = row[1];
             rc[j] = row[2];
         }
     }
-    uint32_t base[kLiveGroups];
+    const uint32_t shard = blockIdx.x % kLiveShards;
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(&live_count[shard * kLiveCntStride], total);
 #pragma unroll
-    for (int j = 0; j < kLiveGroups; j++) {
-        base[j] = 0u;
-        if (lane == 0 && m[j]) base[j] = atomicAdd(&live_count[((q0 + j) % kLiveShards) * kLiveCntStride],
-                                                   (uint32_t)__popcll(m[j]));
-    }
-#pragma unroll
-    for (int j = 0; j < kLiveGroups; j++) {
-        // (the words are cleared after every lane's read of them: the ballots above depend on the loads)
-        if ((lane & 31) == 0 && w[j]) touched[((q0 + j) * 64u + (uint32_t)lane) >> 5] = 0u;
-        base[j] = (uint32_t)__shfl((int)base[j], 0);
-    }
+    for (int j = 0; j < kLiveGroups; j++)  // (after every lane's read of the words: the ballots used them)
+        if ((lane & 31) == 0 && w[j]) touched[(g0 + 64u * j) >> 5] = 0u;
+    base = (uint32_t)__shfl((int)base, 0);
+    const size_t pos0 = (size_t)shard * live_cap + base;
 #pragma unroll
     for (int j = 0; j < kLiveGroups; j++) {
         if ((m[j] >> lane) & 1ull) {
-            const uint32_t g = (q0 + j) * 64u + (uint32_t)lane;
-            const size_t pos = (size_t)((q0 + j) % kLiveShards) * live_cap + base[j] +
-                               (uint32_t)__popcll(m[j] & ((1ull << lane) - 1ull));
+            const uint32_t g = g0 + 64u * j;
+            const size_t pos = pos0 + off[j];
             live[pos] = g;
             sums.a[pos] = ra[j];
             sums.b[pos] = rb[j];

@@ -268,9 +268,14 @@ struct GradRecs {
 // counter took 15625 returning atomics in a row at 1M Gaussians (gauss_reduce 62 -> 201 us).
 constexpr int kLiveShards = 64;
 constexpr int kLiveCntStride = 32;  // uint32 per counter line
-__host__ __device__ inline uint32_t live_list_cap(uint32_t P) {  // entries per shard
-    const uint32_t waves = (P + 63) / 64;
-    return (waves + kLiveShards - 1) / kLiveShards * 64;
+// Entries per shard.  A kernel appending runs of up to 64 x kLiveGroupsMax consecutive Gaussians to
+// shard (run index) % kLiveShards (gauss_live: one run per wave) fills a shard with at most this many;
+// so does gauss_reduce's one 64-Gaussian run per wave (a multiple of 64 rounded up to 64 x G is >= it).
+constexpr uint32_t kLiveGroupsMax = 8;
+__host__ __device__ inline uint32_t live_list_cap(uint32_t P) {
+    constexpr uint32_t run = 64u * kLiveGroupsMax;
+    const uint32_t runs = (P + run - 1) / run;
+    return (runs + kLiveShards - 1) / kLiveShards * run;
 }
 // The render backward's per-instance records (not the per-Gaussian sums, which stay three
 // arrays): GSR_REC_AOS interleaves them as 48-byte records a, b, (c, pad), so one instance's

@@ -68,7 +68,8 @@ constexpr int kBatch = 64;  // list entries staged per round (one per lane)
 
 // Traffic attribution builds only (results are wrong in them): GSR_ATTR bit 0
 // drops the backward's record / content-byte stores, bit 1 its checkpoint loads, bit 2 its
-// per-pixel state loads other than n_contrib.  The control flow is unchanged in all three.
+// per-pixel state loads other than n_contrib; in the atomic backward bit 3 drops the touched-bit ORs,
+// bit 4 the accumulator adds.  The control flow is unchanged in all of them.
 #ifndef GSR_ATTR
 #define GSR_ATTR 0
 #endif
@@ -938,14 +939,14 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
                 s_wgid[slot] = e;
                 s_wj[slot] = (uint32_t)lane;
                 // the Gaussian has a gradient (gauss_live lists it); OR is order-free
-                (void)atomicOr(a.touched + (e >> 5), 1u << (e & 31u));
+                if (!(GSR_ATTR & 8)) (void)atomicOr(a.touched + (e >> 5), 1u << (e & 31u));
             }
             unit_sync();
             // one wave instruction per four listed entries: lane 16 k + v adds value v of entry k
             const int nw = __popcll(written), sub = lane >> 4, v = lane & 15;
             for (int k0 = 0; k0 < nw; k0 += 4) {  // uniform
                 const int k = k0 + sub;
-                if (k < nw && v < 10) {
+                if (k < nw && v < 10 && !(GSR_ATTR & 16)) {
                     const int j = (int)s_wj[k];
                     const float val = reinterpret_cast<const float*>(s_acc)[(v >> 2) * (4 * kBatch) + j * 4 + (v & 3)];
                     (void)atomicAdd(a.acc + (size_t)s_wgid[k] * (4 * kAccRow4) + v, val);  // (no return: fire and forget)
