@@ -464,12 +464,13 @@ hipError_t launch_gauss_reduce(int P, const GeomState& g, const GradRecs& recs, 
 // One wave per run of kLiveGroups x 64 consecutive Gaussians, one lane per Gaussian of each 64-group:
 // the wave reads its touched words, appends the run's touched Gaussians to shard (wave % kLiveShards)
 // with ONE atomic, and each touched lane moves its row's sums to its list position and zeroes the row.
-// What bounds it is the shard counters: one returning atomic per 64 Gaussians (15.6k at 1M@1080p, 244
-// on each counter, serialised where the counter lives) took 15.4 us (r5h); four atomics per wave, one
-// per group, 44 us (r5i).  A run of several groups per atomic divides that chain (live_list_cap bounds
-// a shard for runs up to kLiveGroupsMax groups).
+// It is bound by memory-level parallelism, not by its bytes or its counter atomics: one group per wave
+// (15.6k waves at 1M@1080p) 15.4 us; one atomic per run of 4 or 8 groups, 42 / 30 us (fewer waves, each
+// with more dependent work: r5j); one atomic per group with 4 groups per wave, 44 us (r5i); one lane
+// per 32-bit word walking its bits, 21.5 us (r5f).  (live_list_cap bounds a shard for runs of up to
+// kLiveGroupsMax groups.)
 #ifndef GSR_LIVE_GROUPS
-#define GSR_LIVE_GROUPS 8
+#define GSR_LIVE_GROUPS 1
 #endif
 constexpr int kLiveGroups = GSR_LIVE_GROUPS;
 static_assert(kLiveGroups >= 1 && kLiveGroups <= (int)kLiveGroupsMax, "live_list_cap bounds runs of kLiveGroupsMax");

@@ -65,6 +65,13 @@ constexpr int kBatch = 64;  // list entries staged per round (one per lane)
 #ifndef GSR_PF_ENTRY
 #define GSR_PF_ENTRY 1
 #endif
+// Cost probe for 4x4-block units ("Why the render kernels keep their structure"): the
+// forward's entry index made a per-lane value (the same in every lane, so the results are unchanged), so
+// the entry's data are VGPRs and the quadrant skips are EXEC-mask branches -- what four 16-lane groups
+// walking their own entries would pay before any lane saving.  Off in the product.
+#ifndef GSR_FWD_LANE_ENTRY
+#define GSR_FWD_LANE_ENTRY 0
+#endif
 
 // Traffic attribution builds only (results are wrong in them): GSR_ATTR bit 0
 // drops the backward's record / content-byte stores, bit 1 its checkpoint loads, bit 2 its
@@ -361,8 +368,15 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const ui
         while (todo && alive) {
             const int j = __builtin_ctzll(todo);
             todo &= todo - 1;
+#if GSR_FWD_LANE_ENTRY
+            int jl = j;
+            asm volatile("" : "+v"(jl));  // per lane for the compiler
+            const float4 xy = s_xy[sl][jl], cq = s_cq[sl][jl], col = s_col[sl][jl];
+            const uint32_t m = (SHARED ? __float_as_uint(cq.w) >> qbase : __float_as_uint(cq.w)) & alive;
+#else
             const float4 xy = s_xy[sl][j], cq = s_cq[sl][j], col = s_col[sl][j];
             const uint32_t m = (SHARED ? uniform_u32(__float_as_uint(cq.w)) >> qbase : uniform_u32(__float_as_uint(cq.w))) & alive;
+#endif
             const uint32_t pos1 = (uint32_t)(b0 + j + 1);
 #pragma unroll
             for (int k = 0; k < NQ; k++) {
