@@ -495,7 +495,10 @@ __global__ void __launch_bounds__(64) gauss_live_kernel(int P, uint32_t* __restr
         total += (uint32_t)__popcll(m[j]);
     }
     if (total == 0) return;  // uniform
+    // (initialised whole: arrays written only under a branch were kept in scratch memory, r5j's G > 1 builds)
     float4 ra[kLiveGroups], rb[kLiveGroups], rc[kLiveGroups];
+#pragma unroll
+    for (int j = 0; j < kLiveGroups; j++) ra[j] = rb[j] = rc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int j = 0; j < kLiveGroups; j++) {
         if ((m[j] >> lane) & 1ull) {
