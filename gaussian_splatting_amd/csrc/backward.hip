@@ -464,13 +464,14 @@ hipError_t launch_gauss_reduce(int P, const GeomState& g, const GradRecs& recs, 
 // One wave per run of kLiveGroups x 64 consecutive Gaussians, one lane per Gaussian of each 64-group:
 // the wave reads its touched words, appends the run's touched Gaussians to shard (wave % kLiveShards)
 // with ONE atomic, and each touched lane moves its row's sums to its list position and zeroes the row.
-// It is bound by memory-level parallelism, not by its bytes or its counter atomics: one group per wave
-// (15.6k waves at 1M@1080p) 15.4 us; one atomic per run of 4 or 8 groups, 42 / 30 us (fewer waves, each
-// with more dependent work: r5j); one atomic per group with 4 groups per wave, 44 us (r5i); one lane
-// per 32-bit word walking its bits, 21.5 us (r5f).  (live_list_cap bounds a shard for runs of up to
-// kLiveGroupsMax groups.)
+// A chain of dependent round trips (word -> rows + counter -> stores) over tiny data: 15.6k one-group waves
+// at 1M@1080p need two rounds of the 32 wave slots per CU, so a wave carries four groups and one counter
+// atomic per run: 15.7 -> 12.8 us at 1M, 26.2 -> 22.0 us at 5M@4K, step -2.8 / -8 us (r5m; two groups: 14.4 /
+// 23.2 us).  (r5i / r5j's runs of several groups had measured slower only because their row arrays, written
+// under a branch, were kept in scratch memory; one lane per 32-bit word walking its bits: 21.5 us, r5f.)
+// live_list_cap bounds a shard for runs of up to kLiveGroupsMax groups.
 #ifndef GSR_LIVE_GROUPS
-#define GSR_LIVE_GROUPS 1
+#define GSR_LIVE_GROUPS 4
 #endif
 constexpr int kLiveGroups = GSR_LIVE_GROUPS;
 static_assert(kLiveGroups >= 1 && kLiveGroups <= (int)kLiveGroupsMax, "live_list_cap bounds runs of kLiveGroupsMax");
@@ -996,12 +997,10 @@ __global__ void __launch_bounds__(64) GSR_GB_OCCUPANCY gauss_bwd_kernel(GaussBwd
                 sh_v = v;
                 sh_g = g;
             }
-            __device__ __forceinline__ void dmean(float3 m) const {
-                if (sh_late)
-                    dmean_late = m;  // stored after the SH pass adds the direction term
-                else
-                    store3(a.dL_dmean3D, idx, m.x, m.y, m.z);
-            }
+            // kept in a register and stored by the caller (after the SH pass adds the direction term, when
+            // there is one): choosing here between the global store and the local made the compiler select
+            // between a global and a private address, and dmean_late lived in scratch memory
+            __device__ __forceinline__ void dmean(float3 m) const { dmean_late = m; }
             __device__ __forceinline__ void scale_rot(bool have, float3 ds, float4 dq) const {
                 if (have || a.dL_dscale) store3(a.dL_dscale, idx, ds.x, ds.y, ds.z);
                 if (have || a.dL_drot) reinterpret_cast<float4*>(a.dL_drot)[idx] = dq;
@@ -1015,12 +1014,17 @@ __global__ void __launch_bounds__(64) GSR_GB_OCCUPANCY gauss_bwd_kernel(GaussBwd
             view_backward<kShNow>(cam, gi, sa, sb, sc, cm, do_sh, a.D, M, ShLds{&s_sh[lane * kShStride]}, sink);
         else
             view_backward<kShNow>(cam, gi, sa, sb, sc, cm, do_sh, a.D, M, ShGlobal{sh_src, sh_dst, idx}, sink);
+        if (!sh_late) store3(a.dL_dmean3D, idx, dmean_late.x, dmean_late.y, dmean_late.z);
         if (!do_sh && (a.dL_dsh || a.dL_ddc)) {  // colours precomputed: dL/dSH is zero
             const ShGlobal acc{sh_src, sh_dst, idx};
             for (int k = 0; k < M; k++) acc.store(k, make_float3(0.f, 0.f, 0.f));
         }
     }
 
+// A/B: the view-vector pin for the combined SH layout too (its kernel otherwise holds 165 VGPRs)
+#ifndef GSR_GB_PIN_ALL
+#define GSR_GB_PIN_ALL 0
+#endif
 #ifndef GSR_GB_TIMING_NOSH
 #define GSR_GB_TIMING_NOSH 0  // timing builds only (results wrong): skip the deferred SH pass
 #endif
@@ -1047,7 +1051,8 @@ __global__ void __launch_bounds__(64) GSR_GB_OCCUPANCY gauss_bwd_kernel(GaussBwd
                     // vectorisation off and contraction per expression, build.py, both layouts round
                     // alike -- test_separate_sh.)
                     float3 v = sh_v;
-                    if constexpr (SH_MODE == kShLdsSplit) asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z));
+                    if constexpr (SH_MODE == kShLdsSplit || GSR_GB_PIN_ALL)
+                        asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z));
                     float3 dm = dmean_late;
                     sh_dir_backward(ShLds{row}, a.D, M, v, sh_g, dm);
                     store3(a.dL_dmean3D, idx, dm.x, dm.y, dm.z);
