@@ -863,6 +863,14 @@ __device__ __forceinline__ void view_backward(const ViewCam& c, const GaussIn& g
 // With GSR_GB_HALVES the SH rows go through LDS 32 at a time at the end of the kernel
 // (lanes 0-31, then 32-63): 6.6 KiB of LDS per wave instead of 13, twice the waves per CU.
 constexpr int kGbShRows = GSR_GB_HALVES ? 32 : 64;
+// Live-list entries per gauss_bwd wave (A/B: GSR_GB_LIST_E 32).  The kernel is a chain of dependent round
+// trips (list -> geometry -> SH rows -> stores) with little VALU, so half-filled waves (twice as many, each
+// with one SH half) trade idle lanes for memory-level parallelism.
+#ifndef GSR_GB_LIST_E
+#define GSR_GB_LIST_E 64
+#endif
+constexpr int kGbListE = GSR_GB_LIST_E;
+static_assert(kGbListE == 64 || (kGbListE == 32 && GSR_GB_HALVES), "64, or one SH half of 32 rows");
 // Occupancy target (A/B: GSR_GB_WAVES).  Unconstrained, the body takes 134 VGPRs: 3 waves per
 // SIMD, too few loads in flight for an HBM-bound kernel.
 #ifdef GSR_GB_WAVES
@@ -892,11 +900,11 @@ __global__ void __launch_bounds__(64) GSR_GB_OCCUPANCY gauss_bwd_kernel(GaussBwd
     const int g0 = blockIdx.x * 64;
     int idx = g0 + lane;
     size_t lpos = 0;  // LIST: this lane's position in the live list (sums_by_list: where its sums are)
-    if constexpr (LIST) {  // block b: entries [64 (b / shards), +64) of shard b % shards
-        const uint32_t shard = blockIdx.x % kLiveShards, k0 = (blockIdx.x / kLiveShards) * 64;
+    if constexpr (LIST) {  // block b: entries [E (b / shards), +E) of shard b % shards, E = kGbListE
+        const uint32_t shard = blockIdx.x % kLiveShards, k0 = (blockIdx.x / kLiveShards) * kGbListE;
         const uint32_t n = a.live_count[shard * kLiveCntStride];
         if (k0 >= n) return;  // uniform: past the shard's list (the grid is sized for the worst case)
-        idx = k0 + lane < n ? (int)a.live[(size_t)shard * a.live_cap + k0 + lane] : a.P;
+        idx = lane < kGbListE && k0 + lane < n ? (int)a.live[(size_t)shard * a.live_cap + k0 + lane] : a.P;
         lpos = (size_t)shard * a.live_cap + k0 + lane;
     }
     const int nvalid = min(64, a.P - g0);
@@ -1033,6 +1041,7 @@ __global__ void __launch_bounds__(64) GSR_GB_OCCUPANCY gauss_bwd_kernel(GaussBwd
         // their lanes evaluate it in place, coalesced write-back of the 32 dL/dSH rows
         const unsigned long long need = __ballot(sh_late);  // rows whose SH is read at all
         for (int half = 0; half < 2; half++) {
+            if (LIST && half * kGbShRows >= kGbListE) break;  // (kGbListE 32: the wave's rows are one half)
             const int rows = LIST ? kGbShRows : min(kGbShRows, nvalid - half * kGbShRows);
             if (rows <= 0) break;  // wave-uniform
             if constexpr (LIST)  // the lanes' rows, wherever they are
@@ -1639,7 +1648,7 @@ hipError_t launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t stream) {
                         ((reinterpret_cast<uintptr_t>(a.shs) & 15) == 0) &&
                         ((reinterpret_cast<uintptr_t>(a.dL_dsh) & 15) == 0);
     if (a.live && a.sparse) {  // the live list: kLiveShards x live_cap entries at most
-        const dim3 lgrid(kLiveShards * ((a.live_cap + 63) / 64));
+        const dim3 lgrid(kLiveShards * ((a.live_cap + kGbListE - 1) / kGbListE));
         if (lds_ok && a.dc)
             hipLaunchKernelGGL((gauss_bwd_kernel<kShLdsSplit, true>), lgrid, block, 0, stream, a);
         else if (lds_ok)
