@@ -893,15 +893,15 @@ __device__ __forceinline__ void gb_sync() {
     __syncthreads();
 #endif
 }
-template <int SH_MODE, bool LIST = false>
-__global__ void __launch_bounds__(64) GSR_GB_OCCUPANCY gauss_bwd_kernel(GaussBwdArgs a) {
+template <int SH_MODE, bool LIST>
+__device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const uint32_t blk) {
     __shared__ __attribute__((aligned(16))) float s_sh[SH_MODE != kShGlobal ? kGbShRows * kShStride : 4];
     const int lane = threadIdx.x;
-    const int g0 = blockIdx.x * 64;
+    const int g0 = (int)blk * 64;
     int idx = g0 + lane;
     size_t lpos = 0;  // LIST: this lane's position in the live list (sums_by_list: where its sums are)
     if constexpr (LIST) {  // block b: entries [E (b / shards), +E) of shard b % shards, E = kGbListE
-        const uint32_t shard = blockIdx.x % kLiveShards, k0 = (blockIdx.x / kLiveShards) * kGbListE;
+        const uint32_t shard = blk % kLiveShards, k0 = (blk / kLiveShards) * kGbListE;
         const uint32_t n = a.live_count[shard * kLiveCntStride];
         if (k0 >= n) return;  // uniform: past the shard's list (the grid is sized for the worst case)
         idx = lane < kGbListE && k0 + lane < n ? (int)a.live[(size_t)shard * a.live_cap + k0 + lane] : a.P;
@@ -1087,6 +1087,27 @@ __global__ void __launch_bounds__(64) GSR_GB_OCCUPANCY gauss_bwd_kernel(GaussBwd
         const unsigned long long rows_out = a.sparse ? __ballot(visible) : ~0ull;
         __syncthreads();
         sh_stage_out<64, 64, SH_MODE == kShLdsSplit>(sh_dst, g0, nvalid, s_sh, kShStride, lane, rows_out);
+    }
+}
+
+// The live-list grid is sized for the worst case (every Gaussian listed: 64 shards x live_cap / E blocks, 15.7k
+// at 1M@1080p, 78k at 5M@4K) while ~2000 blocks have entries; every surplus block is a wave launched to read a
+// counter and exit.  GSR_GB_STRIDED: a grid of kGbStridedGrid blocks walks the virtual blocks b, b + G, ...
+// up to the longest shard's end instead.
+#ifndef GSR_GB_STRIDED
+#define GSR_GB_STRIDED 0
+#endif
+constexpr uint32_t kGbStridedGrid = 2048;
+template <int SH_MODE, bool LIST = false>
+__global__ void __launch_bounds__(64) GSR_GB_OCCUPANCY gauss_bwd_kernel(GaussBwdArgs a) {
+    if constexpr (LIST && GSR_GB_STRIDED) {
+        const int lane = threadIdx.x;
+        const uint32_t maxn = (uint32_t)__builtin_amdgcn_readlane(
+            (int)wave_incl_max(lane < kLiveShards ? a.live_count[lane * kLiveCntStride] : 0u), 63);
+        for (uint32_t b = blockIdx.x; (b / kLiveShards) * (uint32_t)kGbListE < maxn; b += gridDim.x)
+            gauss_bwd_block<SH_MODE, true>(a, b);
+    } else {
+        gauss_bwd_block<SH_MODE, LIST>(a, blockIdx.x);
     }
 }
 
@@ -1648,7 +1669,8 @@ hipError_t launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t stream) {
                         ((reinterpret_cast<uintptr_t>(a.shs) & 15) == 0) &&
                         ((reinterpret_cast<uintptr_t>(a.dL_dsh) & 15) == 0);
     if (a.live && a.sparse) {  // the live list: kLiveShards x live_cap entries at most
-        const dim3 lgrid(kLiveShards * ((a.live_cap + kGbListE - 1) / kGbListE));
+        const uint32_t worst = kLiveShards * ((a.live_cap + kGbListE - 1) / kGbListE);
+        const dim3 lgrid(GSR_GB_STRIDED && worst > kGbStridedGrid ? kGbStridedGrid : worst);
         if (lds_ok && a.dc)
             hipLaunchKernelGGL((gauss_bwd_kernel<kShLdsSplit, true>), lgrid, block, 0, stream, a);
         else if (lds_ok)
