@@ -72,6 +72,13 @@ constexpr int kBatch = 64;  // list entries staged per round (one per lane)
 #ifndef GSR_FWD_LANE_ENTRY
 #define GSR_FWD_LANE_ENTRY 0
 #endif
+// A/B: software-pipelined LDS reads of the staged entries in the forward's walk (render_fwd_tile)
+#ifndef GSR_FWD_LDS_PF
+#define GSR_FWD_LDS_PF 0
+#endif
+#ifndef GSR_BWD_LDS_PF
+#define GSR_BWD_LDS_PF 0
+#endif
 
 // Traffic attribution builds only (results are wrong in them): GSR_ATTR bit 0
 // drops the backward's record / content-byte stores, bit 1 its checkpoint loads, bit 2 its
@@ -365,10 +372,28 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const ui
             }
         }
         unsigned long long todo = __ballot((qm >> qbase) & kPartMask);
+#if GSR_FWD_LDS_PF
+        // the next entry's staged rows are read from LDS before this entry is blended, so their latency
+        // overlaps the blend instead of heading the next iteration
+        int jn = todo ? __builtin_ctzll(todo) : 0;
+        float4 nxy = s_xy[sl][jn], ncq = s_cq[sl][jn], ncol = s_col[sl][jn];
+#endif
         while (todo && alive) {
+#if GSR_FWD_LDS_PF
+            const int j = jn;
+            todo &= todo - 1;
+            const float4 xy = nxy, cq = ncq, col = ncol;
+            jn = todo ? __builtin_ctzll(todo) : jn;  // (uniform; a repeated slot when none is left: unused)
+            nxy = s_xy[sl][jn];
+            ncq = s_cq[sl][jn];
+            ncol = s_col[sl][jn];
+            const uint32_t m = (SHARED ? uniform_u32(__float_as_uint(cq.w)) >> qbase : uniform_u32(__float_as_uint(cq.w))) & alive;
+#else
             const int j = __builtin_ctzll(todo);
             todo &= todo - 1;
-#if GSR_FWD_LANE_ENTRY
+#endif
+#if GSR_FWD_LDS_PF
+#elif GSR_FWD_LANE_ENTRY
             int jl = j;
             asm volatile("" : "+v"(jl));  // per lane for the compiler
             const float4 xy = s_xy[sl][jl], cq = s_cq[sl][jl], col = s_col[sl][jl];
@@ -862,11 +887,26 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
         unit_sync();
         unsigned long long todo = __ballot(qm != 0);
         unsigned long long written = 0;
+#if GSR_BWD_LDS_PF  // (as GSR_FWD_LDS_PF: the next entry's rows read before this one is evaluated)
+        int jn = todo ? __builtin_ctzll(todo) : 0;
+        float4 nxy = s_xy[jn], ncq = s_cq[jn], ncol = s_col[jn];
+#endif
         while (todo) {
+#if GSR_BWD_LDS_PF
+            const int j = jn;
+            todo &= todo - 1;
+            const float4 xy = nxy, cq = ncq, col = ncol;
+            jn = todo ? __builtin_ctzll(todo) : jn;
+            nxy = s_xy[jn];
+            ncq = s_cq[jn];
+            ncol = s_col[jn];
+            const int pos = b0 + j;
+#else
             const int j = __builtin_ctzll(todo);
             todo &= todo - 1;
             const int pos = b0 + j;
             const float4 xy = s_xy[j], cq = s_cq[j], col = s_col[j];
+#endif
             if (pos >= next_lim) {  // uniform: retire the slots whose last contributor has passed
                 next_lim = limit;
 #pragma unroll
