@@ -870,6 +870,10 @@ constexpr int kGbShRows = GSR_GB_HALVES ? 32 : 64;
 #define GSR_GB_LIST_E 64
 #endif
 constexpr int kGbListE = GSR_GB_LIST_E;
+// A/B: a listed Gaussian's geometry requested with its sums (gauss_bwd_block)
+#ifndef GSR_GB_HOIST
+#define GSR_GB_HOIST 0
+#endif
 static_assert(kGbListE == 64 || (kGbListE == 32 && GSR_GB_HALVES), "64, or one SH half of 32 rows");
 // Occupancy target (A/B: GSR_GB_WAVES).  Unconstrained, the body takes 134 VGPRs: 3 waves per
 // SIMD, too few loads in flight for an HBM-bound kernel.
@@ -931,12 +935,26 @@ __device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const uin
     float4 sa = make_float4(0.f, 0.f, 0.f, 0.f), sb = sa;
     float2 sc = make_float2(0.f, 0.f);
     int rad = 0;
+    // GSR_GB_HOIST (A/B): a listed Gaussian is all but always visible with a gradient, so its geometry is
+    // requested with the sums, not after them -- one dependent round trip fewer
+    constexpr bool kHoist = LIST && GSR_GB_HOIST;
+    float3 h_mean = make_float3(0.f, 0.f, 0.f), h_sc = h_mean;
+    float4 h_q = make_float4(1.f, 0.f, 0.f, 0.f);
+    uint8_t h_cm = 0;
     if (valid) {
         rad = a.radii[idx];
         const size_t si = LIST && a.sums_by_list ? lpos : (size_t)idx;  // (atomic backward: list order, gauss_live)
         sa = a.sums.a[si];
         sb = a.sums.b[si];
         sc = a.sums.c[si];
+        if constexpr (kHoist) {
+            h_mean = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
+            if (a.scales) {
+                h_sc = make_float3(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]);
+                h_q = reinterpret_cast<const float4*>(a.rotations)[idx];
+            }
+            if (a.shs || a.dc) h_cm = a.geom.clamped[idx];
+        }
     }
     const bool any_grad = (sa.x != 0.f) | (sa.y != 0.f) | (sa.z != 0.f) | (sa.w != 0.f) | (sb.x != 0.f) |
                           (sb.y != 0.f) | (sb.z != 0.f) | (sb.w != 0.f) | (sc.x != 0.f) | (sc.y != 0.f);
@@ -979,13 +997,19 @@ __device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const uin
         const ViewCam cam{a.viewmatrix, a.projmatrix, a.campos, a.tan_fovx, a.tan_fovy,
                           a.focal_x,    a.focal_y,    a.antialiasing, a.have_invdepth};
         GaussIn gi;
-        gi.mean = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
         gi.have_scales = a.scales != nullptr;
-        gi.sc3 = make_float3(0.f, 0.f, 0.f);
-        gi.q = make_float4(1.f, 0.f, 0.f, 0.f);
-        if (a.scales) {
-            gi.sc3 = make_float3(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]);
-            gi.q = reinterpret_cast<const float4*>(a.rotations)[idx];
+        if constexpr (kHoist) {
+            gi.mean = h_mean;
+            gi.sc3 = h_sc;
+            gi.q = h_q;
+        } else {
+            gi.mean = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
+            gi.sc3 = make_float3(0.f, 0.f, 0.f);
+            gi.q = make_float4(1.f, 0.f, 0.f, 0.f);
+            if (a.scales) {
+                gi.sc3 = make_float3(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]);
+                gi.q = reinterpret_cast<const float4*>(a.rotations)[idx];
+            }
         }
         gi.cov3D = a.cov3D_precomp ? a.cov3D_precomp + 6 * idx : nullptr;
         gi.scale_modifier = a.scale_modifier;
@@ -1015,7 +1039,7 @@ __device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const uin
             }
         } sink{a, idx, sh_late, sh_v, sh_g, dmean_late};
         const bool do_sh = a.shs || a.dc;
-        const uint8_t cm = do_sh ? a.geom.clamped[idx] : 0;
+        const uint8_t cm = kHoist ? h_cm : do_sh ? a.geom.clamped[idx] : 0;
         if constexpr (kShLate)
             view_backward<kShDefer>(cam, gi, sa, sb, sc, cm, do_sh, a.D, M, ShLds{nullptr}, sink);
         else if constexpr (SH_MODE != kShGlobal)
