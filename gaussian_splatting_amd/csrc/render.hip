@@ -79,6 +79,15 @@ constexpr int kBatch = 64;  // list entries staged per round (one per lane)
 #ifndef GSR_BWD_LDS_PF
 #define GSR_BWD_LDS_PF 0
 #endif
+// The entry mask the forward leaves for the backward: the quadrants whose footprint the entry touches
+// (0), or the quadrants in which some pixel blended it (1: set after the batch's walk from one wave-uniform
+// bit per (entry, quadrant) evaluation that passed its any-alpha test).  The backward evaluates an entry's
+// quadrant only where a pixel can have a gradient term, and the blend mask is the tighter superset of
+// those; entries with no blending pixel are neither gathered nor walked by the backward.
+#ifndef GSR_BLEND_MASK
+#define GSR_BLEND_MASK 0
+#endif
+static_assert(!GSR_BLEND_MASK || GSR_FWD_OWN_BITS, "the blend mask is written per part");
 
 // Traffic attribution builds only (results are wrong in them): GSR_ATTR bit 0
 // drops the backward's record / content-byte stores, bit 1 its checkpoint loads, bit 2 its
@@ -340,7 +349,9 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const ui
             // backward has retired those slots by then (slot limits from n_contrib).
             qm = quad_bits_exact(v0, v1, v2, tile_x0, tile_y0, kPartMask << qbase);
             s_cq[0][lane] = stage_conic(v0, v1, qm >> qbase);
-            if (NPART == 1)
+            if (GSR_BLEND_MASK) {
+                // (the blend mask is OR-ed in after the walk, below)
+            } else if (NPART == 1)
                 *ent = (gid << kEntryMaskBits) | qm;
             else if (qm)
                 __hip_atomic_fetch_or(ent, qm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -372,6 +383,9 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const ui
             }
         }
         unsigned long long todo = __ballot((qm >> qbase) & kPartMask);
+        unsigned long long blend[NQ];  // GSR_BLEND_MASK: bit j of blend[k]: some pixel of quadrant k blended entry j
+#pragma unroll
+        for (int k = 0; k < NQ; k++) blend[k] = 0ull;
 #if GSR_FWD_LDS_PF
         // the next entry's staged rows are read from LDS before this entry is blended, so their latency
         // overlaps the blend instead of heading the next iteration
@@ -420,6 +434,7 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const ui
                     c_idle += bl ? 0ull : 1ull;
                 }
                 if (!__any(w0 > 0.f)) continue;  // uniform
+                if (GSR_BLEND_MASK && !SHARED) blend[k] |= 1ull << j;
                 const float test_T = Tl[k] * (1.f - alpha);
                 const bool term = test_T < 0.0001f;  // live pixel: ends it, splat not added
                 const float w = term ? 0.f : w0;
@@ -435,6 +450,13 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const ui
                 // it with "some pixel terminated here" cost two VALU to materialise the guard)
                 if (!__any(Tl[k] > 0.f)) alive &= ~(1u << k);
             }
+        }
+        if (GSR_BLEND_MASK && !SHARED && b0 + lane < ns) {
+            uint32_t bq = 0;
+#pragma unroll
+            for (int k = 0; k < NQ; k++) bq |= (uint32_t)((blend[k] >> lane) & 1ull) << (qbase + k);
+            // OR-ed into the entry K4 wrote with clear mask bits (the other part adds its own)
+            if (bq) __hip_atomic_fetch_or(a.gid_sorted + range.x + b0 + lane, bq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (SHARED) {
             if (lane == 0) lds_store_rel(&s_done[part], bk + 1);  // slot sl may be restaged for bk + NB
@@ -864,6 +886,7 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
         if (has) {
             // Gaussian << 4 | quadrant mask (GSR_PF_ENTRY: loaded during the previous batch)
             const uint32_t ent = GSR_PF_ENTRY ? ent_next : a.gid_sorted[range.x + b0 + lane];
+          if (!GSR_BLEND_MASK || (ent & kEntryMask)) {  // (blend mask: an entry no pixel blended is not walked)
             const float4* rec = a.rec + (size_t)kRecRows * (ent >> kEntryMaskBits);
             const float4 v0 = rec[0], v1 = rec[1], v2 = rec[2];
             if (ATOMIC) {
@@ -882,6 +905,7 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
             o = v1.y;
             qm = ent & kEntryMask;
             s_cq[lane] = stage_conic(v0, v1, qm);
+          }
         }
         if (GSR_PF_ENTRY && b0 + kBatch + lane < end) ent_next = a.gid_sorted[range.x + b0 + kBatch + lane];
         unit_sync();

@@ -1,0 +1,15 @@
+#!/bin/bash
+# r5t: the forward leaves the blend mask (quadrants in which some pixel blended the entry) instead of the
+# footprint mask for the backward (libgsr_blend); the whole GPU suite on it, full-size tests, A/B at 1M and 5M
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out/r5t; mkdir -p $OUT
+L=$PWD/gaussian_splatting_amd/lib/libgsr_blend.so
+GSR_LIBRARY=$L timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "not fullsize" > $OUT/pytest_blend.log 2>&1; rc=$?
+echo "blend tests rc=$rc"; tail -n 3 $OUT/pytest_blend.log; [ $rc -eq 0 ] || exit $rc
+VARIANTS="blend" ABN_SKIP_PARITY=1 bash scripts/abn.sh r5t/abn_1m 3 1m_1080p_sh3 > $OUT/abn_1m.txt 2>&1; rc=$?
+cat $OUT/abn_1m.txt; [ $rc -eq 0 ] || exit $rc
+ABN_SKIP_PARITY=1 VARIANTS="blend" bash scripts/abn.sh r5t/abn_5m 2 5m_4k_sh3 > $OUT/abn_5m.txt 2>&1; rc=$?
+cat $OUT/abn_5m.txt; [ $rc -eq 0 ] || exit $rc
+GSR_LIBRARY=$L timeout -k 10 800 python -u -m pytest tests/test_gpu_fullsize.py -m gpu -x -v -s --timeout 600 --timeout-method thread > $OUT/pytest_full_blend.log 2>&1; rc=$?
+echo "blend fullsize rc=$rc"; grep -E "passed|failed|FAIL" $OUT/pytest_full_blend.log | tail -n 5; exit $rc
