@@ -289,6 +289,10 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const ui
     constexpr bool kPf = GSR_PF_ENTRY && !SHARED;
     uint32_t ent_next = kPf && lane < ns ? a.gid_sorted[range.x + lane] : 0u;  // (GSR_PF_ENTRY)
     int bk = 0;  // batch index
+    // GSR_BLEND_MASK: the previous batch's blend bits, OR-ed into its entries once this batch's loads are in
+    // flight (vmcnt counts stores too: issued before the next staging, the ORs made it wait for them)
+    uint32_t pend_bq = 0;
+    int pend_b0 = 0;
     for (int b0 = 0; b0 < ns && alive; b0 += kBatch, bk++) {
         const int sl = SHARED ? bk % NB : 0;
         if (CENSUS && !SHARED) c_staged += (unsigned long long)min(kBatch, ns - b0);
@@ -365,6 +369,9 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const ui
         }
         if (kPf && b0 + kBatch + lane < ns) ent_next = a.gid_sorted[range.x + b0 + kBatch + lane];
         if (!SHARED) unit_sync();
+        if (GSR_BLEND_MASK && !SHARED && pend_bq)  // (the previous batch's bits: see above)
+            __hip_atomic_fetch_or(a.gid_sorted + range.x + pend_b0 + lane, pend_bq, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
         // Blend checkpoint (gsr_common.h): the state before entry b0, stored after this batch's
         // loads have landed.  vmcnt counts stores too, so stores issued ahead of the loads would
         // make the staging wait for them; here they drain while the batch blends.  A part writes
@@ -451,12 +458,14 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const ui
                 if (!__any(Tl[k] > 0.f)) alive &= ~(1u << k);
             }
         }
-        if (GSR_BLEND_MASK && !SHARED && b0 + lane < ns) {
+        if (GSR_BLEND_MASK && !SHARED) {
+            // OR-ed into the entry K4 wrote with clear mask bits (the other part adds its own) during the next
+            // batch, or after the walk
             uint32_t bq = 0;
 #pragma unroll
             for (int k = 0; k < NQ; k++) bq |= (uint32_t)((blend[k] >> lane) & 1ull) << (qbase + k);
-            // OR-ed into the entry K4 wrote with clear mask bits (the other part adds its own)
-            if (bq) __hip_atomic_fetch_or(a.gid_sorted + range.x + b0 + lane, bq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            pend_bq = b0 + lane < ns ? bq : 0u;
+            pend_b0 = b0;
         }
         if (SHARED) {
             if (lane == 0) lds_store_rel(&s_done[part], bk + 1);  // slot sl may be restaged for bk + NB
@@ -468,6 +477,9 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const ui
 #endif
     }
     if (SHARED && lane == 0) lds_store_rel(&s_done[part], kDoneAll);  // the other part stages alone from here
+    if (GSR_BLEND_MASK && !SHARED && pend_bq)  // the last walked batch's bits
+        __hip_atomic_fetch_or(a.gid_sorted + range.x + pend_b0 + lane, pend_bq, __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_AGENT);
     if (CENSUS && lane == 0) {
         atomicAdd(&a.census[0], c_staged);
         atomicAdd(&a.census[1], c_eval);
