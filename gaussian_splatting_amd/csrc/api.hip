@@ -1267,8 +1267,9 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
     // (~13% of a 1M@1080p view) that gauss_reduce appends to, instead of a lane per Gaussian.
     const bool use_list = zmode != 0 && live_list_mode();
     // atomic backward: per-Gaussian rows (zeroed by the forward, which marked its buffer) instead of records +
-    // gauss_reduce; it needs the live list (the record path serves every other mode, and the view blocks)
-    const bool atomic = !screen && use_list && R > 0 && option(OPT_BWD_ATOMIC) != 0 && acc_marked(geom_buffer);
+    // gauss_reduce; it needs the live list, or a view block (gauss_live_views writes the block's sums and flags);
+    // the record path serves every other mode
+    const bool atomic = (screen || use_list) && R > 0 && option(OPT_BWD_ATOMIC) != 0 && acc_marked(geom_buffer);
     // (the atomic backward writes no per-instance records: no record scratch)
     const size_t R_recs = atomic ? 0 : (size_t)R;
     carve_recs(nullptr, R_recs, (size_t)P, &recs, &sums, &live, &live_count, &rec_bytes);
@@ -1366,7 +1367,11 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
         HIP_TRY(launch_render_bwd(ra, max_units, stream, grid_mode), "render_bwd");
     }
     if (int rc = check_debug(debug, stream, "render_bwd")) return rc;
-    if (atomic) {  // (stage "gauss_reduce": the step between render_bwd and gauss_bwd)
+    if (atomic && screen) {  // (stage "gauss_reduce": the step between render_bwd and gauss_bwd / the exchange)
+        StageScope sc(ST_GAUSS_REDUCE, stream);
+        HIP_TRY(launch_gauss_live_views(P, geom.touched, geom.acc, radii, geom.clamped, sums, flags, stream),
+                "gauss_live_views");
+    } else if (atomic) {
         StageScope sc(ST_GAUSS_REDUCE, stream);
         HIP_TRY(launch_gauss_live(P, geom.touched, geom.acc, sums, live, live_count, stream), "gauss_live");
     } else {

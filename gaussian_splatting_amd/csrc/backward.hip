@@ -541,6 +541,43 @@ hipError_t launch_gauss_live(int P, uint32_t* touched, float4* acc, const GradRe
     return hipGetLastError();
 }
 
+// The atomic backward into a view block (gsr_rasterize_backward_screen, multi-GPU view exchange): one lane
+// per Gaussian writes its dense sums -- its accumulator row if its touched bit is set (the row then zeroed),
+// zeros otherwise -- and its flag word, as gauss_reduce does for a view block; the words it read are cleared.
+__global__ void __launch_bounds__(64) gauss_live_views_kernel(int P, uint32_t* __restrict__ touched,
+                                                              float4* __restrict__ acc, const int* __restrict__ radii,
+                                                              const uint8_t* __restrict__ clamped, GradRecs sums,
+                                                              uint32_t* __restrict__ flags) {
+    const int lane = threadIdx.x;
+    const uint32_t g = blockIdx.x * 64u + (uint32_t)lane;
+    if (g >= (uint32_t)P) return;
+    const uint32_t w = touched[g >> 5];
+    const bool lv = (w >> (g & 31u)) & 1u;
+    float4 ra = make_float4(0.f, 0.f, 0.f, 0.f), rb = ra, rc = ra;
+    float4* row = acc + (size_t)g * kAccRow4;
+    if (lv) {
+        ra = row[0];
+        rb = row[1];
+        rc = row[2];
+    }
+    const int rad = radii[g];
+    const uint8_t cm = clamped[g];
+    sums.a[g] = ra;
+    sums.b[g] = rb;
+    sums.c[g] = make_float2(rc.x, rc.y);
+    flags[g] = (rad > 0 ? 1u : 0u) | ((uint32_t)(cm & 7u) << 1);
+    if (lv) row[0] = row[1] = row[2] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if ((lane & 31) == 0 && w) touched[g >> 5] = 0u;  // (after every lane's read: the stores depend on w)
+}
+
+hipError_t launch_gauss_live_views(int P, uint32_t* touched, float4* acc, const int* radii, const uint8_t* clamped,
+                                   const GradRecs& sums, uint32_t* flags, hipStream_t stream) {
+    if (P <= 0) return hipSuccess;
+    hipLaunchKernelGGL(gauss_live_views_kernel, dim3((uint32_t)(((size_t)P + 63) / 64)), dim3(64), 0, stream, P, touched,
+                       acc, radii, clamped, sums, flags);
+    return hipGetLastError();
+}
+
 // ---- 2. SH colour backward, one coefficient at a time ---------------------------
 // Row accessors: coefficient k of this thread's Gaussian (3 floats).
 struct ShLds {

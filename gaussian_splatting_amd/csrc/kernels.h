@@ -553,6 +553,11 @@ hipError_t launch_gauss_reduce(int P, const GeomState& g, const GradRecs& recs, 
 // from its accumulator row (zeroed) to `sums` at its list position -- instead of gauss_reduce
 hipError_t launch_gauss_live(int P, uint32_t* touched, float4* acc, const GradRecs& sums, uint32_t* live,
                              uint32_t* live_count, hipStream_t stream);
+// atomic screen-space backward: the view block's dense sums (a touched Gaussian's row, zeroed after; zeros
+// otherwise) and flag words (visible, SH clamp bits) from the touched bits (re-zeroed) -- gauss_reduce's view
+// block output without records
+hipError_t launch_gauss_live_views(int P, uint32_t* touched, float4* acc, const int* radii, const uint8_t* clamped,
+                                   const GradRecs& sums, uint32_t* flags, hipStream_t stream);
 // multi-view backward over gathered view blocks (backward.hip section 4)
 struct ViewsBwdArgs {
     int P, D, M;

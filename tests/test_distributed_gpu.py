@@ -74,10 +74,14 @@ def _worker(rank, port, outdir):
                torch.Tensor([]), d("viewmatrix"), d("projmatrix"), inp["tanfovx"], inp["tanfovy"], gc.to(dev),
                gd.to(dev), d("shs"), inp["sh_degree"], d("campos"), geom, nr, binning, img, False, False)
         # sparse (default) and dense view blocks, and the sparse blocks in 3 Gaussian-range chunks whose
-        # async all-gathers overlap the earlier chunks' multi-view backward
+        # async all-gathers overlap the earlier chunks' multi-view backward.  The screen-space backward runs once
+        # and its block is copied into each exchange: with the atomic backward (the default) two runs agree to
+        # float32 re-association only, and the modes are compared bit for bit
+        block0 = torch.empty(_C.view_block_floats(CASE.P), device=dev)
+        _C.rasterize_gaussians_backward_screen(*bwd, view_block=block0)
         for mode, sparse, chunks in (("views", True, 1), ("dense", False, 1), ("chunked", True, 3)):
             ex = ViewExchange(CASE.P, dev, sparse=sparse, chunks=chunks)
-            _C.rasterize_gaussians_backward_screen(*bwd, view_block=ex.local_block())
+            ex.local_block().copy_(block0)
             arena2 = GradArena(CASE.P, M, dev)
             arena2.flat.fill_(float("nan"))  # the sparse exchange's zero fill must cover every row
             ex.exchange(zero=arena2.flat if sparse else None)

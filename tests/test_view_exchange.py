@@ -128,6 +128,33 @@ def test_views_sum_equals_sum_of_single_views(split):
         assert err <= 2e-6 * max(scale, 1e-3) + 1e-9, (k, err, scale)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("split", [False, True])
+def test_screen_block_atomic_matches_record(split):
+    """The screen-space backward on the atomic path (the default; gauss_live_views writes the block's sums from
+    the accumulator rows) gives the record path's view block (gauss_reduce) to float32 re-association: every
+    sum plane within 1e-5 of its max |sum|, the flag words (visible, SH clamp bits) and the camera header
+    identical."""
+    from gaussian_splatting_amd import _lib
+
+    dev = torch.device("cuda", 0)
+    inp, case = _view_inputs(dict(P=2000, W=96, H=80), 7.0, dev)
+    blocks = {}
+    for mode in (0, 1):
+        with _lib.options(bwd_atomic=mode):
+            _, blocks[mode], t = _single_and_block(inp, case, dev, split)
+    torch.cuda.synchronize()
+    P = t["means3D"].shape[0]
+    rec, atm = blocks[0], blocks[1]
+    assert torch.equal(rec[:64], atm[:64])
+    assert torch.equal(rec[64 + 10 * P:64 + 11 * P].view(torch.int32), atm[64 + 10 * P:64 + 11 * P].view(torch.int32))
+    for lo, hi in ((0, 4 * P), (4 * P, 8 * P), (8 * P, 10 * P)):
+        r, a = rec[64 + lo:64 + hi], atm[64 + lo:64 + hi]
+        scale = max(float(r.abs().max()), 1e-30)
+        assert float((a - r).abs().max()) <= 1e-5 * scale, (lo, float((a - r).abs().max()), scale)
+    assert float(atm[64:64 + 10 * P].abs().max()) > 0
+
+
 def _live(block, P):
     """Gaussians a packed block keeps: visible (flag bit 0) with a non-zero sum."""
     body = block[64:64 + 11 * P]
