@@ -675,6 +675,11 @@ __device__ u64* g_k3_scratch;
 #ifndef GSR_K3_PRO
 #define GSR_K3_PRO 1
 #endif
+// Timing builds only (the record path's inputs are then missing): K3 without the record starts and the
+// content-bit zeroing, which only the record backward reads
+#ifndef GSR_K3_NO_RECS
+#define GSR_K3_NO_RECS 0
+#endif
 
 template <bool LDS>
 __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
@@ -779,7 +784,7 @@ __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
     // stores, and the scans' __syncthreads for all of them)
     u64 carry = block_sum<u64, true>(before, s_tmp);
     const u64 chunk_base = carry;
-    for (int gq = g0; gq < g1; gq += 4 * kBinThreads) {
+    for (int gq = g0; gq < (GSR_K3_NO_RECS ? g0 : g1); gq += 4 * kBinThreads) {
         uint32_t nr[4];
 #pragma unroll
         for (int u = 0; u < 4; u++) {
@@ -800,7 +805,7 @@ __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
             carry += all;
         }
     }
-    if (rec_flag) {  // (GSR_FLAG_BITS: 128 flags per 16-byte word)
+    if (rec_flag && !GSR_K3_NO_RECS) {  // (GSR_FLAG_BITS: 128 flags per 16-byte word)
         constexpr u64 kPer = GSR_FLAG_BITS ? 128 : 16;
         const u64 e1 = min(chunk_base + chunk_total[blockIdx.x], cap);
         uint4* w = reinterpret_cast<uint4*>(rec_flag);
