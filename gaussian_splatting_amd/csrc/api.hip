@@ -306,9 +306,12 @@ void carve_recs(char* base, size_t R, size_t P, gsr::GradRecs* recs, gsr::GradRe
 // "bwd_atomic": the render backward adds each instance's sums into per-Gaussian rows with float atomics
 // (render.hip ATOMIC) and gauss_live lists the touched Gaussians, instead of per-instance records summed
 // by gauss_reduce (deterministic).  The forward zeroes the rows when the option is on at forward time and
-// marks its buffer (acc_mark below); a backward adds atomically iff the option is on and its buffer is marked.
+// marks its buffer (geom_mark below); a backward adds atomically iff the option is on and its buffer is marked.
 #ifndef GSR_BWD_ATOMIC_DEFAULT
 #define GSR_BWD_ATOMIC_DEFAULT 1
+#endif
+#ifndef GSR_K3_RECS_ALWAYS
+#define GSR_K3_RECS_ALWAYS 0  // A/B: K3 writes the record path's inputs whatever the forward's backward path
 #endif
 #ifndef GSR_FWD_FILL_BLOCKS
 #define GSR_FWD_FILL_BLOCKS 256  // one-wave blocks zeroing the accumulators in render_fwd's launch (a multiple of 8)
@@ -367,32 +370,40 @@ int option_index(const char* name) {
     return -1;
 }
 
-// The geometry buffers whose last forward zeroed the atomic backward's accumulator rows ("bwd_atomic" on at
-// forward time).  The backward takes the atomic path only for them: a buffer from a forward without the
-// option (or one the library never saw, e.g. copied in) gets the record path, which reads no rows.  Every
-// forward re-marks its buffer, so an address the caching allocator hands out again carries its latest
-// forward's choice.  Bounded: past kAccMarksMax entries the table starts over (misses take the record path).
-std::mutex g_acc_mu;
-std::vector<std::pair<const void*, bool>> g_acc_marks;
-constexpr size_t kAccMarksMax = 4096;
+// What each geometry buffer's last forward left for its backwards: whether it zeroed the atomic backward's
+// accumulator rows ("bwd_atomic" on at forward time) and whether its K3 wrote the record path's inputs (record
+// starts, zeroed content bits; skipped when the forward zeroed the rows -- GSR_K3_RECS_ALWAYS keeps them).  A
+// backward adds atomically only into a zeroed buffer, and before a record-path backward of a buffer without
+// record inputs it writes them (launch_rec_prep).  A buffer the library never saw (copied in) is neither: the
+// record path, after the prep.  Every forward re-marks its buffer, so an address the caching allocator hands
+// out again carries its latest forward's state.  Bounded: past kGeomMarksMax entries the table starts over
+// (a miss costs a prep, never a wrong result).
+struct GeomMark {
+    const void* buf;
+    bool zeroed, recs;
+};
+std::mutex g_mark_mu;
+std::vector<GeomMark> g_marks;
+constexpr size_t kGeomMarksMax = 4096;
 
-void acc_mark(const void* geom_buffer, bool zeroed) {
-    std::lock_guard<std::mutex> lk(g_acc_mu);
-    for (auto& m : g_acc_marks)
-        if (m.first == geom_buffer) {
-            m.second = zeroed;
+void geom_mark(const void* geom_buffer, bool zeroed, bool recs) {
+    std::lock_guard<std::mutex> lk(g_mark_mu);
+    for (auto& m : g_marks)
+        if (m.buf == geom_buffer) {
+            m.zeroed = zeroed;
+            m.recs = recs;
             return;
         }
-    if (!zeroed) return;  // (absent = not zeroed)
-    if (g_acc_marks.size() >= kAccMarksMax) g_acc_marks.clear();
-    g_acc_marks.emplace_back(geom_buffer, true);
+    if (!zeroed && !recs) return;  // (absent = neither)
+    if (g_marks.size() >= kGeomMarksMax) g_marks.clear();
+    g_marks.push_back(GeomMark{geom_buffer, zeroed, recs});
 }
 
-bool acc_marked(const void* geom_buffer) {
-    std::lock_guard<std::mutex> lk(g_acc_mu);
-    for (const auto& m : g_acc_marks)
-        if (m.first == geom_buffer) return m.second;
-    return false;
+GeomMark geom_marked(const void* geom_buffer) {
+    std::lock_guard<std::mutex> lk(g_mark_mu);
+    for (const auto& m : g_marks)
+        if (m.buf == geom_buffer) return m;
+    return GeomMark{geom_buffer, false, false};
 }
 
 // K2 folded into K3 in capacity mode.
@@ -887,6 +898,8 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
     const bool opt_fused = fused_binning_mode(), opt_host_total = host_total_store();
     const int opt_count_wait = option(OPT_COUNT_WAIT);
     const bool opt_atomic = option(OPT_BWD_ATOMIC) != 0;
+    // K3 writes the record path's inputs only when this forward's backwards may take it without a prep
+    const bool k3_recs = !opt_atomic || GSR_K3_RECS_ALWAYS;
     const int opt_near_mass = option(OPT_NEAR_MASS);
     // _ex / _dc forwards lay the binning buffer out for a multiple of kCapQuantum (the backward
     // recovers it from the buffer's size); gsr_rasterize_forward keeps the exact C = R layout
@@ -934,7 +947,7 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
     char* gbase = (char*)call_alloc(geom_alloc, geom_ctx, geom_bytes);
     if (!gbase) return fail(GSR_ERR_ALLOC, "rasterize_forward: geometry buffer allocation failed");
     GeomState geom = carve_geom(gbase, P, gx, gy, &geom_bytes);
-    acc_mark(gbase, false);  // (set below once the render's fill blocks are queued)
+    geom_mark(gbase, false, false);  // (set below once the binning and the render's fill blocks are queued)
     carve_image(nullptr, width, height, tiles, &img_bytes);
     char* ibase = (char*)call_alloc(image_alloc, image_ctx, img_bytes);
     if (!ibase) return fail(GSR_ERR_ALLOC, "rasterize_forward: image buffer allocation failed");
@@ -1044,7 +1057,7 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
             // was rendered (fused: also the ranges, classes and the count)
             StageScope sc(ST_BIN_SCATTER, stream);
             HIP_TRY(launch_bin_scatter(P, geom, gx, gy, bin, C, stream, img.ranges, fused_now ? rb->dev : nullptr,
-                                       fused_now, fused_now && near_first),
+                                       fused_now, fused_now && near_first, k3_recs),
                     "bin_scatter");
         }
         if (fused_now)
@@ -1089,7 +1102,7 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
                 ra.fill_blocks = GSR_FWD_FILL_BLOCKS;
             }
             HIP_TRY(launch_render_fwd(ra, stream, opt_quads), "render_fwd");
-            if (opt_atomic) acc_mark(gbase, true);
+            geom_mark(gbase, opt_atomic, k3_recs);
             const bool near_now = fused_now && near_first;
             if ((prefix || near_now) && C > 0) {  // the tiles whose walk passed their sorted prefix (usually none)
                 if (near_now)  // their far instances first (none emitted by K3); their accumulator rows zeroed
@@ -1269,7 +1282,8 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
     // atomic backward: per-Gaussian rows (zeroed by the forward, which marked its buffer) instead of records +
     // gauss_reduce; it needs the live list, or a view block (gauss_live_views writes the block's sums and flags);
     // the record path serves every other mode
-    const bool atomic = (screen || use_list) && R > 0 && option(OPT_BWD_ATOMIC) != 0 && acc_marked(geom_buffer);
+    const GeomMark mark = geom_marked(geom_buffer);
+    const bool atomic = (screen || use_list) && R > 0 && option(OPT_BWD_ATOMIC) != 0 && mark.zeroed;
     // (the atomic backward writes no per-instance records: no record scratch)
     const size_t R_recs = atomic ? 0 : (size_t)R;
     carve_recs(nullptr, R_recs, (size_t)P, &recs, &sums, &live, &live_count, &rec_bytes);
@@ -1345,6 +1359,10 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
     // the records' content bytes (zeroed by the forward's K3): render_bwd sets those of the records
     // it writes, gauss_reduce reads them to find the records
     recs.flag = bin.rec_flag;
+    if (!atomic && R > 0 && !mark.recs) {  // a forward that left no record inputs (or a buffer never seen)
+        HIP_TRY(launch_rec_prep(P, geom, bin, C, stream), "record prep");
+        geom_mark(geom_buffer, mark.zeroed, true);
+    }
     if (R > 0) {
         StageScope sc(ST_RENDER_BWD, stream);
         RenderBwdArgs ra{};

@@ -681,6 +681,47 @@ __device__ u64* g_k3_scratch;
 #define GSR_K3_NO_RECS 0
 #endif
 
+// The record path's inputs for chunk blockIdx.x (Gaussians [g0, g1), their instances starting at `chunk_base`):
+// every Gaussian's first record index -- chunk base + in-order scan of tiles_touched -- and the zeroed content
+// bits of the chunk's emission range.  The counts of up to four rounds are requested before the first scan,
+// the scans' barriers are LDS-only, and the content-bit zeroing is issued last -- the memory counter is in
+// order, so a load issued after a store waits for that store too.  K3 runs it when the forward's backward may
+// take the record path; rec_prep_kernel when a backward takes it after a forward that skipped it.
+__device__ __forceinline__ void rec_starts_chunk(int g0, int g1, u64 chunk_base, const uint32_t* __restrict__ tiles_touched,
+                                                 const u64* __restrict__ chunk_total, uint32_t* __restrict__ rec_start,
+                                                 float4* __restrict__ rec, uint8_t* __restrict__ rec_flag, u64 cap,
+                                                 u64* s_tmp) {
+    u64 carry = chunk_base;
+    for (int gq = g0; gq < g1; gq += 4 * kBinThreads) {
+        uint32_t nr[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int g = gq + u * kBinThreads + (int)threadIdx.x;
+            nr[u] = g < g1 ? tiles_touched[g] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int gb = gq + u * kBinThreads;
+            if (gb >= g1) break;  // uniform
+            const int g = gb + (int)threadIdx.x;
+            u64 all = 0;
+            const u64 at = carry + block_exclusive_scan<u64, true>((u64)nr[u], s_tmp, &all);
+            if (g < g1) {
+                rec_start[g] = (uint32_t)at;
+                if (!GSR_REC_START_GATHER && nr[u]) reinterpret_cast<uint32_t*>(rec + (size_t)kRecRows * g + 3)[3] = (uint32_t)at;
+            }
+            carry += all;
+        }
+    }
+    if (rec_flag) {  // (GSR_FLAG_BITS: 128 flags per 16-byte word)
+        constexpr u64 kPer = GSR_FLAG_BITS ? 128 : 16;
+        const u64 e1 = min(chunk_base + chunk_total[blockIdx.x], cap);
+        uint4* w = reinterpret_cast<uint4*>(rec_flag);
+        for (u64 i = chunk_base / kPer + threadIdx.x; i < (e1 + kPer - 1) / kPer; i += blockDim.x)
+            w[i] = make_uint4(0u, 0u, 0u, 0u);
+    }
+}
+
 template <bool LDS>
 __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
     int P, int chunk, const uint2* __restrict__ rect, const uint32_t* __restrict__ tiles_touched,
@@ -782,40 +823,15 @@ __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
     // LDS-only, and the content-byte zeroing issued last -- the memory counter is in order, so a load
     // issued after a store waits for that store too: each round had waited for the previous round's
     // stores, and the scans' __syncthreads for all of them)
-    u64 carry = block_sum<u64, true>(before, s_tmp);
-    const u64 chunk_base = carry;
-    for (int gq = g0; gq < (GSR_K3_NO_RECS ? g0 : g1); gq += 4 * kBinThreads) {
-        uint32_t nr[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int g = gq + u * kBinThreads + (int)threadIdx.x;
-            nr[u] = g < g1 ? tiles_touched[g] : 0u;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int gb = gq + u * kBinThreads;
-            if (gb >= g1) break;  // uniform
-            const int g = gb + (int)threadIdx.x;
-            u64 all = 0;
-            const u64 at = carry + block_exclusive_scan<u64, true>((u64)nr[u], s_tmp, &all);
-            if (g < g1) {
-                rec_start[g] = (uint32_t)at;
-                if (!GSR_REC_START_GATHER && nr[u]) reinterpret_cast<uint32_t*>(rec + (size_t)kRecRows * g + 3)[3] = (uint32_t)at;
-            }
-            carry += all;
-        }
-    }
-    if (rec_flag && !GSR_K3_NO_RECS) {  // (GSR_FLAG_BITS: 128 flags per 16-byte word)
-        constexpr u64 kPer = GSR_FLAG_BITS ? 128 : 16;
-        const u64 e1 = min(chunk_base + chunk_total[blockIdx.x], cap);
-        uint4* w = reinterpret_cast<uint4*>(rec_flag);
-        for (u64 i = chunk_base / kPer + threadIdx.x; i < (e1 + kPer - 1) / kPer; i += blockDim.x)
-            w[i] = make_uint4(0u, 0u, 0u, 0u);
+    // (rec_start null: the forward's backward takes the atomic path, which reads neither)
+    if (rec_start && !GSR_K3_NO_RECS) {
+        const u64 chunk_base = block_sum<u64, true>(before, s_tmp);
+        rec_starts_chunk(g0, g1, chunk_base, tiles_touched, chunk_total, rec_start, rec, rec_flag, cap, s_tmp);
     }
     if (LDS) lds_barrier();
 #else
     u64 carry = block_sum(before, s_tmp);
-    if (rec_flag) {
+    if (rec_flag && rec_start) {
         // the gradient records' content bytes of this chunk's emission range [carry, carry + total),
         // zeroed for the backward (render_bwd sets them): 16-byte words, rounded outward -- a word
         // shared with the next chunk gets zeros from both.  Clamped to the capacity (a truncated pass
@@ -831,7 +847,7 @@ __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
         const uint32_t n = g < g1 ? tiles_touched[g] : 0u;
         u64 all = 0;
         const u64 at = carry + block_exclusive_scan((u64)n, s_tmp, &all);
-        if (g < g1) {
+        if (g < g1 && rec_start) {
             rec_start[g] = (uint32_t)at;
             if (!GSR_REC_START_GATHER && n) reinterpret_cast<uint32_t*>(rec + (size_t)kRecRows * g + 3)[3] = (uint32_t)at;
         }
@@ -1560,7 +1576,7 @@ hipError_t launch_bin_count(int P, const GeomState& g, uint32_t gx, uint32_t gy,
 // K3: scatter the keys into a binning buffer of capacity `cap` (after launch_bin_count).
 hipError_t launch_bin_scatter(int P, const GeomState& g, uint32_t gx, uint32_t gy, const BinningState& b, size_t cap,
                               hipStream_t stream, uint2* ranges, unsigned long long* host_total, bool fused,
-                              bool near_first) {
+                              bool near_first, bool recs) {
     const uint32_t tiles = gx * gy;
     int chunk = 0;
     const int nchunks = bin_chunks(P, &chunk);
@@ -1587,11 +1603,35 @@ hipError_t launch_bin_scatter(int P, const GeomState& g, uint32_t gx, uint32_t g
     if (lds)
         hipLaunchKernelGGL(tile_scatter_kernel<true>, grid, block, cur_bytes, stream, P, chunk, g.rect,
                            g.tiles_touched, g.depth_key, g.order, g.n_visible, tiles, gx, g.tile_base, g.chunk_off,
-                           g.chunk_total, b.keys, (u64)cap, g.rec_start, g.rec, b.rec_flag, fs, na);
+                           g.chunk_total, b.keys, (u64)cap, recs ? g.rec_start : nullptr, g.rec,
+                           recs ? b.rec_flag : nullptr, fs, na);
     else
         hipLaunchKernelGGL(tile_scatter_kernel<false>, grid, block, 0, stream, P, chunk, g.rect, g.tiles_touched,
                            g.depth_key, g.order, g.n_visible, tiles, gx, g.tile_base, g.chunk_off, g.chunk_total,
-                           b.keys, (u64)cap, g.rec_start, g.rec, b.rec_flag, fs, na);
+                           b.keys, (u64)cap, recs ? g.rec_start : nullptr, g.rec, recs ? b.rec_flag : nullptr, fs, na);
+    return hipGetLastError();
+}
+
+// The record path's inputs after a forward that skipped them (launch_bin_scatter's `recs` false): K3's chunks,
+// each its base from K0a's chunk totals, its record starts and its content bits.
+__global__ void __launch_bounds__(kBinThreads) rec_prep_kernel(int P, int chunk, const uint32_t* __restrict__ tiles_touched,
+                                                               const u64* __restrict__ chunk_total,
+                                                               uint32_t* __restrict__ rec_start, float4* __restrict__ rec,
+                                                               uint8_t* __restrict__ rec_flag, u64 cap) {
+    __shared__ u64 s_tmp[kBinWaves];
+    const int g0 = blockIdx.x * chunk, g1 = min(P, g0 + chunk);
+    u64 before = 0;
+    for (uint32_t c = threadIdx.x; c < blockIdx.x; c += blockDim.x) before += chunk_total[c];
+    const u64 chunk_base = block_sum<u64, true>(before, s_tmp);
+    rec_starts_chunk(g0, g1, chunk_base, tiles_touched, chunk_total, rec_start, rec, rec_flag, cap, s_tmp);
+}
+
+hipError_t launch_rec_prep(int P, const GeomState& g, const BinningState& b, size_t cap, hipStream_t stream) {
+    if (P <= 0) return hipSuccess;
+    int chunk = 0;
+    const int nchunks = bin_chunks(P, &chunk);
+    hipLaunchKernelGGL(rec_prep_kernel, dim3(nchunks), dim3(kBinThreads), 0, stream, P, chunk, g.tiles_touched,
+                       g.chunk_total, g.rec_start, g.rec, b.rec_flag, (u64)cap);
     return hipGetLastError();
 }
 

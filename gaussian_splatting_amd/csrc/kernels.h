@@ -500,7 +500,9 @@ hipError_t launch_bin_count(int P, const GeomState& g, uint32_t gx, uint32_t gy,
                             unsigned long long near_target = 0);
 hipError_t launch_bin_scatter(int P, const GeomState& g, uint32_t gx, uint32_t gy, const BinningState& b, size_t cap,
                               hipStream_t stream, uint2* ranges = nullptr, unsigned long long* host_total = nullptr,
-                              bool fused = false, bool near_first = false);
+                              bool fused = false, bool near_first = false, bool recs = true);
+// The record path's inputs (record starts, zeroed content bits) after a forward whose K3 skipped them
+hipError_t launch_rec_prep(int P, const GeomState& g, const BinningState& b, size_t cap, hipStream_t stream);
 // the far instances of the tiles the forward filed for a redo (redo), behind their near entries
 // acc (atomic backward, redo only): the accumulator rows of the far Gaussians filled in are zeroed too
 hipError_t launch_far_fill(int P, const GeomState& g, uint32_t gx, uint32_t tiles, const uint2* ranges,
