@@ -1359,7 +1359,8 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
     // the records' content bytes (zeroed by the forward's K3): render_bwd sets those of the records
     // it writes, gauss_reduce reads them to find the records
     recs.flag = bin.rec_flag;
-    if (!atomic && R > 0 && !mark.recs) {  // a forward that left no record inputs (or a buffer never seen)
+    // (also with R == 0: gauss_reduce still reads every Gaussian's record start)
+    if (!atomic && !mark.recs) {  // a forward that left no record inputs (or a buffer never seen)
         HIP_TRY(launch_rec_prep(P, geom, bin, C, stream), "record prep");
         geom_mark(geom_buffer, mark.zeroed, true);
     }
