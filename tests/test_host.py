@@ -36,12 +36,17 @@ def test_library_exports_every_header_symbol(lib):
     assert set(_lib.SIGNATURES) == set(names)
 
 
-def test_library_is_gfx950(lib):
+def test_library_is_gfx950(lib, tmp_path):
     assert lib.gsr_version().decode().endswith("gfx950")
+    import shutil
+
     from gaussian_splatting_amd import _lib
 
-    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", _lib.LIB_PATH, "-d", "--no-show-raw-insn"],
-                         capture_output=True, text=True)
+    # (on a copy: `--offloading` extracts the device images next to the file it reads)
+    copy = tmp_path / "libgsr.so"
+    shutil.copy(_lib.LIB_PATH, copy)
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", str(copy), "-d", "--no-show-raw-insn"],
+                         capture_output=True, text=True, cwd=tmp_path)
     if out.returncode == 0 and out.stdout:
         assert "gfx950" in out.stdout or "gfx950" in out.stderr
 
