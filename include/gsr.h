@@ -337,6 +337,8 @@ int gsr_host_stats(double* values, int n, int reset);
  *                        which zeroes the rows when it is 1 and marks its geometry buffer; a backward takes
  *                        the atomic path iff the option is 1 and its geometry buffer carries that mark (a
  *                        buffer from a forward without the option, or one copied in, gets the record path).
+ *                        A forward with the option also skips the record path's inputs (record starts,
+ *                        content bits); a record-path backward of its buffer writes them first.
  *                        The screen-space backward (view blocks) follows the same rule: its block's sums
  *                        come from the rows (gauss_live_views) instead of gauss_reduce
  *   "near_mass"  M|0    near-first binning (capacity-hinted forwards with the fused scan): only the Gaussians
