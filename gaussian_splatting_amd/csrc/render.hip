@@ -90,6 +90,9 @@ constexpr int kBatch = 64;  // list entries staged per round (one per lane)
 #ifndef GSR_BLEND_MASK
 #define GSR_BLEND_MASK 1
 #endif
+#ifndef GSR_BLEND_VGPR
+#define GSR_BLEND_VGPR 0
+#endif
 static_assert(!GSR_BLEND_MASK || GSR_FWD_OWN_BITS, "the blend mask is written per part");
 
 // Traffic attribution builds only (results are wrong in them): GSR_ATTR bit 0
@@ -393,9 +396,14 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const ui
             }
         }
         unsigned long long todo = __ballot((qm >> qbase) & kPartMask);
-        unsigned long long blend[NQ];  // GSR_BLEND_MASK: bit j of blend[k]: some pixel of quadrant k blended entry j
+        // GSR_BLEND_MASK: bit (qbase + k) of lane j's bq: some pixel of quadrant k blended entry j.  GSR_BLEND_VGPR 1:
+        // an entry's bits gather in one SGPR (one 32-bit OR per evaluation) and go to lane j's VGPR once per entry
+        // (a compare and a select); 0: one 64-bit mask per quadrant in SGPRs (under the 80-SGPR budget those spill
+        // to VGPR lanes)
+        unsigned long long blend[NQ];
 #pragma unroll
         for (int k = 0; k < NQ; k++) blend[k] = 0ull;
+        uint32_t bq_lane = 0;
 #if GSR_FWD_LDS_PF
         // the next entry's staged rows are read from LDS before this entry is blended, so their latency
         // overlaps the blend instead of heading the next iteration
@@ -427,6 +435,7 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const ui
             const uint32_t m = (SHARED ? uniform_u32(__float_as_uint(cq.w)) >> qbase : uniform_u32(__float_as_uint(cq.w))) & alive;
 #endif
             const uint32_t pos1 = (uint32_t)(b0 + j + 1);
+            uint32_t ebits = 0;  // (GSR_BLEND_VGPR: this entry's blend bits, uniform)
 #pragma unroll
             for (int k = 0; k < NQ; k++) {
                 if (!(m & (1u << k))) continue;  // uniform: footprint misses this quadrant
@@ -444,7 +453,12 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const ui
                     c_idle += bl ? 0ull : 1ull;
                 }
                 if (!__any(w0 > 0.f)) continue;  // uniform
-                if (GSR_BLEND_MASK && !SHARED) blend[k] |= 1ull << j;
+                if (GSR_BLEND_MASK && !SHARED) {
+                    if (GSR_BLEND_VGPR)
+                        ebits |= 1u << (qbase + k);
+                    else
+                        blend[k] |= 1ull << j;
+                }
                 const float test_T = Tl[k] * (1.f - alpha);
                 const bool term = test_T < 0.0001f;  // live pixel: ends it, splat not added
                 const float w = term ? 0.f : w0;
@@ -460,13 +474,16 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const ui
                 // it with "some pixel terminated here" cost two VALU to materialise the guard)
                 if (!__any(Tl[k] > 0.f)) alive &= ~(1u << k);
             }
+            if (GSR_BLEND_MASK && GSR_BLEND_VGPR && !SHARED) bq_lane = lane == j ? ebits : bq_lane;
         }
         if (GSR_BLEND_MASK && !SHARED) {
             // OR-ed into the entry K4 wrote with clear mask bits (the other part adds its own) during the next
             // batch, or after the walk
-            uint32_t bq = 0;
+            uint32_t bq = bq_lane;
+            if (!GSR_BLEND_VGPR) {
 #pragma unroll
-            for (int k = 0; k < NQ; k++) bq |= (uint32_t)((blend[k] >> lane) & 1ull) << (qbase + k);
+                for (int k = 0; k < NQ; k++) bq |= (uint32_t)((blend[k] >> lane) & 1ull) << (qbase + k);
+            }
             pend_bq = b0 + lane < ns ? bq : 0u;
             pend_b0 = b0;
         }
