@@ -38,8 +38,9 @@ constexpr float SH_C3_0 = -0.5900435899266435f, SH_C3_1 = 2.890611442640554f, SH
 // (int16 lo | int16 hi << 16), used to skip whole waves (DESIGN.md "footprint
 // culling"); lo > hi means "never contributes".  Row 3 is the tile rectangle of
 // getRect.  The Gaussian's first emission index e0 is in the record-start array
-// (GeomState::rec_start, written by K3; GSR_REC_START_GATHER, the default) -- only a
-// GSR_REC_START_GATHER=0 build patches it into row 3's .w: the instance of this
+// (GeomState::rec_start; GSR_REC_START_GATHER, the default), which only the record-path
+// backward reads: K3 writes it after a bwd_atomic=0 forward, rec_prep_kernel on demand
+// otherwise. Only a GSR_REC_START_GATHER=0 build patches e0 into row 3's .w: the instance of this
 // Gaussian in tile (tx, ty) has emission index e0 + (ty - min.y) * width + (tx - min.x),
 // the row-major order of duplicateWithKeys (CR/rasterizer_impl.cu:108-124).
 // ---------------------------------------------------------------------------
@@ -47,9 +48,10 @@ constexpr int kRecRows = 4;
 
 // Tile-list entries (BinningState::gid_sorted) are Gaussian << 4 | quadrant mask: bit k set
 // when the splat's alpha >= 1/255 footprint reaches a pixel centre of the tile's 8x8
-// quadrant k (footprint.h).  Binning writes the mask bits as 0; the forward render computes
-// the masks of the entries it stages and writes them back, and the backward, which only
-// visits entries the forward staged, reads them.  Hence P < 2^28.
+// quadrant k (footprint.h).  Binning writes the mask bits as 0; the forward render writes
+// back, for each entry it stages, the quadrants in which some pixel blended it
+// (GSR_BLEND_MASK, a subset of the footprint's), and the backward, which only visits
+// entries the forward staged, skips entries whose mask is 0.  Hence P < 2^28.
 constexpr int kEntryMaskBits = 4;
 constexpr uint32_t kEntryMask = 0xfu;
 constexpr int kMaxGaussians = 1 << (32 - kEntryMaskBits);
