@@ -1404,7 +1404,11 @@ tile_sort_prefix_kernel(const uint2* __restrict__ ranges,
 #ifndef GSR_CLASS0_WINDOW
 #define GSR_CLASS0_WINDOW 1
 #endif
-__global__ void __launch_bounds__(kClassThreads) __attribute__((amdgpu_waves_per_eu(GSR_PREFIX_WAVES)))
+// Its occupancy (A/B: at five waves its 96-VGPR budget spills one VGPR to scratch; four gives 128).
+#ifndef GSR_WINDOW_WAVES
+#define GSR_WINDOW_WAVES GSR_PREFIX_WAVES
+#endif
+__global__ void __launch_bounds__(kClassThreads) __attribute__((amdgpu_waves_per_eu(GSR_WINDOW_WAVES)))
 tile_sort_window_kernel(const uint2* __restrict__ ranges, u64* __restrict__ keys, u64 cap,
                         uint32_t* __restrict__ gid_sorted, const uint32_t* __restrict__ list,
                         const uint32_t* __restrict__ count, uint32_t* __restrict__ sorted_len) {
