@@ -161,52 +161,66 @@ def cpu_only(cfg_name: str) -> None:
                       "cpu_baseline": base}), flush=True)
 
 
-def multi_rank_diagnostics(args, world, exchange, ex, arena, per_rank, cand_ms, dev):
-    """N > 1: which exchange ran and why (the warm-up timings of both candidates when ``auto``), its
-    time alone (an untimed pass after the timed region, every rank running the same collective count),
-    the bytes each rank receives, and every rank's own ms/step -- so a straggler or a wrong pick shows
-    in the record."""
-    reps = 5
+def _time_exchange(kind, E, arena, dev, reps=5):
+    """One exchange alone (no render): ``reps`` passes, every rank the same collective count; the max over
+    ranks of the mean wall time per pass (ms)."""
     torch.cuda.synchronize()
     dist.barrier()
     t0 = time.perf_counter()
     for _ in range(reps):
-        if exchange in ("views", "chunked"):
-            ex.exchange()
-            if exchange == "chunked":  # the chunks' gathers are waited for by the backward; here by hand
-                for w in ex._cworks or []:
+        if kind in ("views", "chunked"):
+            E.exchange()
+            if kind == "chunked":  # the chunks' gathers are waited for by the backward; here by hand
+                for w in E._cworks or []:
                     if w is not None:
                         w.wait()
-                ex._cworks = None
-            ex.finish()
+                E._cworks = None
+            E.finish()
         else:
             arena.all_reduce()
     torch.cuda.synchronize()
     ms = torch.tensor([(time.perf_counter() - t0) / reps * 1e3], dtype=torch.float64, device=dev)
     dist.all_reduce(ms, op=dist.ReduceOp.MAX)
+    return float(ms.item())
+
+
+def multi_rank_diagnostics(args, world, exchange, ex, exc, arena, per_rank, cand_ms, cand_spread, dev):
+    """With a process group: which exchange ran and why (the interleaved warm-up timings of the candidates
+    when ``auto``: median and spread), every candidate exchange's time alone (untimed passes after the
+    timed region, every rank running the same collective count), the bytes each rank receives, and every
+    rank's own ms/step -- so a straggler or a wrong pick shows in the record."""
+    E = exc if exchange == "chunked" else ex
+    alone = {"allreduce": _time_exchange("allreduce", None, arena, dev)}
+    if ex is not None:
+        alone["views" if ex.sparse else "dense"] = _time_exchange("views", ex, arena, dev)
+    if exc is not None:
+        alone["chunked"] = _time_exchange("chunked", exc, arena, dev)
+    ms = alone["dense" if exchange == "views" and not ex.sparse else exchange]
     if exchange in ("views", "chunked"):
-        recv = ex.received_bytes()
+        recv = E.received_bytes()
         what = ("all-gather of sparse view blocks (48 B per Gaussian with a non-zero render gradient; "
-                f"{ex.last_entries} entries gathered per rank at the capacity hint; "
-                f"{ex.resyncs} re-gathers after a hint below the count)" if ex.sparse and ex.last_entries else
+                f"{E.last_entries} entries gathered per rank at the capacity hint; "
+                f"{E.resyncs} re-gathers after a hint below the count)" if E.sparse and E.last_entries else
                 "all-gather of dense 44-B/Gaussian view blocks") + " + the multi-view backward on every rank"
         if exchange == "chunked":
-            what = (f"{ex.chunks} Gaussian-range chunks, each an async " + what +
+            what = (f"{E.chunks} Gaussian-range chunks, each an async " + what +
                     "; chunk k+1's all-gather runs during chunk k's backward")
     else:
         recv = int(2 * (world - 1) / world * arena.flat.numel() * 4)
         what = "RCCL all-reduce of the 59-float/Gaussian parameter-gradient arena"
     if args.exchange == "auto":
-        why = ("--exchange auto: the candidate exchanges timed in the warm-up on this fabric (whole steps, max over "
-               f"ranks, {args.auto_steps} steps each): " + ", ".join(f"{k} {v:.4f} ms/step" for k, v in cand_ms.items())
-               + f"; the faster is {exchange}")
+        why = ("--exchange auto: the candidates timed in the warm-up on this fabric in interleaved rounds (whole "
+               f"steps, max over ranks, {args.auto_steps} steps per candidate and round), median over "
+               f"{max(3, args.auto_rounds)} rounds: " + ", ".join(f"{k} {v:.4f} ms/step" for k, v in cand_ms.items())
+               + f"; the fastest is {exchange}")
     else:
         why = f"--exchange {args.exchange}"
     return {"exchange": exchange, "what": what, "why": why, "candidates_ms_per_step": cand_ms or None,
-            "exchange_ms": float(ms.item()), "received_bytes_per_rank": recv,
-            "exchange_GBs_per_rank": recv / (float(ms.item()) * 1e-3) / 1e9 if ms.item() > 0 else None,
+            "candidates_spread_ms": cand_spread or None,
+            "exchange_ms": ms, "exchange_ms_alone": alone, "received_bytes_per_rank": recv,
+            "exchange_GBs_per_rank": recv / (ms * 1e-3) / 1e9 if ms > 0 else None,
             "per_rank_ms_per_step": [round(e / args.steps * 1e3, 4) for e in per_rank],
-            "backend": dist.get_backend()}
+            "backend": dist.get_backend(), "world_size": world, "group_of_one": world == 1}
 
 
 class HostClock:
@@ -303,7 +317,14 @@ def parse_args(argv=None):
                          "view blocks (dense), or all-reduce the parameter gradients (allreduce); auto times views, "
                          "chunked and allreduce in the warm-up and keeps the fastest (DESIGN.md section 7)")
     ap.add_argument("--exchange-chunks", type=int, default=4, help="Gaussian-range chunks of --exchange chunked")
-    ap.add_argument("--auto-steps", type=int, default=5, help="timed warm-up steps per candidate of --exchange auto")
+    ap.add_argument("--auto-steps", type=int, default=3,
+                    help="timed steps per candidate and round of --exchange auto")
+    ap.add_argument("--auto-rounds", type=int, default=3,
+                    help="--exchange auto: interleaved rounds (views, chunked, allreduce, then again); the pick is "
+                         "the lowest median over the rounds (at least 3)")
+    ap.add_argument("--nccl-group", action="store_true",
+                    help="N = 1 inside an nccl (RCCL) process group of one: the step runs the --exchange path "
+                         "with every collective issued, so the line's multi_gpu object carries RCCL times at N = 1")
     ap.add_argument("--separate-sh", action="store_true",
                     help="SH as train.py's separate_sh path passes it: dc [P,1,3] + rest [P,M-1,3] (3DGS-accel surface)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="threads of the C-restatement figure (default: the process's CPU set, capped by OMP_NUM_THREADS)")
@@ -346,9 +367,14 @@ def main():
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
     ranks_seen = 1
-    if world > 1:
+    # a process group whenever N > 1, or at N = 1 with --nccl-group (RCCL exercised by a group of one)
+    grouped = world > 1 or args.nccl_group
+    if grouped:
         if rehearse:
             dist.init_process_group("gloo")
+        elif world == 1 and "MASTER_ADDR" not in os.environ:
+            dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
+                                    device_id=dev)
         else:
             dist.init_process_group("nccl", device_id=dev)
         # the rank count the collective backend really connects: a SUM of ones over the group
@@ -385,13 +411,13 @@ def main():
         sh_dc, sh_rest = None, scene.shs
         sh_in = (scene.shs,)
     arena = GradArena(P, scene.shs.shape[1], dev, separate_sh=args.separate_sh)
-    uses_views = world > 1 and args.exchange in ("auto", "views", "dense")
+    uses_views = grouped and args.exchange in ("auto", "views", "dense")
     ex = ViewExchange(P, dev, sparse=args.exchange != "dense") if uses_views else None
     exc = (ViewExchange(P, dev, chunks=args.exchange_chunks)
-           if world > 1 and args.exchange in ("auto", "chunked") else None)
+           if grouped and args.exchange in ("auto", "chunked") else None)
     # the exchange the steps run: fixed by --exchange, or (auto) picked by timing in the warm-up below
-    exchange = "none" if world == 1 else ("allreduce" if args.exchange == "allreduce" else
-                                          "chunked" if args.exchange == "chunked" else "views")
+    exchange = "none" if not grouped else ("allreduce" if args.exchange == "allreduce" else
+                                           "chunked" if args.exchange == "chunked" else "views")
     clock = HostClock()
     pc = time.perf_counter
 
@@ -416,13 +442,13 @@ def main():
         else:
             _C.rasterize_gaussians_backward(*bwd, out=arena.views())
             t3 = pc()
-            if world > 1 and collective:
+            if grouped and collective:
                 arena.all_reduce()
         t4 = pc()
         clock.add("forward_call", t1 - t0)
         clock.add("fwd_return_to_bwd_call", t2 - t1)
         clock.add("backward_call", t3 - t2)
-        if world > 1 and collective:
+        if grouped and collective:
             clock.add("exchange", t4 - t3)
         return nr
 
@@ -434,28 +460,36 @@ def main():
     while time.perf_counter() - t_ramp < args.ramp_seconds:
         step(collective=False)
         torch.cuda.synchronize()
-    if world > 1:
+    if grouped:
         dist.barrier()
     for _ in range(args.warmup):
         nr = step()
     torch.cuda.synchronize()
-    # --exchange auto at N > 1: time whole steps with each exchange on this fabric (the same number of
-    # steps and collectives on every rank, the max over ranks), keep the faster
-    cand_ms = {}
-    if world > 1 and args.exchange == "auto":
-        for cand in ("views", "chunked", "allreduce"):
-            exchange = cand
-            for _ in range(2):
-                step()
-            torch.cuda.synchronize()
-            dist.barrier()
-            t0 = time.perf_counter()
-            for _ in range(args.auto_steps):
-                step()
-            torch.cuda.synchronize()
-            tt = torch.tensor([(time.perf_counter() - t0) / args.auto_steps * 1e3], dtype=torch.float64, device=dev)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            cand_ms[cand] = float(tt.item())
+    # --exchange auto with a group: time whole steps with each exchange on this fabric, in interleaved rounds
+    # (views, chunked, allreduce, then again: a one-off stall hits one sample, not one candidate), the same
+    # number of steps and collectives on every rank, the max over ranks; keep the lowest median
+    cand_ms, cand_spread = {}, {}
+    if grouped and args.exchange == "auto":
+        import statistics
+
+        samples = {c: [] for c in ("views", "chunked", "allreduce")}
+        for _ in range(max(3, args.auto_rounds)):
+            for cand in samples:
+                exchange = cand
+                step()  # one untimed step after the switch
+                torch.cuda.synchronize()
+                dist.barrier()
+                t0 = time.perf_counter()
+                for _ in range(args.auto_steps):
+                    step()
+                torch.cuda.synchronize()
+                tt = torch.tensor([(time.perf_counter() - t0) / args.auto_steps * 1e3], dtype=torch.float64,
+                                  device=dev)
+                dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+                samples[cand].append(float(tt.item()))
+        cand_ms = {c: statistics.median(v) for c, v in samples.items()}
+        cand_spread = {c: {"min": min(v), "max": max(v), "rounds": [round(x, 4) for x in v]}
+                       for c, v in samples.items()}
         exchange = min(cand_ms, key=cand_ms.get)
         for _ in range(2):
             step()
@@ -478,7 +512,7 @@ def main():
 
     _lib.profile_reset()
     every = max(1, args.roofline_every)
-    if world > 1:
+    if grouped:
         dist.barrier()
     torch.cuda.synchronize()
     import gc as _gc
@@ -500,7 +534,7 @@ def main():
         nr = step()
         clock.add("step_wall", pc() - ts)
     torch.cuda.synchronize()
-    if world > 1:
+    if grouped:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     clock.on = False
@@ -510,14 +544,14 @@ def main():
     dom_total, dom_calls = _lib.profile_collect()[dom]
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     per_rank = [elapsed]
-    if world > 1:
+    if grouped:
         gathered = [torch.zeros_like(t) for _ in range(world)]
         dist.all_gather(gathered, t)
         per_rank = [float(g.item()) for g in gathered]
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
-    multi = (multi_rank_diagnostics(args, world, exchange, exc if exchange == "chunked" else ex, arena, per_rank,
-                                    cand_ms, dev) if world > 1 else None)
+    multi = (multi_rank_diagnostics(args, world, exchange, ex, exc, arena, per_rank, cand_ms, cand_spread, dev)
+             if grouped else None)
     if multi is not None:
         multi.update({"ranks_seen_by_backend": ranks_seen, "rank_devices": rank_devices,
                       "visible_devices_per_rank": ndev, "shared_gpu_rehearsal": rehearse})
@@ -575,7 +609,7 @@ def main():
         metric = ("Gaussian-splats/sec fwd+bwd @1080p, 1M Gaussians" if args.config == "1m_1080p_sh3" else
                   f"Gaussian-splats/sec fwd+bwd @{W}x{H}, {P} Gaussians ({args.config}; not the headline metric)")
         par = f"view-sharded x{world}"
-        if world > 1:
+        if grouped:
             # the backend that really ran (gloo in the one-GPU rehearsal, nccl = RCCL on ROCm)
             be = "RCCL" if multi["backend"] == "nccl" else multi["backend"]
             par += {"views": f" + {be} all-gather of " + ("sparse " if ex is not None and ex.sparse else "dense ")
@@ -636,7 +670,7 @@ def main():
         else:
             line["cpu_baseline"] = None
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if grouped:
         dist.destroy_process_group()
 
 

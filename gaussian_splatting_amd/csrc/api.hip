@@ -279,43 +279,23 @@ void carve_recs(char* base, size_t R, size_t P, gsr::GradRecs* recs, gsr::GradRe
 // The library's alternative kernel paths.  Each default comes from GSR_<NAME> in the environment
 // at first use; gsr_option_set changes it for later calls (tests/test_gpu_options.py runs every
 // path against the oracle).
-#ifndef GSR_FUSED_BIN_DEFAULT
 #define GSR_FUSED_BIN_DEFAULT 1
-#endif
-#ifndef GSR_ZERO_FILL_DEFAULT
 #define GSR_ZERO_FILL_DEFAULT 3
-#endif
-#ifndef GSR_FUSED_FILL_BLOCKS
 #define GSR_FUSED_FILL_BLOCKS 256  // one-wave fill blocks in render_bwd's launch (the side-stream kernel: 64 x 4 waves)
-#endif
-#ifndef GSR_LIVE_LIST_DEFAULT
 #define GSR_LIVE_LIST_DEFAULT 1
-#endif
-#ifndef GSR_SORT_PREFIX_DEFAULT
 #define GSR_SORT_PREFIX_DEFAULT 1024
-#endif
-#ifndef GSR_COUNT_WAIT_DEFAULT
 #define GSR_COUNT_WAIT_DEFAULT 2
-#endif
 // "near_mass": near-first binning (binning.hip) -- only the Gaussians in front of the depth at which the
 // screen-averaged opacity mass reaches this value get keys and are sorted; 0 = off.  Capacity-hinted
 // forwards with the fused scan only.
-#ifndef GSR_NEAR_MASS_DEFAULT
 #define GSR_NEAR_MASS_DEFAULT 30
-#endif
 // "bwd_atomic": the render backward adds each instance's sums into per-Gaussian rows with float atomics
 // (render.hip ATOMIC) and gauss_live lists the touched Gaussians, instead of per-instance records summed
 // by gauss_reduce (deterministic).  The forward zeroes the rows when the option is on at forward time and
 // marks its buffer (geom_mark below); a backward adds atomically iff the option is on and its buffer is marked.
-#ifndef GSR_BWD_ATOMIC_DEFAULT
 #define GSR_BWD_ATOMIC_DEFAULT 1
-#endif
-#ifndef GSR_K3_RECS_ALWAYS
 #define GSR_K3_RECS_ALWAYS 0  // A/B: K3 writes the record path's inputs whatever the forward's backward path
-#endif
-#ifndef GSR_FWD_FILL_BLOCKS
 #define GSR_FWD_FILL_BLOCKS 256  // one-wave blocks zeroing the accumulators in render_fwd's launch (a multiple of 8)
-#endif
 static_assert(GSR_FWD_FILL_BLOCKS % 8 == 0, "the forward's fill blocks keep the tiles' XCD mapping");
 enum Opt {
     OPT_FUSED_BIN = 0, OPT_FWD_QUADS, OPT_BWD_SEG_CK, OPT_HOST_TOTAL, OPT_ZERO_FILL, OPT_LIVE_LIST, OPT_SORT_PREFIX,

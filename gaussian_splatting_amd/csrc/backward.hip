@@ -23,14 +23,8 @@
 namespace gsr {
 
 // A/B: the gradient records are read once (gauss_reduce): streaming loads.
-#ifndef GSR_NT_REC
 #define GSR_NT_REC 0
-#endif
-#if GSR_NT_REC
-#define GSR_LD_REC(p) load_nt(p)
-#else
 #define GSR_LD_REC(p) (*(p))
-#endif
 
 // ---- 1. segmented sums of the per-instance records ------------------------------
 // One wave per 64 consecutive Gaussians.  Their records form one contiguous range
@@ -42,9 +36,7 @@ namespace gsr {
 // zeroed by the forward's K3, binning.hip): the range is scanned 1024 bytes per wave-wide load, and only the
 // 64-instance chunks that start at a record are loaded and reduced -- 5M@4K: 7.6M records of
 // 114.7M instances, the rest behind saturated pixels.
-#ifndef GSR_REDUCE_WIN_LDS
 #define GSR_REDUCE_WIN_LDS 1
-#endif
 constexpr int kRecStride = 12;  // floats per Gaussian in the LDS hand-off of chunk totals (10 used), 48 B
 
 // Sums of the records of the wave's 64 consecutive Gaussians [g0, g0 + 64), one
@@ -83,19 +75,13 @@ __device__ __forceinline__ void reduce_records(int P, int g0, const uint32_t* __
     // start (lane + 1) in LDS and a DPP max-scan spreads the marks (one wave's LDS accesses
     // execute in order, so no dependent ds_bpermute chain).
     __shared__ uint32_t s_mark[64];
-#if GSR_REDUCE_WIN_LDS
     // the current window's content bytes (masked at E1), mirrored in LDS: a chunk's record test is
     // an LDS byte read inside the window (a global reload only for the part past its end)
     __shared__ __attribute__((aligned(16))) uint8_t s_win[1024];
-#endif
     uint32_t wa = 0;  // the current window's first byte
     auto chunk = [&](uint32_t base) -> Slot {
         const uint32_t e = base + lane;
-#if GSR_REDUCE_WIN_LDS
         const bool has = e < E1 && (e - wa < 1024u ? s_win[e - wa] != 0 : recs.flag[e] != 0);
-#else
-        const bool has = e < E1 && recs.flag[e] != 0;
-#endif
         const unsigned long long st = __ballot(n && my0 < base);
         const uint32_t carry = st ? 64u - (uint32_t)__clzll((long long)st) : 0u;
         s_mark[lane] = 0u;
@@ -168,12 +154,10 @@ __device__ __forceinline__ void reduce_records(int P, int g0, const uint32_t* __
             if (k < 8) { lo &= (1ull << (8 * k)) - 1ull; hi = 0; }
             else if (k < 16) hi &= (1ull << (8 * (k - 8))) - 1ull;  // k == 8 clears hi
         }
-#if GSR_REDUCE_WIN_LDS
         wave_lds_sync();  // the previous window's readers are done (in-order LDS)
         reinterpret_cast<uint4*>(s_win)[lane] =
             make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
         wave_lds_sync();
-#endif
         while (true) {
             // drop the bytes below base (already reduced or before the range)
             if (base > p) {
@@ -204,21 +188,13 @@ __device__ __forceinline__ void reduce_records(int P, int g0, const uint32_t* __
 // A Gaussian's records are its slots [r0, r1) of the list (counted from the bytes below its range
 // start and end); the owner search, segmented scan and hand-off are the chunked variant's, in slot
 // space.  Deterministic (fixed order), though grouped differently from the chunked variant.
-#ifndef GSR_REDUCE_COMPACT
 #define GSR_REDUCE_COMPACT 1
-#endif
 static_assert(GSR_REDUCE_COMPACT || !GSR_FLAG_BITS, "the flag bits are read by the compacted reduction only");
 // GSR_REDUCE_PIPE: the records of a window's next group requested before its current group is
 // reduced, the radius read at the start, and wave-local LDS hand-offs (the workgroup is one wave).
-#ifndef GSR_REDUCE_PIPE
 #define GSR_REDUCE_PIPE 1
-#endif
 __device__ __forceinline__ void reduce_sync() {
-#if GSR_REDUCE_PIPE
     wave_lds_sync();
-#else
-    __syncthreads();
-#endif
 }
 __device__ __forceinline__ uint64_t byte_flags(uint64_t x) {  // each nonzero byte -> 0x01, zero -> 0x00
     x |= x >> 4;
@@ -248,7 +224,6 @@ __device__ __forceinline__ void reduce_records_compact(int P, int g0, const uint
     for (uint32_t wa = E0 & ~15u; wa < E1; wa += 1024u) {  // uniform
         // content bytes [wa, wa + 1024): lane l holds wa + 16 l .. + 15, masked to [E0, E1)
         const uint32_t p = wa + 16u * (uint32_t)lane;
-#if GSR_FLAG_BITS
         // (flag bits: this lane's 16 positions are half of one 32-bit word, wa being a multiple of 16)
         uint32_t m16 = 0;
         if (p < E1) {
@@ -274,48 +249,9 @@ __device__ __forceinline__ void reduce_records_compact(int P, int g0, const uint
             const uint32_t b = d - 16u * (uint32_t)L;  // positions of lane L below q (16: all of them)
             return offL + (uint32_t)__popc(mL & (b >= 16 ? 0xffffu : (1u << b) - 1u));
         };
-#else
-        uint64_t lo = 0, hi = 0;
-        if (p < E1) {
-            const uint4 f = *reinterpret_cast<const uint4*>(recs.flag + p);
-            lo = byte_flags((uint64_t)f.x | ((uint64_t)f.y << 32));
-            hi = byte_flags((uint64_t)f.z | ((uint64_t)f.w << 32));
-            const uint32_t k = E1 - p;  // bytes of this lane below E1
-            if (k < 8) { lo &= (1ull << (8 * k)) - 1ull; hi = 0; }
-            else if (k < 16) hi &= (1ull << (8 * (k - 8))) - 1ull;
-            if (p < E0) {  // (first window, lane 0 only) bytes below E0 are the previous wave's
-                const uint32_t d = E0 - p;
-                if (d >= 8) { lo = 0; hi &= ~0ull << (8 * (d - 8)); }
-                else lo &= ~0ull << (8 * d);
-            }
-        }
-        const uint32_t c = (uint32_t)(__popcll(lo) + __popcll(hi));
-        const uint32_t incl = wave_incl_sum(c), off = incl - c;
-        const uint32_t R = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);  // records in the window
-        if (R == 0) continue;  // uniform
-        wave_lds_sync();  // the previous window's readers are done (in-order LDS)
-        {
-            uint32_t k = off;
-            for (uint64_t t = lo; t; t &= t - 1) s_list[k++] = (uint16_t)(16 * lane + (__builtin_ctzll(t) >> 3));
-            for (uint64_t t = hi; t; t &= t - 1) s_list[k++] = (uint16_t)(16 * lane + 8 + (__builtin_ctzll(t) >> 3));
-        }
-        wave_lds_sync();
-        // this lane's Gaussian: its record slots [r0, r1) of the list (records at positions below q)
-        auto slots_below = [&](uint32_t q) -> uint32_t {
-            const uint32_t d = q <= wa ? 0u : min(q - wa, 1024u);
-            const int L = (int)min(d >> 4, 63u);
-            const uint32_t offL = (uint32_t)__shfl((int)off, L);
-            const uint64_t loL = __shfl(lo, L), hiL = __shfl(hi, L);
-            const uint32_t b = d - 16u * (uint32_t)L;  // bytes of lane L below q (16: all of them)
-            const uint64_t mlo = b >= 8 ? ~0ull : (1ull << (8 * b)) - 1ull;
-            const uint64_t mhi = b >= 16 ? ~0ull : b <= 8 ? 0ull : (1ull << (8 * (b - 8))) - 1ull;
-            return offL + (uint32_t)(__popcll(loL & mlo) + __popcll(hiL & mhi));
-        };
-#endif
         // (both calls on every lane: slots_below shuffles across lanes, so it must not sit in a branch)
         const uint32_t r0 = slots_below(my0), r1e = slots_below(my1), r1 = n ? r1e : r0;
         const bool mine = r1 > r0;
-#if GSR_REDUCE_PIPE
         // the next group's records are requested before this group is reduced (one latency per window
         // instead of one per group)
         float4 xn = make_float4(0.f, 0.f, 0.f, 0.f), yn = xn;
@@ -326,11 +262,9 @@ __device__ __forceinline__ void reduce_records_compact(int P, int g0, const uint
             yn = GSR_LD_REC(recs.b + (size_t)kRecAB * e);
             zn = GSR_LD_REC(recs.c + (size_t)kRecC * e);
         }
-#endif
         for (uint32_t k0 = 0; k0 < R; k0 += 64) {  // uniform: 64 records at a time
             const uint32_t k = k0 + (uint32_t)lane;
             const bool has = k < R;
-#if GSR_REDUCE_PIPE
             const float4 x = xn, y = yn;
             const float2 z = zn;
             if (k + 64 < R) {
@@ -342,7 +276,6 @@ __device__ __forceinline__ void reduce_records_compact(int P, int g0, const uint
                 xn = yn = make_float4(0.f, 0.f, 0.f, 0.f);
                 zn = make_float2(0.f, 0.f);
             }
-#endif
             // owner of slot k: the largest lane with records whose first slot is <= k
             const unsigned long long st = __ballot(mine && r0 < k0);
             const uint32_t carry = st ? 64u - (uint32_t)__clzll((long long)st) : 0u;
@@ -355,16 +288,6 @@ __device__ __forceinline__ void reduce_records_compact(int P, int g0, const uint
             const int owner = has && m ? (int)m - 1 : -1;
             const uint32_t o0 = (uint32_t)__shfl((int)r0, owner < 0 ? 0 : owner);
             const int seg0 = has ? (o0 > k0 ? (int)(o0 - k0) : 0) : lane;
-#if !GSR_REDUCE_PIPE
-            float4 x = make_float4(0.f, 0.f, 0.f, 0.f), y = x;
-            float2 z = make_float2(0.f, 0.f);
-            if (has) {
-                const uint32_t e = wa + (uint32_t)s_list[k];
-                x = GSR_LD_REC(recs.a + (size_t)kRecAB * e);
-                y = GSR_LD_REC(recs.b + (size_t)kRecAB * e);
-                z = GSR_LD_REC(recs.c + (size_t)kRecC * e);
-            }
-#endif
             const int r = lane & 15, row = lane >> 4;
             const float m1 = lane - 1 >= seg0 && r >= 1 ? 1.f : 0.f, m2 = lane - 2 >= seg0 && r >= 2 ? 1.f : 0.f,
                         m4 = lane - 4 >= seg0 && r >= 4 ? 1.f : 0.f, m8 = lane - 8 >= seg0 && r >= 8 ? 1.f : 0.f,
@@ -407,9 +330,7 @@ __global__ void __launch_bounds__(64) gauss_reduce_kernel(int P, const uint32_t*
                                                           uint32_t* __restrict__ live_count, uint32_t live_cap) {
     __shared__ __attribute__((aligned(16))) float s_rec[64 * kRecStride];
     const int g = blockIdx.x * 64 + (int)threadIdx.x;
-#if GSR_REDUCE_PIPE
     const int rad = g < P ? radii[g] : 0;  // requested with the range loads, not after the reduction
-#endif
     float4 sa, sb;
     float2 sc;
     if (GSR_REDUCE_COMPACT)
@@ -417,9 +338,6 @@ __global__ void __launch_bounds__(64) gauss_reduce_kernel(int P, const uint32_t*
     else
         reduce_records(P, blockIdx.x * 64, rec_start, tiles_touched, recs, s_rec, sa, sb, sc);
     // a Gaussian with a gradient (gauss_bwd's condition)
-#if !GSR_REDUCE_PIPE
-    const int rad = g < P ? radii[g] : 0;
-#endif
     const bool lv = g < P && rad > 0 &&
                     ((sa.x != 0.f) | (sa.y != 0.f) | (sa.z != 0.f) | (sa.w != 0.f) | (sb.x != 0.f) |
                      (sb.y != 0.f) | (sb.z != 0.f) | (sb.w != 0.f) | (sc.x != 0.f) | (sc.y != 0.f));
@@ -470,9 +388,7 @@ hipError_t launch_gauss_reduce(int P, const GeomState& g, const GradRecs& recs, 
 // 23.2 us).  (r5i / r5j's runs of several groups had measured slower only because their row arrays, written
 // under a branch, were kept in scratch memory; one lane per 32-bit word walking its bits: 21.5 us, r5f.)
 // live_list_cap bounds a shard for runs of up to kLiveGroupsMax groups.
-#ifndef GSR_LIVE_GROUPS
 #define GSR_LIVE_GROUPS 4
-#endif
 constexpr int kLiveGroups = GSR_LIVE_GROUPS;
 static_assert(kLiveGroups >= 1 && kLiveGroups <= (int)kLiveGroupsMax, "live_list_cap bounds runs of kLiveGroupsMax");
 __global__ void __launch_bounds__(64) gauss_live_kernel(int P, uint32_t* __restrict__ touched, float4* __restrict__ acc,
@@ -894,45 +810,29 @@ __device__ __forceinline__ void view_backward(const ViewCam& c, const GaussIn& g
 // ---- 3. fused per-Gaussian backward ---------------------------------------------
 // (Folding the record sums into this kernel was measured slower: the sums' dependent loads
 // then run at this kernel's LDS-limited occupancy.)
-#ifndef GSR_GB_HALVES
 #define GSR_GB_HALVES 1
-#endif
 // With GSR_GB_HALVES the SH rows go through LDS 32 at a time at the end of the kernel
 // (lanes 0-31, then 32-63): 6.6 KiB of LDS per wave instead of 13, twice the waves per CU.
 constexpr int kGbShRows = GSR_GB_HALVES ? 32 : 64;
 // Live-list entries per gauss_bwd wave (A/B: GSR_GB_LIST_E 32).  The kernel is a chain of dependent round
 // trips (list -> geometry -> SH rows -> stores) with little VALU, so half-filled waves (twice as many, each
 // with one SH half) trade idle lanes for memory-level parallelism.
-#ifndef GSR_GB_LIST_E
 #define GSR_GB_LIST_E 64
-#endif
 constexpr int kGbListE = GSR_GB_LIST_E;
 // A/B: a listed Gaussian's geometry requested with its sums (gauss_bwd_block)
-#ifndef GSR_GB_HOIST
 #define GSR_GB_HOIST 0
-#endif
 static_assert(kGbListE == 64 || (kGbListE == 32 && GSR_GB_HALVES), "64, or one SH half of 32 rows");
 // Occupancy target (A/B: GSR_GB_WAVES).  Unconstrained, the body takes 134 VGPRs: 3 waves per
 // SIMD, too few loads in flight for an HBM-bound kernel.
-#ifdef GSR_GB_WAVES
-#define GSR_GB_OCCUPANCY __attribute__((amdgpu_waves_per_eu(GSR_GB_WAVES, GSR_GB_WAVES)))
-#else
 #define GSR_GB_OCCUPANCY
-#endif
 // LIST: lane i of the grid takes entry i of the live list (the Gaussians with a gradient,
 // gauss_reduce), with per-lane SH access (kShGlobal); the outputs were zero-filled, so no other
 // row is touched.  At 1M@1080p that is ~2000 waves instead of 15625.
 // The workgroup is one wave: the SH pass's LDS hand-offs need only the wave's own in-order LDS
 // (GSR_GB_WAVESYNC), not __syncthreads, whose fence also waits for every store the wave has issued.
-#ifndef GSR_GB_WAVESYNC
 #define GSR_GB_WAVESYNC 1
-#endif
 __device__ __forceinline__ void gb_sync() {
-#if GSR_GB_WAVESYNC
     wave_lds_sync();
-#else
-    __syncthreads();
-#endif
 }
 template <int SH_MODE, bool LIST>
 __device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const uint32_t blk) {
@@ -1091,12 +991,8 @@ __device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const uin
     }
 
 // A/B: the view-vector pin for the combined SH layout too (its kernel otherwise holds 165 VGPRs)
-#ifndef GSR_GB_PIN_ALL
 #define GSR_GB_PIN_ALL 0
-#endif
-#ifndef GSR_GB_TIMING_NOSH
 #define GSR_GB_TIMING_NOSH 0  // timing builds only (results wrong): skip the deferred SH pass
-#endif
     if constexpr (kShLate && !GSR_GB_TIMING_NOSH) {
         // SH backward, half a wave at a time through LDS: coalesced stage-in of 32 rows,
         // their lanes evaluate it in place, coalesced write-back of the 32 dL/dSH rows
@@ -1155,9 +1051,7 @@ __device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const uin
 // at 1M@1080p, 78k at 5M@4K) while ~2000 blocks have entries; every surplus block is a wave launched to read a
 // counter and exit.  GSR_GB_STRIDED: a grid of kGbStridedGrid blocks walks the virtual blocks b, b + G, ...
 // up to the longest shard's end instead.
-#ifndef GSR_GB_STRIDED
 #define GSR_GB_STRIDED 0
-#endif
 constexpr uint32_t kGbStridedGrid = 2048;
 template <int SH_MODE, bool LIST = false>
 __global__ void __launch_bounds__(64) GSR_GB_OCCUPANCY gauss_bwd_kernel(GaussBwdArgs a) {
@@ -1281,23 +1175,13 @@ __device__ __forceinline__ void views_sh_band(const ViewsBwdArgs& a, int idx, fl
     }
 }
 
-#ifndef GSR_VIEWS_ONE_PASS
 #define GSR_VIEWS_ONE_PASS 1
-#endif
-#ifndef GSR_VIEWS_FLAG_PREFETCH
 #define GSR_VIEWS_FLAG_PREFETCH 1
-#endif
 template <int SH_MODE, bool PACKED, bool LIST = false>
 // 3 waves per SIMD (the LDS limit of the SH staging): the register allocator then spills a
 // few values but the per-view latency chains overlap better (8 views: 0.50 -> 0.44 ms, r1af)
-#ifndef GSR_VIEWS_WAVES
 #define GSR_VIEWS_WAVES 3
-#endif
-#ifdef GSR_VIEWS_WAVES
 #define GSR_VIEWS_OCCUPANCY __attribute__((amdgpu_waves_per_eu(GSR_VIEWS_WAVES, GSR_VIEWS_WAVES)))
-#else
-#define GSR_VIEWS_OCCUPANCY
-#endif
 __global__ void __launch_bounds__(64) GSR_VIEWS_OCCUPANCY gauss_bwd_views_kernel(ViewsBwdArgs a) {
     __shared__ __attribute__((aligned(16))) float s_sh[SH_MODE != kShGlobal ? 64 * kShStride : 4];
     const int lane = threadIdx.x;
@@ -1351,18 +1235,12 @@ __global__ void __launch_bounds__(64) GSR_VIEWS_OCCUPANCY gauss_bwd_views_kernel
                 drot_sum.x += dq.x; drot_sum.y += dq.y; drot_sum.z += dq.z; drot_sum.w += dq.w;
             }
         } sink;
-#if GSR_VIEWS_FLAG_PREFETCH  // (the next view's flag word loads while this view is evaluated)
         uint32_t flags_next = a.n_views > 0 ? view_flag<PACKED>(a, a.blocks, 0, idx) : 0u;
-#endif
 #pragma unroll 1
         for (int v = 0; v < a.n_views; v++) {
             const float* blk = a.blocks + (size_t)v * a.block_floats;
-#if GSR_VIEWS_FLAG_PREFETCH
             const uint32_t flags = flags_next;
             if (v + 1 < a.n_views) flags_next = view_flag<PACKED>(a, blk + a.block_floats, v + 1, idx);
-#else
-            const uint32_t flags = view_flag<PACKED>(a, blk, v, idx);
-#endif
             if (!(flags & 1u)) continue;  // not visible in view v: no gradient from it
             const ViewCam cam{blk + kViewCamView, blk + kViewCamProj, blk + kViewCamPos, blk[kViewCamTanX],
                               blk[kViewCamTanY],  blk[kViewCamFocalX], blk[kViewCamFocalY],
@@ -1381,7 +1259,6 @@ __global__ void __launch_bounds__(64) GSR_VIEWS_OCCUPANCY gauss_bwd_views_kernel
     if constexpr (SH_MODE != kShGlobal) __syncthreads();  // the staged SH rows are read for the last time
     float* row = SH_MODE != kShGlobal ? &s_sh[lane * kShStride] : nullptr;
     if (valid) {
-#if GSR_VIEWS_ONE_PASS
         // one walk over the views for every band: phase 1's registers are dead here, so the 48
         // accumulators fit under its peak (four walks -- one per band -- cost 0.12 of 0.28 ms at 8
         // views, r3z)
@@ -1389,12 +1266,6 @@ __global__ void __launch_bounds__(64) GSR_VIEWS_OCCUPANCY gauss_bwd_views_kernel
         else if (a.D > 1) views_sh_band<0, 9, SH_MODE, PACKED>(a, idx, mean, row, sh_dst);
         else if (a.D > 0) views_sh_band<0, 4, SH_MODE, PACKED>(a, idx, mean, row, sh_dst);
         else views_sh_band<0, 1, SH_MODE, PACKED>(a, idx, mean, row, sh_dst);
-#else
-        views_sh_band<0, 1, SH_MODE, PACKED>(a, idx, mean, row, sh_dst);
-        if (a.D > 0) views_sh_band<1, 4, SH_MODE, PACKED>(a, idx, mean, row, sh_dst);
-        if (a.D > 1) views_sh_band<4, 9, SH_MODE, PACKED>(a, idx, mean, row, sh_dst);
-        if (a.D > 2) views_sh_band<9, 16, SH_MODE, PACKED>(a, idx, mean, row, sh_dst);
-#endif
         const int K = (a.D + 1) * (a.D + 1);
         if constexpr (SH_MODE != kShGlobal) {
             for (int k = K; k < 16; k++) row[3 * k] = row[3 * k + 1] = row[3 * k + 2] = 0.f;
@@ -1709,9 +1580,7 @@ hipError_t launch_view_header(float* blk, const float* view, const float* proj, 
 // records and pixel state render_bwd and gauss_reduce re-read (r2zv: render_bwd 298 -> 290 us,
 // gauss_reduce 67 -> 63, preprocess 75.6 -> 72, step -19 us; 32 / 64 / 96 / 128 workgroups
 // within noise once the stores stream, r2zw).
-#ifndef GSR_FILL_BLOCKS
 #define GSR_FILL_BLOCKS 64
-#endif
 __global__ void __launch_bounds__(256) zero_fill_kernel(FillArgs f) {
     zero_fill_part(f, (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x,
                    (unsigned long long)gridDim.x * blockDim.x);

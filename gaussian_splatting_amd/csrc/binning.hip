@@ -45,9 +45,7 @@ namespace gsr {
 
 constexpr int kBinThreads = 1024;
 constexpr int kBinWaves = kBinThreads / 64;
-#ifndef GSR_BIN_UNROLL
 #define GSR_BIN_UNROLL 4
-#endif
 constexpr int kBinUnroll = GSR_BIN_UNROLL;  // K0 / K1 Gaussians per thread per round (loads in flight together)
 constexpr uint32_t kLdsTilesMax = 36864;  // K3 keeps one u32 per tile in LDS (144 KiB)
 constexpr uint32_t kSortWaveMax = 1024;   // longest list tile_sort_kernel sorts (one workgroup of kSortT per tile)
@@ -133,19 +131,12 @@ __device__ T block_exclusive_scan(T v, T* s_tmp, T* total) {
 // Gaussians (lane l: n tiles in rectangle r), each once; `owner` is the lane of the
 // instance's Gaussian, (tx, ty) the tile's column and row.  f may shuffle from `owner`
 // (all lanes are active).
-#ifndef GSR_FEI_DPP
 #define GSR_FEI_DPP 1
-#endif
-#ifndef GSR_FEI_FDIV
 #define GSR_FEI_FDIV 1
-#endif
-#ifndef GSR_FEI_U24
 #define GSR_FEI_U24 1
-#endif
 template <class F>
 __device__ __forceinline__ void for_each_instance(uint32_t n, uint2 r, uint32_t gx, F&& f) {
     const int lane = threadIdx.x & 63;
-#if GSR_FEI_DPP
     // Owner of slot s: the largest lane whose run starts at or before s.  Each round, the lanes
     // whose runs start inside it mark their start in the wave's LDS row (lane + 1), and an
     // inclusive max-scan over the wave spreads the marks; the previous round's last owner
@@ -167,29 +158,9 @@ __device__ __forceinline__ void for_each_instance(uint32_t n, uint2 r, uint32_t 
         wave_lds_sync();
         carry = (uint32_t)__builtin_amdgcn_readlane((int)m, 63);
         const int owner = (int)m - 1;
-#else
-    uint32_t incl = n;
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t u = __shfl_up(incl, off);
-        if (lane >= off) incl += u;
-    }
-    const uint32_t excl = incl - n;
-    const uint32_t total = __shfl(incl, 63);
-    const uint32_t w = (r.y & 0xffffu) - (r.x & 0xffffu);
-    for (uint32_t base = 0; base < total; base += 64) {
-        const uint32_t s = base + lane;
-        // owner: the largest lane whose exclusive offset is <= s (its count covers s)
-        int owner = 0;
-#pragma unroll
-        for (int step = 32; step > 0; step >>= 1) {
-            const int cand = owner + step;
-            if (__shfl(excl, cand) <= s) owner = cand;
-        }
-#endif
         const uint32_t k = s - __shfl(excl, owner);
         const uint32_t ow = __shfl(w, owner), org = __shfl(r.x, owner);
         const bool valid = s < total;
-#if GSR_FEI_FDIV
         // k / ow in fp32, branch-free (so the caller's shuffles from `owner` issue with these):
         // (k + 1/2) / ow is at least 1/(2 ow) from an integer, and rcp + mul err by < 2^-22
         // relative, so the floor is exact while k < 2^21 (a Gaussian touches < 2^21 tiles:
@@ -197,22 +168,8 @@ __device__ __forceinline__ void for_each_instance(uint32_t n, uint2 r, uint32_t 
         const uint32_t dy = (uint32_t)(((float)k + 0.5f) * __builtin_amdgcn_rcpf((float)max(ow, 1u)));
         // 24-bit multiplies (full rate; v_mul_lo_u32 / v_mad_u64_u32 are quarter rate): every
         // operand is < 2^16 (tile coordinates and widths, gx)
-#if GSR_FEI_U24
         const uint32_t tx = (org & 0xffffu) + (k - __umul24(dy, ow)), ty = (org >> 16) + dy;
         const uint32_t tile = __umul24(ty, gx) + tx;
-#else
-        const uint32_t tx = (org & 0xffffu) + (k - dy * ow), ty = (org >> 16) + dy;
-        const uint32_t tile = ty * gx + tx;
-#endif
-#else
-        uint32_t tile = 0, tx = 0, ty = 0;
-        if (valid) {
-            const uint32_t dy = k / ow;
-            tx = (org & 0xffffu) + (k - dy * ow);
-            ty = (org >> 16) + dy;
-            tile = ty * gx + tx;
-        }
-#endif
         f(valid, owner, tile, tx, ty);
     }
 }
@@ -223,9 +180,7 @@ __device__ __forceinline__ void for_each_instance(uint32_t n, uint2 r, uint32_t 
 // Gaussians in this order, so a chunk covers a compact screen region: it touches
 // few tiles, with long runs per tile, and K3's key stores land in long contiguous
 // runs instead of a few bytes per (chunk, tile) across the whole image.
-#ifndef GSR_CELL
 #define GSR_CELL 4
-#endif
 constexpr uint32_t kCell = GSR_CELL;
 static_assert(kCell >= 1 && kCell <= 64 && (kCell & (kCell - 1)) == 0,
               "GSR_CELL: a power of two in [1, 64] (cells are formed by shifts; bin_cells coarsens them by powers of two)");
@@ -233,9 +188,7 @@ static_assert(kCell >= 1 && kCell <= 64 && (kCell & (kCell - 1)) == 0,
 // GSR_CELL_MORTON: cells in Z order (Morton code of the cell column and row, over the power-of-two
 // square that holds the grid), so a chunk of the order covers a square-ish block of cells rather than
 // a strip of a cell row (5M@4K: 936 instead of 1062 tiles per chunk, tools/k3_runs.py --order).
-#ifndef GSR_CELL_MORTON
 #define GSR_CELL_MORTON 1  // r4c: bin_scatter 852-855 -> 827-831 us at 5M@4K, 1M unchanged
-#endif
 __host__ __device__ inline uint32_t spread_bits16(uint32_t x) {
     x &= 0xffffu;
     x = (x | (x << 8)) & 0x00ff00ffu;
@@ -422,9 +375,7 @@ struct FusedZero {
 // then columns in register blocks -- turns the differences into the counts.  Four LDS atomics per
 // Gaussian instead of one per instance (5M@4K: 20M instead of 114.7M) and no instance walk; the
 // counts are exactly the walk's, so everything downstream is unchanged.
-#ifndef GSR_K1_RECT
 #define GSR_K1_RECT 1
-#endif
 constexpr int kColBlock = 8;  // rows per register block of the column pass
 
 // cut != kZCutNone (near-first binning): each Gaussian counts 1 in the low 16 bits (all instances) and,
@@ -665,21 +616,12 @@ struct FusedScan {
 
 // Store-cost attribution builds only (GSR_K3_ATTR): K3 writes its keys a second
 // time into a scratch buffer, scattered as the real stores (1) or coalesced (2).
-#ifndef GSR_K3_ATTR
 #define GSR_K3_ATTR 0
-#endif
-#if GSR_K3_ATTR
-__device__ u64* g_k3_scratch;
-#endif
 
-#ifndef GSR_K3_PRO
 #define GSR_K3_PRO 1
-#endif
 // Timing builds only (the record path's inputs are then missing): K3 without the record starts and the
 // content-bit zeroing, which only the record backward reads
-#ifndef GSR_K3_NO_RECS
 #define GSR_K3_NO_RECS 0
-#endif
 
 // The record path's inputs for chunk blockIdx.x (Gaussians [g0, g1), their instances starting at `chunk_base`):
 // every Gaussian's first record index -- chunk base + in-order scan of tiles_touched -- and the zeroed content
@@ -818,7 +760,6 @@ __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
         for (uint32_t i = threadIdx.x; i < tiles; i += blockDim.x) s_cur[i] = tile_base[i] + off[i];
     }
     // first record index of every Gaussian: chunk base + in-order scan of tiles_touched
-#if GSR_K3_PRO
     // (GSR_K3_PRO: the counts of up to four rounds requested before the first scan, the scans' barriers
     // LDS-only, and the content-byte zeroing issued last -- the memory counter is in order, so a load
     // issued after a store waits for that store too: each round had waited for the previous round's
@@ -829,39 +770,10 @@ __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
         rec_starts_chunk(g0, g1, chunk_base, tiles_touched, chunk_total, rec_start, rec, rec_flag, cap, s_tmp);
     }
     if (LDS) lds_barrier();
-#else
-    u64 carry = block_sum(before, s_tmp);
-    if (rec_flag && rec_start) {
-        // the gradient records' content bytes of this chunk's emission range [carry, carry + total),
-        // zeroed for the backward (render_bwd sets them): 16-byte words, rounded outward -- a word
-        // shared with the next chunk gets zeros from both.  Clamped to the capacity (a truncated pass
-        // is rebuilt).
-        constexpr u64 kPer = GSR_FLAG_BITS ? 128 : 16;  // flags per 16-byte word
-        const u64 e1 = min(carry + chunk_total[blockIdx.x], cap);
-        uint4* w = reinterpret_cast<uint4*>(rec_flag);
-        for (u64 i = carry / kPer + threadIdx.x; i < (e1 + kPer - 1) / kPer; i += blockDim.x)
-            w[i] = make_uint4(0u, 0u, 0u, 0u);
-    }
-    for (int gb = g0; gb < g1; gb += kBinThreads) {
-        const int g = gb + (int)threadIdx.x;
-        const uint32_t n = g < g1 ? tiles_touched[g] : 0u;
-        u64 all = 0;
-        const u64 at = carry + block_exclusive_scan((u64)n, s_tmp, &all);
-        if (g < g1 && rec_start) {
-            rec_start[g] = (uint32_t)at;
-            if (!GSR_REC_START_GATHER && n) reinterpret_cast<uint32_t*>(rec + (size_t)kRecRows * g + 3)[3] = (uint32_t)at;
-        }
-        carry += all;
-    }
-    if (LDS) __syncthreads();
-#endif
     GSR_STAMP(g_st_scatter, blockIdx.x, 1);
     // the keys: chunk positions [q0, q1) of the spatial order (K0), as K1 counted them
     const int V = (int)n_visible[0];
     const int q0 = blockIdx.x * chunk, q1 = min(V, q0 + chunk);
-#if GSR_K3_ATTR
-    u64 attr_ctr = 0;
-#endif
     for (int pb = q0 + wave * 64; pb < q1; pb += kBinThreads) {
         const int p = pb + lane;
         const uint4 o = p < q1 ? order[p] : make_uint4(0u, 0u, 0u, 0u);
@@ -873,16 +785,6 @@ __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
             if (!valid) return;
             const uint32_t pos = LDS ? atomicAdd(&s_cur[t], 1u) : atomicAdd(&tile_base[t], 1u);
             if (pos < cap) keys[pos] = ((u64)kh << 32) | (kg << kEntryMaskBits);  // cap: redone if exceeded
-#if GSR_K3_ATTR == 1  // attribution: the same scattered stores again, into a scratch buffer
-            if (pos < cap) g_k3_scratch[pos] = ((u64)kh << 32) | (kg << kEntryMaskBits);
-#elif GSR_K3_ATTR == 2  // attribution: as many stores again, coalesced (lane-contiguous per step)
-            {
-                const u64 region = cap / ((u64)gridDim.x * kBinWaves);
-                const u64 at = ((u64)blockIdx.x * kBinWaves + (u64)wave) * region;
-                g_k3_scratch[at + (attr_ctr + (u64)lane) % region] = ((u64)kh << 32) | (kg << kEntryMaskBits);
-                attr_ctr += 64;
-            }
-#endif
         });
     }
 #ifdef GSR_STAMPS
@@ -892,14 +794,8 @@ __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
 }
 
 // A/B: K4 reads each key once: streaming loads.
-#ifndef GSR_NT_KEYS
 #define GSR_NT_KEYS 0
-#endif
-#if GSR_NT_KEYS
-#define GSR_LD_KEY(p) __builtin_nontemporal_load(p)
-#else
 #define GSR_LD_KEY(p) (*(p))
-#endif
 // ---- K4 ---------------------------------------------------------------------
 // Bitonic sorting network over N2 = T * E keys, element i = thread * E + r held in
 // register a[r] (keys past the list are +infinity = ~0).  Exchange distance j:
@@ -1056,12 +952,8 @@ __device__ void sort_list_global(u64* __restrict__ keys, uint32_t lo, uint32_t n
 // the tile's depths cluster in a sliver of their range, sum of squares above kSkew * n -- the
 // list goes to the bitonic network instead (the caller's fallback).  The result is the
 // reference's (depth, index) order exactly: keys are compared whole.
-#ifndef GSR_BIN_SHIFT
 #define GSR_BIN_SHIFT 1
-#endif
-#ifndef GSR_SKEW
 #define GSR_SKEW 48
-#endif
 constexpr int kBinShift = GSR_BIN_SHIFT;  // bins = pow2 >= n >> kBinShift (about two keys per bin)
 constexpr uint32_t kSkew = GSR_SKEW;      // fallback when sum(bin size^2) > kSkew * n
 
@@ -1232,17 +1124,13 @@ __device__ bool bucket_sort_list(const u64* __restrict__ keys, uint32_t lo, uint
 // Lists of up to kSortWaveMax keys: one workgroup (kSortT threads) per tile.  Short lists (<= kBucketMinN) are
 // sorted by a bitonic network in registers (no LDS, no barrier); longer ones by the bucket
 // sort, with the register network as its skew fallback.
-#ifndef GSR_BUCKET_MIN_N
 #define GSR_BUCKET_MIN_N 128
-#endif
 constexpr uint32_t kBucketMinN = GSR_BUCKET_MIN_N;
 // Threads per tile of the bucket sort below: 128 = two waves per tile, each holding half of the
 // tile's keys (the same LDS per tile as one wave, half the serial chain per thread: tile_sort
 // 66.6 -> 55.6-58.1 us at 1M@1080p against one wave, 62 us with four; r3y1).  The register
 // network for short or skewed lists runs on the first wave alone.
-#ifndef GSR_SORT_T
 #define GSR_SORT_T 128
-#endif
 constexpr int kSortT = GSR_SORT_T;
 static_assert(kSortT == 64 || kSortT == 128 || kSortT == 256, "tile_sort_kernel: 1, 2 or 4 waves");
 
@@ -1304,9 +1192,7 @@ __global__ void __launch_bounds__(kSortT) tile_sort_kernel(const uint2* __restri
 constexpr int kClassThreads = 256;
 // Class 0's workgroup size (A/B: its tiles hold 1-4k keys; more threads per tile shorten each
 // tile's barrier-separated phases at the same LDS per workgroup).
-#ifndef GSR_CLASS0_THREADS
 #define GSR_CLASS0_THREADS 256
-#endif
 template <int CLASS>
 constexpr int class_threads() { return CLASS == 0 ? GSR_CLASS0_THREADS : kClassThreads; }
 
@@ -1354,9 +1240,7 @@ __global__ void __launch_bounds__(class_threads<CLASS>()) tile_sort_class_kernel
 // kPrefixBins bins: 24 KiB, twice the class-0 kernel's occupancy), the keys themselves in
 // registers (up to kBucketMax per tile).  Skewed bins, a prefix over the buffer or a list over
 // kBucketMax fall back to the global-memory network (whole list).
-#ifndef GSR_PREFIX_KERNEL
 #define GSR_PREFIX_KERNEL 1
-#endif
 constexpr int kPrefixBuf = 2048;
 static_assert(kPrefixBuf >= 2 * (int)kSortPrefixMax, "a prefix plus the rest of its bucket fits the LDS buffer");
 constexpr int kPrefixBins = 2048;
@@ -1365,9 +1249,7 @@ constexpr int kPrefixBins = 2048;
 // (<= kBucketMax).  16 keys in at most 96 VGPRs: five workgroups per CU (the LDS would allow six;
 // 80 VGPRs spill): tile_sort 372-373 -> 357-360 us at 5M@4K against four; 512 x 8 measured 450
 // (six waves per SIMD) and 397 us (eight) (r3y3).
-#ifndef GSR_PREFIX_WAVES
 #define GSR_PREFIX_WAVES 5
-#endif
 template <int T, int E>
 __global__ void __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(E <= 16 ? GSR_PREFIX_WAVES : 2)))
 tile_sort_prefix_kernel(const uint2* __restrict__ ranges,
@@ -1401,13 +1283,9 @@ tile_sort_prefix_kernel(const uint2* __restrict__ ranges,
 // with the bins ranked in windows of at most kPrefixBuf keys; a skewed list or one bin over the
 // buffer takes the global-memory network.  tile_sort 57.5-57.9 -> 52.3-52.4 us at 1M@1080p (r3y6);
 // GSR_CLASS0_WINDOW=0 builds the class-0 kernel instead.
-#ifndef GSR_CLASS0_WINDOW
 #define GSR_CLASS0_WINDOW 1
-#endif
 // Its occupancy (A/B: at five waves its 96-VGPR budget spills one VGPR to scratch; four gives 128).
-#ifndef GSR_WINDOW_WAVES
 #define GSR_WINDOW_WAVES GSR_PREFIX_WAVES
-#endif
 __global__ void __launch_bounds__(kClassThreads) __attribute__((amdgpu_waves_per_eu(GSR_WINDOW_WAVES)))
 tile_sort_window_kernel(const uint2* __restrict__ ranges, u64* __restrict__ keys, u64 cap,
                         uint32_t* __restrict__ gid_sorted, const uint32_t* __restrict__ list,
@@ -1488,9 +1366,7 @@ __global__ void __launch_bounds__(64) copy_sorted_prefix_kernel(const uint2* __r
 
 // ---- launchers ----------------------------------------------------------------
 // Most binning chunks (A/B: GSR_BIN_CHUNKS_MAX).
-#ifndef GSR_BIN_CHUNKS_MAX
 #define GSR_BIN_CHUNKS_MAX 256
-#endif
 int bin_chunks(int P, int* chunk) {
     // ~256 chunks (enough workgroups for the chip), each < 65536 Gaussians (16-bit LDS counters)
     int n = (P + 1023) / 1024;
@@ -1594,16 +1470,6 @@ hipError_t launch_bin_scatter(int P, const GeomState& g, uint32_t gx, uint32_t g
     const NearArgs na = near_first && fused && lds && GSR_K1_RECT
                             ? NearArgs{g.zhist, 1ull, g.zcut, g.near_cnt, g.sranges}
                             : NearArgs{nullptr, 0ull, nullptr, nullptr, nullptr};
-#if GSR_K3_ATTR
-    static u64* scratch = nullptr;
-    static size_t scratch_cap = 0;
-    if (cap > scratch_cap) {
-        if (scratch) (void)hipFree(scratch);
-        if (hipMalloc(&scratch, cap * sizeof(u64)) != hipSuccess) return hipErrorOutOfMemory;
-        scratch_cap = cap;
-        if (hipMemcpyToSymbol(HIP_SYMBOL(g_k3_scratch), &scratch, sizeof(scratch)) != hipSuccess) return hipErrorUnknown;
-    }
-#endif
     if (lds)
         hipLaunchKernelGGL(tile_scatter_kernel<true>, grid, block, cur_bytes, stream, P, chunk, g.rect,
                            g.tiles_touched, g.depth_key, g.order, g.n_visible, tiles, gx, g.tile_base, g.chunk_off,
@@ -1639,9 +1505,7 @@ hipError_t launch_rec_prep(int P, const GeomState& g, const BinningState& b, siz
     return hipGetLastError();
 }
 
-#ifndef GSR_C1_GRID_SMALL
 #define GSR_C1_GRID_SMALL 64
-#endif
 hipError_t launch_tile_sort(uint32_t tiles, const uint2* ranges, const GeomState& g, const BinningState& b,
                             size_t cap, hipStream_t stream, bool zero_counts, uint32_t cells, uint32_t prefix) {
     if (tiles == 0 || cap == 0) return hipSuccess;

@@ -65,17 +65,11 @@ __host__ __device__ inline size_t align_up(size_t x, size_t a = kAlign) { return
 // before another lane's load, which wave_barrier alone (IntrNoMem: a scheduling barrier only) does not
 // (the form rocPRIM's wave_barrier uses).
 // (GSR_WAVE_FENCE=0: the bare wave_barrier, for A/B of the schedule the fences leave the compiler)
-#ifndef GSR_WAVE_FENCE
 #define GSR_WAVE_FENCE 1
-#endif
 __device__ __forceinline__ void wave_lds_sync() {
-#if GSR_WAVE_FENCE
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-#endif
     __builtin_amdgcn_wave_barrier();
-#if GSR_WAVE_FENCE
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#endif
 }
 
 // Bump allocator over a caller-provided chunk (the three opaque uint8 tensors of
@@ -196,9 +190,7 @@ struct BinningState {
 // Layout of a slot: [5 values][4 quadrant slots][64 lanes] floats, the values being
 // T, C.r, C.g, C.b, invdepth.
 // ---------------------------------------------------------------------------
-#ifndef GSR_CK_STRIDE
 #define GSR_CK_STRIDE 256  // a multiple of the render batch (64); A/B builds override it
-#endif
 constexpr int kCkStride = GSR_CK_STRIDE;
 constexpr int kCkFloats = 5 * 4 * 64;
 
@@ -244,12 +236,8 @@ __host__ __device__ inline size_t view_pack_floats(size_t entries) {
 // GSR_REC_START_GATHER: render_bwd reads each entry's first emission index from rec_start[] instead of
 // the splat record's row 3, so K3 no longer patches every visible Gaussian's record (one 4-byte store
 // into a 64-byte record each: a partial 32-byte write per Gaussian, 160 MB at 5M@4K).
-#ifndef GSR_REC_START_GATHER
 #define GSR_REC_START_GATHER 1
-#endif
-#ifndef GSR_FLAG_BITS
 #define GSR_FLAG_BITS 1
-#endif
 struct GradRecs {
     float4* a;  // (dcolor.r, dcolor.g, dcolor.b, dinvdepth)
     float4* b;  // (dmean2D.x, dmean2D.y, dopacity_eff, dconic.b)
@@ -282,9 +270,7 @@ __host__ __device__ inline uint32_t live_list_cap(uint32_t P) {
 // The render backward's per-instance records (not the per-Gaussian sums, which stay three
 // arrays): GSR_REC_AOS interleaves them as 48-byte records a, b, (c, pad), so one instance's
 // three stores land in one or two cache lines instead of three.  Index strides:
-#ifndef GSR_REC_AOS
 #define GSR_REC_AOS 1
-#endif
 constexpr int kRecAB = GSR_REC_AOS ? 3 : 1;  // float4 units between records (a, b)
 constexpr int kRecC = GSR_REC_AOS ? 6 : 1;   // float2 units between records (c)
 

@@ -155,9 +155,7 @@ hipError_t launch_zero_fill(const FillArgs& f, hipStream_t stream);
 // each range's aligned body (non-temporal: 236 MB of zeros written through the caches evicted the
 // records and pixel state render_bwd and gauss_reduce re-read, r2zv), dwords for the unaligned head
 // and tail.
-#ifndef GSR_FILL_NT
 #define GSR_FILL_NT 1
-#endif
 __device__ __forceinline__ void zero_fill_part(const FillArgs& f, unsigned long long tid, unsigned long long stride) {
     for (int s = 0; s < f.count; s++) {
         float* p = f.ptr[s];
@@ -167,12 +165,8 @@ __device__ __forceinline__ void zero_fill_part(const FillArgs& f, unsigned long 
         const unsigned long long n4 = (n - h) / 4;
         float4* body = reinterpret_cast<float4*>(p + h);
         for (unsigned long long i = tid; i < n4; i += stride) {
-#if GSR_FILL_NT
             typedef float v4f __attribute__((ext_vector_type(4)));
             __builtin_nontemporal_store((v4f){0.f, 0.f, 0.f, 0.f}, reinterpret_cast<v4f*>(body + i));
-#else
-            body[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-#endif
         }
         if (tid < h) p[tid] = 0.f;
         const unsigned long long t0 = h + 4 * n4;
@@ -194,9 +188,7 @@ constexpr int kShRestF = 45;    // floats per rest row in the split layout
 // displacing the lines the next kernels re-read (r2zx: preprocess 69.5 -> 62.7 us, bin_count
 // 45.6 -> 43.3, step -8 us).  Streaming stores of render_fwd's image outputs and streaming loads
 // of render_bwd's dL/dpixel (render.hip GSR_NT_OUT / GSR_NT_DPIX) measured no gain.
-#ifndef GSR_NT_SH
 #define GSR_NT_SH 1
-#endif
 template <int ROWS, int THREADS, bool SPLIT>
 // rowmask: bit r set = stage row r (rows left out are not read; their LDS contents are undefined).
 __device__ __forceinline__ void sh_stage_in(const ShAddr& sa, int r0, int rows, float* lds, int stride, int tid,
@@ -209,13 +201,9 @@ __device__ __forceinline__ void sh_stage_in(const ShAddr& sa, int r0, int rows, 
             const int i4 = k * THREADS + tid;
             const int d = i4 * 4, row = d / kShRowF, col = d - row * kShRowF;
             if (i4 < n4 && ((rowmask >> row) & 1ull)) {
-#if GSR_NT_SH
                 typedef float v4f __attribute__((ext_vector_type(4)));
                 *reinterpret_cast<v4f*>(&lds[row * stride + col]) =
                     __builtin_nontemporal_load(reinterpret_cast<const v4f*>(src) + i4);
-#else
-                *reinterpret_cast<float4*>(&lds[row * stride + col]) = src[i4];
-#endif
             }
         }
         return;
@@ -251,9 +239,7 @@ __device__ __forceinline__ void sh_stage_in(const ShAddr& sa, int r0, int rows, 
 // displacing the lines the next kernels re-read (r2zx: preprocess 69.5 -> 62.7 us, bin_count
 // 45.6 -> 43.3, step -8 us).  Streaming stores of render_fwd's image outputs and streaming loads
 // of render_bwd's dL/dpixel (render.hip GSR_NT_OUT / GSR_NT_DPIX) measured no gain.
-#ifndef GSR_NT_SH
 #define GSR_NT_SH 1
-#endif
 template <int ROWS, int THREADS, bool SPLIT>
 // rowmask: bit r set = write row r (rows left out are not written).
 __device__ __forceinline__ void sh_stage_out(const ShGradAddr& ga, int r0, int rows, const float* lds, int stride,
@@ -308,16 +294,11 @@ __device__ __forceinline__ void sh_stage_out(const ShGradAddr& ga, int r0, int r
 // fully unrolled loop kept ~23 iterations' addresses live across the kernel: 308 VGPRs, one wave
 // per SIMD; one iteration at a time serialised the loads.)
 #define GSR_PRAGMA(x) _Pragma(#x)
-#ifndef GSR_GATHER_BATCH
 #define GSR_GATHER_BATCH 1
-#endif
-#ifndef GSR_GATHER_UNROLL_COMB
 #define GSR_GATHER_UNROLL_COMB 12
-#endif
 template <int ROWS, int THREADS, bool SPLIT>
 __device__ __forceinline__ void sh_gather_in(const ShAddr& sa, int g, int row0, float* lds, int stride, int tid) {
     if constexpr (!SPLIT) {
-#if GSR_GATHER_BATCH
         // every piece loaded before any is stored (a row not wanted loads row 0's piece, which the
         // caller's tensor always has): one memory latency for the block, where a load inside the
         // per-lane branch made each piece wait for its own (six dependent round trips per 32 rows)
@@ -338,16 +319,6 @@ __device__ __forceinline__ void sh_gather_in(const ShAddr& sa, int g, int row0, 
             const int i4 = k * THREADS + tid, row = i4 / (kShRowF / 4), c4 = i4 - row * (kShRowF / 4);
             if (gk[k] >= 0) *reinterpret_cast<v4f*>(&lds[row * stride + 4 * c4]) = v[k];
         }
-#else
-GSR_PRAGMA(unroll GSR_GATHER_UNROLL_COMB)
-        for (int k = 0; k < ROWS * (kShRowF / 4) / THREADS; k++) {
-            const int i4 = k * THREADS + tid, row = i4 / (kShRowF / 4), c4 = i4 - row * (kShRowF / 4);
-            const int gr = __shfl(g, row0 + row);
-            if (gr >= 0)
-                *reinterpret_cast<float4*>(&lds[row * stride + 4 * c4]) =
-                    reinterpret_cast<const float4*>(sa.shs + (size_t)gr * kShRowF)[c4];
-        }
-#endif
     } else {
         // THREADS / ROWS lanes per row, each copying its share of the row's 45 rest floats (one base
         // address, immediate offsets, every load independent) and the last of them the dc triple

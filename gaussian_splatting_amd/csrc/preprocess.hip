@@ -92,9 +92,7 @@ __device__ __forceinline__ float3 sh_to_rgb(int deg, const float3* sh, float x, 
 // read just before its terms (GSR_PRE_SH_BANDS): the same expressions as sh_to_rgb, so the same roundings,
 // without the 48 floats of a whole row held at once (the kernel's register peak: 96 VGPRs, five waves per
 // SIMD; capped at six it spilled).
-#ifndef GSR_PRE_SH_BANDS
 #define GSR_PRE_SH_BANDS 0
-#endif
 template <class Coef>
 __device__ __forceinline__ float3 sh_to_rgb_acc(int deg, const Coef& c, float x, float y, float z) {
     const float3 s0 = c(0);
@@ -160,9 +158,7 @@ __device__ __forceinline__ void load_sh(const ShAddr& sa, int idx, int K, float3
 //  * the 64-byte splat records are assembled in LDS and written as one 4 KiB block.
 // A culled Gaussian gets the reference's zero radius / tiles_touched, a 0xffffffff depth
 // key and an all-zero record (never read).
-#ifndef GSR_PRE_PREFETCH
 #define GSR_PRE_PREFETCH 2
-#endif
 constexpr int kPreThreads = 64;
 static_assert(!GSR_PRE_PREFETCH || kPreThreads == 64, "the prefetching path's LDS hand-offs are wave-local: one wave");
 constexpr int kShHalfRows = 32;
@@ -172,15 +168,9 @@ constexpr int kShRowStride = 52;   // padded LDS row stride (16-byte aligned, co
 // instruction writes 1 KiB lane-linearly, so that half's image is piece-major -- 16-byte piece c of row r at
 // float4 (c * 32 + r): instruction k, lane l carries piece index 64 k + l -- and its rows are read through
 // that index (sh_to_rgb_acc).
-#ifndef GSR_PRE_GLDS
 #define GSR_PRE_GLDS 0
-#endif
 
-#ifdef GSR_PRE_WAVES
-#define GSR_PRE_OCCUPANCY __attribute__((amdgpu_waves_per_eu(GSR_PRE_WAVES)))
-#else
 #define GSR_PRE_OCCUPANCY
-#endif
 template <int SH_MODE>
 __global__ void __launch_bounds__(kPreThreads) GSR_PRE_OCCUPANCY preprocess_kernel(PreprocessArgs a) {
     __shared__ __attribute__((aligned(16))) float s_buf[SH_MODE != kShGlobal ? kShHalfRows * kShRowStride : 64 * 16];
@@ -192,7 +182,6 @@ __global__ void __launch_bounds__(kPreThreads) GSR_PRE_OCCUPANCY preprocess_kern
     const bool valid = idx < a.P;
     const int nvalid = min(kPreThreads, a.P - g0);
     for (uint32_t i = blockIdx.x * kPreThreads + lane; i < a.zero_n; i += gridDim.x * kPreThreads) a.zero[i] = 0u;
-#if GSR_PRE_PREFETCH
     // Every input of the wave requested up front (GSR_PRE_PREFETCH): the scale, rotation and opacity of
     // each lane's Gaussian, and both halves of the wave's SH block in registers (6 x 16 B per lane and
     // half) -- one memory latency for the wave, where the geometry's loads waited for the view
@@ -234,7 +223,6 @@ __global__ void __launch_bounds__(kPreThreads) GSR_PRE_OCCUPANCY preprocess_kern
         }
         pf_op = a.opacities[idx];
     }
-#endif
 
     // ---- geometry (CR/forward.cu:255-326): `ok` replaces the reference's early returns
     bool ok = valid;
@@ -261,13 +249,7 @@ __global__ void __launch_bounds__(kPreThreads) GSR_PRE_OCCUPANCY preprocess_kern
 #pragma unroll
             for (int i = 0; i < 6; i++) cov3[i] = a.cov3D_precomp[6 * idx + i];
         } else {
-#if GSR_PRE_PREFETCH
             cov3d_from_scale_rot(pf_sc, a.scale_modifier, pf_q, cov3);
-#else
-            const float3 sc = make_float3(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]);
-            const float4 q = reinterpret_cast<const float4*>(a.rotations)[idx];
-            cov3d_from_scale_rot(sc, a.scale_modifier, q, cov3);
-#endif
         }
         cov = cov2d_project(p_view, a.focal_x, a.focal_y, a.tan_fovx, a.tan_fovy, a.viewmatrix, cov3);
         constexpr float h_var = 0.3f;
@@ -312,7 +294,6 @@ __global__ void __launch_bounds__(kPreThreads) GSR_PRE_OCCUPANCY preprocess_kern
         for (int half = 0; half < 2; half++) {
             const int rows = min(kShHalfRows, nvalid - half * kShHalfRows);
             if (rows > 0) {  // wave-uniform
-#if GSR_PRE_PREFETCH
                 (void)sa;
                 if (kGlds && half == 0) {
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA's LDS writes have landed
@@ -333,10 +314,6 @@ __global__ void __launch_bounds__(kPreThreads) GSR_PRE_OCCUPANCY preprocess_kern
                     }
                 }
                 wave_lds_sync();  // (one wave: its LDS accesses complete in order)
-#else
-                sh_stage_in<kShHalfRows, kPreThreads, false>(sa, g0 + half * kShHalfRows, rows, s_buf, kShRowStride, lane);
-                __syncthreads();
-#endif
                 if ((lane >> 5) == half && ok) {
                     const float* row = &s_buf[(lane & 31) * kShRowStride];
                     if (kGlds && half == 0) {  // the piece-major image: float f of row r at 4 (32 (f / 4) + r) + f % 4
@@ -357,11 +334,7 @@ __global__ void __launch_bounds__(kPreThreads) GSR_PRE_OCCUPANCY preprocess_kern
                         rgb = sh_to_rgb(a.D, sh, dir.x, dir.y, dir.z);
                     }
                 }
-#if GSR_PRE_PREFETCH
                 wave_lds_sync();
-#else
-                __syncthreads();
-#endif
             }
         }
     } else if constexpr (SH_MODE == kShLdsSplit) {
@@ -416,11 +389,7 @@ __global__ void __launch_bounds__(kPreThreads) GSR_PRE_OCCUPANCY preprocess_kern
     // ---- footprint box and outputs
     float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0, r2 = r0, r3 = r0;
     if (ok) {
-#if GSR_PRE_PREFETCH
         const float o_eff = pf_op * h_scale;
-#else
-        const float o_eff = a.opacities[idx] * h_scale;
-#endif
         // Conservative box of the alpha >= 1/255 footprint: o*exp(-q/2) >= 1/255 <=> q <= 2 ln(255 o).
         uint32_t bbx = pack_i16x2(-32768, 32767), bby = pack_i16x2(-32768, 32767);
         if (a.footprint_cull) {
@@ -451,11 +420,7 @@ __global__ void __launch_bounds__(kPreThreads) GSR_PRE_OCCUPANCY preprocess_kern
         // the near-first binning's depth cut (binning.hip); fixed point, saturating
         float mass = 0.f;
         if (ok) {
-#if GSR_PRE_PREFETCH
             mass = pf_op * h_scale * 6.2831853f * sqrtf(fmaxf(det, 0.f)) * kMassScale;
-#else
-            mass = a.opacities[idx] * h_scale * 6.2831853f * sqrtf(fmaxf(det, 0.f)) * kMassScale;
-#endif
         }
         a.geom.mass[idx] = (uint32_t)fminf(mass, 4.0e9f);
     }
@@ -465,11 +430,7 @@ __global__ void __launch_bounds__(kPreThreads) GSR_PRE_OCCUPANCY preprocess_kern
     s_rec[lane * kRecRows + 1] = r1;
     s_rec[lane * kRecRows + 2] = r2;
     s_rec[lane * kRecRows + 3] = r3;
-#if GSR_PRE_PREFETCH
     wave_lds_sync();  // (not __syncthreads: its fence would wait for the stores above)
-#else
-    __syncthreads();
-#endif
     float4* dst = a.geom.rec + (size_t)kRecRows * g0;
 #pragma unroll
     for (int k = 0; k < kRecRows; k++) {

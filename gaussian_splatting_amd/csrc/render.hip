@@ -46,39 +46,25 @@ namespace gsr {
 constexpr int kBatch = 64;  // list entries staged per round (one per lane)
 
 // A/B switch: skip a backward quadrant whose pixels all have alpha = 0.
-#ifndef GSR_BWD_ANYSKIP
 #define GSR_BWD_ANYSKIP 1
-#endif
 // A/B switch: a half-tile forward wave tests only its own two quadrants of each entry's footprint
 // and ORs those bits into the entry (the other half adds its own).
-#ifndef GSR_FWD_OWN_BITS
 #define GSR_FWD_OWN_BITS 1
-#endif
 // A/B switch: the backward's ten per-entry sums carried across entries (zeroed after each
 // reduction) instead of declared per entry.
-#ifndef GSR_BWD_CARRY_R
 #define GSR_BWD_CARRY_R 0
-#endif
 
 // Each lane's tile-list entry of the NEXT batch is loaded during the current batch's walk, so a
 // batch's staging waits for one round trip (the splat records) instead of two (entry, then record).
-#ifndef GSR_PF_ENTRY
 #define GSR_PF_ENTRY 1
-#endif
 // Cost probe for 4x4-block units ("Why the render kernels keep their structure"): the
 // forward's entry index made a per-lane value (the same in every lane, so the results are unchanged), so
 // the entry's data are VGPRs and the quadrant skips are EXEC-mask branches -- what four 16-lane groups
 // walking their own entries would pay before any lane saving.  Off in the product.
-#ifndef GSR_FWD_LANE_ENTRY
 #define GSR_FWD_LANE_ENTRY 0
-#endif
 // A/B: software-pipelined LDS reads of the staged entries in the forward's walk (render_fwd_tile)
-#ifndef GSR_FWD_LDS_PF
 #define GSR_FWD_LDS_PF 0
-#endif
-#ifndef GSR_BWD_LDS_PF
 #define GSR_BWD_LDS_PF 0
-#endif
 // The entry mask the forward leaves for the backward: the quadrants whose footprint the entry touches
 // (0), or the quadrants in which some pixel blended it (1: set after the batch's walk from one wave-uniform
 // bit per (entry, quadrant) evaluation that passed its any-alpha test).  The backward evaluates an entry's
@@ -87,29 +73,19 @@ constexpr int kBatch = 64;  // list entries staged per round (one per lane)
 // (r5u, interleaved: 1M@1080p 0.7227 -> 0.7213 ms, 5M@4K 2.222 -> 2.207, 500k 0.7258 -> 0.7222; render_bwd
 // -4 / -19 / -8 us, render_fwd +4 / +8 / +5 us for the bits.  The ORs are issued once the next batch's
 // loads are in flight: issued before its staging they made it wait for them, render_fwd +5 us more, r5t.)
-#ifndef GSR_BLEND_MASK
 #define GSR_BLEND_MASK 1
-#endif
-#ifndef GSR_BLEND_VGPR
 #define GSR_BLEND_VGPR 0
-#endif
 static_assert(!GSR_BLEND_MASK || GSR_FWD_OWN_BITS, "the blend mask is written per part");
 
 // Traffic attribution builds only (results are wrong in them): GSR_ATTR bit 0
 // drops the backward's record / content-byte stores, bit 1 its checkpoint loads, bit 2 its
 // per-pixel state loads other than n_contrib; in the atomic backward bit 3 drops the touched-bit ORs,
 // bit 4 the accumulator adds.  The control flow is unchanged in all of them.
-#ifndef GSR_ATTR
 #define GSR_ATTR 0
-#endif
 // Cache policy A/B switches: non-temporal stores of the forward's image outputs, non-temporal
 // loads of the backward's dL/dpixel.
-#ifndef GSR_NT_OUT
 #define GSR_NT_OUT 0
-#endif
-#ifndef GSR_NT_DPIX
 #define GSR_NT_DPIX 0
-#endif
 
 GSR_STAMP_BUFFER(g_st_rfwd);
 GSR_STAMP_BUFFER(g_st_rbwd);
@@ -119,14 +95,8 @@ GSR_STAMP_BUFFER(g_st_rbwd);
 // Occupancy hint (0 = none): with the fused zero-fill blocks (RenderBwdArgs::fill) the kernel takes
 // 82 VGPRs, five waves per SIMD; GSR_BWD_WAVES=6 holds it at 79 (six), which measured the same
 // (r4c: 0.7626 vs 0.7610 ms/step, render_bwd 284-289 us either way) -- not occupancy-bound.
-#ifndef GSR_BWD_WAVES
 #define GSR_BWD_WAVES 0
-#endif
-#if GSR_BWD_WAVES
-#define GSR_BWD_OCCUPANCY __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVES, GSR_BWD_WAVES)))
-#else
 #define GSR_BWD_OCCUPANCY
-#endif
 
 __device__ __forceinline__ uint32_t uniform_u32(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
@@ -158,19 +128,9 @@ __device__ __forceinline__ float splat_alpha(float p2, float opacity, float& G) 
 // lane of this slot blend this splat" and "is any pixel of this slot still live".
 // SGPR budget of the forward: at .sgpr_count 82-96 the hardware admits 7 one-wave workgroups per
 // SIMD, at <= 80 eight (MI355X_MICROARCH.md "Residency"); the VGPRs (61) allow eight.
-#ifndef GSR_FWD_SGPRS
 #define GSR_FWD_SGPRS 80  // r4b: render_fwd 199-200 -> 195-197 us (8 SGPRs spill to VGPR lanes, prologue only); 0 = off
-#endif
-#if GSR_FWD_SGPRS
 #define GSR_FWD_SGPR_ATTR __attribute__((amdgpu_num_sgpr(GSR_FWD_SGPRS)))
-#else
-#define GSR_FWD_SGPR_ATTR
-#endif
-#ifdef GSR_FWD_WAVES
-#define GSR_FWD_OCCUPANCY __attribute__((amdgpu_waves_per_eu(GSR_FWD_WAVES, GSR_FWD_WAVES)))
-#else
 #define GSR_FWD_OCCUPANCY GSR_FWD_SGPR_ATTR
-#endif
 // One wave per PART of a tile: NQ = 4 quadrants (the whole 16x16 tile) or NQ = 2 (its top or
 // bottom half).  Each lane owns one pixel in each of the part's NQ quadrants ("slots").  With
 // half tiles the 8160 tiles of a 1080p view become 16320 waves of half the blend work each, so
@@ -200,12 +160,8 @@ __device__ __forceinline__ float splat_alpha(float p2, float opacity, float& G) 
 // Measured (r4c, 1M@1080p, three interleaved rounds): render_fwd 236-240 us against 194-196 for the
 // two independent half-tile waves -- seven waves per SIMD instead of eight (the staging of both
 // parts' footprints needs 72 VGPRs), and a part that runs ahead waits for slot reuse.  Off.
-#ifndef GSR_FWD_SHARED
 #define GSR_FWD_SHARED 0
-#endif
-#ifndef GSR_FWD_SHARED_NB
 #define GSR_FWD_SHARED_NB 3
-#endif
 constexpr int kDoneAll = 1 << 30;
 __device__ __forceinline__ int lds_load_acq(int* p) {
     return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -219,15 +175,9 @@ __device__ __forceinline__ void lds_store_rel(int* p, int v) {
 // the compiler kept from moving LDS accesses across it (GSR_RENDER_WAVESYNC) -- __syncthreads'
 // workgroup fence also makes the wave wait for every store it has in flight (the backward's gradient
 // records, the forward's entry masks and checkpoints) before the next batch's loads.
-#ifndef GSR_RENDER_WAVESYNC
 #define GSR_RENDER_WAVESYNC 1
-#endif
 __device__ __forceinline__ void unit_sync() {
-#if GSR_RENDER_WAVESYNC
     wave_lds_sync();
-#else
-    __syncthreads();
-#endif
 }
 
 template <int NB>
@@ -352,7 +302,6 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const ui
             const float4 v0 = rec[0], v1 = rec[1], v2 = rec[2];
             s_xy[0][lane] = make_float4(v0.x, v0.y, v1.y, v1.z);
             s_col[0][lane] = v2;
-#if GSR_FWD_OWN_BITS
             // this part's quadrants only; the backward (which visits only staged entries) gets every
             // part's bits OR-ed into the entry K4 wrote with clear mask bits.  A part that stopped
             // before an entry leaves its bits clear there: its pixels all ended earlier, so the
@@ -365,13 +314,6 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const ui
                 *ent = (gid << kEntryMaskBits) | qm;
             else if (qm)
                 __hip_atomic_fetch_or(ent, qm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#else
-            qm = quad_bits_exact(v0, v1, v2, tile_x0, tile_y0);
-            s_cq[0][lane] = stage_conic(v0, v1, (qm >> qbase) & kPartMask);
-            // all four bits, for the backward (which visits only staged entries); with two parts
-            // both may store the entry, the same value
-            *ent = (gid << kEntryMaskBits) | qm;
-#endif
         }
         if (kPf && b0 + kBatch + lane < ns) ent_next = a.gid_sorted[range.x + b0 + kBatch + lane];
         if (!SHARED) unit_sync();
@@ -404,36 +346,11 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const ui
 #pragma unroll
         for (int k = 0; k < NQ; k++) blend[k] = 0ull;
         uint32_t bq_lane = 0;
-#if GSR_FWD_LDS_PF
-        // the next entry's staged rows are read from LDS before this entry is blended, so their latency
-        // overlaps the blend instead of heading the next iteration
-        int jn = todo ? __builtin_ctzll(todo) : 0;
-        float4 nxy = s_xy[sl][jn], ncq = s_cq[sl][jn], ncol = s_col[sl][jn];
-#endif
         while (todo && alive) {
-#if GSR_FWD_LDS_PF
-            const int j = jn;
-            todo &= todo - 1;
-            const float4 xy = nxy, cq = ncq, col = ncol;
-            jn = todo ? __builtin_ctzll(todo) : jn;  // (uniform; a repeated slot when none is left: unused)
-            nxy = s_xy[sl][jn];
-            ncq = s_cq[sl][jn];
-            ncol = s_col[sl][jn];
-            const uint32_t m = (SHARED ? uniform_u32(__float_as_uint(cq.w)) >> qbase : uniform_u32(__float_as_uint(cq.w))) & alive;
-#else
             const int j = __builtin_ctzll(todo);
             todo &= todo - 1;
-#endif
-#if GSR_FWD_LDS_PF
-#elif GSR_FWD_LANE_ENTRY
-            int jl = j;
-            asm volatile("" : "+v"(jl));  // per lane for the compiler
-            const float4 xy = s_xy[sl][jl], cq = s_cq[sl][jl], col = s_col[sl][jl];
-            const uint32_t m = (SHARED ? __float_as_uint(cq.w) >> qbase : __float_as_uint(cq.w)) & alive;
-#else
             const float4 xy = s_xy[sl][j], cq = s_cq[sl][j], col = s_col[sl][j];
             const uint32_t m = (SHARED ? uniform_u32(__float_as_uint(cq.w)) >> qbase : uniform_u32(__float_as_uint(cq.w))) & alive;
-#endif
             const uint32_t pos1 = (uint32_t)(b0 + j + 1);
             uint32_t ebits = 0;  // (GSR_BLEND_VGPR: this entry's blend bits, uniform)
 #pragma unroll
@@ -532,17 +449,10 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const ui
             a.img.accum[NT + t] = C1[k];
             a.img.accum[2 * NT + t] = C2[k];
             a.img.accum[3 * NT + t] = D[k];
-#if GSR_NT_OUT  // the image outputs are not read again in the step: streaming stores
-            __builtin_nontemporal_store(C0[k] + T * a.bg[0], a.out_color + pix);
-            __builtin_nontemporal_store(C1[k] + T * a.bg[1], a.out_color + N + pix);
-            __builtin_nontemporal_store(C2[k] + T * a.bg[2], a.out_color + 2 * N + pix);
-            __builtin_nontemporal_store(D[k], a.out_invdepth + pix);
-#else
             a.out_color[pix] = C0[k] + T * a.bg[0];
             a.out_color[N + pix] = C1[k] + T * a.bg[1];
             a.out_color[2 * N + pix] = C2[k] + T * a.bg[2];
             a.out_invdepth[pix] = D[k];
-#endif
         }
     }
 
@@ -637,9 +547,7 @@ __global__ void __launch_bounds__(64) GSR_FWD_OCCUPANCY render_fwd_kernel(Render
 // one unit's duration after its last units start, and a half tile's cost (set by how soon its pixels
 // saturate) is not known in advance, so the units dispatched last are made short instead: the tail
 // shrinks, for ~2x the staging work on those tiles only.
-#ifndef GSR_FWD_TAIL_QUADS
 #define GSR_FWD_TAIL_QUADS 10
-#endif
 __global__ void __launch_bounds__(64) GSR_FWD_OCCUPANCY render_fwd_hybrid_kernel(RenderFwdArgs a) {
     uint32_t bid = 0;
     if (fwd_fill_block(a, bid)) return;
@@ -660,9 +568,7 @@ __global__ void __launch_bounds__(64) GSR_FWD_OCCUPANCY render_fwd_hybrid_kernel
 // Shared staging (GSR_FWD_SHARED): one 128-thread workgroup per tile, its two waves the halves.
 // (72 VGPRs at seven waves per SIMD: the staging of both parts' footprints holds more registers
 // beside the blend state; left alone the compiler took 84, five waves)
-#ifndef GSR_FWD_SHARED_WAVES
 #define GSR_FWD_SHARED_WAVES 7
-#endif
 template <bool CENSUS>
 __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(GSR_FWD_SHARED_WAVES, GSR_FWD_SHARED_WAVES)))
 GSR_FWD_SGPR_ATTR render_fwd_shared_kernel(RenderFwdArgs a) {
@@ -836,17 +742,10 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
         if (GSR_ATTR & 4) {
             g0[q] = g1[q] = g2[q] = gi[q] = c0[q] = c1[q] = c2[q] = cd[q] = fT[q] = 0.5f;
         } else {
-#if GSR_NT_DPIX  // read once per step: streaming loads
-            g0[q] = __builtin_nontemporal_load(a.dL_dpix + pix);
-            g1[q] = __builtin_nontemporal_load(a.dL_dpix + N + pix);
-            g2[q] = __builtin_nontemporal_load(a.dL_dpix + 2 * N + pix);
-            gi[q] = a.dL_dinvdepth ? __builtin_nontemporal_load(a.dL_dinvdepth + pix) : 0.f;
-#else
             g0[q] = a.dL_dpix[pix];
             g1[q] = a.dL_dpix[N + pix];
             g2[q] = a.dL_dpix[2 * N + pix];
             gi[q] = a.dL_dinvdepth ? a.dL_dinvdepth[pix] : 0.f;
-#endif
             c0[q] = a.img.accum[t];
             c1[q] = a.img.accum[NT + t];
             c2[q] = a.img.accum[2 * NT + t];
@@ -906,9 +805,6 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
     unsigned long long c_staged = 0, c_eval = 0, c_alpha = 0, c_red = 0, c_idle = 0;  // CENSUS only
     // The ten per-entry sums stay zero between entries (reset after each reduction), so an entry
     // whose first quadrants are inactive does not materialise zeros (10 VALU) before accumulating.
-#if GSR_BWD_CARRY_R
-    float r0 = 0.f, r1 = 0.f, r2 = 0.f, r3 = 0.f, r4 = 0.f, r5 = 0.f, r6 = 0.f, r7 = 0.f, r8 = 0.f, r9 = 0.f;
-#endif
     uint32_t ent_next = GSR_PF_ENTRY && start + lane < end ? a.gid_sorted[range.x + start + lane] : 0u;
     for (int b0 = start; b0 < end; b0 += kBatch) {
         const bool has = b0 + lane < end;
@@ -943,26 +839,11 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
         unit_sync();
         unsigned long long todo = __ballot(qm != 0);
         unsigned long long written = 0;
-#if GSR_BWD_LDS_PF  // (as GSR_FWD_LDS_PF: the next entry's rows read before this one is evaluated)
-        int jn = todo ? __builtin_ctzll(todo) : 0;
-        float4 nxy = s_xy[jn], ncq = s_cq[jn], ncol = s_col[jn];
-#endif
         while (todo) {
-#if GSR_BWD_LDS_PF
-            const int j = jn;
-            todo &= todo - 1;
-            const float4 xy = nxy, cq = ncq, col = ncol;
-            jn = todo ? __builtin_ctzll(todo) : jn;
-            nxy = s_xy[jn];
-            ncq = s_cq[jn];
-            ncol = s_col[jn];
-            const int pos = b0 + j;
-#else
             const int j = __builtin_ctzll(todo);
             todo &= todo - 1;
             const int pos = b0 + j;
             const float4 xy = s_xy[j], cq = s_cq[j], col = s_col[j];
-#endif
             if (pos >= next_lim) {  // uniform: retire the slots whose last contributor has passed
                 next_lim = limit;
 #pragma unroll
@@ -973,9 +854,7 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
             }
             const uint32_t m = uniform_u32(__float_as_uint(cq.w)) & live;
             if (m == 0) continue;
-#if !GSR_BWD_CARRY_R
             float r0 = 0.f, r1 = 0.f, r2 = 0.f, r3 = 0.f, r4 = 0.f, r5 = 0.f, r6 = 0.f, r7 = 0.f, r8 = 0.f, r9 = 0.f;
-#endif
             bool contrib = false;
 #pragma unroll
             for (int q = 0; q < 4; q++) {
@@ -993,9 +872,7 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
                     c_alpha += (unsigned long long)__popcll(__ballot(alpha > 0.f));
                     c_idle += __any(on) ? 0ull : 1ull;
                 }
-#if GSR_BWD_ANYSKIP
                 if (!__any(on)) continue;  // uniform
-#endif
                 contrib = true;
                 const float w = alpha * T[q];
                 const float sdot = g0[q] * col.x + g1[q] * col.y + g2[q] * col.z + gi[q] * xy.w;
@@ -1027,9 +904,6 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
                 const float f = half_row_allsum(eight_fold(row_fold(h0, h1), row_fold(h2, h3), hi8));
                 const float g4 = row_allsum(h4);
                 if (acc_wr) reinterpret_cast<float*>(s_acc)[j * 4 + acc_lane] = acc_h4 ? g4 : f;
-#if GSR_BWD_CARRY_R
-                r0 = r1 = r2 = r3 = r4 = r5 = r6 = r7 = r8 = r9 = 0.f;
-#endif
                 written |= 1ull << j;
                 if (CENSUS) c_red++;
             }
@@ -1063,11 +937,7 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
                 }
             }
         } else if (has && content && !(GSR_ATTR & 1)) {
-#if GSR_FLAG_BITS  // (the bits were zeroed by the forward's K3, binning.hip; OR is order-free: deterministic)
             (void)atomicOr(reinterpret_cast<uint32_t*>(a.recs.flag) + (e >> 5), 1u << (e & 31u));
-#else
-            a.recs.flag[e] = 1;  // (the bytes were zeroed by the forward's K3, binning.hip)
-#endif
             float4 ra = make_float4(0.f, 0.f, 0.f, 0.f), rb = ra;
             float2 rc = make_float2(0.f, 0.f);
             if (content) {

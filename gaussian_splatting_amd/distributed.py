@@ -73,7 +73,7 @@ class GradArena:
 
     def all_reduce(self, op=None, group: Optional[dist.ProcessGroup] = None, average: bool = False) -> None:
         """Sum (or average) the arena over all ranks in one collective."""
-        if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        if not dist.is_initialized():  # a group of one still runs the collective (RCCL exercised at N = 1)
             return
         dist.all_reduce(self.flat, op=op or dist.ReduceOp.SUM, group=group)
         if average:
@@ -98,7 +98,7 @@ def reduce_densification_stats(grad_norm_sum: torch.Tensor, denom: torch.Tensor,
     ``add_densification_stats``), and this one reduction makes every rank's accumulators the sum
     over all ranks' views.  The SUM is in place, so a second call on the same accumulators would
     add the other ranks' totals again (N-fold growth per call)."""
-    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+    if not dist.is_initialized():
         return
     stats = torch.cat([grad_norm_sum.reshape(-1), denom.reshape(-1)])
     dist.all_reduce(stats, op=dist.ReduceOp.SUM, group=group)
@@ -157,7 +157,10 @@ class ViewExchange:
         # own (async all-gathers, all queued at once on the collective stream), so chunk k+1's all-gather
         # runs while the multi-view backward works on chunk k ("Chunked exchange")
         self.chunks = max(1, int(chunks)) if self.sparse else 1
-        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        # every collective runs whenever a process group exists, a group of one included, so the N = 1
+        # bench and the nccl-group-of-one GPU test drive RCCL exactly as the N-rank run does
+        self.collective = dist.is_initialized()
+        self.world = dist.get_world_size(group) if self.collective else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.block_floats = _C.view_block_floats(P) if P > 0 else 0
         self._gathered = None  # dense [N, block] buffer: allocated on first use (dense mode or fallback)
@@ -189,7 +192,7 @@ class ViewExchange:
             self._ccount = torch.zeros(K, dtype=torch.int32, device=device)
             self._ccount64 = torch.zeros(K, dtype=torch.int64, device=device)
             self._ccount_host = torch.zeros(K, dtype=torch.int64, pin_memory=True)
-            self._ccap_last = [0] * K
+            self._ccap_last = [-1] * K  # -1: no history yet (0 is a real, empty chunk)
             self._cworks = None   # the chunks' async all-gathers, waited for one at a time
             self._chint = None    # entries gathered per chunk
             self._crecv_views = [None] * K
@@ -220,7 +223,7 @@ class ViewExchange:
 
     def chunk_hint(self, k: int) -> int:
         """Entries the next chunked exchange gathers per rank for chunk k (0: none yet)."""
-        if self._ccap_last[k] <= 0:
+        if self._ccap_last[k] < 0:
             return 0
         n = self.bounds[k + 1] - self.bounds[k]
         return min(n, int(self._ccap_last[k] * self.CAP_MARGIN) + 256)
@@ -236,7 +239,7 @@ class ViewExchange:
             _C.view_block_pack(self._local, self._cpacked[k], self._scratch, self._ccount[k:k + 1], self.P,
                                rng=(self.bounds[k], self.bounds[k + 1]))
         self._ccount64.copy_(self._ccount)
-        if self.world > 1:
+        if self.collective:
             if dist.get_backend(self.group) == "nccl":
                 dist.all_reduce(self._ccount64, op=dist.ReduceOp.MAX, group=self.group)
                 self._ccount_host.copy_(self._ccount64, non_blocking=True)
@@ -248,7 +251,7 @@ class ViewExchange:
             self._ccount_host.copy_(self._ccount64, non_blocking=True)
         self._count_ev.record()
         hints = [self.chunk_hint(k) for k in range(K)]
-        if min(hints) == 0:  # no history: wait for this step's counts
+        if min(self._ccap_last) < 0:  # no history: wait for this step's counts
             self._count_ev.synchronize()
             hints = [min(int(self._ccount_host[k]), self.bounds[k + 1] - self.bounds[k]) for k in range(K)]
         self._chint = hints
@@ -262,7 +265,7 @@ class ViewExchange:
         size = _C.view_pack_floats(n)
         recv = self._crecv[k][: self.world * size].view(self.world, size)
         self._crecv_views[k] = recv
-        if self.world > 1:
+        if self.collective:
             return dist.all_gather_into_tensor(recv.view(-1), self._cpacked[k][:size], group=self.group,
                                                async_op=async_op)
         recv[0].copy_(self._cpacked[k][:size])
@@ -276,12 +279,12 @@ class ViewExchange:
         rng = (self.bounds[k], self.bounds[k + 1])
         recv = self._crecv_views[k]
         _C.view_block_index(recv, self._flags, self.P, rng=rng)
-        live = None
-        if self._zeroed is not None:
-            _C.views_live_list(self._flags, self._live, self.P, rng=rng)
-            live = self._live
+        # always the live-list form: chunk k's pass must write only chunk k's rows (a pass over all P rows
+        # would read other chunks' stale flags and overwrite their results); the outputs were zeroed, either
+        # on the side stream (exchange(zero=...)) or by _run_views_backward
+        _C.views_live_list(self._flags, self._live, self.P, rng=rng)
         _C.gauss_backward_views(means3D, dc, sh, degree, opacities, scales, rotations, scale_modifier, recv, out,
-                                flags=self._flags, live=live)
+                                flags=self._flags, live=self._live)
 
     def _finish_chunked(self) -> bool:
         hints, _ = self._pending
@@ -333,7 +336,7 @@ class ViewExchange:
             zero.record_stream(self._side)
             self._zeroed = zero
         if not self.sparse:
-            if self.world > 1:
+            if self.collective:
                 dist.all_gather_into_tensor(self.gathered.view(-1), self.local_block(), group=self.group)
             self._view_blocks = self.gathered
             return
@@ -342,7 +345,7 @@ class ViewExchange:
             return
         _C.view_block_pack(self._local, self._packed, self._scratch, self._count, self.P)
         self._count64.copy_(self._count)
-        if self.world > 1:
+        if self.collective:
             if dist.get_backend(self.group) == "nccl":
                 dist.all_reduce(self._count64, op=dist.ReduceOp.MAX, group=self.group)
                 self._count_host.copy_(self._count64, non_blocking=True)
@@ -368,14 +371,14 @@ class ViewExchange:
         size = _C.view_pack_floats(n)
         if size >= self.block_floats:  # hardly any occlusion: the dense blocks are the smaller message
             self.gathered[self.rank].copy_(self._local)
-            if self.world > 1:
+            if self.collective:
                 dist.all_gather_into_tensor(self.gathered.view(-1), self.gathered[self.rank], group=self.group)
             self.last_entries = None
             self._view_blocks, self._view_flags, self._view_live = self.gathered, None, None
             return
         self.last_entries = n
         recv = self._recv[: self.world * size].view(self.world, size)
-        if self.world > 1:
+        if self.collective:
             dist.all_gather_into_tensor(recv.view(-1), self._packed[:size], group=self.group)
         else:
             recv[0].copy_(self._packed[:size])
@@ -422,6 +425,9 @@ class ViewExchange:
             torch.cuda.current_stream(self._zeroed.device).wait_stream(self._side)
         if self.chunks > 1:
             args = (means3D, dc, sh, degree, opacities, scales, rotations, scale_modifier, out)
+            if self._zeroed is None:  # no side-stream fill: the live-list passes need zeroed outputs
+                for t in out.values():
+                    t.zero_()
             for k in range(self.chunks):
                 w = self._cworks[k] if self._cworks is not None else None
                 if w is not None:
