@@ -95,7 +95,7 @@ def cpu_threads():
                      "threads_policy": policy}
 
 
-def cpu_baseline(cfg_name: str, P: int, W: int, H: int, forward_only: bool = False):
+def cpu_baseline(cfg_name: str, P: int, W: int, H: int, forward_only: bool = False, gpu_num_rendered=None):
     """north_star's CPU baseline: the pure-PyTorch fallback rasterizer (oracle/torch_fallback.py, fp32)
     on this host's cores, forward + autograd backward on the same frame as the GPU -- one FULL frame
     (every tile rendered; SURVEY.md section 8d: 1 rep at configs 2/3, 5 forward reps at config 1),
@@ -113,7 +113,12 @@ def cpu_baseline(cfg_name: str, P: int, W: int, H: int, forward_only: bool = Fal
     wall = time.perf_counter() - t0
     what = "forward" if forward_only else "forward + autograd backward"
     t = res["timings"]
+    # the same workload as the GPU's: its instance count (tests/test_torch_fallback.py pins the integers)
+    same = {} if gpu_num_rendered is None else {
+        "num_rendered_gpu": int(gpu_num_rendered),
+        "num_rendered_diff": int(res["num_rendered"]) - int(gpu_num_rendered)}
     return {"value": value, "unit": "Gaussian-splats/s", "cores": torch.get_num_threads(), **cpus,
+            "num_rendered": int(res["num_rendered"]), **same,
             "kind": "port", "impl": "pure-PyTorch fallback rasterizer (oracle/torch_fallback.py, fp32)",
             "sample": f"{cfg_name} ({P} Gaussians, {W}x{H}) {what}: {reps} full frame(s), every tile rendered "
                       f"({res['num_rendered']} list entries); {t_frame:.2f} s per frame (preprocess "
@@ -665,7 +670,7 @@ def main():
         if multi is not None:
             line["multi_gpu"] = multi
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(args.config, P, W, H)
+            line["cpu_baseline"] = cpu_baseline(args.config, P, W, H, gpu_num_rendered=nr)
             line["cpu_baseline_c"] = cpu_baseline_c(args.config, P, W, H, args.cpu_threads or cpu_threads()[0])
         else:
             line["cpu_baseline"] = None

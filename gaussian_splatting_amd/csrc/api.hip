@@ -252,15 +252,11 @@ void carve_recs(char* base, size_t R, size_t P, gsr::GradRecs* recs, gsr::GradRe
                 uint32_t** live_count, size_t* total) {
     using namespace gsr;
     Carver c{base, 0};
-    if (GSR_REC_AOS) {  // interleaved 48-byte records (gsr_common.h)
+    {  // interleaved 48-byte records (gsr_common.h kRecAB / kRecC)
         float4* r48 = c.take<float4>(3 * R);
         recs->a = r48;
         recs->b = r48 + 1;
         recs->c = reinterpret_cast<float2*>(r48 + 2);
-    } else {
-        recs->a = c.take<float4>(R);
-        recs->b = c.take<float4>(R);
-        recs->c = c.take<float2>(R);
     }
     recs->flag = nullptr;  // in the binning buffer (BinningState::rec_flag)
     // (per Gaussian for gauss_reduce, per live-list position for the atomic backward's gauss_live)
@@ -279,24 +275,16 @@ void carve_recs(char* base, size_t R, size_t P, gsr::GradRecs* recs, gsr::GradRe
 // The library's alternative kernel paths.  Each default comes from GSR_<NAME> in the environment
 // at first use; gsr_option_set changes it for later calls (tests/test_gpu_options.py runs every
 // path against the oracle).
-#define GSR_FUSED_BIN_DEFAULT 1
-#define GSR_ZERO_FILL_DEFAULT 3
-#define GSR_FUSED_FILL_BLOCKS 256  // one-wave fill blocks in render_bwd's launch (the side-stream kernel: 64 x 4 waves)
-#define GSR_LIVE_LIST_DEFAULT 1
-#define GSR_SORT_PREFIX_DEFAULT 1024
-#define GSR_COUNT_WAIT_DEFAULT 2
+constexpr uint32_t kFusedFillBlocks = 256;  // one-wave fill blocks in render_bwd's launch (the side-stream kernel: 64 x 4 waves)
 // "near_mass": near-first binning (binning.hip) -- only the Gaussians in front of the depth at which the
 // screen-averaged opacity mass reaches this value get keys and are sorted; 0 = off.  Capacity-hinted
 // forwards with the fused scan only.
-#define GSR_NEAR_MASS_DEFAULT 30
 // "bwd_atomic": the render backward adds each instance's sums into per-Gaussian rows with float atomics
 // (render.hip ATOMIC) and gauss_live lists the touched Gaussians, instead of per-instance records summed
 // by gauss_reduce (deterministic).  The forward zeroes the rows when the option is on at forward time and
 // marks its buffer (geom_mark below); a backward adds atomically iff the option is on and its buffer is marked.
-#define GSR_BWD_ATOMIC_DEFAULT 1
-#define GSR_K3_RECS_ALWAYS 0  // A/B: K3 writes the record path's inputs whatever the forward's backward path
-#define GSR_FWD_FILL_BLOCKS 256  // one-wave blocks zeroing the accumulators in render_fwd's launch (a multiple of 8)
-static_assert(GSR_FWD_FILL_BLOCKS % 8 == 0, "the forward's fill blocks keep the tiles' XCD mapping");
+constexpr uint32_t kFwdFillBlocks = 256;  // one-wave blocks zeroing the accumulators in render_fwd's launch (a multiple of 8)
+static_assert(kFwdFillBlocks % 8 == 0, "the forward's fill blocks keep the tiles' XCD mapping");
 enum Opt {
     OPT_FUSED_BIN = 0, OPT_FWD_QUADS, OPT_BWD_SEG_CK, OPT_HOST_TOTAL, OPT_ZERO_FILL, OPT_LIVE_LIST, OPT_SORT_PREFIX,
     OPT_COUNT_WAIT, OPT_BWD_GRID, OPT_BWD_ATOMIC, OPT_NEAR_MASS, OPT_COUNT
@@ -307,17 +295,17 @@ struct OptionSpec {
     int def, lo, hi;
 };
 const OptionSpec kOptions[OPT_COUNT] = {
-    {"fused_bin", "GSR_FUSED_BIN", GSR_FUSED_BIN_DEFAULT, 0, 1},
+    {"fused_bin", "GSR_FUSED_BIN", 1, 0, 1},
     {"fwd_quads", "GSR_FWD_QUADS", 2, 2, 4},
     {"bwd_seg_ck", "GSR_BWD_SEG_CK", 1, 1, 1 << 20},
     {"host_total", "GSR_HOST_TOTAL", 1, 0, 1},
-    {"zero_fill", "GSR_ZERO_FILL", GSR_ZERO_FILL_DEFAULT, 0, 3},
-    {"live_list", "GSR_LIVE_LIST", GSR_LIVE_LIST_DEFAULT, 0, 1},
-    {"sort_prefix", "GSR_SORT_PREFIX", GSR_SORT_PREFIX_DEFAULT, 0, (int)gsr::kSortPrefixMax},
-    {"count_wait", "GSR_COUNT_WAIT", GSR_COUNT_WAIT_DEFAULT, 0, 2},
+    {"zero_fill", "GSR_ZERO_FILL", 3, 0, 3},
+    {"live_list", "GSR_LIVE_LIST", 1, 0, 1},
+    {"sort_prefix", "GSR_SORT_PREFIX", 1024, 0, (int)gsr::kSortPrefixMax},
+    {"count_wait", "GSR_COUNT_WAIT", 2, 0, 2},
     {"bwd_grid", "GSR_BWD_GRID", 0, 0, 2},
-    {"bwd_atomic", "GSR_BWD_ATOMIC", GSR_BWD_ATOMIC_DEFAULT, 0, 1},
-    {"near_mass", "GSR_NEAR_MASS", GSR_NEAR_MASS_DEFAULT, 0, 1 << 20},
+    {"bwd_atomic", "GSR_BWD_ATOMIC", 1, 0, 1},
+    {"near_mass", "GSR_NEAR_MASS", 30, 0, 1 << 20},
 };
 std::atomic<int> g_opt[OPT_COUNT];
 std::once_flag g_opt_once;
@@ -352,7 +340,7 @@ int option_index(const char* name) {
 
 // What each geometry buffer's last forward left for its backwards: whether it zeroed the atomic backward's
 // accumulator rows ("bwd_atomic" on at forward time) and whether its K3 wrote the record path's inputs (record
-// starts, zeroed content bits; skipped when the forward zeroed the rows -- GSR_K3_RECS_ALWAYS keeps them).  A
+// starts, zeroed content bits; skipped when the forward zeroed the rows).  A
 // backward adds atomically only into a zeroed buffer, and before a record-path backward of a buffer without
 // record inputs it writes them (launch_rec_prep).  A buffer the library never saw (copied in) is neither: the
 // record path, after the prep.  Every forward re-marks its buffer, so an address the caching allocator hands
@@ -879,7 +867,7 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
     const int opt_count_wait = option(OPT_COUNT_WAIT);
     const bool opt_atomic = option(OPT_BWD_ATOMIC) != 0;
     // K3 writes the record path's inputs only when this forward's backwards may take it without a prep
-    const bool k3_recs = !opt_atomic || GSR_K3_RECS_ALWAYS;
+    const bool k3_recs = !opt_atomic;
     const int opt_near_mass = option(OPT_NEAR_MASS);
     // _ex / _dc forwards lay the binning buffer out for a multiple of kCapQuantum (the backward
     // recovers it from the buffer's size); gsr_rasterize_forward keeps the exact C = R layout
@@ -916,7 +904,7 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
         return fail(GSR_ERR_ARGUMENT, "rasterize_forward: image of %dx%d has more than 65535 tile columns/rows",
                     width, height);
     // the binning's instance walk divides tile offsets inside a rectangle in fp32 (exact below 2^21,
-    // binning.hip GSR_FEI_FDIV): a 536-Mpx frame, far beyond any camera
+    // binning.hip for_each_instance): a 536-Mpx frame, far beyond any camera
     constexpr size_t kMaxTiles = size_t(1) << 21;
     if ((size_t)gx * gy >= kMaxTiles)
         return fail(GSR_ERR_ARGUMENT, "rasterize_forward: image of %dx%d has %zu tiles (the limit is %zu)", width,
@@ -1079,7 +1067,7 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
                 ra.depth_key = geom.depth_key;
                 ra.zcut = geom.zcut;
                 ra.n_gauss = (uint32_t)P;
-                ra.fill_blocks = GSR_FWD_FILL_BLOCKS;
+                ra.fill_blocks = kFwdFillBlocks;
             }
             HIP_TRY(launch_render_fwd(ra, stream, opt_quads), "render_fwd");
             geom_mark(gbase, opt_atomic, k3_recs);
@@ -1357,7 +1345,7 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
         ra.live_count = live_count;  // zeroed by its first workgroup
         if (zmode == 3 && fill.count) {  // the zero fill rides in this launch
             ra.fill = fill;
-            ra.fill_blocks = GSR_FUSED_FILL_BLOCKS;
+            ra.fill_blocks = kFusedFillBlocks;
         }
         if (atomic) {
             ra.acc = reinterpret_cast<float*>(geom.acc);

@@ -22,177 +22,23 @@
 
 namespace gsr {
 
-// A/B: the gradient records are read once (gauss_reduce): streaming loads.
-#define GSR_NT_REC 0
-#define GSR_LD_REC(p) (*(p))
-
 // ---- 1. segmented sums of the per-instance records ------------------------------
 // One wave per 64 consecutive Gaussians.  Their records form one contiguous range
 // [E0, E1) (record index = rec_start[g] + k, k = the tile's row-major index in g's
-// rectangle); it is read 64 records at a time with fully coalesced loads (one record
-// per lane) and each Gaussian's run is summed by a segmented scan over the wave, in a
-// fixed order, so the result does not depend on scheduling.  A record exists iff its content
-// byte is set (render.hip writes records only for entries with a gradient term; the bytes are
-// zeroed by the forward's K3, binning.hip): the range is scanned 1024 bytes per wave-wide load, and only the
-// 64-instance chunks that start at a record are loaded and reduced -- 5M@4K: 7.6M records of
-// 114.7M instances, the rest behind saturated pixels.
-#define GSR_REDUCE_WIN_LDS 1
-constexpr int kRecStride = 12;  // floats per Gaussian in the LDS hand-off of chunk totals (10 used), 48 B
-
-// Sums of the records of the wave's 64 consecutive Gaussians [g0, g0 + 64), one
-// Gaussian per lane (zeros for lanes past P).  s_rec: 64 * kRecStride floats of LDS.
-__device__ __forceinline__ void reduce_records(int P, int g0, const uint32_t* __restrict__ rec_start,
-                                               const uint32_t* __restrict__ tiles_touched, const GradRecs& recs,
-                                               float* s_rec, float4& sa, float4& sb, float2& sc) {
-    const int lane = threadIdx.x;
-    const int g = g0 + lane;
-    const bool valid = g < P;
-    const int g_last = min(g0 + 63, P - 1);
-    const uint32_t E0 = rec_start[g0];
-    const uint32_t E1 = rec_start[g_last] + tiles_touched[g_last];
-    const uint32_t n = valid ? tiles_touched[g] : 0u;
-    const uint32_t my0 = valid ? rec_start[g] : E1;
-    const uint32_t my1 = my0 + n;
-    sa = make_float4(0.f, 0.f, 0.f, 0.f);
-    sb = sa;
-    sc = make_float2(0.f, 0.f);
-    // Wave-parallel segmented sums: a chunk's 64 records stay in registers (one per lane);
-    // a segmented inclusive scan over the wave (DPP row shifts and row broadcasts, the add
-    // masked where the source lane belongs to another Gaussian) leaves each Gaussian's chunk
-    // total in the last lane of its run, which hands it to the owner lane through LDS.  The
-    // cost does not depend on the longest run in the chunk.
-    //
-    // Finding the records: the range is walked in windows of 1024 content bytes (one aligned
-    // 16-byte load per lane, a ballot); a window without records costs that load alone.  Inside
-    // a window each chunk starts AT the next record (found from the bytes already in registers),
-    // so runs of records fall into as few chunks as possible.
-    struct Slot {
-        bool has;
-        int owner, seg0;
-    };
-    // The owner of record e in [base, base + 64): the largest lane whose (non-empty) range starts
-    // at or before e.  Lanes starting before the chunk: one ballot; lanes starting in it mark the
-    // start (lane + 1) in LDS and a DPP max-scan spreads the marks (one wave's LDS accesses
-    // execute in order, so no dependent ds_bpermute chain).
-    __shared__ uint32_t s_mark[64];
-    // the current window's content bytes (masked at E1), mirrored in LDS: a chunk's record test is
-    // an LDS byte read inside the window (a global reload only for the part past its end)
-    __shared__ __attribute__((aligned(16))) uint8_t s_win[1024];
-    uint32_t wa = 0;  // the current window's first byte
-    auto chunk = [&](uint32_t base) -> Slot {
-        const uint32_t e = base + lane;
-        const bool has = e < E1 && (e - wa < 1024u ? s_win[e - wa] != 0 : recs.flag[e] != 0);
-        const unsigned long long st = __ballot(n && my0 < base);
-        const uint32_t carry = st ? 64u - (uint32_t)__clzll((long long)st) : 0u;
-        s_mark[lane] = 0u;
-        wave_lds_sync();
-        if (n && my0 >= base && my0 < base + 64) s_mark[my0 - base] = (uint32_t)lane + 1u;
-        wave_lds_sync();
-        const uint32_t m = max(wave_incl_max(s_mark[lane]), carry);
-        wave_lds_sync();
-        const int owner = m ? (int)m - 1 : 0;
-        const uint32_t o0 = __shfl(my0, owner);
-        if (e >= E1) return Slot{false, -1, lane};
-        return Slot{has, owner, o0 > base ? (int)(o0 - base) : 0};
-    };
-    float4* part = reinterpret_cast<float4*>(s_rec);  // [64][3] float4: a Gaussian's chunk total
-    auto reduce_chunk = [&](uint32_t base) {
-        const Slot cur = chunk(base);
-        float4 x = make_float4(0.f, 0.f, 0.f, 0.f), y = x;
-        float2 z = make_float2(0.f, 0.f);
-        if (cur.has) {
-            x = GSR_LD_REC(recs.a + (size_t)kRecAB * (base + lane));
-            y = GSR_LD_REC(recs.b + (size_t)kRecAB * (base + lane));
-            z = GSR_LD_REC(recs.c + (size_t)kRecC * (base + lane));
-        }
-        // segmented inclusive scan, one DPP step per distance (gsr_common.h wave_sum_to_lane63)
-        const int r = lane & 15, row = lane >> 4;
-        // the masks as 0/1 factors: v += shifted * m is one FMA (records are finite)
-        const float m1 = lane - 1 >= cur.seg0 && r >= 1 ? 1.f : 0.f, m2 = lane - 2 >= cur.seg0 && r >= 2 ? 1.f : 0.f,
-                    m4 = lane - 4 >= cur.seg0 && r >= 4 ? 1.f : 0.f, m8 = lane - 8 >= cur.seg0 && r >= 8 ? 1.f : 0.f,
-                    mb15 = (row & 1) && row * 16 - 1 >= cur.seg0 ? 1.f : 0.f,
-                    mb31 = row >= 2 && 31 >= cur.seg0 ? 1.f : 0.f;
-        float v[10] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w, z.x, z.y};
-#pragma unroll
-        for (int i = 0; i < 10; i++) {
-            v[i] = fmaf(dpp_f32<0x111, 0xf, true>(v[i]), m1, v[i]);
-            v[i] = fmaf(dpp_f32<0x112, 0xf, true>(v[i]), m2, v[i]);
-            v[i] = fmaf(dpp_f32<0x114, 0xf, true>(v[i]), m4, v[i]);
-            v[i] = fmaf(dpp_f32<0x118, 0xf, true>(v[i]), m8, v[i]);
-            v[i] = fmaf(dpp_f32<0x142, 0xa, false>(v[i]), mb15, v[i]);
-            v[i] = fmaf(dpp_f32<0x143, 0xc, false>(v[i]), mb31, v[i]);
-        }
-        // the last lane of each run hands the total to its owner
-        const int next_owner = __shfl_down(cur.owner, 1);
-        if (cur.owner >= 0 && (lane == 63 || next_owner != cur.owner)) {
-            part[cur.owner * 3 + 0] = make_float4(v[0], v[1], v[2], v[3]);
-            part[cur.owner * 3 + 1] = make_float4(v[4], v[5], v[6], v[7]);
-            part[cur.owner * 3 + 2] = make_float4(v[8], v[9], 0.f, 0.f);
-        }
-        __syncthreads();
-        if ((my0 > base ? my0 : base) < (my1 < base + 64 ? my1 : base + 64)) {  // this Gaussian has records here
-            const float4 p = part[lane * 3 + 0], q = part[lane * 3 + 1], ww = part[lane * 3 + 2];
-            sa.x += p.x; sa.y += p.y; sa.z += p.z; sa.w += p.w;
-            sb.x += q.x; sb.y += q.y; sb.z += q.z; sb.w += q.w;
-            sc.x += ww.x; sc.y += ww.y;
-        }
-        __syncthreads();
-    };
-    uint32_t base = E0;
-    while (base < E1) {  // uniform
-        // content bytes [wa, wa + 1024): lane l holds bytes wa + 16 l .. + 15 (the byte buffer is
-        // padded to a multiple of 16, api.hip carve_recs); bytes at or past E1 are another wave's
-        wa = base & ~15u;
-        const uint32_t wend = wa + 1024u;
-        const uint32_t p = wa + 16u * (uint32_t)lane;
-        uint64_t lo = 0, hi = 0;
-        if (p < E1) {
-            const uint4 f = *reinterpret_cast<const uint4*>(recs.flag + p);
-            lo = (uint64_t)f.x | ((uint64_t)f.y << 32);
-            hi = (uint64_t)f.z | ((uint64_t)f.w << 32);
-            const uint32_t k = E1 - p;  // bytes of this lane below E1
-            if (k < 8) { lo &= (1ull << (8 * k)) - 1ull; hi = 0; }
-            else if (k < 16) hi &= (1ull << (8 * (k - 8))) - 1ull;  // k == 8 clears hi
-        }
-        wave_lds_sync();  // the previous window's readers are done (in-order LDS)
-        reinterpret_cast<uint4*>(s_win)[lane] =
-            make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
-        wave_lds_sync();
-        while (true) {
-            // drop the bytes below base (already reduced or before the range)
-            if (base > p) {
-                const uint32_t k = base - p;
-                if (k >= 16) { lo = 0; hi = 0; }
-                else if (k >= 8) { lo = 0; hi &= ~0ull << (8 * (k - 8)); }
-                else lo &= ~0ull << (8 * k);
-            }
-            const unsigned long long nz = __ballot((lo | hi) != 0ull);
-            if (!nz) {
-                base = wend;
-                break;
-            }
-            const uint32_t mine = p + (lo ? (uint32_t)__builtin_ctzll(lo) >> 3 : 8u + ((uint32_t)__builtin_ctzll(hi | (1ull << 63)) >> 3));
-            const uint32_t first = (uint32_t)__builtin_amdgcn_readlane((int)mine, __builtin_ctzll(nz));
-            reduce_chunk(first);
-            base = first + 64;
-            if (base >= wend) break;
-        }
-    }
-}
-
-// Compacted variant (GSR_REDUCE_COMPACT, the default): per window of 1024 content bytes the
-// positions of the records are compacted into an LDS list (per-lane popcounts of the set bytes, a
-// wave prefix sum, each lane writing its own positions), and the list is reduced 64 RECORDS at a
-// time instead of 64 positions at a time -- at 1M@1080p a wave's ~508 instance positions hold ~80
-// records: two groups instead of a chain of ~8 chunks, each a dependent load + scan + hand-off.
-// A Gaussian's records are its slots [r0, r1) of the list (counted from the bytes below its range
-// start and end); the owner search, segmented scan and hand-off are the chunked variant's, in slot
-// space.  Deterministic (fixed order), though grouped differently from the chunked variant.
-#define GSR_REDUCE_COMPACT 1
-static_assert(GSR_REDUCE_COMPACT || !GSR_FLAG_BITS, "the flag bits are read by the compacted reduction only");
-// GSR_REDUCE_PIPE: the records of a window's next group requested before its current group is
-// reduced, the radius read at the start, and wave-local LDS hand-offs (the workgroup is one wave).
-#define GSR_REDUCE_PIPE 1
+// rectangle).  A record exists iff its content bit is set (render.hip writes records only for
+// entries with a gradient term; the bits are zeroed by the forward's K3, binning.hip) -- 5M@4K:
+// 7.6M records of 114.7M instances, the rest behind saturated pixels.  Per window of 1024
+// positions the positions of the records are compacted into an LDS list (per-lane popcounts of
+// the set bits, a wave prefix sum, each lane writing its own positions), and the list is reduced
+// 64 RECORDS at a time: at 1M@1080p a wave's ~508 instance positions hold ~80 records, two
+// groups.  A Gaussian's records are its slots [r0, r1) of the list (counted from the bits below
+// its range start and end); each group is summed by a segmented scan over the wave (DPP row
+// shifts and row broadcasts, the add masked where the source lane belongs to another Gaussian),
+// which leaves each Gaussian's group total in the last lane of its run, handed to the owner lane
+// through LDS.  A fixed order: the result does not depend on scheduling.  The records of a
+// window's next group are requested before its current group is reduced, the radius is read at
+// the start, and the LDS hand-offs are wave-local (the workgroup is one wave).
+constexpr int kRecStride = 12;  // floats per Gaussian in the LDS hand-off of group totals (10 used), 48 B
 __device__ __forceinline__ void reduce_sync() {
     wave_lds_sync();
 }
@@ -258,9 +104,9 @@ __device__ __forceinline__ void reduce_records_compact(int P, int g0, const uint
         float2 zn = make_float2(0.f, 0.f);
         if ((uint32_t)lane < R) {
             const uint32_t e = wa + (uint32_t)s_list[lane];
-            xn = GSR_LD_REC(recs.a + (size_t)kRecAB * e);
-            yn = GSR_LD_REC(recs.b + (size_t)kRecAB * e);
-            zn = GSR_LD_REC(recs.c + (size_t)kRecC * e);
+            xn = recs.a[(size_t)kRecAB * e];
+            yn = recs.b[(size_t)kRecAB * e];
+            zn = recs.c[(size_t)kRecC * e];
         }
         for (uint32_t k0 = 0; k0 < R; k0 += 64) {  // uniform: 64 records at a time
             const uint32_t k = k0 + (uint32_t)lane;
@@ -269,9 +115,9 @@ __device__ __forceinline__ void reduce_records_compact(int P, int g0, const uint
             const float2 z = zn;
             if (k + 64 < R) {
                 const uint32_t e = wa + (uint32_t)s_list[k + 64];
-                xn = GSR_LD_REC(recs.a + (size_t)kRecAB * e);
-                yn = GSR_LD_REC(recs.b + (size_t)kRecAB * e);
-                zn = GSR_LD_REC(recs.c + (size_t)kRecC * e);
+                xn = recs.a[(size_t)kRecAB * e];
+                yn = recs.b[(size_t)kRecAB * e];
+                zn = recs.c[(size_t)kRecC * e];
             } else {  // (lanes past the window's records: zeros, as unloaded lanes always held)
                 xn = yn = make_float4(0.f, 0.f, 0.f, 0.f);
                 zn = make_float2(0.f, 0.f);
@@ -333,10 +179,7 @@ __global__ void __launch_bounds__(64) gauss_reduce_kernel(int P, const uint32_t*
     const int rad = g < P ? radii[g] : 0;  // requested with the range loads, not after the reduction
     float4 sa, sb;
     float2 sc;
-    if (GSR_REDUCE_COMPACT)
-        reduce_records_compact(P, blockIdx.x * 64, rec_start, tiles_touched, recs, s_rec, sa, sb, sc);
-    else
-        reduce_records(P, blockIdx.x * 64, rec_start, tiles_touched, recs, s_rec, sa, sb, sc);
+    reduce_records_compact(P, blockIdx.x * 64, rec_start, tiles_touched, recs, s_rec, sa, sb, sc);
     // a Gaussian with a gradient (gauss_bwd's condition)
     const bool lv = g < P && rad > 0 &&
                     ((sa.x != 0.f) | (sa.y != 0.f) | (sa.z != 0.f) | (sa.w != 0.f) | (sb.x != 0.f) |
@@ -388,8 +231,7 @@ hipError_t launch_gauss_reduce(int P, const GeomState& g, const GradRecs& recs, 
 // 23.2 us).  (r5i / r5j's runs of several groups had measured slower only because their row arrays, written
 // under a branch, were kept in scratch memory; one lane per 32-bit word walking its bits: 21.5 us, r5f.)
 // live_list_cap bounds a shard for runs of up to kLiveGroupsMax groups.
-#define GSR_LIVE_GROUPS 4
-constexpr int kLiveGroups = GSR_LIVE_GROUPS;
+constexpr int kLiveGroups = 4;
 static_assert(kLiveGroups >= 1 && kLiveGroups <= (int)kLiveGroupsMax, "live_list_cap bounds runs of kLiveGroupsMax");
 __global__ void __launch_bounds__(64) gauss_live_kernel(int P, uint32_t* __restrict__ touched, float4* __restrict__ acc,
                                                         GradRecs sums, uint32_t* __restrict__ live,
@@ -810,27 +652,16 @@ __device__ __forceinline__ void view_backward(const ViewCam& c, const GaussIn& g
 // ---- 3. fused per-Gaussian backward ---------------------------------------------
 // (Folding the record sums into this kernel was measured slower: the sums' dependent loads
 // then run at this kernel's LDS-limited occupancy.)
-#define GSR_GB_HALVES 1
-// With GSR_GB_HALVES the SH rows go through LDS 32 at a time at the end of the kernel
-// (lanes 0-31, then 32-63): 6.6 KiB of LDS per wave instead of 13, twice the waves per CU.
-constexpr int kGbShRows = GSR_GB_HALVES ? 32 : 64;
-// Live-list entries per gauss_bwd wave (A/B: GSR_GB_LIST_E 32).  The kernel is a chain of dependent round
-// trips (list -> geometry -> SH rows -> stores) with little VALU, so half-filled waves (twice as many, each
-// with one SH half) trade idle lanes for memory-level parallelism.
-#define GSR_GB_LIST_E 64
-constexpr int kGbListE = GSR_GB_LIST_E;
-// A/B: a listed Gaussian's geometry requested with its sums (gauss_bwd_block)
-#define GSR_GB_HOIST 0
-static_assert(kGbListE == 64 || (kGbListE == 32 && GSR_GB_HALVES), "64, or one SH half of 32 rows");
-// Occupancy target (A/B: GSR_GB_WAVES).  Unconstrained, the body takes 134 VGPRs: 3 waves per
-// SIMD, too few loads in flight for an HBM-bound kernel.
-#define GSR_GB_OCCUPANCY
+// The SH rows go through LDS 32 at a time at the end of the kernel (lanes 0-31, then 32-63): 6.6 KiB
+// of LDS per wave instead of 13, twice the waves per CU.
+constexpr int kGbShRows = 32;
+// Live-list entries per gauss_bwd wave (one per lane).
+constexpr int kGbListE = 64;
 // LIST: lane i of the grid takes entry i of the live list (the Gaussians with a gradient,
-// gauss_reduce), with per-lane SH access (kShGlobal); the outputs were zero-filled, so no other
-// row is touched.  At 1M@1080p that is ~2000 waves instead of 15625.
-// The workgroup is one wave: the SH pass's LDS hand-offs need only the wave's own in-order LDS
-// (GSR_GB_WAVESYNC), not __syncthreads, whose fence also waits for every store the wave has issued.
-#define GSR_GB_WAVESYNC 1
+// gauss_reduce / gauss_live); the outputs were zero-filled, so no other row is touched.  At
+// 1M@1080p that is ~2000 waves instead of 15625.
+// The workgroup is one wave: the SH pass's LDS hand-offs need only the wave's own in-order LDS,
+// not __syncthreads, whose fence also waits for every store the wave has issued.
 __device__ __forceinline__ void gb_sync() {
     wave_lds_sync();
 }
@@ -853,13 +684,7 @@ __device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const uin
 
     const ShAddr sh_src{a.shs, a.dc, M};
     const ShGradAddr sh_dst{a.dL_dsh, a.dL_ddc, M};
-    constexpr bool kShLate = SH_MODE != kShGlobal && GSR_GB_HALVES;
-    static_assert(!LIST || kShLate || SH_MODE == kShGlobal, "the live list stages SH rows late (halves)");
-    if constexpr (SH_MODE != kShGlobal && !kShLate) {
-        // coalesced stage-in of the wave's SH rows (64 x 48 floats, either layout)
-        sh_stage_in<64, 64, SH_MODE == kShLdsSplit>(sh_src, g0, nvalid, s_sh, kShStride, lane);
-        __syncthreads();
-    }
+    constexpr bool kShLate = SH_MODE != kShGlobal;  // the SH backward deferred to the LDS pass at the end
     // deferred SH backward (kShLate): its inputs, and the 3-D mean gradient it adds to
     bool sh_late = false;
     float3 sh_v = make_float3(0.f, 0.f, 0.f), sh_g = sh_v, dmean_late = sh_v;
@@ -872,26 +697,12 @@ __device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const uin
     float4 sa = make_float4(0.f, 0.f, 0.f, 0.f), sb = sa;
     float2 sc = make_float2(0.f, 0.f);
     int rad = 0;
-    // GSR_GB_HOIST (A/B): a listed Gaussian is all but always visible with a gradient, so its geometry is
-    // requested with the sums, not after them -- one dependent round trip fewer
-    constexpr bool kHoist = LIST && GSR_GB_HOIST;
-    float3 h_mean = make_float3(0.f, 0.f, 0.f), h_sc = h_mean;
-    float4 h_q = make_float4(1.f, 0.f, 0.f, 0.f);
-    uint8_t h_cm = 0;
     if (valid) {
         rad = a.radii[idx];
         const size_t si = LIST && a.sums_by_list ? lpos : (size_t)idx;  // (atomic backward: list order, gauss_live)
         sa = a.sums.a[si];
         sb = a.sums.b[si];
         sc = a.sums.c[si];
-        if constexpr (kHoist) {
-            h_mean = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
-            if (a.scales) {
-                h_sc = make_float3(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]);
-                h_q = reinterpret_cast<const float4*>(a.rotations)[idx];
-            }
-            if (a.shs || a.dc) h_cm = a.geom.clamped[idx];
-        }
     }
     const bool any_grad = (sa.x != 0.f) | (sa.y != 0.f) | (sa.z != 0.f) | (sa.w != 0.f) | (sb.x != 0.f) |
                           (sb.y != 0.f) | (sb.z != 0.f) | (sb.w != 0.f) | (sc.x != 0.f) | (sc.y != 0.f);
@@ -911,11 +722,6 @@ __device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const uin
         if (a.dL_dsh || a.dL_ddc) {
             if constexpr (kShLate) {
                 // rows zeroed in the SH pass below
-            } else if constexpr (SH_MODE != kShGlobal) {
-                // the LDS row is zeroed even when sparse: a split-layout piece straddling into a
-                // wanted row writes this row's floats too (sh_stage_out)
-                for (int k = 0; k < kShRowF; k += 4)
-                    *reinterpret_cast<float4*>(&s_sh[lane * kShStride + k]) = make_float4(0.f, 0.f, 0.f, 0.f);
             } else if (!a.sparse) {
                 const ShGlobal acc{sh_src, sh_dst, idx};
                 for (int k = 0; k < M; k++) acc.store(k, make_float3(0.f, 0.f, 0.f));
@@ -935,18 +741,12 @@ __device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const uin
                           a.focal_x,    a.focal_y,    a.antialiasing, a.have_invdepth};
         GaussIn gi;
         gi.have_scales = a.scales != nullptr;
-        if constexpr (kHoist) {
-            gi.mean = h_mean;
-            gi.sc3 = h_sc;
-            gi.q = h_q;
-        } else {
-            gi.mean = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
-            gi.sc3 = make_float3(0.f, 0.f, 0.f);
-            gi.q = make_float4(1.f, 0.f, 0.f, 0.f);
-            if (a.scales) {
-                gi.sc3 = make_float3(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]);
-                gi.q = reinterpret_cast<const float4*>(a.rotations)[idx];
-            }
+        gi.mean = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
+        gi.sc3 = make_float3(0.f, 0.f, 0.f);
+        gi.q = make_float4(1.f, 0.f, 0.f, 0.f);
+        if (a.scales) {
+            gi.sc3 = make_float3(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]);
+            gi.q = reinterpret_cast<const float4*>(a.rotations)[idx];
         }
         gi.cov3D = a.cov3D_precomp ? a.cov3D_precomp + 6 * idx : nullptr;
         gi.scale_modifier = a.scale_modifier;
@@ -976,11 +776,9 @@ __device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const uin
             }
         } sink{a, idx, sh_late, sh_v, sh_g, dmean_late};
         const bool do_sh = a.shs || a.dc;
-        const uint8_t cm = kHoist ? h_cm : do_sh ? a.geom.clamped[idx] : 0;
+        const uint8_t cm = do_sh ? a.geom.clamped[idx] : 0;
         if constexpr (kShLate)
             view_backward<kShDefer>(cam, gi, sa, sb, sc, cm, do_sh, a.D, M, ShLds{nullptr}, sink);
-        else if constexpr (SH_MODE != kShGlobal)
-            view_backward<kShNow>(cam, gi, sa, sb, sc, cm, do_sh, a.D, M, ShLds{&s_sh[lane * kShStride]}, sink);
         else
             view_backward<kShNow>(cam, gi, sa, sb, sc, cm, do_sh, a.D, M, ShGlobal{sh_src, sh_dst, idx}, sink);
         if (!sh_late) store3(a.dL_dmean3D, idx, dmean_late.x, dmean_late.y, dmean_late.z);
@@ -990,15 +788,11 @@ __device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const uin
         }
     }
 
-// A/B: the view-vector pin for the combined SH layout too (its kernel otherwise holds 165 VGPRs)
-#define GSR_GB_PIN_ALL 0
-#define GSR_GB_TIMING_NOSH 0  // timing builds only (results wrong): skip the deferred SH pass
-    if constexpr (kShLate && !GSR_GB_TIMING_NOSH) {
+    if constexpr (kShLate) {
         // SH backward, half a wave at a time through LDS: coalesced stage-in of 32 rows,
         // their lanes evaluate it in place, coalesced write-back of the 32 dL/dSH rows
         const unsigned long long need = __ballot(sh_late);  // rows whose SH is read at all
         for (int half = 0; half < 2; half++) {
-            if (LIST && half * kGbShRows >= kGbListE) break;  // (kGbListE 32: the wave's rows are one half)
             const int rows = LIST ? kGbShRows : min(kGbShRows, nvalid - half * kGbShRows);
             if (rows <= 0) break;  // wave-uniform
             if constexpr (LIST)  // the lanes' rows, wherever they are
@@ -1017,7 +811,7 @@ __device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const uin
                     // vectorisation off and contraction per expression, build.py, both layouts round
                     // alike -- test_separate_sh.)
                     float3 v = sh_v;
-                    if constexpr (SH_MODE == kShLdsSplit || GSR_GB_PIN_ALL)
+                    if constexpr (SH_MODE == kShLdsSplit)
                         asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z));
                     float3 dm = dmean_late;
                     sh_dir_backward(ShLds{row}, a.D, M, v, sh_g, dm);
@@ -1039,31 +833,15 @@ __device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const uin
             }
             gb_sync();
         }
-    } else if constexpr (SH_MODE != kShGlobal) {
-        // coalesced write-back of the wave's dL/dSH rows
-        const unsigned long long rows_out = a.sparse ? __ballot(visible) : ~0ull;
-        __syncthreads();
-        sh_stage_out<64, 64, SH_MODE == kShLdsSplit>(sh_dst, g0, nvalid, s_sh, kShStride, lane, rows_out);
     }
 }
 
 // The live-list grid is sized for the worst case (every Gaussian listed: 64 shards x live_cap / E blocks, 15.7k
 // at 1M@1080p, 78k at 5M@4K) while ~2000 blocks have entries; every surplus block is a wave launched to read a
-// counter and exit.  GSR_GB_STRIDED: a grid of kGbStridedGrid blocks walks the virtual blocks b, b + G, ...
-// up to the longest shard's end instead.
-#define GSR_GB_STRIDED 0
-constexpr uint32_t kGbStridedGrid = 2048;
+// counter and exit (a grid-strided walk over the virtual blocks measured no better).
 template <int SH_MODE, bool LIST = false>
-__global__ void __launch_bounds__(64) GSR_GB_OCCUPANCY gauss_bwd_kernel(GaussBwdArgs a) {
-    if constexpr (LIST && GSR_GB_STRIDED) {
-        const int lane = threadIdx.x;
-        const uint32_t maxn = (uint32_t)__builtin_amdgcn_readlane(
-            (int)wave_incl_max(lane < kLiveShards ? a.live_count[lane * kLiveCntStride] : 0u), 63);
-        for (uint32_t b = blockIdx.x; (b / kLiveShards) * (uint32_t)kGbListE < maxn; b += gridDim.x)
-            gauss_bwd_block<SH_MODE, true>(a, b);
-    } else {
-        gauss_bwd_block<SH_MODE, LIST>(a, blockIdx.x);
-    }
+__global__ void __launch_bounds__(64) gauss_bwd_kernel(GaussBwdArgs a) {
+    gauss_bwd_block<SH_MODE, LIST>(a, blockIdx.x);
 }
 
 // ---- 4. the same backward over several views' summed render gradients -----------
@@ -1175,14 +953,10 @@ __device__ __forceinline__ void views_sh_band(const ViewsBwdArgs& a, int idx, fl
     }
 }
 
-#define GSR_VIEWS_ONE_PASS 1
-#define GSR_VIEWS_FLAG_PREFETCH 1
-template <int SH_MODE, bool PACKED, bool LIST = false>
 // 3 waves per SIMD (the LDS limit of the SH staging): the register allocator then spills a
 // few values but the per-view latency chains overlap better (8 views: 0.50 -> 0.44 ms, r1af)
-#define GSR_VIEWS_WAVES 3
-#define GSR_VIEWS_OCCUPANCY __attribute__((amdgpu_waves_per_eu(GSR_VIEWS_WAVES, GSR_VIEWS_WAVES)))
-__global__ void __launch_bounds__(64) GSR_VIEWS_OCCUPANCY gauss_bwd_views_kernel(ViewsBwdArgs a) {
+template <int SH_MODE, bool PACKED, bool LIST = false>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3, 3))) gauss_bwd_views_kernel(ViewsBwdArgs a) {
     __shared__ __attribute__((aligned(16))) float s_sh[SH_MODE != kShGlobal ? 64 * kShStride : 4];
     const int lane = threadIdx.x;
     const int g0 = blockIdx.x * 64;
@@ -1574,13 +1348,13 @@ hipError_t launch_view_header(float* blk, const float* view, const float* proj, 
 }
 
 // 16-byte stores (1 KiB per wave-instruction) over each range's aligned body, dwords for its
-// unaligned head and tail.  A small grid (GSR_FILL_BLOCKS workgroups of 256): beside render_bwd
+// unaligned head and tail.  A small grid (kFillBlocks workgroups of 256): beside render_bwd
 // it should take few wave slots and only the HBM bandwidth render_bwd leaves idle.  The body
 // stores are non-temporal (`nt`): 236 MB of zeros written through the caches evicted the
 // records and pixel state render_bwd and gauss_reduce re-read (r2zv: render_bwd 298 -> 290 us,
 // gauss_reduce 67 -> 63, preprocess 75.6 -> 72, step -19 us; 32 / 64 / 96 / 128 workgroups
 // within noise once the stores stream, r2zw).
-#define GSR_FILL_BLOCKS 64
+constexpr uint32_t kFillBlocks = 64;
 __global__ void __launch_bounds__(256) zero_fill_kernel(FillArgs f) {
     zero_fill_part(f, (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x,
                    (unsigned long long)gridDim.x * blockDim.x);
@@ -1588,7 +1362,7 @@ __global__ void __launch_bounds__(256) zero_fill_kernel(FillArgs f) {
 
 hipError_t launch_zero_fill(const FillArgs& f, hipStream_t stream) {
     if (f.count == 0) return hipSuccess;
-    hipLaunchKernelGGL(zero_fill_kernel, dim3(GSR_FILL_BLOCKS), dim3(256), 0, stream, f);
+    hipLaunchKernelGGL(zero_fill_kernel, dim3(kFillBlocks), dim3(256), 0, stream, f);
     return hipGetLastError();
 }
 
@@ -1600,7 +1374,7 @@ hipError_t launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t stream) {
                         ((reinterpret_cast<uintptr_t>(a.dL_dsh) & 15) == 0);
     if (a.live && a.sparse) {  // the live list: kLiveShards x live_cap entries at most
         const uint32_t worst = kLiveShards * ((a.live_cap + kGbListE - 1) / kGbListE);
-        const dim3 lgrid(GSR_GB_STRIDED && worst > kGbStridedGrid ? kGbStridedGrid : worst);
+        const dim3 lgrid(worst);
         if (lds_ok && a.dc)
             hipLaunchKernelGGL((gauss_bwd_kernel<kShLdsSplit, true>), lgrid, block, 0, stream, a);
         else if (lds_ok)

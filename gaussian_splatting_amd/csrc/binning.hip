@@ -45,8 +45,7 @@ namespace gsr {
 
 constexpr int kBinThreads = 1024;
 constexpr int kBinWaves = kBinThreads / 64;
-#define GSR_BIN_UNROLL 4
-constexpr int kBinUnroll = GSR_BIN_UNROLL;  // K0 / K1 Gaussians per thread per round (loads in flight together)
+constexpr int kBinUnroll = 4;  // K0 / K1 Gaussians per thread per round (loads in flight together)
 constexpr uint32_t kLdsTilesMax = 36864;  // K3 keeps one u32 per tile in LDS (144 KiB)
 constexpr uint32_t kSortWaveMax = 1024;   // longest list tile_sort_kernel sorts (one workgroup of kSortT per tile)
 // Longer lists go to two persistent 256-thread kernels walking K2's class lists: class 0
@@ -131,9 +130,6 @@ __device__ T block_exclusive_scan(T v, T* s_tmp, T* total) {
 // Gaussians (lane l: n tiles in rectangle r), each once; `owner` is the lane of the
 // instance's Gaussian, (tx, ty) the tile's column and row.  f may shuffle from `owner`
 // (all lanes are active).
-#define GSR_FEI_DPP 1
-#define GSR_FEI_FDIV 1
-#define GSR_FEI_U24 1
 template <class F>
 __device__ __forceinline__ void for_each_instance(uint32_t n, uint2 r, uint32_t gx, F&& f) {
     const int lane = threadIdx.x & 63;
@@ -180,15 +176,13 @@ __device__ __forceinline__ void for_each_instance(uint32_t n, uint2 r, uint32_t 
 // Gaussians in this order, so a chunk covers a compact screen region: it touches
 // few tiles, with long runs per tile, and K3's key stores land in long contiguous
 // runs instead of a few bytes per (chunk, tile) across the whole image.
-#define GSR_CELL 4
-constexpr uint32_t kCell = GSR_CELL;
+constexpr uint32_t kCell = 4;
 static_assert(kCell >= 1 && kCell <= 64 && (kCell & (kCell - 1)) == 0,
-              "GSR_CELL: a power of two in [1, 64] (cells are formed by shifts; bin_cells coarsens them by powers of two)");
+              "kCell: a power of two in [1, 64] (cells are formed by shifts; bin_cells coarsens them by powers of two)");
 
-// GSR_CELL_MORTON: cells in Z order (Morton code of the cell column and row, over the power-of-two
-// square that holds the grid), so a chunk of the order covers a square-ish block of cells rather than
-// a strip of a cell row (5M@4K: 936 instead of 1062 tiles per chunk, tools/k3_runs.py --order).
-#define GSR_CELL_MORTON 1  // r4c: bin_scatter 852-855 -> 827-831 us at 5M@4K, 1M unchanged
+// Cells in Z order (Morton code of the cell column and row, over the power-of-two square that holds the
+// grid), so a chunk of the order covers a square-ish block of cells rather than a strip of a cell row
+// (5M@4K: 936 instead of 1062 tiles per chunk; r4c: bin_scatter 852-855 -> 827-831 us at 5M@4K).
 __host__ __device__ inline uint32_t spread_bits16(uint32_t x) {
     x &= 0xffffu;
     x = (x | (x << 8)) & 0x00ff00ffu;
@@ -368,14 +362,14 @@ struct FusedZero {
     uint32_t* cls_count;
 };
 
-// K1 by rectangles (GSR_K1_RECT, the default with LDS counters): a chunk's per-tile counts are the
+// K1 by rectangles (with LDS counters): a chunk's per-tile counts are the
 // number of its Gaussians whose tile rectangle covers the tile, so each Gaussian adds +1 / -1 at its
 // rectangle's four corners of a 2-D difference array in LDS (one u32 per tile; a corner on the far
 // edge of the grid is dropped) and a 2-D inclusive prefix sum -- rows by DPP scans, one wave per row,
 // then columns in register blocks -- turns the differences into the counts.  Four LDS atomics per
 // Gaussian instead of one per instance (5M@4K: 20M instead of 114.7M) and no instance walk; the
-// counts are exactly the walk's, so everything downstream is unchanged.
-#define GSR_K1_RECT 1
+// counts are exactly an instance walk's, so everything downstream is unchanged.  (Without LDS
+// counters -- a grid over kLdsTilesMax tiles -- K1 walks the instances with global atomics.)
 constexpr int kColBlock = 8;  // rows per register block of the column pass
 
 // cut != kZCutNone (near-first binning): each Gaussian counts 1 in the low 16 bits (all instances) and,
@@ -451,7 +445,7 @@ __global__ void __launch_bounds__(kBinThreads) tile_count_kernel(int P, int chun
                                                                  uint32_t tiles, uint32_t gx, uint32_t* __restrict__ cnt,
                                                                  uint32_t* __restrict__ chunk_off, FusedZero fz,
                                                                  NearArgs na) {
-    extern __shared__ uint32_t s_hist[];  // by rectangles: tiles words; walk: (tiles + 1) / 2 words of 16-bit counters (a chunk has < 65536 Gaussians)
+    extern __shared__ uint32_t s_hist[];  // (LDS) the 2-D difference array: tiles words
     if (fz.unit_cnt) {
         if (blockIdx.x == 0 && threadIdx.x < kUnitLists * kUnitShards) fz.unit_cnt[threadIdx.x * kUnitCntStride] = 0u;
         if (blockIdx.x == 0 && threadIdx.x < kSortClasses) fz.cls_count[threadIdx.x] = 0u;
@@ -461,10 +455,9 @@ __global__ void __launch_bounds__(kBinThreads) tile_count_kernel(int P, int chun
     if (!na.zhist && na.zcut && blockIdx.x == 0 && threadIdx.x == 0) *na.zcut = kZCutNone;  // (inspection, far fill)
     const int V = (int)n_visible[0];
     const int g0 = blockIdx.x * chunk, g1 = min(V, g0 + chunk);  // positions in order[]
-    const uint32_t words = (tiles + 1) / 2;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     GSR_STAMP(g_st_count, blockIdx.x, 0);
-    if (LDS && GSR_K1_RECT) {
+    if (LDS) {
         uint32_t cut = kZCutNone;
         if (na.zhist) {  // near-first binning: the cut, from K0a's depth-mass histogram (each workgroup alike)
             __shared__ uint32_t s_cut;
@@ -498,10 +491,6 @@ __global__ void __launch_bounds__(kBinThreads) tile_count_kernel(int P, int chun
         GSR_STAMP(g_st_count, blockIdx.x, 3);
         return;
     }
-    if (LDS) {
-        for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) s_hist[i] = 0;
-        __syncthreads();
-    }
     GSR_STAMP(g_st_count, blockIdx.x, 1);
     for (int pb = g0 + wave * 64; pb < g1; pb += kBinThreads) {
         const int p = pb + lane;
@@ -509,24 +498,8 @@ __global__ void __launch_bounds__(kBinThreads) tile_count_kernel(int P, int chun
         const uint2 r = make_uint2(o.y, o.z);
         const uint32_t n = rect_tiles(r);
         for_each_instance(n, r, gx, [&](bool valid, int, uint32_t t, uint32_t, uint32_t) {
-            if (!valid) return;
-            if (LDS)
-                atomicAdd(&s_hist[t >> 1], 1u << ((t & 1u) * 16));
-            else
-                atomicAdd(&cnt[t], 1u);
+            if (valid) atomicAdd(&cnt[t], 1u);
         });
-    }
-    if (LDS) {
-        __syncthreads();
-        GSR_STAMP(g_st_count, blockIdx.x, 2);
-        uint32_t* off = chunk_off + (size_t)blockIdx.x * tiles;
-        for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) {
-            const uint32_t w = s_hist[i];
-            if (w & 0xffffu) off[2 * i] = atomicAdd(&cnt[2 * i], w & 0xffffu);
-            if ((w >> 16) && 2 * i + 1 < tiles) off[2 * i + 1] = atomicAdd(&cnt[2 * i + 1], w >> 16);
-        }
-        __syncthreads();
-        GSR_STAMP(g_st_count, blockIdx.x, 3);
     }
 }
 
@@ -614,15 +587,6 @@ struct FusedScan {
     uint32_t* cls_count;
 };
 
-// Store-cost attribution builds only (GSR_K3_ATTR): K3 writes its keys a second
-// time into a scratch buffer, scattered as the real stores (1) or coalesced (2).
-#define GSR_K3_ATTR 0
-
-#define GSR_K3_PRO 1
-// Timing builds only (the record path's inputs are then missing): K3 without the record starts and the
-// content-bit zeroing, which only the record backward reads
-#define GSR_K3_NO_RECS 0
-
 // The record path's inputs for chunk blockIdx.x (Gaussians [g0, g1), their instances starting at `chunk_base`):
 // every Gaussian's first record index -- chunk base + in-order scan of tiles_touched -- and the zeroed content
 // bits of the chunk's emission range.  The counts of up to four rounds are requested before the first scan,
@@ -648,15 +612,12 @@ __device__ __forceinline__ void rec_starts_chunk(int g0, int g1, u64 chunk_base,
             const int g = gb + (int)threadIdx.x;
             u64 all = 0;
             const u64 at = carry + block_exclusive_scan<u64, true>((u64)nr[u], s_tmp, &all);
-            if (g < g1) {
-                rec_start[g] = (uint32_t)at;
-                if (!GSR_REC_START_GATHER && nr[u]) reinterpret_cast<uint32_t*>(rec + (size_t)kRecRows * g + 3)[3] = (uint32_t)at;
-            }
+            if (g < g1) rec_start[g] = (uint32_t)at;
             carry += all;
         }
     }
-    if (rec_flag) {  // (GSR_FLAG_BITS: 128 flags per 16-byte word)
-        constexpr u64 kPer = GSR_FLAG_BITS ? 128 : 16;
+    if (rec_flag) {  // (content bits: 128 per 16-byte word)
+        constexpr u64 kPer = 128;
         const u64 e1 = min(chunk_base + chunk_total[blockIdx.x], cap);
         uint4* w = reinterpret_cast<uint4*>(rec_flag);
         for (u64 i = chunk_base / kPer + threadIdx.x; i < (e1 + kPer - 1) / kPer; i += blockDim.x)
@@ -759,13 +720,9 @@ __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
         const uint32_t* off = chunk_off + (size_t)blockIdx.x * tiles;
         for (uint32_t i = threadIdx.x; i < tiles; i += blockDim.x) s_cur[i] = tile_base[i] + off[i];
     }
-    // first record index of every Gaussian: chunk base + in-order scan of tiles_touched
-    // (GSR_K3_PRO: the counts of up to four rounds requested before the first scan, the scans' barriers
-    // LDS-only, and the content-byte zeroing issued last -- the memory counter is in order, so a load
-    // issued after a store waits for that store too: each round had waited for the previous round's
-    // stores, and the scans' __syncthreads for all of them)
+    // first record index of every Gaussian: chunk base + in-order scan of tiles_touched (rec_starts_chunk)
     // (rec_start null: the forward's backward takes the atomic path, which reads neither)
-    if (rec_start && !GSR_K3_NO_RECS) {
+    if (rec_start) {
         const u64 chunk_base = block_sum<u64, true>(before, s_tmp);
         rec_starts_chunk(g0, g1, chunk_base, tiles_touched, chunk_total, rec_start, rec, rec_flag, cap, s_tmp);
     }
@@ -793,9 +750,6 @@ __global__ void __launch_bounds__(kBinThreads) tile_scatter_kernel(
     GSR_STAMP(g_st_scatter, blockIdx.x, 2);
 }
 
-// A/B: K4 reads each key once: streaming loads.
-#define GSR_NT_KEYS 0
-#define GSR_LD_KEY(p) (*(p))
 // ---- K4 ---------------------------------------------------------------------
 // Bitonic sorting network over N2 = T * E keys, element i = thread * E + r held in
 // register a[r] (keys past the list are +infinity = ~0).  Exchange distance j:
@@ -897,7 +851,7 @@ __device__ __forceinline__ void sort_list(const u64* __restrict__ keys, uint32_t
     u64 a[E];
     const uint32_t i0 = threadIdx.x * E;
 #pragma unroll
-    for (int r = 0; r < E; r++) a[r] = i0 + r < n ? GSR_LD_KEY(keys + lo + i0 + r) : ~0ull;
+    for (int r = 0; r < E; r++) a[r] = i0 + r < n ? *(keys + lo + i0 + r) : ~0ull;
     bitonic_regs<T, E>(a, s_x);
 #pragma unroll
     for (int r = 0; r < E; r++)
@@ -952,10 +906,8 @@ __device__ void sort_list_global(u64* __restrict__ keys, uint32_t lo, uint32_t n
 // the tile's depths cluster in a sliver of their range, sum of squares above kSkew * n -- the
 // list goes to the bitonic network instead (the caller's fallback).  The result is the
 // reference's (depth, index) order exactly: keys are compared whole.
-#define GSR_BIN_SHIFT 1
-#define GSR_SKEW 48
-constexpr int kBinShift = GSR_BIN_SHIFT;  // bins = pow2 >= n >> kBinShift (about two keys per bin)
-constexpr uint32_t kSkew = GSR_SKEW;      // fallback when sum(bin size^2) > kSkew * n
+constexpr int kBinShift = 1;       // bins = pow2 >= n >> kBinShift (about two keys per bin)
+constexpr uint32_t kSkew = 48;     // fallback when sum(bin size^2) > kSkew * n
 
 template <int T, int NMAX, int NBMAX>
 struct BucketLds {
@@ -1016,7 +968,7 @@ __device__ bool bucket_sort_list(const u64* __restrict__ keys, uint32_t lo, uint
 #pragma unroll
     for (int e = 0; e < E; e++) {
         const uint32_t i = (uint32_t)e * T + tid;
-        k[e] = i < n ? GSR_LD_KEY(keys + lo + i) : 0ull;
+        k[e] = i < n ? *(keys + lo + i) : 0ull;
     }
 #pragma unroll
     for (int e = 0; e < E; e++) {
@@ -1124,14 +1076,12 @@ __device__ bool bucket_sort_list(const u64* __restrict__ keys, uint32_t lo, uint
 // Lists of up to kSortWaveMax keys: one workgroup (kSortT threads) per tile.  Short lists (<= kBucketMinN) are
 // sorted by a bitonic network in registers (no LDS, no barrier); longer ones by the bucket
 // sort, with the register network as its skew fallback.
-#define GSR_BUCKET_MIN_N 128
-constexpr uint32_t kBucketMinN = GSR_BUCKET_MIN_N;
+constexpr uint32_t kBucketMinN = 128;
 // Threads per tile of the bucket sort below: 128 = two waves per tile, each holding half of the
 // tile's keys (the same LDS per tile as one wave, half the serial chain per thread: tile_sort
 // 66.6 -> 55.6-58.1 us at 1M@1080p against one wave, 62 us with four; r3y1).  The register
 // network for short or skewed lists runs on the first wave alone.
-#define GSR_SORT_T 128
-constexpr int kSortT = GSR_SORT_T;
+constexpr int kSortT = 128;
 static_assert(kSortT == 64 || kSortT == 128 || kSortT == 256, "tile_sort_kernel: 1, 2 or 4 waves");
 
 __global__ void __launch_bounds__(kSortT) tile_sort_kernel(const uint2* __restrict__ ranges,
@@ -1186,34 +1136,27 @@ __global__ void __launch_bounds__(kSortT) tile_sort_kernel(const uint2* __restri
 }
 
 // Persistent: 256-thread workgroups walk one class list of long tiles (K2).  Class 0
-// (kSortWaveMax, kClass0Max]: bucket sort, skew fallback a 256 x 16 register network (its
-// exchange buffer aliases the bucket buffer).  Class 1 (> kClass0Max): bucket sort up to
-// kBucketMax keys, the global-memory network beyond or on skew.
+// (kSortWaveMax, kClass0Max]: tile_sort_window_kernel below.  Class 1 (> kClass0Max): bucket sort
+// up to kBucketMax keys, a 256 x 16 register network (its exchange buffer aliases the bucket
+// buffer) on skew up to 4096 keys, the global-memory network beyond.
 constexpr int kClassThreads = 256;
-// Class 0's workgroup size (A/B: its tiles hold 1-4k keys; more threads per tile shorten each
-// tile's barrier-separated phases at the same LDS per workgroup).
-#define GSR_CLASS0_THREADS 256
-template <int CLASS>
-constexpr int class_threads() { return CLASS == 0 ? GSR_CLASS0_THREADS : kClassThreads; }
 
 // lim: sort only the reachable prefix of each list (the "sort_prefix" option; ~0u = whole lists):
 // the bucket sort then ranks the smallest lim (+ the rest of a bin) keys and leaves the tail
 // unwritten, and sorted_len records how many entries are in order.  The skew fallbacks sort the
 // whole list.
-template <int CLASS>
-__global__ void __launch_bounds__(class_threads<CLASS>()) tile_sort_class_kernel(const uint2* __restrict__ ranges,
-                                                                        u64* __restrict__ keys, u64 cap,
-                                                                        uint32_t* __restrict__ gid_sorted,
-                                                                        const uint32_t* __restrict__ list,
-                                                                        const uint32_t* __restrict__ count,
-                                                                        uint32_t lim,
-                                                                        uint32_t* __restrict__ sorted_len) {
-    constexpr int T = class_threads<CLASS>();
-    constexpr int NMAX = CLASS == 0 ? (int)kClass0Max : (int)kBucketMax;
-    constexpr int EF = CLASS == 0 ? NMAX / T : 16;  // the fallback network's keys per thread
+__global__ void __launch_bounds__(kClassThreads) tile_sort_class1_kernel(const uint2* __restrict__ ranges,
+                                                                         u64* __restrict__ keys, u64 cap,
+                                                                         uint32_t* __restrict__ gid_sorted,
+                                                                         const uint32_t* __restrict__ list,
+                                                                         const uint32_t* __restrict__ count,
+                                                                         uint32_t lim,
+                                                                         uint32_t* __restrict__ sorted_len) {
+    constexpr int T = kClassThreads;
+    constexpr int NMAX = (int)kBucketMax;
+    constexpr int EF = 16;  // the fallback network's keys per thread
     __shared__ BucketLds<T, NMAX, NMAX / 2> s;
     static_assert(sizeof(s.buf) >= T * EF * sizeof(u64), "the fallback network's buffer");
-    static_assert(CLASS != 0 || T * EF == NMAX, "class 0's fallback network covers the class");
     const uint32_t nb = count[0];
     for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
         const uint32_t t = list[b];
@@ -1225,7 +1168,7 @@ __global__ void __launch_bounds__(class_threads<CLASS>()) tile_sort_class_kernel
         } else if (n > (uint32_t)NMAX || !bucket_sort_list<T, NMAX / T>(keys, r.x, n, gid_sorted, s, lim,
                                                                           sorted_len + t)) {
             __syncthreads();
-            if (CLASS == 0 || n <= (uint32_t)T * EF)
+            if (n <= (uint32_t)T * EF)
                 sort_list<T, EF>(keys, r.x, n, gid_sorted, s.buf);
             else
                 sort_list_global(keys, r.x, n, gid_sorted);
@@ -1240,7 +1183,6 @@ __global__ void __launch_bounds__(class_threads<CLASS>()) tile_sort_class_kernel
 // kPrefixBins bins: 24 KiB, twice the class-0 kernel's occupancy), the keys themselves in
 // registers (up to kBucketMax per tile).  Skewed bins, a prefix over the buffer or a list over
 // kBucketMax fall back to the global-memory network (whole list).
-#define GSR_PREFIX_KERNEL 1
 constexpr int kPrefixBuf = 2048;
 static_assert(kPrefixBuf >= 2 * (int)kSortPrefixMax, "a prefix plus the rest of its bucket fits the LDS buffer");
 constexpr int kPrefixBins = 2048;
@@ -1249,9 +1191,9 @@ constexpr int kPrefixBins = 2048;
 // (<= kBucketMax).  16 keys in at most 96 VGPRs: five workgroups per CU (the LDS would allow six;
 // 80 VGPRs spill): tile_sort 372-373 -> 357-360 us at 5M@4K against four; 512 x 8 measured 450
 // (six waves per SIMD) and 397 us (eight) (r3y3).
-#define GSR_PREFIX_WAVES 5
+constexpr int kPrefixWaves = 5;
 template <int T, int E>
-__global__ void __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(E <= 16 ? GSR_PREFIX_WAVES : 2)))
+__global__ void __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(E <= 16 ? kPrefixWaves : 2)))
 tile_sort_prefix_kernel(const uint2* __restrict__ ranges,
                                                                         u64* __restrict__ keys, u64 cap,
                                                                         uint32_t* __restrict__ gid_sorted,
@@ -1281,12 +1223,10 @@ tile_sort_prefix_kernel(const uint2* __restrict__ ranges,
 // Class 0 in whole-list mode: the prefix kernel's layout -- the keys in registers, an LDS buffer of
 // kPrefixBuf keys (24 KiB: five workgroups per CU, against three for the 41-KiB class-0 kernel) --
 // with the bins ranked in windows of at most kPrefixBuf keys; a skewed list or one bin over the
-// buffer takes the global-memory network.  tile_sort 57.5-57.9 -> 52.3-52.4 us at 1M@1080p (r3y6);
-// GSR_CLASS0_WINDOW=0 builds the class-0 kernel instead.
-#define GSR_CLASS0_WINDOW 1
-// Its occupancy (A/B: at five waves its 96-VGPR budget spills one VGPR to scratch; four gives 128).
-#define GSR_WINDOW_WAVES GSR_PREFIX_WAVES
-__global__ void __launch_bounds__(kClassThreads) __attribute__((amdgpu_waves_per_eu(GSR_WINDOW_WAVES)))
+// buffer takes the global-memory network.  tile_sort 57.5-57.9 -> 52.3-52.4 us at 1M@1080p (r3y6),
+// against a class-0 kernel with the whole 41-KiB list buffer in LDS.  Five waves (at four, no spill
+// but slower, r6e).
+__global__ void __launch_bounds__(kClassThreads) __attribute__((amdgpu_waves_per_eu(kPrefixWaves)))
 tile_sort_window_kernel(const uint2* __restrict__ ranges, u64* __restrict__ keys, u64 cap,
                         uint32_t* __restrict__ gid_sorted, const uint32_t* __restrict__ list,
                         const uint32_t* __restrict__ count, uint32_t* __restrict__ sorted_len) {
@@ -1365,12 +1305,11 @@ __global__ void __launch_bounds__(64) copy_sorted_prefix_kernel(const uint2* __r
 }
 
 // ---- launchers ----------------------------------------------------------------
-// Most binning chunks (A/B: GSR_BIN_CHUNKS_MAX).
-#define GSR_BIN_CHUNKS_MAX 256
+constexpr int kBinChunksMax = 256;
 int bin_chunks(int P, int* chunk) {
     // ~256 chunks (enough workgroups for the chip), each < 65536 Gaussians (16-bit LDS counters)
     int n = (P + 1023) / 1024;
-    if (n > GSR_BIN_CHUNKS_MAX) n = GSR_BIN_CHUNKS_MAX;
+    if (n > kBinChunksMax) n = kBinChunksMax;
     if (n < 1) n = 1;
     int c = (P + n - 1) / n;
     if (c > 65535) {
@@ -1392,7 +1331,7 @@ uint32_t bin_cells(uint32_t gx, uint32_t gy, CellGrid* cg) {
     while ((1u << shift) < kCell) shift++;
     for (;; shift++) {
         const uint32_t cgx = (gx + (1u << shift) - 1) >> shift, cgy = (gy + (1u << shift) - 1) >> shift;
-        if (GSR_CELL_MORTON) {  // Morton codes of the cells: the power-of-two square around the grid
+        {  // Morton codes of the cells: the power-of-two square around the grid
             uint32_t side = 1;
             while (side < cgx || side < cgy) side <<= 1;
             if ((size_t)side * side <= kLdsTilesMax) {
@@ -1408,7 +1347,7 @@ uint32_t bin_cells(uint32_t gx, uint32_t gy, CellGrid* cg) {
 }
 
 bool bin_fused_ok(uint32_t tiles) { return tiles <= kLdsTilesMax; }
-bool bin_near_ok(uint32_t tiles) { return tiles <= kLdsTilesMax && GSR_K1_RECT; }
+bool bin_near_ok(uint32_t tiles) { return tiles <= kLdsTilesMax; }
 
 size_t bin_cell_count(uint32_t gx, uint32_t gy) {
     CellGrid cg{};
@@ -1429,7 +1368,7 @@ hipError_t launch_bin_count(int P, const GeomState& g, uint32_t gx, uint32_t gy,
     // g.tile_cnt / g.cell_cnt are zero here: preprocess zeroes them, tile_scan_kernel re-zeroes them
     const size_t cell_bytes = cells * sizeof(uint32_t);
     // near-first binning (near_target > 0; fused, K1 by rectangles only): K0a's depth-mass histogram, K1's cut
-    const bool near = near_target > 0 && fused && lds && GSR_K1_RECT;
+    const bool near = near_target > 0 && fused && lds;
     const NearArgs na = near ? NearArgs{g.zhist, near_target, g.zcut, g.near_cnt, g.sranges}
                              : NearArgs{nullptr, 0ull, g.zcut, nullptr, nullptr};  // (K1 records "no cut")
     hipLaunchKernelGGL(cell_count_kernel, grid, block, cell_bytes, stream, P, chunk, g.rect, g.tiles_touched, cells,
@@ -1437,7 +1376,7 @@ hipError_t launch_bin_count(int P, const GeomState& g, uint32_t gx, uint32_t gy,
     hipLaunchKernelGGL(cell_scatter_kernel, grid, block, cell_bytes, stream, P, chunk, g.rect, g.tiles_touched,
                        cells, cgx, g.cell_cnt, g.cell_off, g.depth_key, g.order, g.n_visible);
     // K1's LDS: one u32 per tile (by rectangles) or two 16-bit walk counters per word
-    const size_t hist_bytes = !lds ? 0 : GSR_K1_RECT ? tiles * sizeof(uint32_t) : ((tiles + 1) / 2) * sizeof(uint32_t);
+    const size_t hist_bytes = !lds ? 0 : tiles * sizeof(uint32_t);
     if (fused && !lds) return hipErrorInvalidValue;  // the fused scan needs the LDS cursors
     const FusedZero fz = fused ? FusedZero{g.unit_cnt, g.tile_join, g.cls_count} : FusedZero{nullptr, nullptr, nullptr};
     if (lds)
@@ -1467,7 +1406,7 @@ hipError_t launch_bin_scatter(int P, const GeomState& g, uint32_t gx, uint32_t g
     const FusedScan fs = fused ? FusedScan{g.tile_cnt, ranges, g.total, (u64*)host_total, g.cls_list, g.cls_count}
                                : FusedScan{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     // (as launch_bin_count decided it: the target is K1's business, K3 reads the cut)
-    const NearArgs na = near_first && fused && lds && GSR_K1_RECT
+    const NearArgs na = near_first && fused && lds
                             ? NearArgs{g.zhist, 1ull, g.zcut, g.near_cnt, g.sranges}
                             : NearArgs{nullptr, 0ull, nullptr, nullptr, nullptr};
     if (lds)
@@ -1505,7 +1444,7 @@ hipError_t launch_rec_prep(int P, const GeomState& g, const BinningState& b, siz
     return hipGetLastError();
 }
 
-#define GSR_C1_GRID_SMALL 64
+constexpr uint32_t kClass1GridSmall = 64;
 hipError_t launch_tile_sort(uint32_t tiles, const uint2* ranges, const GeomState& g, const BinningState& b,
                             size_t cap, hipStream_t stream, bool zero_counts, uint32_t cells, uint32_t prefix) {
     if (tiles == 0 || cap == 0) return hipSuccess;
@@ -1516,7 +1455,7 @@ hipError_t launch_tile_sort(uint32_t tiles, const uint2* ranges, const GeomState
                        zero_counts ? g.tile_cnt : nullptr, n_zero, g.sorted_len, g.redo_flag, g.redo_cnt, g.far_cur);
     // persistent class kernels: grids sized to fill the chip when their lists are long
     const auto grid = [&](uint32_t want) { return dim3(tiles < want ? tiles : want); };
-    if (GSR_PREFIX_KERNEL && prefix) {
+    if (prefix) {
         hipLaunchKernelGGL((tile_sort_prefix_kernel<kClassThreads, kClass0Max / kClassThreads>), grid(4096), dim3(kClassThreads), 0,
                            stream, ranges, b.keys, c, b.gid_sorted, g.cls_list, g.cls_count, lim, g.sorted_len);
         hipLaunchKernelGGL((tile_sort_prefix_kernel<kClassThreads, kBucketMax / kClassThreads>), grid(1024), dim3(kClassThreads), 0,
@@ -1524,17 +1463,13 @@ hipError_t launch_tile_sort(uint32_t tiles, const uint2* ranges, const GeomState
                            g.sorted_len);
         return hipGetLastError();
     }
-    if (GSR_CLASS0_WINDOW)
-        hipLaunchKernelGGL(tile_sort_window_kernel, grid(2048), dim3(kClassThreads), 0, stream, ranges, b.keys, c,
-                           b.gid_sorted, g.cls_list, g.cls_count, g.sorted_len);
-    else
-        hipLaunchKernelGGL(tile_sort_class_kernel<0>, grid(2048), dim3(class_threads<0>()), 0, stream, ranges, b.keys,
-                           c, b.gid_sorted, g.cls_list, g.cls_count, lim, g.sorted_len);
+    hipLaunchKernelGGL(tile_sort_window_kernel, grid(2048), dim3(kClassThreads), 0, stream, ranges, b.keys, c,
+                       b.gid_sorted, g.cls_list, g.cls_count, g.sorted_len);
     // class 1 (lists > kClass0Max) is empty or nearly so while the mean list is short (1M@1080p: mean
     // 973 keys): then a small persistent grid -- 512 workgroups of 82 KiB LDS cost 4.6 us to dispatch
     // and retire with nothing to do (r4a trace)
-    const uint32_t c1_grid = cap / tiles <= kClass0Max / 2 ? (uint32_t)GSR_C1_GRID_SMALL : 512u;
-    hipLaunchKernelGGL(tile_sort_class_kernel<1>, grid(c1_grid), dim3(class_threads<1>()), 0, stream, ranges, b.keys, c,
+    const uint32_t c1_grid = cap / tiles <= kClass0Max / 2 ? kClass1GridSmall : 512u;
+    hipLaunchKernelGGL(tile_sort_class1_kernel, grid(c1_grid), dim3(kClassThreads), 0, stream, ranges, b.keys, c,
                        b.gid_sorted, g.cls_list + tiles, g.cls_count + 1, lim, g.sorted_len);
     return hipGetLastError();
 }

@@ -38,11 +38,10 @@ constexpr float SH_C3_0 = -0.5900435899266435f, SH_C3_1 = 2.890611442640554f, SH
 // (int16 lo | int16 hi << 16), used to skip whole waves (DESIGN.md "footprint
 // culling"); lo > hi means "never contributes".  Row 3 is the tile rectangle of
 // getRect.  The Gaussian's first emission index e0 is in the record-start array
-// (GeomState::rec_start; GSR_REC_START_GATHER, the default), which only the record-path
-// backward reads: K3 writes it after a bwd_atomic=0 forward, rec_prep_kernel on demand
-// otherwise. Only a GSR_REC_START_GATHER=0 build patches e0 into row 3's .w: the instance of this
-// Gaussian in tile (tx, ty) has emission index e0 + (ty - min.y) * width + (tx - min.x),
-// the row-major order of duplicateWithKeys (CR/rasterizer_impl.cu:108-124).
+// (GeomState::rec_start), which only the record-path backward reads: K3 writes it after a
+// bwd_atomic=0 forward, rec_prep_kernel on demand otherwise.  The instance of this Gaussian
+// in tile (tx, ty) has emission index e0 + (ty - min.y) * width + (tx - min.x), the row-major
+// order of duplicateWithKeys (CR/rasterizer_impl.cu:108-124).
 // ---------------------------------------------------------------------------
 constexpr int kRecRows = 4;
 
@@ -50,7 +49,7 @@ constexpr int kRecRows = 4;
 // when the splat's alpha >= 1/255 footprint reaches a pixel centre of the tile's 8x8
 // quadrant k (footprint.h).  Binning writes the mask bits as 0; the forward render writes
 // back, for each entry it stages, the quadrants in which some pixel blended it
-// (GSR_BLEND_MASK, a subset of the footprint's), and the backward, which only visits
+// (the blend mask, a subset of the footprint's), and the backward, which only visits
 // entries the forward staged, skips entries whose mask is 0.  Hence P < 2^28.
 constexpr int kEntryMaskBits = 4;
 constexpr uint32_t kEntryMask = 0xfu;
@@ -64,8 +63,6 @@ __host__ __device__ inline size_t align_up(size_t x, size_t a = kAlign) { return
 // release / acquire fences emit no instructions; they give the IR the ordering of one lane's LDS store
 // before another lane's load, which wave_barrier alone (IntrNoMem: a scheduling barrier only) does not
 // (the form rocPRIM's wave_barrier uses).
-// (GSR_WAVE_FENCE=0: the bare wave_barrier, for A/B of the schedule the fences leave the compiler)
-#define GSR_WAVE_FENCE 1
 __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -190,8 +187,7 @@ struct BinningState {
 // Layout of a slot: [5 values][4 quadrant slots][64 lanes] floats, the values being
 // T, C.r, C.g, C.b, invdepth.
 // ---------------------------------------------------------------------------
-#define GSR_CK_STRIDE 256  // a multiple of the render batch (64); A/B builds override it
-constexpr int kCkStride = GSR_CK_STRIDE;
+constexpr int kCkStride = 256;  // a multiple of the render batch (64)
 constexpr int kCkFloats = 5 * 4 * 64;
 
 // ---------------------------------------------------------------------------
@@ -229,29 +225,24 @@ __host__ __device__ inline size_t view_pack_floats(size_t entries) {
     return (kViewBlockHeader + kViewPackEntry * entries + 63) / 64 * 64;
 }
 
-// Per-instance gradient records (backward scratch), SoA so stores are aligned.
-// GSR_FLAG_BITS: the records' content flags as one BIT per emission index (render_bwd ORs it in with a
-// global atomic, order-free) instead of one byte: 8x less for K3 to zero and gauss_reduce to scan
-// (5M@4K: 14 MB instead of 115 MB each way).
-// GSR_REC_START_GATHER: render_bwd reads each entry's first emission index from rec_start[] instead of
-// the splat record's row 3, so K3 no longer patches every visible Gaussian's record (one 4-byte store
-// into a 64-byte record each: a partial 32-byte write per Gaussian, 160 MB at 5M@4K).
-#define GSR_REC_START_GATHER 1
-#define GSR_FLAG_BITS 1
+// Gradient records (backward scratch): the per-instance records of the record path, and the
+// per-Gaussian sums (three arrays).
+// The records' content flags are one BIT per emission index (render_bwd ORs it in with a global
+// atomic, order-free): 5M@4K 14 MB for K3 to zero and gauss_reduce to scan, against 115 MB as bytes.
+// render_bwd reads each entry's first emission index from rec_start[] (not the splat record's row 3,
+// which K3 would then patch for every visible Gaussian: 160 MB of partial writes at 5M@4K).
 struct GradRecs {
     float4* a;  // (dcolor.r, dcolor.g, dcolor.b, dinvdepth)
     float4* b;  // (dmean2D.x, dmean2D.y, dopacity_eff, dconic.b)
     float2* c;  // (dconic.a, dconic.c)
-    uint8_t* flag;  // per-instance records only: 1 = the record exists (BinningState::rec_flag)
+    uint8_t* flag;  // per-instance records only: the content bits (BinningState::rec_flag)
 };
-// The render backward writes a record and its content byte only for an entry with a gradient term
-// (~half of the staged entries at 1M@1080p, 7.6M of 114.7M instances at 5M@4K); the content bytes
+// The render backward writes a record and its content bit only for an entry with a gradient term
+// (~half of the staged entries at 1M@1080p, 7.6M of 114.7M instances at 5M@4K); the content bits
 // live in the binning buffer and are zeroed by the forward's K3 (each chunk clears its emission
-// range with 16-byte stores, no memset launch), so gauss_reduce finds the records from the bytes
-// alone (1024 per wave-wide load) and skips the rest.  Whether an entry has a gradient term depends
-// on the geometry only, not on the upstream gradient, so a second backward of the same forward sets
-// the same bytes.
-#define GSR_REC_FLAG 1
+// range with 16-byte stores, no memset launch), so gauss_reduce finds the records from the bits
+// alone and skips the rest.  Whether an entry has a gradient term depends on the geometry only,
+// not on the upstream gradient, so a second backward of the same forward sets the same bits.
 
 // The live list (backward scratch): the Gaussians with a gradient, appended by gauss_reduce for
 // the sparse gauss_bwd.  Sharded by reduction workgroup (one counter per 128-byte line): a single
@@ -268,11 +259,10 @@ __host__ __device__ inline uint32_t live_list_cap(uint32_t P) {
     return (runs + kLiveShards - 1) / kLiveShards * run;
 }
 // The render backward's per-instance records (not the per-Gaussian sums, which stay three
-// arrays): GSR_REC_AOS interleaves them as 48-byte records a, b, (c, pad), so one instance's
-// three stores land in one or two cache lines instead of three.  Index strides:
-#define GSR_REC_AOS 1
-constexpr int kRecAB = GSR_REC_AOS ? 3 : 1;  // float4 units between records (a, b)
-constexpr int kRecC = GSR_REC_AOS ? 6 : 1;   // float2 units between records (c)
+// arrays) are interleaved as 48-byte records a, b, (c, pad), so one instance's three stores land
+// in one or two cache lines instead of three.  Index strides:
+constexpr int kRecAB = 3;  // float4 units between records (a, b)
+constexpr int kRecC = 6;   // float2 units between records (c)
 
 // ---------------------------------------------------------------------------
 // SH coefficient addressing.  Two layouts reach the kernels:

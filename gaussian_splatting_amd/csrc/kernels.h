@@ -59,7 +59,7 @@ struct RenderFwdArgs {
     int seg_ck;
     uint32_t* seg_ck_out;           // GeomState::fwd_seg_ck: seg_ck recorded for the backward
     uint32_t* fault;                // GeomState::status + 1: bit 0 = a shared-staging wait gave up (never expected)
-    uint32_t half_tiles;            // hybrid grid (render.hip GSR_FWD_TAIL_QUADS): tiles done as half-tile units
+    uint32_t half_tiles;            // hybrid grid (render.hip kFwdTailQuadsPct): tiles done as half-tile units
     unsigned long long* census;     // diagnostic pair counts (gsr_census_set) or null
     // reachable-prefix sort (GeomState): entries in order per tile, and the redo filing
     const uint32_t* sorted_len;
@@ -95,7 +95,7 @@ struct RenderBwdArgs {
     const uint2* unit_part;
     const uint2* unit_full;
     uint32_t full_cap;
-    const uint32_t* rec_start;          // GeomState::rec_start (GSR_REC_START_GATHER)
+    const uint32_t* rec_start;          // GeomState::rec_start (record path: each Gaussian's first emission index)
     const uint32_t* seg_ck;             // GeomState::fwd_seg_ck: checkpoints per backward segment as the
                                         // forward that built the work list used it (segment = seg_ck * kCkStride)
     unsigned long long* census;         // diagnostic pair counts (gsr_census_set) or null
@@ -155,7 +155,6 @@ hipError_t launch_zero_fill(const FillArgs& f, hipStream_t stream);
 // each range's aligned body (non-temporal: 236 MB of zeros written through the caches evicted the
 // records and pixel state render_bwd and gauss_reduce re-read, r2zv), dwords for the unaligned head
 // and tail.
-#define GSR_FILL_NT 1
 __device__ __forceinline__ void zero_fill_part(const FillArgs& f, unsigned long long tid, unsigned long long stride) {
     for (int s = 0; s < f.count; s++) {
         float* p = f.ptr[s];
@@ -187,8 +186,7 @@ constexpr int kShRestF = 45;    // floats per rest row in the split layout
 // SH rows are read once per pass (preprocess: 192 MB at 1M): non-temporal loads keep them from
 // displacing the lines the next kernels re-read (r2zx: preprocess 69.5 -> 62.7 us, bin_count
 // 45.6 -> 43.3, step -8 us).  Streaming stores of render_fwd's image outputs and streaming loads
-// of render_bwd's dL/dpixel (render.hip GSR_NT_OUT / GSR_NT_DPIX) measured no gain.
-#define GSR_NT_SH 1
+// of render_bwd's dL/dpixel measured no gain.
 template <int ROWS, int THREADS, bool SPLIT>
 // rowmask: bit r set = stage row r (rows left out are not read; their LDS contents are undefined).
 __device__ __forceinline__ void sh_stage_in(const ShAddr& sa, int r0, int rows, float* lds, int stride, int tid,
@@ -238,8 +236,7 @@ __device__ __forceinline__ void sh_stage_in(const ShAddr& sa, int r0, int rows, 
 // SH rows are read once per pass (preprocess: 192 MB at 1M): non-temporal loads keep them from
 // displacing the lines the next kernels re-read (r2zx: preprocess 69.5 -> 62.7 us, bin_count
 // 45.6 -> 43.3, step -8 us).  Streaming stores of render_fwd's image outputs and streaming loads
-// of render_bwd's dL/dpixel (render.hip GSR_NT_OUT / GSR_NT_DPIX) measured no gain.
-#define GSR_NT_SH 1
+// of render_bwd's dL/dpixel measured no gain.
 template <int ROWS, int THREADS, bool SPLIT>
 // rowmask: bit r set = write row r (rows left out are not written).
 __device__ __forceinline__ void sh_stage_out(const ShGradAddr& ga, int r0, int rows, const float* lds, int stride,
@@ -293,9 +290,6 @@ __device__ __forceinline__ void sh_stage_out(const ShGradAddr& ga, int r0, int r
 // address).  (Striped over the wave -- one dword of the block per lane and iteration -- the
 // fully unrolled loop kept ~23 iterations' addresses live across the kernel: 308 VGPRs, one wave
 // per SIMD; one iteration at a time serialised the loads.)
-#define GSR_PRAGMA(x) _Pragma(#x)
-#define GSR_GATHER_BATCH 1
-#define GSR_GATHER_UNROLL_COMB 12
 template <int ROWS, int THREADS, bool SPLIT>
 __device__ __forceinline__ void sh_gather_in(const ShAddr& sa, int g, int row0, float* lds, int stride, int tid) {
     if constexpr (!SPLIT) {
@@ -351,7 +345,7 @@ template <int ROWS, int THREADS, bool SPLIT>
 __device__ __forceinline__ void sh_gather_out(const ShGradAddr& ga, int g, int row0, const float* lds, int stride,
                                               int tid) {
     if constexpr (!SPLIT) {
-GSR_PRAGMA(unroll GSR_GATHER_UNROLL_COMB)
+#pragma unroll 12
         for (int k = 0; k < ROWS * (kShRowF / 4) / THREADS; k++) {
             const int i4 = k * THREADS + tid, row = i4 / (kShRowF / 4), c4 = i4 - row * (kShRowF / 4);
             const int gr = __shfl(g, row0 + row);

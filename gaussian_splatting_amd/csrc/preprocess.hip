@@ -88,50 +88,6 @@ __device__ __forceinline__ float3 sh_to_rgb(int deg, const float3* sh, float x, 
     return res;
 }
 
-// sh_to_rgb over a staged LDS row (coefficient k at row[3k..3k+2]) band by band, each band's coefficients
-// read just before its terms (GSR_PRE_SH_BANDS): the same expressions as sh_to_rgb, so the same roundings,
-// without the 48 floats of a whole row held at once (the kernel's register peak: 96 VGPRs, five waves per
-// SIMD; capped at six it spilled).
-#define GSR_PRE_SH_BANDS 0
-template <class Coef>
-__device__ __forceinline__ float3 sh_to_rgb_acc(int deg, const Coef& c, float x, float y, float z) {
-    const float3 s0 = c(0);
-    float3 res = make_float3(SH_C0 * s0.x, SH_C0 * s0.y, SH_C0 * s0.z);
-    if (deg > 0) {
-        asm volatile("" ::: "memory");  // (this band's reads after the previous band's terms)
-        const float3 s1 = c(1), s2 = c(2), s3 = c(3);
-        const float c1 = -SH_C1 * y, c2 = SH_C1 * z, c3 = -SH_C1 * x;
-        res.x += c1 * s1.x + c2 * s2.x + c3 * s3.x;
-        res.y += c1 * s1.y + c2 * s2.y + c3 * s3.y;
-        res.z += c1 * s1.z + c2 * s2.z + c3 * s3.z;
-        if (deg > 1) {
-            asm volatile("" ::: "memory");
-            const float3 s4 = c(4), s5 = c(5), s6 = c(6), s7 = c(7), s8 = c(8);
-            const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
-            const float k4 = SH_C2_0 * xy, k5 = SH_C2_1 * yz, k6 = SH_C2_2 * (2.f * zz - xx - yy), k7 = SH_C2_3 * xz,
-                        k8 = SH_C2_4 * (xx - yy);
-            res.x += k4 * s4.x + k5 * s5.x + k6 * s6.x + k7 * s7.x + k8 * s8.x;
-            res.y += k4 * s4.y + k5 * s5.y + k6 * s6.y + k7 * s7.y + k8 * s8.y;
-            res.z += k4 * s4.z + k5 * s5.z + k6 * s6.z + k7 * s7.z + k8 * s8.z;
-            if (deg > 2) {
-                asm volatile("" ::: "memory");
-                const float3 s9 = c(9), s10 = c(10), s11 = c(11), s12 = c(12), s13 = c(13), s14 = c(14), s15 = c(15);
-                const float k9 = SH_C3_0 * y * (3.f * xx - yy), k10 = SH_C3_1 * xy * z,
-                            k11 = SH_C3_2 * y * (4.f * zz - xx - yy), k12 = SH_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy),
-                            k13 = SH_C3_4 * x * (4.f * zz - xx - yy), k14 = SH_C3_5 * z * (xx - yy),
-                            k15 = SH_C3_6 * x * (xx - 3.f * yy);
-                res.x += k9 * s9.x + k10 * s10.x + k11 * s11.x + k12 * s12.x + k13 * s13.x + k14 * s14.x + k15 * s15.x;
-                res.y += k9 * s9.y + k10 * s10.y + k11 * s11.y + k12 * s12.y + k13 * s13.y + k14 * s14.y + k15 * s15.y;
-                res.z += k9 * s9.z + k10 * s10.z + k11 * s11.z + k12 * s12.z + k13 * s13.z + k14 * s14.z + k15 * s15.z;
-            }
-        }
-    }
-    res.x += 0.5f;
-    res.y += 0.5f;
-    res.z += 0.5f;
-    return res;
-}
-
 // Load the first K = (deg+1)^2 coefficients (K <= 16) of Gaussian idx, either layout.
 __device__ __forceinline__ void load_sh(const ShAddr& sa, int idx, int K, float3 sh[16]) {
 #pragma unroll
@@ -158,21 +114,11 @@ __device__ __forceinline__ void load_sh(const ShAddr& sa, int idx, int K, float3
 //  * the 64-byte splat records are assembled in LDS and written as one 4 KiB block.
 // A culled Gaussian gets the reference's zero radius / tiles_touched, a 0xffffffff depth
 // key and an all-zero record (never read).
-#define GSR_PRE_PREFETCH 2
-constexpr int kPreThreads = 64;
-static_assert(!GSR_PRE_PREFETCH || kPreThreads == 64, "the prefetching path's LDS hand-offs are wave-local: one wave");
+constexpr int kPreThreads = 64;  // (the SH prefetch's LDS hand-offs are wave-local: one wave)
 constexpr int kShHalfRows = 32;
 constexpr int kShRowStride = 52;   // padded LDS row stride (16-byte aligned, conflict-free b128)
-// GSR_PRE_GLDS (A/B, combined layout with GSR_PRE_PREFETCH 2): the first SH half goes global -> LDS by
-// global_load_lds_dwordx4 (no VGPR destination) instead of through 24 VGPRs held across the geometry.  A DMA
-// instruction writes 1 KiB lane-linearly, so that half's image is piece-major -- 16-byte piece c of row r at
-// float4 (c * 32 + r): instruction k, lane l carries piece index 64 k + l -- and its rows are read through
-// that index (sh_to_rgb_acc).
-#define GSR_PRE_GLDS 0
-
-#define GSR_PRE_OCCUPANCY
 template <int SH_MODE>
-__global__ void __launch_bounds__(kPreThreads) GSR_PRE_OCCUPANCY preprocess_kernel(PreprocessArgs a) {
+__global__ void __launch_bounds__(kPreThreads) preprocess_kernel(PreprocessArgs a) {
     __shared__ __attribute__((aligned(16))) float s_buf[SH_MODE != kShGlobal ? kShHalfRows * kShRowStride : 64 * 16];
     static_assert(kShHalfRows * kShRowStride >= 64 * 16, "the record block reuses the SH buffer");
     static_assert(kShHalfRows * kShRowStride >= kShHalfRows * (kShRestF + 3), "the split staging fits the buffer");
@@ -182,36 +128,22 @@ __global__ void __launch_bounds__(kPreThreads) GSR_PRE_OCCUPANCY preprocess_kern
     const bool valid = idx < a.P;
     const int nvalid = min(kPreThreads, a.P - g0);
     for (uint32_t i = blockIdx.x * kPreThreads + lane; i < a.zero_n; i += gridDim.x * kPreThreads) a.zero[i] = 0u;
-    // Every input of the wave requested up front (GSR_PRE_PREFETCH): the scale, rotation and opacity of
-    // each lane's Gaussian, and both halves of the wave's SH block in registers (6 x 16 B per lane and
-    // half) -- one memory latency for the wave, where the geometry's loads waited for the view
-    // transform and each SH half for the previous half's colours.
+    // The wave's inputs requested up front: the scale, rotation and opacity of each lane's Gaussian and
+    // the first half of the wave's SH block in registers (6 x 16 B per lane), the second half once the
+    // first is in LDS -- where the geometry's loads waited for the view transform and each SH half for
+    // the previous half's colours.
     typedef float v4f __attribute__((ext_vector_type(4)));
     constexpr bool kPf = SH_MODE == kShLdsCombined;
     constexpr int kPieces = kShHalfRows * (kShRowF / 4) / kPreThreads;  // 16-byte pieces per lane and half
     v4f shp[2][kPieces];
-    constexpr bool kGlds = kPf && GSR_PRE_GLDS && GSR_PRE_PREFETCH == 2;
-    if constexpr (kGlds) {
-        // half 0 straight into LDS: instruction k moves pieces [64 k, 64 k + 64) of the half's piece-major image
-        const v4f* src = reinterpret_cast<const v4f*>(a.shs);
-#pragma unroll
-        for (int k = 0; k < kPieces; k++) {
-            const int i = k * kPreThreads + lane, r = i & (kShHalfRows - 1), c = i >> 5;
-            const int row = g0 + min(r, nvalid - 1);  // (rows past P read a valid row, unused)
-            __builtin_amdgcn_global_load_lds(
-                (const __attribute__((address_space(1))) void*)(src + (size_t)row * (kShRowF / 4) + c),
-                (__attribute__((address_space(3))) void*)(s_buf + k * kPreThreads * 4), 16, 0, 0);
-        }
-    } else if constexpr (kPf) {
+    if constexpr (kPf) {  // the first half
         const v4f* src = reinterpret_cast<const v4f*>(a.shs + (size_t)g0 * kShRowF);
         const int n4 = nvalid * (kShRowF / 4);
 #pragma unroll
-        for (int h = 0; h < (GSR_PRE_PREFETCH == 2 ? 1 : 2); h++)
-#pragma unroll
-            for (int k = 0; k < kPieces; k++) {
-                const int i4 = h * kShHalfRows * (kShRowF / 4) + k * kPreThreads + lane;
-                shp[h][k] = i4 < n4 ? __builtin_nontemporal_load(src + i4) : (v4f){0.f, 0.f, 0.f, 0.f};
-            }
+        for (int k = 0; k < kPieces; k++) {
+            const int i4 = k * kPreThreads + lane;
+            shp[0][k] = i4 < n4 ? __builtin_nontemporal_load(src + i4) : (v4f){0.f, 0.f, 0.f, 0.f};
+        }
     }
     float3 pf_sc = make_float3(0.f, 0.f, 0.f);
     float4 pf_q = make_float4(1.f, 0.f, 0.f, 0.f);
@@ -295,16 +227,12 @@ __global__ void __launch_bounds__(kPreThreads) GSR_PRE_OCCUPANCY preprocess_kern
             const int rows = min(kShHalfRows, nvalid - half * kShHalfRows);
             if (rows > 0) {  // wave-uniform
                 (void)sa;
-                if (kGlds && half == 0) {
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA's LDS writes have landed
-                } else {
 #pragma unroll
-                    for (int k = 0; k < kPieces; k++) {
-                        const int i4 = k * kPreThreads + lane, row = i4 / (kShRowF / 4), c4 = i4 - row * (kShRowF / 4);
-                        *reinterpret_cast<v4f*>(&s_buf[row * kShRowStride + 4 * c4]) = shp[half][k];
-                    }
+                for (int k = 0; k < kPieces; k++) {
+                    const int i4 = k * kPreThreads + lane, row = i4 / (kShRowF / 4), c4 = i4 - row * (kShRowF / 4);
+                    *reinterpret_cast<v4f*>(&s_buf[row * kShRowStride + 4 * c4]) = shp[half][k];
                 }
-                if (GSR_PRE_PREFETCH == 2 && half == 0) {  // the second half requested now, read after this one
+                if (half == 0) {  // the second half requested now, read after this one
                     const v4f* src = reinterpret_cast<const v4f*>(a.shs + (size_t)g0 * kShRowF);
                     const int n4 = nvalid * (kShRowF / 4);
 #pragma unroll
@@ -316,23 +244,10 @@ __global__ void __launch_bounds__(kPreThreads) GSR_PRE_OCCUPANCY preprocess_kern
                 wave_lds_sync();  // (one wave: its LDS accesses complete in order)
                 if ((lane >> 5) == half && ok) {
                     const float* row = &s_buf[(lane & 31) * kShRowStride];
-                    if (kGlds && half == 0) {  // the piece-major image: float f of row r at 4 (32 (f / 4) + r) + f % 4
-                        const float* base = &s_buf[4 * (lane & 31)];
-                        auto coef = [&](int k) {
-                            const int f = 3 * k;
-                            return make_float3(base[128 * (f >> 2) + (f & 3)], base[128 * ((f + 1) >> 2) + ((f + 1) & 3)],
-                                               base[128 * ((f + 2) >> 2) + ((f + 2) & 3)]);
-                        };
-                        rgb = sh_to_rgb_acc(a.D, coef, dir.x, dir.y, dir.z);
-                    } else if (GSR_PRE_SH_BANDS) {
-                        auto coef = [&](int k) { return make_float3(row[3 * k], row[3 * k + 1], row[3 * k + 2]); };
-                        rgb = sh_to_rgb_acc(a.D, coef, dir.x, dir.y, dir.z);
-                    } else {
-                        float3 sh[16];
+                    float3 sh[16];
 #pragma unroll
-                        for (int k = 0; k < 16; k++) sh[k] = make_float3(row[3 * k], row[3 * k + 1], row[3 * k + 2]);
-                        rgb = sh_to_rgb(a.D, sh, dir.x, dir.y, dir.z);
-                    }
+                    for (int k = 0; k < 16; k++) sh[k] = make_float3(row[3 * k], row[3 * k + 1], row[3 * k + 2]);
+                    rgb = sh_to_rgb(a.D, sh, dir.x, dir.y, dir.z);
                 }
                 wave_lds_sync();
             }

@@ -29,10 +29,11 @@
 // A slot is retired once the walk passes the last contributor of all its pixels
 // (n_contrib from the forward).  Per-Gaussian sums over the tile's pixels are
 // first summed over the lane's four slots in registers, then over the wave with a
-// lane-swap reduce-scatter and DPP row sums -- once per
-// (tile, Gaussian) instance -- and written with plain stores.  There are no
-// float atomics anywhere, so the result is bitwise reproducible (the reference
-// issues 10 global float atomics per pixel-Gaussian pair, CR/backward.cu:569-609).
+// lane-swap reduce-scatter and DPP row sums -- once per (tile, Gaussian) instance.
+// The atomic path (the default) adds those sums into the Gaussian's accumulator row with
+// one float atomic per value and instance; the record path writes them with plain stores
+// for gauss_reduce and is bitwise reproducible.  The reference issues 10 global float
+// atomics per pixel-Gaussian pair (CR/backward.cu:569-609).
 #include <cstdlib>
 
 #include "footprint.h"
@@ -45,58 +46,22 @@ namespace gsr {
 
 constexpr int kBatch = 64;  // list entries staged per round (one per lane)
 
-// A/B switch: skip a backward quadrant whose pixels all have alpha = 0.
-#define GSR_BWD_ANYSKIP 1
-// A/B switch: a half-tile forward wave tests only its own two quadrants of each entry's footprint
-// and ORs those bits into the entry (the other half adds its own).
-#define GSR_FWD_OWN_BITS 1
-// A/B switch: the backward's ten per-entry sums carried across entries (zeroed after each
-// reduction) instead of declared per entry.
-#define GSR_BWD_CARRY_R 0
-
 // Each lane's tile-list entry of the NEXT batch is loaded during the current batch's walk, so a
 // batch's staging waits for one round trip (the splat records) instead of two (entry, then record).
-#define GSR_PF_ENTRY 1
-// Cost probe for 4x4-block units ("Why the render kernels keep their structure"): the
-// forward's entry index made a per-lane value (the same in every lane, so the results are unchanged), so
-// the entry's data are VGPRs and the quadrant skips are EXEC-mask branches -- what four 16-lane groups
-// walking their own entries would pay before any lane saving.  Off in the product.
-#define GSR_FWD_LANE_ENTRY 0
-// A/B: software-pipelined LDS reads of the staged entries in the forward's walk (render_fwd_tile)
-#define GSR_FWD_LDS_PF 0
-#define GSR_BWD_LDS_PF 0
-// The entry mask the forward leaves for the backward: the quadrants whose footprint the entry touches
-// (0), or the quadrants in which some pixel blended it (1: set after the batch's walk from one wave-uniform
-// bit per (entry, quadrant) evaluation that passed its any-alpha test).  The backward evaluates an entry's
-// quadrant only where a pixel can have a gradient term, and the blend mask is the tighter superset of
-// those; entries with no blending pixel are neither gathered nor walked by the backward.
-// (r5u, interleaved: 1M@1080p 0.7227 -> 0.7213 ms, 5M@4K 2.222 -> 2.207, 500k 0.7258 -> 0.7222; render_bwd
-// -4 / -19 / -8 us, render_fwd +4 / +8 / +5 us for the bits.  The ORs are issued once the next batch's
-// loads are in flight: issued before its staging they made it wait for them, render_fwd +5 us more, r5t.)
-#define GSR_BLEND_MASK 1
-#define GSR_BLEND_VGPR 0
-static_assert(!GSR_BLEND_MASK || GSR_FWD_OWN_BITS, "the blend mask is written per part");
-
-// Traffic attribution builds only (results are wrong in them): GSR_ATTR bit 0
-// drops the backward's record / content-byte stores, bit 1 its checkpoint loads, bit 2 its
-// per-pixel state loads other than n_contrib; in the atomic backward bit 3 drops the touched-bit ORs,
-// bit 4 the accumulator adds.  The control flow is unchanged in all of them.
-#define GSR_ATTR 0
-// Cache policy A/B switches: non-temporal stores of the forward's image outputs, non-temporal
-// loads of the backward's dL/dpixel.
-#define GSR_NT_OUT 0
-#define GSR_NT_DPIX 0
+//
+// The entry mask the forward leaves for the backward is the blend mask: the quadrants in which some
+// pixel blended the entry (set after the batch's walk from one wave-uniform bit per (entry, quadrant)
+// evaluation that passed its any-alpha test), each half-tile part OR-ing its own quadrants' bits.  The
+// backward evaluates an entry's quadrant only where a pixel can have a gradient term, and the blend mask
+// is the tightest superset of those; entries with no blending pixel are neither gathered nor walked by
+// the backward.  (r5u, interleaved: 1M@1080p 0.7227 -> 0.7213 ms, 5M@4K 2.222 -> 2.207; the ORs are
+// issued once the next batch's loads are in flight -- before its staging they made it wait, r5t.)
+// Variants measured and rejected (DESIGN.md "Measured and rejected"; git history keeps their code):
+// shared two-wave staging, lane-held entries, the blend bits in one VGPR, software-pipelined LDS reads,
+// non-temporal image stores / dL/dpixel loads, an occupancy cap on the backward.
 
 GSR_STAMP_BUFFER(g_st_rfwd);
 GSR_STAMP_BUFFER(g_st_rbwd);
-
-// Occupancy target of the backward (waves per SIMD).  One wave per tile means 8160
-// waves at 1080p for 1024 SIMDs; the register budget decides how many run at once.
-// Occupancy hint (0 = none): with the fused zero-fill blocks (RenderBwdArgs::fill) the kernel takes
-// 82 VGPRs, five waves per SIMD; GSR_BWD_WAVES=6 holds it at 79 (six), which measured the same
-// (r4c: 0.7626 vs 0.7610 ms/step, render_bwd 284-289 us either way) -- not occupancy-bound.
-#define GSR_BWD_WAVES 0
-#define GSR_BWD_OCCUPANCY
 
 __device__ __forceinline__ uint32_t uniform_u32(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
@@ -128,9 +93,8 @@ __device__ __forceinline__ float splat_alpha(float p2, float opacity, float& G) 
 // lane of this slot blend this splat" and "is any pixel of this slot still live".
 // SGPR budget of the forward: at .sgpr_count 82-96 the hardware admits 7 one-wave workgroups per
 // SIMD, at <= 80 eight (MI355X_MICROARCH.md "Residency"); the VGPRs (61) allow eight.
-#define GSR_FWD_SGPRS 80  // r4b: render_fwd 199-200 -> 195-197 us (8 SGPRs spill to VGPR lanes, prologue only); 0 = off
-#define GSR_FWD_SGPR_ATTR __attribute__((amdgpu_num_sgpr(GSR_FWD_SGPRS)))
-#define GSR_FWD_OCCUPANCY GSR_FWD_SGPR_ATTR
+// (r4b: render_fwd 199-200 -> 195-197 us; 8 SGPRs spill to VGPR lanes, prologue only)
+#define GSR_FWD_OCCUPANCY __attribute__((amdgpu_num_sgpr(80)))
 // One wave per PART of a tile: NQ = 4 quadrants (the whole 16x16 tile) or NQ = 2 (its top or
 // bottom half).  Each lane owns one pixel in each of the part's NQ quadrants ("slots").  With
 // half tiles the 8160 tiles of a 1080p view become 16320 waves of half the blend work each, so
@@ -146,58 +110,29 @@ __device__ __forceinline__ float splat_alpha(float p2, float opacity, float& G) 
 // launch the tile's whole list is sorted and both parts render it again from the start
 // (render_fwd_redo_kernel).  The forward walks ~7% of a 4K tile's list and ~34% of a 1080p
 // one, so with a prefix of 1024 entries a redo is rare.
-//
-// SHARED (NQ = 2 only; GSR_FWD_SHARED): the two half-tile waves are one 128-thread workgroup and
-// stage each 64-entry batch ONCE, into a ring of NB batch slots in LDS: the first part to need
-// batch k claims slot k % NB (an LDS compare-and-swap), loads the entries' records, tests the
-// footprint against the quadrants of both parts (of the other part only while it still runs) and
-// publishes the slot (a release store of its tag); the other part finds it staged.  No workgroup
-// barrier after the first: a part that runs ahead is held back only when it would overwrite a
-// slot the other part has not finished walking (NB - 1 batches of lead), and a part whose pixels
-// are all done leaves the protocol (done = kDoneAll) and the other stages alone.  The entries'
-// mask bits are written once, by the stager (no atomic OR).  No deadlock: a part waiting to reuse
-// a slot has claimed nothing, and a claimed slot is staged without waiting.
-// Measured (r4c, 1M@1080p, three interleaved rounds): render_fwd 236-240 us against 194-196 for the
-// two independent half-tile waves -- seven waves per SIMD instead of eight (the staging of both
-// parts' footprints needs 72 VGPRs), and a part that runs ahead waits for slot reuse.  Off.
-#define GSR_FWD_SHARED 0
-#define GSR_FWD_SHARED_NB 3
-constexpr int kDoneAll = 1 << 30;
-__device__ __forceinline__ int lds_load_acq(int* p) {
-    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void lds_store_rel(int* p, int v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
 
-// The render kernels' per-batch LDS hand-offs (staged entries, the backward's reduced sums).  A
-// non-shared render unit is one wave, whose LDS accesses complete in order, so the hand-off needs only
-// the compiler kept from moving LDS accesses across it (GSR_RENDER_WAVESYNC) -- __syncthreads'
-// workgroup fence also makes the wave wait for every store it has in flight (the backward's gradient
-// records, the forward's entry masks and checkpoints) before the next batch's loads.
-#define GSR_RENDER_WAVESYNC 1
+// The render kernels' per-batch LDS hand-offs (staged entries, the backward's reduced sums).  A render
+// unit is one wave, whose LDS accesses complete in order, so the hand-off needs only the compiler kept
+// from moving LDS accesses across it -- __syncthreads' workgroup fence also makes the wave wait for
+// every store it has in flight (the backward's gradient records, the forward's entry masks and
+// checkpoints) before the next batch's loads.
 __device__ __forceinline__ void unit_sync() {
     wave_lds_sync();
 }
 
-template <int NB>
 struct FwdLds {
-    float4 xy[NB][kBatch], cq[NB][kBatch], col[NB][kBatch];
-    int tag[NB], claim[NB], done[2];
+    float4 xy[kBatch], cq[kBatch], col[kBatch];
 };
-template <int NB>
-__device__ __forceinline__ FwdLds<NB>& fwd_lds() {
-    __shared__ FwdLds<NB> s;
+__device__ __forceinline__ FwdLds& fwd_lds() {
+    __shared__ FwdLds s;
     return s;
 }
 
-template <int NQ, bool CENSUS, bool SHARED = false>
+template <int NQ, bool CENSUS>
 __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const uint32_t tile, const int part) {
   {
-    static_assert(!SHARED || NQ == 2, "shared staging pairs the two half-tile parts");
-    constexpr int NPART = 4 / NQ;
     constexpr uint32_t kPartMask = (1u << NQ) - 1u;
-    constexpr int NB = SHARED ? GSR_FWD_SHARED_NB : 1;  // batch slots in LDS
+    constexpr int NPART = 4 / NQ;
     const uint32_t tiles = a.gx * a.gy;
     const int qbase = part * NQ;  // first quadrant of this part
     const int tile_x0 = (int)(tile % a.gx) * kTile, tile_y0 = (int)(tile / a.gx) * kTile;
@@ -210,19 +145,11 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const ui
         GSR_STAMP_RT(g_st_rfwd, tile, 4);
     }
 
-    // (one LDS block per NB, whatever NQ: the hybrid launch's half-tile and quadrant units share it)
-    FwdLds<NB>& L = fwd_lds<NB>();
+    // (one LDS block whatever NQ: the hybrid launch's half-tile and quadrant units share it)
+    FwdLds& L = fwd_lds();
     auto& s_xy = L.xy;  // (x, y, o, 1/z)
     auto& s_cq = L.cq;  // (A, B, C, quads)
     auto& s_col = L.col;  // rgb
-    auto& s_tag = L.tag;  // SHARED: slot k % NB holds batch s_tag
-    auto& s_claim = L.claim;
-    auto& s_done = L.done;  // SHARED: batches walked per part
-    if (SHARED) {
-        if (threadIdx.x < NB) s_tag[threadIdx.x] = s_claim[threadIdx.x] = (int)threadIdx.x - NB;
-        if (threadIdx.x < 2) s_done[threadIdx.x] = 0;
-        __syncthreads();  // (both parts are running here; the only workgroup barrier)
-    }
 
     float Tl[NQ], Tc[NQ], C0[NQ], C1[NQ], C2[NQ], D[NQ];
     uint32_t last[NQ];
@@ -242,82 +169,32 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const ui
     const int n = (int)(range.y - range.x);
     const int ns = a.sorted_len ? min(n, (int)a.sorted_len[tile]) : n;  // entries in order
     unsigned long long c_staged = 0, c_eval = 0, c_alpha = 0, c_blend = 0, c_idle = 0;  // CENSUS only
-    constexpr bool kPf = GSR_PF_ENTRY && !SHARED;
-    uint32_t ent_next = kPf && lane < ns ? a.gid_sorted[range.x + lane] : 0u;  // (GSR_PF_ENTRY)
-    int bk = 0;  // batch index
-    // GSR_BLEND_MASK: the previous batch's blend bits, OR-ed into its entries once this batch's loads are in
-    // flight (vmcnt counts stores too: issued before the next staging, the ORs made it wait for them)
+    uint32_t ent_next = lane < ns ? a.gid_sorted[range.x + lane] : 0u;  // the next batch's entry
+    // the previous batch's blend bits, OR-ed into its entries once this batch's loads are in flight
+    // (vmcnt counts stores too: issued before the next staging, the ORs made it wait for them)
     uint32_t pend_bq = 0;
     int pend_b0 = 0;
-    for (int b0 = 0; b0 < ns && alive; b0 += kBatch, bk++) {
-        const int sl = SHARED ? bk % NB : 0;
-        if (CENSUS && !SHARED) c_staged += (unsigned long long)min(kBatch, ns - b0);
+    for (int b0 = 0; b0 < ns && alive; b0 += kBatch) {
+        if (CENSUS) c_staged += (unsigned long long)min(kBatch, ns - b0);
         uint32_t qm = 0;
-        if (SHARED) {
-            // acquire batch bk in slot sl (uniform decisions).  Bounded: a protocol fault (none is
-            // known) ends this part's walk with a flag in the status word instead of hanging the GPU
-            uint32_t spins = 0;
-            for (;; spins++) {
-                if (spins > (1u << 22)) {
-                    if (lane == 0) atomicOr(a.fault, 1u);
-                    alive = 0;
-                    break;
-                }
-                if (lds_load_acq(&s_tag[sl]) == bk) break;  // staged, by either part
-                const bool mine_to_stage = s_claim[sl] != bk &&
-                                           (bk < NB || lds_load_acq(&s_done[part ^ 1]) > bk - NB);  // slot free
-                if (mine_to_stage) {
-                    int prev = 0;
-                    if (lane == 0) prev = atomicCAS(&s_claim[sl], bk - NB, bk);
-                    if (__builtin_amdgcn_readfirstlane(prev) == bk - NB) {
-                        if (CENSUS) c_staged += (unsigned long long)min(kBatch, ns - b0);
-                        if (b0 + lane < ns) {
-                            uint32_t* ent = a.gid_sorted + range.x + b0 + lane;
-                            const uint32_t gid = *ent >> kEntryMaskBits;
-                            const float4* rec = a.rec + (size_t)kRecRows * gid;
-                            const float4 v0 = rec[0], v1 = rec[1], v2 = rec[2];
-                            // both parts' quadrants, the other's only while it runs
-                            const uint32_t only = (kPartMask << qbase) |
-                                                  (lds_load_acq(&s_done[part ^ 1]) < kDoneAll ? kPartMask << (NQ - qbase) : 0u);
-                            const uint32_t q4 = quad_bits_exact(v0, v1, v2, tile_x0, tile_y0, only);
-                            s_xy[sl][lane] = make_float4(v0.x, v0.y, v1.y, v1.z);
-                            s_col[sl][lane] = v2;
-                            s_cq[sl][lane] = stage_conic(v0, v1, q4);
-                            *ent = (gid << kEntryMaskBits) | q4;  // for the backward, all parts' bits at once
-                        }
-                        lds_store_rel(&s_tag[sl], bk);
-                        break;
-                    }
-                }
-                __builtin_amdgcn_s_sleep(1);
-            }
-            if (!alive) break;
-            // (all four bits, this part's taken below; lanes past the list hold a stale slot: none)
-            qm = b0 + lane < ns ? __float_as_uint(s_cq[sl][lane].w) : 0u;
-        } else if (b0 + lane < ns) {
-            uint32_t* ent = a.gid_sorted + range.x + b0 + lane;  // Gaussian << 4 | quadrant mask
-            // (the other part may be OR-ing its mask bits into *ent: only the Gaussian bits are used)
-            const uint32_t gid = (kPf ? ent_next : *ent) >> kEntryMaskBits;
+        if (b0 + lane < ns) {
+            // Gaussian << 4 | quadrant mask (the other part may be OR-ing its mask bits into the entry:
+            // only the Gaussian bits are used)
+            const uint32_t gid = ent_next >> kEntryMaskBits;
             const float4* rec = a.rec + (size_t)kRecRows * gid;
             const float4 v0 = rec[0], v1 = rec[1], v2 = rec[2];
-            s_xy[0][lane] = make_float4(v0.x, v0.y, v1.y, v1.z);
-            s_col[0][lane] = v2;
+            s_xy[lane] = make_float4(v0.x, v0.y, v1.y, v1.z);
+            s_col[lane] = v2;
             // this part's quadrants only; the backward (which visits only staged entries) gets every
-            // part's bits OR-ed into the entry K4 wrote with clear mask bits.  A part that stopped
+            // part's blend bits OR-ed into the entry K4 wrote with clear mask bits.  A part that stopped
             // before an entry leaves its bits clear there: its pixels all ended earlier, so the
             // backward has retired those slots by then (slot limits from n_contrib).
             qm = quad_bits_exact(v0, v1, v2, tile_x0, tile_y0, kPartMask << qbase);
-            s_cq[0][lane] = stage_conic(v0, v1, qm >> qbase);
-            if (GSR_BLEND_MASK) {
-                // (the blend mask is OR-ed in after the walk, below)
-            } else if (NPART == 1)
-                *ent = (gid << kEntryMaskBits) | qm;
-            else if (qm)
-                __hip_atomic_fetch_or(ent, qm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_cq[lane] = stage_conic(v0, v1, qm >> qbase);
         }
-        if (kPf && b0 + kBatch + lane < ns) ent_next = a.gid_sorted[range.x + b0 + kBatch + lane];
-        if (!SHARED) unit_sync();
-        if (GSR_BLEND_MASK && !SHARED && pend_bq)  // (the previous batch's bits: see above)
+        if (b0 + kBatch + lane < ns) ent_next = a.gid_sorted[range.x + b0 + kBatch + lane];
+        unit_sync();
+        if (pend_bq)  // (the previous batch's bits: see above)
             __hip_atomic_fetch_or(a.gid_sorted + range.x + pend_b0 + lane, pend_bq, __ATOMIC_RELAXED,
                                   __HIP_MEMORY_SCOPE_AGENT);
         // Blend checkpoint (gsr_common.h): the state before entry b0, stored after this batch's
@@ -338,21 +215,17 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const ui
             }
         }
         unsigned long long todo = __ballot((qm >> qbase) & kPartMask);
-        // GSR_BLEND_MASK: bit (qbase + k) of lane j's bq: some pixel of quadrant k blended entry j.  GSR_BLEND_VGPR 1:
-        // an entry's bits gather in one SGPR (one 32-bit OR per evaluation) and go to lane j's VGPR once per entry
-        // (a compare and a select); 0: one 64-bit mask per quadrant in SGPRs (under the 80-SGPR budget those spill
-        // to VGPR lanes)
+        // bit j of blend[k]: some pixel of quadrant k blended entry j (one 64-bit mask per quadrant in
+        // SGPRs; under the 80-SGPR budget those spill to VGPR lanes)
         unsigned long long blend[NQ];
 #pragma unroll
         for (int k = 0; k < NQ; k++) blend[k] = 0ull;
-        uint32_t bq_lane = 0;
         while (todo && alive) {
             const int j = __builtin_ctzll(todo);
             todo &= todo - 1;
-            const float4 xy = s_xy[sl][j], cq = s_cq[sl][j], col = s_col[sl][j];
-            const uint32_t m = (SHARED ? uniform_u32(__float_as_uint(cq.w)) >> qbase : uniform_u32(__float_as_uint(cq.w))) & alive;
+            const float4 xy = s_xy[j], cq = s_cq[j], col = s_col[j];
+            const uint32_t m = uniform_u32(__float_as_uint(cq.w)) & alive;
             const uint32_t pos1 = (uint32_t)(b0 + j + 1);
-            uint32_t ebits = 0;  // (GSR_BLEND_VGPR: this entry's blend bits, uniform)
 #pragma unroll
             for (int k = 0; k < NQ; k++) {
                 if (!(m & (1u << k))) continue;  // uniform: footprint misses this quadrant
@@ -370,12 +243,7 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const ui
                     c_idle += bl ? 0ull : 1ull;
                 }
                 if (!__any(w0 > 0.f)) continue;  // uniform
-                if (GSR_BLEND_MASK && !SHARED) {
-                    if (GSR_BLEND_VGPR)
-                        ebits |= 1u << (qbase + k);
-                    else
-                        blend[k] |= 1ull << j;
-                }
+                blend[k] |= 1ull << j;
                 const float test_T = Tl[k] * (1.f - alpha);
                 const bool term = test_T < 0.0001f;  // live pixel: ends it, splat not added
                 const float w = term ? 0.f : w0;
@@ -391,30 +259,22 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const ui
                 // it with "some pixel terminated here" cost two VALU to materialise the guard)
                 if (!__any(Tl[k] > 0.f)) alive &= ~(1u << k);
             }
-            if (GSR_BLEND_MASK && GSR_BLEND_VGPR && !SHARED) bq_lane = lane == j ? ebits : bq_lane;
         }
-        if (GSR_BLEND_MASK && !SHARED) {
+        {
             // OR-ed into the entry K4 wrote with clear mask bits (the other part adds its own) during the next
             // batch, or after the walk
-            uint32_t bq = bq_lane;
-            if (!GSR_BLEND_VGPR) {
+            uint32_t bq = 0;
 #pragma unroll
-                for (int k = 0; k < NQ; k++) bq |= (uint32_t)((blend[k] >> lane) & 1ull) << (qbase + k);
-            }
+            for (int k = 0; k < NQ; k++) bq |= (uint32_t)((blend[k] >> lane) & 1ull) << (qbase + k);
             pend_bq = b0 + lane < ns ? bq : 0u;
             pend_b0 = b0;
         }
-        if (SHARED) {
-            if (lane == 0) lds_store_rel(&s_done[part], bk + 1);  // slot sl may be restaged for bk + NB
-        } else {
-            unit_sync();
-        }
+        unit_sync();
 #ifdef GSR_STAMPS
         if (lane == 0 && part == 0) g_st_rfwd[(size_t)tile * kStampSlots + 3] = (unsigned long long)(b0 + kBatch);
 #endif
     }
-    if (SHARED && lane == 0) lds_store_rel(&s_done[part], kDoneAll);  // the other part stages alone from here
-    if (GSR_BLEND_MASK && !SHARED && pend_bq)  // the last walked batch's bits
+    if (pend_bq)  // the last walked batch's bits
         __hip_atomic_fetch_or(a.gid_sorted + range.x + pend_b0 + lane, pend_bq, __ATOMIC_RELAXED,
                               __HIP_MEMORY_SCOPE_AGENT);
     if (CENSUS && lane == 0) {
@@ -542,12 +402,12 @@ __global__ void __launch_bounds__(64) GSR_FWD_OCCUPANCY render_fwd_kernel(Render
     render_fwd_tile<NQ, CENSUS>(a, tile, part);
 }
 
-// Hybrid grid (GSR_FWD_TAIL_QUADS): half-tile units for the first tiles in dispatch order, quadrant
-// units (one wave per 8x8 quadrant, four per tile) for the last `quad_tiles` tiles.  A launch ends about
+// Hybrid grid: half-tile units for the first tiles in dispatch order, quadrant units (one wave per 8x8
+// quadrant, four per tile) for the last kFwdTailQuadsPct percent of the tiles.  A launch ends about
 // one unit's duration after its last units start, and a half tile's cost (set by how soon its pixels
 // saturate) is not known in advance, so the units dispatched last are made short instead: the tail
 // shrinks, for ~2x the staging work on those tiles only.
-#define GSR_FWD_TAIL_QUADS 10
+constexpr uint32_t kFwdTailQuadsPct = 10;
 __global__ void __launch_bounds__(64) GSR_FWD_OCCUPANCY render_fwd_hybrid_kernel(RenderFwdArgs a) {
     uint32_t bid = 0;
     if (fwd_fill_block(a, bid)) return;
@@ -563,20 +423,6 @@ __global__ void __launch_bounds__(64) GSR_FWD_OCCUPANCY render_fwd_hybrid_kernel
         if (tile >= a.gx * a.gy) return;
         render_fwd_tile<1, false>(a, tile, (int)((b / 8) % 4));
     }
-}
-
-// Shared staging (GSR_FWD_SHARED): one 128-thread workgroup per tile, its two waves the halves.
-// (72 VGPRs at seven waves per SIMD: the staging of both parts' footprints holds more registers
-// beside the blend state; left alone the compiler took 84, five waves)
-#define GSR_FWD_SHARED_WAVES 7
-template <bool CENSUS>
-__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(GSR_FWD_SHARED_WAVES, GSR_FWD_SHARED_WAVES)))
-GSR_FWD_SGPR_ATTR render_fwd_shared_kernel(RenderFwdArgs a) {
-    uint32_t bid = 0;
-    if (fwd_fill_block(a, bid)) return;
-    if (bid == 0 && threadIdx.x == 0) *a.seg_ck_out = (uint32_t)a.seg_ck;  // for the backward
-    if (bid >= a.gx * a.gy) return;  // (uniform over the workgroup)
-    render_fwd_tile<2, CENSUS, true>(a, bid, (int)(threadIdx.x >> 6));
 }
 
 // The redo of the tiles render_fwd_kernel filed (their whole lists sorted since, by
@@ -635,21 +481,16 @@ hipError_t launch_render_fwd(const RenderFwdArgs& a, hipStream_t stream, int qua
         }
     }
     const uint32_t fb = a.fill_blocks;  // (fill blocks first: a multiple of 8)
-    if (GSR_FWD_TAIL_QUADS && quads == 2 && !a.census && tiles >= 16 && tiles <= 64 * cus) {
-        // the last tiles (whole groups of 8) as quadrant units: GSR_FWD_TAIL_QUADS percent of them, at most
+    if (quads == 2 && !a.census && tiles >= 16 && tiles <= 64 * cus) {
+        // the last tiles (whole groups of 8) as quadrant units: kFwdTailQuadsPct percent of them, at most
         // ~0.4 groups per CU.  Measured (profiles/r04/r4k, r4l): 1M@1080p render_fwd 194 -> 188 us, 500k@1080p
         // 217 -> 212 us; at 5M@4K (32400 tiles, ~8 rounds of half tiles per wave slot) the tail is a smaller
         // share and the quadrants' extra staging cost more than it saves (+3..8 us), hence the tile bound.
-        const uint32_t qgroups = min((cus * 2) / 5 + 1, max(1u, groups * (uint32_t)GSR_FWD_TAIL_QUADS / 100u));
+        const uint32_t qgroups = min((cus * 2) / 5 + 1, max(1u, groups * kFwdTailQuadsPct / 100u));
         const uint32_t hgroups = groups - qgroups;
         RenderFwdArgs h = a;
         h.half_tiles = hgroups * 8;
         hipLaunchKernelGGL(render_fwd_hybrid_kernel, dim3(fb + hgroups * 16 + qgroups * 32), dim3(kWave), 0, stream, h);
-    } else if (GSR_FWD_SHARED && quads == 2) {
-        if (a.census)
-            hipLaunchKernelGGL((render_fwd_shared_kernel<true>), dim3(fb + tiles), dim3(2 * kWave), 0, stream, a);
-        else
-            hipLaunchKernelGGL((render_fwd_shared_kernel<false>), dim3(fb + tiles), dim3(2 * kWave), 0, stream, a);
     } else if (a.census)
         hipLaunchKernelGGL((render_fwd_kernel<2, true>), dim3(fb + groups * 16), dim3(kWave), 0, stream, a);
     else if (quads == 4)
@@ -671,7 +512,7 @@ hipError_t launch_render_fwd(const RenderFwdArgs& a, hipStream_t stream, int qua
 // the result is not bitwise reproducible; the record path (bwd_atomic=0) is.  The default since r5f:
 // 1M@1080p 0.7335 -> 0.7320 ms, 5M@4K 2.328 -> 2.224 ms (gauss_reduce gone; profiles/r05/r5f).
 template <bool CENSUS, bool STRIDED, bool ATOMIC>
-__global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(RenderBwdArgs a) {
+__global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a) {
   {
     // One wave per unit = (tile, segment): the entries [start, end) of the tile's list, start a
     // multiple of the checkpoint stride.  Units come longest first (bwd_units_kernel), so the
@@ -739,22 +580,18 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
         const int px = min(tile_x0 + (q & 1) * 8 + lx, a.W - 1), py = min(tile_y0 + (q >> 1) * 8 + ly, a.H - 1);
         const size_t pix = (size_t)py * a.W + px, t = tile_px(tile, q, lane), NT = (size_t)a.gx * a.gy * 256;
         nc[q] = (int)a.img.n_contrib[t];
-        if (GSR_ATTR & 4) {
-            g0[q] = g1[q] = g2[q] = gi[q] = c0[q] = c1[q] = c2[q] = cd[q] = fT[q] = 0.5f;
-        } else {
-            g0[q] = a.dL_dpix[pix];
-            g1[q] = a.dL_dpix[N + pix];
-            g2[q] = a.dL_dpix[2 * N + pix];
-            gi[q] = a.dL_dinvdepth ? a.dL_dinvdepth[pix] : 0.f;
-            c0[q] = a.img.accum[t];
-            c1[q] = a.img.accum[NT + t];
-            c2[q] = a.img.accum[2 * NT + t];
-            cd[q] = a.img.accum[3 * NT + t];
-            fT[q] = a.img.final_T[t];
-        }
+        g0[q] = a.dL_dpix[pix];
+        g1[q] = a.dL_dpix[N + pix];
+        g2[q] = a.dL_dpix[2 * N + pix];
+        gi[q] = a.dL_dinvdepth ? a.dL_dinvdepth[pix] : 0.f;
+        c0[q] = a.img.accum[t];
+        c1[q] = a.img.accum[NT + t];
+        c2[q] = a.img.accum[2 * NT + t];
+        cd[q] = a.img.accum[3 * NT + t];
+        fT[q] = a.img.final_T[t];
         // blend state at `start`: the forward's checkpoint (gsr_common.h), or the empty state
         const float* ck = a.ckpt + (size_t)((range.x + (uint32_t)start) / kCkStride) * kCkFloats + lane;
-        const bool has_ck = start > 0 && !(GSR_ATTR & 2);
+        const bool has_ck = start > 0;
         k0[q] = has_ck ? ck[(0 * 4 + q) * 64] : 1.f;
         k1[q] = has_ck ? ck[(1 * 4 + q) * 64] : 0.f;
         k2[q] = has_ck ? ck[(2 * 4 + q) * 64] : 0.f;
@@ -805,16 +642,16 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
     unsigned long long c_staged = 0, c_eval = 0, c_alpha = 0, c_red = 0, c_idle = 0;  // CENSUS only
     // The ten per-entry sums stay zero between entries (reset after each reduction), so an entry
     // whose first quadrants are inactive does not materialise zeros (10 VALU) before accumulating.
-    uint32_t ent_next = GSR_PF_ENTRY && start + lane < end ? a.gid_sorted[range.x + start + lane] : 0u;
+    uint32_t ent_next = start + lane < end ? a.gid_sorted[range.x + start + lane] : 0u;  // the next batch's entry
     for (int b0 = start; b0 < end; b0 += kBatch) {
         const bool has = b0 + lane < end;
         if (CENSUS) c_staged += (unsigned long long)min(kBatch, end - b0);
         uint32_t qm = 0, e = 0;
         float ca = 0.f, cb = 0.f, cc = 0.f, o = 0.f;  // this lane's entry: raw conic and opacity, for the flush
         if (has) {
-            // Gaussian << 4 | quadrant mask (GSR_PF_ENTRY: loaded during the previous batch)
-            const uint32_t ent = GSR_PF_ENTRY ? ent_next : a.gid_sorted[range.x + b0 + lane];
-          if (!GSR_BLEND_MASK || (ent & kEntryMask)) {  // (blend mask: an entry no pixel blended is not walked)
+            // Gaussian << 4 | quadrant mask (loaded during the previous batch)
+            const uint32_t ent = ent_next;
+          if (ent & kEntryMask) {  // (blend mask: an entry no pixel blended is not walked)
             const float4* rec = a.rec + (size_t)kRecRows * (ent >> kEntryMaskBits);
             const float4 v0 = rec[0], v1 = rec[1], v2 = rec[2];
             if (ATOMIC) {
@@ -822,7 +659,7 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
             } else {
                 const float4 v3 = rec[3];
                 // this instance's emission index (row 3: tile rectangle [and first emission])
-                const uint32_t first = GSR_REC_START_GATHER ? a.rec_start[ent >> kEntryMaskBits] : __float_as_uint(v3.w);
+                const uint32_t first = a.rec_start[ent >> kEntryMaskBits];
                 e = first + (tty - __float_as_uint(v3.y)) * __float_as_uint(v3.z) + (ttx - __float_as_uint(v3.x));
             }
             s_xy[lane] = make_float4(v0.x, v0.y, v1.y, v1.z);
@@ -835,7 +672,7 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
             s_cq[lane] = stage_conic(v0, v1, qm);
           }
         }
-        if (GSR_PF_ENTRY && b0 + kBatch + lane < end) ent_next = a.gid_sorted[range.x + b0 + kBatch + lane];
+        if (b0 + kBatch + lane < end) ent_next = a.gid_sorted[range.x + b0 + kBatch + lane];
         unit_sync();
         unsigned long long todo = __ballot(qm != 0);
         unsigned long long written = 0;
@@ -923,20 +760,20 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
                 s_wgid[slot] = e;
                 s_wj[slot] = (uint32_t)lane;
                 // the Gaussian has a gradient (gauss_live lists it); OR is order-free
-                if (!(GSR_ATTR & 8)) (void)atomicOr(a.touched + (e >> 5), 1u << (e & 31u));
+                (void)atomicOr(a.touched + (e >> 5), 1u << (e & 31u));
             }
             unit_sync();
             // one wave instruction per four listed entries: lane 16 k + v adds value v of entry k
             const int nw = __popcll(written), sub = lane >> 4, v = lane & 15;
             for (int k0 = 0; k0 < nw; k0 += 4) {  // uniform
                 const int k = k0 + sub;
-                if (k < nw && v < 10 && !(GSR_ATTR & 16)) {
+                if (k < nw && v < 10) {
                     const int j = (int)s_wj[k];
                     const float val = reinterpret_cast<const float*>(s_acc)[(v >> 2) * (4 * kBatch) + j * 4 + (v & 3)];
                     (void)atomicAdd(a.acc + (size_t)s_wgid[k] * (4 * kAccRow4) + v, val);  // (no return: fire and forget)
                 }
             }
-        } else if (has && content && !(GSR_ATTR & 1)) {
+        } else if (has && content) {
             (void)atomicOr(reinterpret_cast<uint32_t*>(a.recs.flag) + (e >> 5), 1u << (e & 31u));
             float4 ra = make_float4(0.f, 0.f, 0.f, 0.f), rb = ra;
             float2 rc = make_float2(0.f, 0.f);
@@ -951,16 +788,11 @@ __global__ void __launch_bounds__(64) GSR_BWD_OCCUPANCY render_bwd_kernel(Render
                                  -0.5f * (float)a.H * o * (cc * B.y + cb * B.x), s9, -0.5f * o * B.w);
                 rc = make_float2(-0.5f * o * B.z, -0.5f * o * s8);
             }
-            if (GSR_REC_AOS) {  // one 48-byte record (a, b, c + pad at recs.a + 0/1/2): one address, full-width stores
-                float4* r = a.recs.a + (size_t)kRecAB * e;
-                r[0] = ra;
-                r[1] = rb;
-                r[2] = make_float4(rc.x, rc.y, 0.f, 0.f);
-            } else {
-                a.recs.a[e] = ra;
-                a.recs.b[e] = rb;
-                a.recs.c[e] = rc;
-            }
+            // one 48-byte record (a, b, c + pad at recs.a + 0/1/2): one address, full-width stores
+            float4* r = a.recs.a + (size_t)kRecAB * e;
+            r[0] = ra;
+            r[1] = rb;
+            r[2] = make_float4(rc.x, rc.y, 0.f, 0.f);
         }
         unit_sync();
     }

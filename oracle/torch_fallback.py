@@ -101,8 +101,10 @@ def preprocess(means3D, opacities, viewmatrix, projmatrix, campos, tanfovx, tanf
     Pm = projmatrix.detach().reshape(-1).to(F32)
     cp = campos.detach().reshape(-1).to(F32)
     gx, gy = (W + BLOCK - 1) // BLOCK, (H + BLOCK - 1) // BLOCK
-    fx, fy = W / (2.0 * float(tanfovx)), H / (2.0 * float(tanfovy))
-    fx, fy = float(_f(fx)), float(_f(fy))
+    # focal = W / (2 tan(fov/2)) in float32, as the reference computes it (CR/rasterizer_impl.cu:256-257;
+    # gsr_oracle.c forward): the double quotient rounded once differs by an ulp on some frames, which moved
+    # two radii and 6 instances at 1M@1080p
+    fx, fy = float(_f(W) / (_f(2.0) * _f(tanfovx))), float(_f(H) / (_f(2.0) * _f(tanfovy)))
     pv = _xform(means3D, V, (0, 1, 2))
     front = pv[2].detach() > 0.2  # in_frustum; culled Gaussians get a harmless depth so autograd stays finite
     pv[2] = torch.where(front, pv[2], torch.ones_like(pv[2]))

@@ -89,3 +89,29 @@ def test_tile_sample_renders_a_subset():
     assert 0 < half["rendered_instances"] < full["rendered_instances"]
     assert none["rendered_instances"] == 0
     assert set(full["timings"]) == {"preprocess", "binning", "render", "preprocess_backward"}
+
+
+@pytest.mark.parametrize("cfg", ["500k_1080p_sh3", "1m_1080p_sh3"])
+def test_fullsize_integers_match_oracle(cfg):
+    """The CPU baseline's workload is the GPU's: at BASELINE's full 1080p sizes the fallback's radii, tile
+    rectangles (hence num_rendered) and sorted tile lists equal the f32 C oracle's, which the GPU's equal
+    (test_gpu_fullsize.py).  (The focal length is formed in float32 as the reference forms it; a double
+    quotient rounded once moved two radii and 6 instances at 1M.)"""
+    scene, cam = syn.config_scene(cfg, seed=0)
+    with torch.no_grad():
+        pre = tf.preprocess(scene.means3D, scene.opacities, cam.viewmatrix, cam.projmatrix, cam.campos, cam.tanfovx,
+                            cam.tanfovy, cam.height, cam.width, shs=scene.shs, sh_degree=scene.sh_degree,
+                            scales=scene.scales, rotations=scene.rotations)
+        point_list, starts, counts = tf.binning(pre)
+    inp = dict(bg=torch.zeros(3), means3D=scene.means3D, opacities=scene.opacities, shs=scene.shs,
+               sh_degree=scene.sh_degree, scales=scene.scales, rotations=scene.rotations, colors_precomp=None,
+               cov3D_precomp=None, viewmatrix=cam.viewmatrix, projmatrix=cam.projmatrix, campos=cam.campos,
+               tanfovx=cam.tanfovx, tanfovy=cam.tanfovy, H=cam.height, W=cam.width, scale_modifier=1.0,
+               antialiasing=False)
+    ref = C.run_oracle(inp, nthreads=8)
+    np.testing.assert_array_equal(pre["radii"].numpy(), ref.radii.astype(np.int64))
+    assert int(counts.sum()) == ref.num_rendered
+    rb = ref.handle.binning()
+    np.testing.assert_array_equal(point_list.numpy(), rb["point_list"].astype(np.int64))
+    er = rb["ranges"].astype(np.int64)
+    np.testing.assert_array_equal(counts.numpy(), er[:, 1] - er[:, 0])
