@@ -259,11 +259,10 @@ void carve_recs(char* base, size_t R, size_t P, gsr::GradRecs* recs, gsr::GradRe
         recs->c = reinterpret_cast<float2*>(r48 + 2);
     }
     recs->flag = nullptr;  // in the binning buffer (BinningState::rec_flag)
-    // (per Gaussian for gauss_reduce, per live-list position for the atomic backward's gauss_live)
-    const size_t ns = std::max(P, (size_t)kLiveShards * live_list_cap((uint32_t)P));
-    sums->a = c.take<float4>(ns);
-    sums->b = c.take<float4>(ns);
-    sums->c = c.take<float2>(ns);
+    // (per Gaussian, gauss_reduce's; the atomic backward reads its accumulator rows instead)
+    sums->a = c.take<float4>(P);
+    sums->b = c.take<float4>(P);
+    sums->c = c.take<float2>(P);
     sums->flag = nullptr;
     // the Gaussians with a gradient (gauss_reduce appends, gauss_bwd walks), kLiveShards shards
     *live = c.take<uint32_t>((size_t)kLiveShards * live_list_cap((uint32_t)P));
@@ -280,7 +279,7 @@ constexpr uint32_t kFusedFillBlocks = 256;  // one-wave fill blocks in render_bw
 // screen-averaged opacity mass reaches this value get keys and are sorted; 0 = off.  Capacity-hinted
 // forwards with the fused scan only.
 // "bwd_atomic": the render backward adds each instance's sums into per-Gaussian rows with float atomics
-// (render.hip ATOMIC) and gauss_live lists the touched Gaussians, instead of per-instance records summed
+// (render.hip ATOMIC) and gauss_bwd lists the touched Gaussians itself, instead of per-instance records summed
 // by gauss_reduce (deterministic).  The forward zeroes the rows when the option is on at forward time and
 // marks its buffer (geom_mark below); a backward adds atomically iff the option is on and its buffer is marked.
 constexpr uint32_t kFwdFillBlocks = 256;  // one-wave blocks zeroing the accumulators in render_fwd's launch (a multiple of 8)
@@ -1359,8 +1358,7 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
         HIP_TRY(launch_gauss_live_views(P, geom.touched, geom.acc, radii, geom.clamped, sums, flags, stream),
                 "gauss_live_views");
     } else if (atomic) {
-        StageScope sc(ST_GAUSS_REDUCE, stream);
-        HIP_TRY(launch_gauss_live(P, geom.touched, geom.acc, sums, live, live_count, stream), "gauss_live");
+        // (nothing between render_bwd and gauss_bwd: gauss_bwd lists the touched Gaussians itself)
     } else {
         StageScope sc(ST_GAUSS_REDUCE, stream);
         HIP_TRY(launch_gauss_reduce(P, geom, recs, sums, flags, radii, live, live_count, stream),
@@ -1383,7 +1381,6 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
         ga.viewmatrix = viewmatrix; ga.projmatrix = projmatrix; ga.campos = campos;
         ga.tan_fovx = tan_fovx; ga.tan_fovy = tan_fovy; ga.focal_x = focal_x; ga.focal_y = focal_y;
         ga.antialiasing = antialiasing; ga.radii = radii; ga.geom = geom; ga.sums = sums;
-        ga.sums_by_list = atomic ? 1 : 0;  // (gauss_live moved the rows' sums to list order)
         ga.have_invdepth = dL_dinvdepths != nullptr;
         ga.dL_dmean2D = dL_dmean2D; ga.dL_dconic = dL_dconic; ga.dL_dopacity = dL_dopacity; ga.dL_dcolor = dL_dcolor;
         ga.dL_dinvdepth = dL_dinvdepth; ga.dL_dmean3D = dL_dmean3D; ga.dL_dcov3D = dL_dcov3D;
@@ -1398,6 +1395,10 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
         ga.live = live;
         ga.live_count = live_count;
         ga.live_cap = live_list_cap((uint32_t)P);
+        if (atomic) {  // the sums are the accumulator rows of the touched Gaussians (render_bwd ATOMIC)
+            ga.touched = geom.touched;
+            ga.acc = geom.acc;
+        }
         HIP_TRY(launch_gauss_bwd(ga, stream), "gauss_bwd");
     }
     if (int rc = check_debug(debug, stream, "gauss_bwd")) return rc;

@@ -217,87 +217,10 @@ hipError_t launch_gauss_reduce(int P, const GeomState& g, const GradRecs& recs, 
     return hipGetLastError();
 }
 
-// ---- 1b. atomic backward: the live list from the touched bits ----------------------
+// ---- 1b. atomic backward ----------------------------------------------------------
 // render_bwd ("bwd_atomic") added every instance's sums into its Gaussian's accumulator row and set
-// the Gaussian's bit; this lists the Gaussians with a bit (gauss_bwd's live list), moves their sums to
-// list order and clears the rows and words it read, so the next backward of the same forward starts
-// from zero.
-// One wave per run of kLiveGroups x 64 consecutive Gaussians, one lane per Gaussian of each 64-group:
-// the wave reads its touched words, appends the run's touched Gaussians to shard (wave % kLiveShards)
-// with ONE atomic, and each touched lane moves its row's sums to its list position and zeroes the row.
-// A chain of dependent round trips (word -> rows + counter -> stores) over tiny data: 15.6k one-group waves
-// at 1M@1080p need two rounds of the 32 wave slots per CU, so a wave carries four groups and one counter
-// atomic per run: 15.7 -> 12.8 us at 1M, 26.2 -> 22.0 us at 5M@4K, step -2.8 / -8 us (r5m; two groups: 14.4 /
-// 23.2 us).  (r5i / r5j's runs of several groups had measured slower only because their row arrays, written
-// under a branch, were kept in scratch memory; one lane per 32-bit word walking its bits: 21.5 us, r5f.)
-// live_list_cap bounds a shard for runs of up to kLiveGroupsMax groups.
-constexpr int kLiveGroups = 4;
-static_assert(kLiveGroups >= 1 && kLiveGroups <= (int)kLiveGroupsMax, "live_list_cap bounds runs of kLiveGroupsMax");
-__global__ void __launch_bounds__(64) gauss_live_kernel(int P, uint32_t* __restrict__ touched, float4* __restrict__ acc,
-                                                        GradRecs sums, uint32_t* __restrict__ live,
-                                                        uint32_t* __restrict__ live_count, uint32_t live_cap) {
-    const int lane = threadIdx.x;
-    const uint32_t g0 = blockIdx.x * (64u * kLiveGroups) + (uint32_t)lane;  // this lane's Gaussian in group 0
-    uint32_t w[kLiveGroups];
-#pragma unroll
-    for (int j = 0; j < kLiveGroups; j++) {
-        const uint32_t g = g0 + 64u * j;
-        w[j] = g < (uint32_t)P ? touched[g >> 5] : 0u;  // (two words per group, each read by 32 lanes)
-    }
-    unsigned long long m[kLiveGroups];
-    uint32_t off[kLiveGroups], total = 0;
-    const unsigned long long below = (1ull << lane) - 1ull;
-#pragma unroll
-    for (int j = 0; j < kLiveGroups; j++) {
-        m[j] = __ballot((w[j] >> (lane & 31)) & 1u);
-        off[j] = total + (uint32_t)__popcll(m[j] & below);  // this lane's place in the run, if listed
-        total += (uint32_t)__popcll(m[j]);
-    }
-    if (total == 0) return;  // uniform
-    // (initialised whole: arrays written only under a branch were kept in scratch memory, r5j's G > 1 builds)
-    float4 ra[kLiveGroups], rb[kLiveGroups], rc[kLiveGroups];
-#pragma unroll
-    for (int j = 0; j < kLiveGroups; j++) ra[j] = rb[j] = rc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int j = 0; j < kLiveGroups; j++) {
-        if ((m[j] >> lane) & 1ull) {
-            const float4* row = acc + (size_t)(g0 + 64u * j) * kAccRow4;
-            ra[j] = row[0];
-            rb[j] = row[1];
-            rc[j] = row[2];
-        }
-    }
-    const uint32_t shard = blockIdx.x % kLiveShards;
-    uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(&live_count[shard * kLiveCntStride], total);
-#pragma unroll
-    for (int j = 0; j < kLiveGroups; j++)  // (after every lane's read of the words: the ballots used them)
-        if ((lane & 31) == 0 && w[j]) touched[(g0 + 64u * j) >> 5] = 0u;
-    base = (uint32_t)__shfl((int)base, 0);
-    const size_t pos0 = (size_t)shard * live_cap + base;
-#pragma unroll
-    for (int j = 0; j < kLiveGroups; j++) {
-        if ((m[j] >> lane) & 1ull) {
-            const uint32_t g = g0 + 64u * j;
-            const size_t pos = pos0 + off[j];
-            live[pos] = g;
-            sums.a[pos] = ra[j];
-            sums.b[pos] = rb[j];
-            sums.c[pos] = make_float2(rc[j].x, rc[j].y);
-            float4* row = acc + (size_t)g * kAccRow4;
-            row[0] = row[1] = row[2] = make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-    }
-}
-
-hipError_t launch_gauss_live(int P, uint32_t* touched, float4* acc, const GradRecs& sums, uint32_t* live,
-                             uint32_t* live_count, hipStream_t stream) {
-    if (P <= 0) return hipSuccess;
-    const size_t blocks = (((size_t)P + 63) / 64 + kLiveGroups - 1) / kLiveGroups;
-    hipLaunchKernelGGL(gauss_live_kernel, dim3((uint32_t)blocks), dim3(64), 0, stream, P, touched, acc, sums, live,
-                       live_count, live_list_cap((uint32_t)P));
-    return hipGetLastError();
-}
+// the Gaussian's touched bit; gauss_bwd_touched_kernel (section 3) reads the rows of the touched
+// Gaussians and restores them to zero, gauss_live_views (below) fills a view block from them.
 
 // The atomic backward into a view block (gsr_rasterize_backward_screen, multi-GPU view exchange): one lane
 // per Gaussian writes its dense sums -- its accumulator row if its touched bit is set (the row then zeroed),
@@ -658,27 +581,19 @@ constexpr int kGbShRows = 32;
 // Live-list entries per gauss_bwd wave (one per lane).
 constexpr int kGbListE = 64;
 // LIST: lane i of the grid takes entry i of the live list (the Gaussians with a gradient,
-// gauss_reduce / gauss_live); the outputs were zero-filled, so no other row is touched.  At
+// gauss_reduce); the outputs were zero-filled, so no other row is touched.  At
 // 1M@1080p that is ~2000 waves instead of 15625.
 // The workgroup is one wave: the SH pass's LDS hand-offs need only the wave's own in-order LDS,
 // not __syncthreads, whose fence also waits for every store the wave has issued.
 __device__ __forceinline__ void gb_sync() {
     wave_lds_sync();
 }
-template <int SH_MODE, bool LIST>
-__device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const uint32_t blk) {
-    __shared__ __attribute__((aligned(16))) float s_sh[SH_MODE != kShGlobal ? kGbShRows * kShStride : 4];
-    const int lane = threadIdx.x;
-    const int g0 = (int)blk * 64;
-    int idx = g0 + lane;
-    size_t lpos = 0;  // LIST: this lane's position in the live list (sums_by_list: where its sums are)
-    if constexpr (LIST) {  // block b: entries [E (b / shards), +E) of shard b % shards, E = kGbListE
-        const uint32_t shard = blk % kLiveShards, k0 = (blk / kLiveShards) * kGbListE;
-        const uint32_t n = a.live_count[shard * kLiveCntStride];
-        if (k0 >= n) return;  // uniform: past the shard's list (the grid is sized for the worst case)
-        idx = lane < kGbListE && k0 + lane < n ? (int)a.live[(size_t)shard * a.live_cap + k0 + lane] : a.P;
-        lpos = (size_t)shard * a.live_cap + k0 + lane;
-    }
+// The rows of one wave: Gaussians g0 + lane (dense), or each lane's idx (LIST; a.P: none).  TOUCHED (the
+// atomic backward): the sums are the accumulator rows render_bwd added into, read and zeroed here.
+constexpr int kGbShFloats = kGbShRows * kShStride;  // one wave's SH staging (LDS)
+template <int SH_MODE, bool LIST, bool TOUCHED>
+__device__ __forceinline__ void gauss_bwd_rows(const GaussBwdArgs& a, const int g0, const int idx, float* s_sh) {
+    const int lane = threadIdx.x & 63;
     const int nvalid = min(64, a.P - g0);
     const int M = a.M;
 
@@ -699,13 +614,26 @@ __device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const uin
     int rad = 0;
     if (valid) {
         rad = a.radii[idx];
-        const size_t si = LIST && a.sums_by_list ? lpos : (size_t)idx;  // (atomic backward: list order, gauss_live)
-        sa = a.sums.a[si];
-        sb = a.sums.b[si];
-        sc = a.sums.c[si];
+        if constexpr (TOUCHED) {
+            const float4* row = a.acc + (size_t)idx * kAccRow4;
+            sa = row[0];
+            sb = row[1];
+            const float4 c4 = row[2];
+            sc = make_float2(c4.x, c4.y);
+        } else {  // (record path: gauss_reduce's per-Gaussian sums)
+            sa = a.sums.a[idx];
+            sb = a.sums.b[idx];
+            sc = a.sums.c[idx];
+        }
     }
     const bool any_grad = (sa.x != 0.f) | (sa.y != 0.f) | (sa.z != 0.f) | (sa.w != 0.f) | (sb.x != 0.f) |
                           (sb.y != 0.f) | (sb.z != 0.f) | (sb.w != 0.f) | (sc.x != 0.f) | (sc.y != 0.f);
+    if constexpr (TOUCHED) {  // the row back to zero for the next backward of the same forward (its sums are read)
+        if (valid) {
+            float4* row = a.acc + (size_t)idx * kAccRow4;
+            row[0] = row[1] = row[2] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    }
     const bool visible = valid && rad > 0 && any_grad;
     if (valid && !visible) {
         if (!a.sparse) {  // (sparse: the outputs were zero-filled beforehand)
@@ -841,7 +769,53 @@ __device__ __forceinline__ void gauss_bwd_block(const GaussBwdArgs& a, const uin
 // counter and exit (a grid-strided walk over the virtual blocks measured no better).
 template <int SH_MODE, bool LIST = false>
 __global__ void __launch_bounds__(64) gauss_bwd_kernel(GaussBwdArgs a) {
-    gauss_bwd_block<SH_MODE, LIST>(a, blockIdx.x);
+    __shared__ __attribute__((aligned(16))) float s_sh[SH_MODE != kShGlobal ? kGbShFloats : 4];
+    const int lane = threadIdx.x;
+    const uint32_t blk = blockIdx.x;
+    if constexpr (LIST) {  // block b: entries [E (b / shards), +E) of shard b % shards, E = kGbListE
+        const uint32_t shard = blk % kLiveShards, k0 = (blk / kLiveShards) * kGbListE;
+        const uint32_t n = a.live_count[shard * kLiveCntStride];
+        if (k0 >= n) return;  // uniform: past the shard's list (the grid is sized for the worst case)
+        const int idx = lane < kGbListE && k0 + lane < n ? (int)a.live[(size_t)shard * a.live_cap + k0 + lane] : a.P;
+        gauss_bwd_rows<SH_MODE, true, false>(a, (int)blk * 64, idx, s_sh);
+    } else {
+        gauss_bwd_rows<SH_MODE, false, false>(a, (int)blk * 64, (int)blk * 64 + lane, s_sh);
+    }
+}
+
+// The atomic backward's per-Gaussian pass (bwd_atomic): a workgroup of kTouchedWaves waves per run of
+// 64 x kTouchedWaves consecutive Gaussians reads the run's touched bits (render_bwd set them), lists the
+// touched Gaussians in LDS, clears the words, and wave w runs the live-list backward over list entries
+// [64 w, 64 w + 64) -- the waves past the list exit -- with the sums read from, and the rows then zeroed in,
+// the accumulator.  One kernel where a gauss_live pass listed the Gaussians into shards and moved their sums
+// to list order for the list kernel: 1M@1080p -6.8 us per step, 500k -9.3 (r7e, four interleaved rounds;
+// one wave per run of 256 serialising its passes: -7.0 / -3.4).
+constexpr int kTouchedWaves = 4;
+template <int SH_MODE>
+__global__ void __launch_bounds__(64 * kTouchedWaves) gauss_bwd_touched_kernel(GaussBwdArgs a) {
+    __shared__ __attribute__((aligned(16))) float s_sh[kTouchedWaves][SH_MODE != kShGlobal ? kGbShFloats : 4];
+    __shared__ uint32_t s_list[64 * kTouchedWaves];
+    __shared__ uint32_t s_cnt[kTouchedWaves];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t g = blockIdx.x * (64u * kTouchedWaves) + threadIdx.x;
+    const uint32_t w = g < (uint32_t)a.P ? a.touched[g >> 5] : 0u;  // (each word read by 32 lanes)
+    const unsigned long long m = __ballot((w >> (lane & 31)) & 1u);
+    if (lane == 0) s_cnt[wave] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t base = 0, total = 0;
+#pragma unroll
+    for (int k = 0; k < kTouchedWaves; k++) {
+        const uint32_t c = s_cnt[k];
+        base += k < wave ? c : 0u;
+        total += c;
+    }
+    if ((m >> lane) & 1ull) s_list[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = g;
+    if ((lane & 31) == 0 && w) a.touched[g >> 5] = 0u;  // (after the ballot read it)
+    __syncthreads();
+    const uint32_t k0 = 64u * (uint32_t)wave;
+    if (k0 >= total) return;  // uniform per wave
+    const int idx = k0 + (uint32_t)lane < total ? (int)s_list[k0 + lane] : a.P;
+    gauss_bwd_rows<SH_MODE, true, true>(a, 0, idx, s_sh[wave]);
 }
 
 // ---- 4. the same backward over several views' summed render gradients -----------
@@ -1372,6 +1346,17 @@ hipError_t launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t stream) {
     const bool lds_ok = a.shs && a.dL_dsh && a.M == 16 && (!a.dc || a.dL_ddc) &&
                         ((reinterpret_cast<uintptr_t>(a.shs) & 15) == 0) &&
                         ((reinterpret_cast<uintptr_t>(a.dL_dsh) & 15) == 0);
+    if (a.touched) {  // the atomic backward: runs of touched Gaussians (outputs zero-filled)
+        const dim3 tgrid((uint32_t)(((size_t)a.P + 64 * kTouchedWaves - 1) / (64 * kTouchedWaves))),
+            tblock(64 * kTouchedWaves);
+        if (lds_ok && a.dc)
+            hipLaunchKernelGGL((gauss_bwd_touched_kernel<kShLdsSplit>), tgrid, tblock, 0, stream, a);
+        else if (lds_ok)
+            hipLaunchKernelGGL((gauss_bwd_touched_kernel<kShLdsCombined>), tgrid, tblock, 0, stream, a);
+        else
+            hipLaunchKernelGGL((gauss_bwd_touched_kernel<kShGlobal>), tgrid, tblock, 0, stream, a);
+        return hipGetLastError();
+    }
     if (a.live && a.sparse) {  // the live list: kLiveShards x live_cap entries at most
         const uint32_t worst = kLiveShards * ((a.live_cap + kGbListE - 1) / kGbListE);
         const dim3 lgrid(worst);

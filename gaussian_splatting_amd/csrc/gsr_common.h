@@ -122,8 +122,8 @@ struct GeomState {
     // Atomic backward ("bwd_atomic" option, gsr_common.h "Per-Gaussian accumulators"): the render
     // backward adds each (tile, Gaussian) instance's ten reduced sums straight into the Gaussian's row
     // and sets its bit in `touched`.  Both are zeroed by the forward (fill blocks in render_fwd's launch)
-    // and restored to zero by the backward that consumed them (gauss_live: the bits; gauss_bwd: the
-    // rows), so any number of backwards of one forward start from zero.
+    // and restored to zero by the backward that consumed them (gauss_bwd_touched_kernel, or
+    // gauss_live_views for a view block), so any number of backwards of one forward start from zero.
     float4* acc;                // [P][kAccRow4]: (dcolour, dinvdepth), (dmean2D, dopacity, dconic.b), (dconic.a, .c, 0, 0), pad
     uint32_t* touched;          // [touched_words(P)] bit g: Gaussian g has a gradient term
     // Near-first binning ("near_mass" option, binning.hip "Near-first binning"): only the Gaussians in
@@ -244,17 +244,16 @@ struct GradRecs {
 // alone and skips the rest.  Whether an entry has a gradient term depends on the geometry only,
 // not on the upstream gradient, so a second backward of the same forward sets the same bits.
 
-// The live list (backward scratch): the Gaussians with a gradient, appended by gauss_reduce for
-// the sparse gauss_bwd.  Sharded by reduction workgroup (one counter per 128-byte line): a single
-// counter took 15625 returning atomics in a row at 1M Gaussians (gauss_reduce 62 -> 201 us).
+// The live list (backward scratch): the Gaussians with a gradient, appended by gauss_reduce (record
+// path) and views_live for the sparse gauss_bwd.  Sharded by the appending wave (one counter per
+// 128-byte line): a single counter took 15625 returning atomics in a row at 1M Gaussians
+// (gauss_reduce 62 -> 201 us).
 constexpr int kLiveShards = 64;
 constexpr int kLiveCntStride = 32;  // uint32 per counter line
-// Entries per shard.  A kernel appending runs of up to 64 x kLiveGroupsMax consecutive Gaussians to
-// shard (run index) % kLiveShards (gauss_live: one run per wave) fills a shard with at most this many;
-// so does gauss_reduce's one 64-Gaussian run per wave (a multiple of 64 rounded up to 64 x G is >= it).
-constexpr uint32_t kLiveGroupsMax = 8;
+// Entries per shard: the appenders' wave w adds at most its run of 64 consecutive Gaussians to shard
+// w % kLiveShards, so a shard holds at most ceil(runs / kLiveShards) x 64.
 __host__ __device__ inline uint32_t live_list_cap(uint32_t P) {
-    constexpr uint32_t run = 64u * kLiveGroupsMax;
+    constexpr uint32_t run = 64u;
     const uint32_t runs = (P + run - 1) / run;
     return (runs + kLiveShards - 1) / kLiveShards * run;
 }

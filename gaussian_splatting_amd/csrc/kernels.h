@@ -128,8 +128,7 @@ struct GaussBwdArgs {
     int antialiasing;
     const int* radii;
     GeomState geom;
-    GradRecs sums;  // per Gaussian: summed render gradients (gauss_reduce_kernel), or per live-list position
-    int sums_by_list;  // 1: sums indexed by live-list position (the atomic backward's gauss_live_kernel)
+    GradRecs sums;  // per Gaussian: summed render gradients (gauss_reduce_kernel; the record path)
     int have_invdepth;
     float* dL_dmean2D;    // [P,3]
     float* dL_dconic;     // [P,4] or null
@@ -146,6 +145,8 @@ struct GaussBwdArgs {
     const uint32_t* live;        // sparse: the Gaussians with a gradient (gauss_reduce), or null
     const uint32_t* live_count;  // per shard: its length (device), kLiveCntStride apart
     uint32_t live_cap;           // entries per shard (live_list_cap)
+    uint32_t* touched;           // atomic backward (sparse): the touched bits render_bwd set, or null; cleared here
+    float4* acc;                 // with touched: the accumulator rows (the sums), zeroed after reading
 };
 
 hipError_t launch_zero_fill(const FillArgs& f, hipStream_t stream);
@@ -516,10 +517,6 @@ hipError_t launch_ssim_bwd(int planes, int H, int W, const float* img1, const fl
 hipError_t launch_gauss_reduce(int P, const GeomState& g, const GradRecs& recs, const GradRecs& sums,
                                uint32_t* flags, const int* radii, uint32_t* live, uint32_t* live_count,
                                hipStream_t stream);
-// atomic backward: the live list from the touched bits (which it re-zeroes), each listed Gaussian's sums moved
-// from its accumulator row (zeroed) to `sums` at its list position -- instead of gauss_reduce
-hipError_t launch_gauss_live(int P, uint32_t* touched, float4* acc, const GradRecs& sums, uint32_t* live,
-                             uint32_t* live_count, hipStream_t stream);
 // atomic screen-space backward: the view block's dense sums (a touched Gaussian's row, zeroed after; zeros
 // otherwise) and flag words (visible, SH clamp bits) from the touched bits (re-zeroed) -- gauss_reduce's view
 // block output without records

@@ -81,7 +81,7 @@ __device__ __forceinline__ float4 stage_conic(float4 v0, float4 v1, uint32_t qm)
 __device__ __forceinline__ float splat_alpha(float p2, float opacity, float& G) {
     G = __builtin_amdgcn_exp2f(p2);  // raw v_exp_f32 (+inf for a large positive p2: masked below)
     const float alpha = fminf(0.99f, opacity * G);
-    return (p2 <= 0.f) & (alpha >= 1.0f / 255.0f) ? alpha : 0.f;  // one mask, one select
+    return ((p2 <= 0.f) & (alpha >= 1.0f / 255.0f)) ? alpha : 0.f;  // one mask, one select
 }
 
 // ---------------------------------------------------------------------------
@@ -759,7 +759,7 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a) {
                 const int slot = __popcll(written & ((1ull << lane) - 1ull));
                 s_wgid[slot] = e;
                 s_wj[slot] = (uint32_t)lane;
-                // the Gaussian has a gradient (gauss_live lists it); OR is order-free
+                // the Gaussian has a gradient (gauss_bwd lists it); OR is order-free
                 (void)atomicOr(a.touched + (e >> 5), 1u << (e & 31u));
             }
             unit_sync();

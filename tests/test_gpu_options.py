@@ -145,7 +145,7 @@ def test_seg_ck_set_around_forward_only(seg_ck, case_name):
 @pytest.mark.parametrize("case_name", ["sh3_scalerot", "lists_4k_8k"])
 def test_atomic_backward_repeats(case_name):
     """bwd_atomic: the forward zeroes the accumulator rows and touched bits, and each backward restores
-    what it used to zero (gauss_live the bits, gauss_bwd the rows), so three backwards of one forward
+    what it used to zero (gauss_bwd the bits and the rows), so three backwards of one forward
     agree to float rounding of the add order (a row left over would double a Gaussian's gradient);
     a record-path backward of a forward run with the option on equals the record path bitwise, and so
     does a backward with the option on of a forward without it (its buffer is not marked: no rows zeroed)."""
