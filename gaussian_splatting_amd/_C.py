@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import weakref
 from typing import Optional, Tuple
 
 import torch
@@ -147,8 +148,23 @@ def _present(t) -> bool:
     return t is not None and t.numel() != 0 and t.size(0) != 0
 
 
-def rasterize_gaussians(*args) -> Tuple[int, torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor, torch.Tensor,
-                                        torch.Tensor]:
+# The geometry buffers this process's forwards returned, by device address (weak: a freed buffer drops out).
+# A backward given any other tensor at such an address -- a copy, a buffer restored from a checkpoint, a
+# view -- makes the library forget that address's forward state first (include/gsr.h gsr_geom_forget), so
+# the backward takes the record path after writing the record inputs instead of trusting a stale mark.
+_FORWARD_GEOMS: "weakref.WeakValueDictionary[int, torch.Tensor]" = weakref.WeakValueDictionary()
+
+
+def _own_geometry(geomBuffer: torch.Tensor) -> None:
+    if geomBuffer.numel() == 0:
+        return
+    t = _FORWARD_GEOMS.get(geomBuffer.data_ptr())
+    if t is None or t._cdata != geomBuffer._cdata:
+        _lib.load().gsr_geom_forget(geomBuffer.data_ptr())
+
+
+def rasterize_gaussians(*args, no_backward: bool = False) -> Tuple[int, torch.Tensor, torch.Tensor, torch.Tensor,
+                                                                     torch.Tensor, torch.Tensor, torch.Tensor]:
     """RasterizeGaussiansCUDA (rasterize_points.cu:45-146).
 
     Positional arguments, as the pybind function takes them:
@@ -158,6 +174,10 @@ def rasterize_gaussians(*args) -> Tuple[int, torch.Tensor, torch.Tensor, torch.T
     (then the rest coefficients [P,M,3]); see include/gsr.h gsr_rasterize_forward_dc.
 
     Returns ``(num_rendered, color[3,H,W], radii[P] int32, geomBuffer, binningBuffer, imgBuffer, invdepth[1,H,W])``.
+
+    ``no_backward`` (an extension): no backward will follow (an eval / no_grad render), so the forward does not
+    zero the atomic backward's accumulator rows beside its render ("bwd_atomic" 0 for this call; a backward
+    of it would take the record path).
     """
     if len(args) == 21:
         (background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp, viewmatrix,
@@ -209,8 +229,13 @@ def rasterize_gaussians(*args) -> Tuple[int, torch.Tensor, torch.Tensor, torch.T
         _capacity_hint(key, P), ctypes.byref(cap))
     fn = lib.gsr_rasterize_forward_dc if split else lib.gsr_rasterize_forward_ex
     with torch.cuda.device(device):
-        rc = fn(*common_head, *sh_args, *common_tail)
+        if no_backward:
+            with _lib.thread_options(bwd_atomic=0):
+                rc = fn(*common_head, *sh_args, *common_tail)
+        else:
+            rc = fn(*common_head, *sh_args, *common_tail)
     _lib.check(rc, "rasterize_gaussians")
+    _FORWARD_GEOMS[geom.data_ptr()] = geom
     _note_rendered(key, P, nr.value)
     # The binning buffer's layout (its capacity) is recovered by the backward from the buffer's
     # size (include/gsr.h gsr_rasterize_backward_ex), so nothing rides on the tensor object.
@@ -287,6 +312,7 @@ def rasterize_gaussians_backward(*args, out=None):
     ins = _Inputs(device)
     scratch = torch.empty(0, dtype=torch.uint8, device=device)
     rs = _Resizer(scratch)
+    _own_geometry(geomBuffer)
     head = (P, int(degree), M, int(R), ins.req(background, "bg", small=True), W, H, ins.req(means3D, "means3D"))
     sh_args = ((ins.req(dc, "dc"), ins.opt(sh, "sh")) if split else (ins.opt(sh, "sh"),))
     mid = (ins.opt(colors, "colors_precomp"),
@@ -515,6 +541,7 @@ def rasterize_gaussians_backward_screen(*args, view_block: torch.Tensor) -> None
     ins = _Inputs(device)
     scratch = torch.empty(0, dtype=torch.uint8, device=device)
     rs = _Resizer(scratch)
+    _own_geometry(geomBuffer)
     with torch.cuda.device(device):
         rc = lib.gsr_rasterize_backward_screen(
             P, int(degree), M, int(R), ins.req(background, "bg", small=True), W, H, ins.req(means3D, "means3D"),

@@ -96,6 +96,9 @@ SIGNATURES = {
     "gsr_option_set": (_i, [ctypes.c_char_p, _i]),
     "gsr_host_stats": (_i, [ctypes.POINTER(ctypes.c_double), _i, _i]),
     "gsr_option_get": (_i, [ctypes.c_char_p]),
+    "gsr_option_set_thread": (_i, [ctypes.c_char_p, _i]),
+    "gsr_option_clear_thread": (_i, [ctypes.c_char_p]),
+    "gsr_geom_forget": (_i, [_vp]),
     "gsr_last_error": (ctypes.c_char_p, []),
     "gsr_version": (ctypes.c_char_p, []),
     "gsr_build_id": (ctypes.c_char_p, []),
@@ -210,6 +213,25 @@ def option_get(name: str) -> int:
 
 def option_set(name: str, value: int) -> None:
     check(load().gsr_option_set(name.encode(), int(value)), "option_set")
+
+
+class thread_options:
+    """Context manager: options for the library calls THIS thread makes in the block (include/gsr.h
+    gsr_option_set_thread), over the process-wide values; the overrides are cleared on exit (no nesting)."""
+
+    def __init__(self, **values):
+        self.values = values
+
+    def __enter__(self):
+        lib = load()
+        for k, v in self.values.items():
+            check(lib.gsr_option_set_thread(k.encode(), int(v)), "option_set_thread")
+        return self
+
+    def __exit__(self, *exc):
+        lib = load()
+        for k in self.values:
+            lib.gsr_option_clear_thread(k.encode())
 
 
 class options:

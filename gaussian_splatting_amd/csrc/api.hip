@@ -325,7 +325,14 @@ void options_init() {
     });
 }
 
+// Per-thread overrides (gsr_option_set_thread): kOptNone where the process-wide value applies.
+constexpr int kOptNone = INT_MIN;
+thread_local int t_opt[OPT_COUNT] = {kOptNone, kOptNone, kOptNone, kOptNone, kOptNone, kOptNone, kOptNone, kOptNone,
+                                     kOptNone, kOptNone, kOptNone};
+static_assert(OPT_COUNT == 11, "one kOptNone per option above");
+
 int option(int id) {
+    if (t_opt[id] != kOptNone) return t_opt[id];
     options_init();
     return g_opt[id].load(std::memory_order_relaxed);
 }
@@ -364,6 +371,16 @@ void geom_mark(const void* geom_buffer, bool zeroed, bool recs) {
     if (!zeroed && !recs) return;  // (absent = neither)
     if (g_marks.size() >= kGeomMarksMax) g_marks.clear();
     g_marks.push_back(GeomMark{geom_buffer, zeroed, recs});
+}
+
+void geom_forget(const void* geom_buffer) {
+    std::lock_guard<std::mutex> lk(g_mark_mu);
+    for (size_t i = 0; i < g_marks.size(); i++)
+        if (g_marks[i].buf == geom_buffer) {
+            g_marks[i] = g_marks.back();
+            g_marks.pop_back();
+            return;
+        }
 }
 
 GeomMark geom_marked(const void* geom_buffer) {
@@ -553,6 +570,35 @@ int gsr_option_set(const char* name, int value) {
 int gsr_option_get(const char* name) {
     const int i = option_index(name);
     return i < 0 ? -1 : option(i);
+}
+
+int gsr_option_set_thread(const char* name, int value) {
+    g_err[0] = 0;
+    const int i = option_index(name);
+    if (i < 0) return fail(GSR_ERR_ARGUMENT, "option_set_thread: unknown option '%s'", name ? name : "(null)");
+    const OptionSpec& o = kOptions[i];
+    if (value < o.lo || value > o.hi || (i == OPT_FWD_QUADS && value != 2 && value != 4))
+        return fail(GSR_ERR_ARGUMENT, "option_set_thread: %s = %d out of range [%d, %d]", name, value, o.lo, o.hi);
+    t_opt[i] = value;
+    return GSR_OK;
+}
+
+int gsr_option_clear_thread(const char* name) {
+    g_err[0] = 0;
+    if (!name) {
+        for (int i = 0; i < OPT_COUNT; i++) t_opt[i] = kOptNone;
+        return GSR_OK;
+    }
+    const int i = option_index(name);
+    if (i < 0) return fail(GSR_ERR_ARGUMENT, "option_clear_thread: unknown option '%s'", name);
+    t_opt[i] = kOptNone;
+    return GSR_OK;
+}
+
+int gsr_geom_forget(const void* geom_buffer) {
+    g_err[0] = 0;
+    geom_forget(geom_buffer);
+    return GSR_OK;
 }
 
 int gsr_fused_ssim_forward(int B, int CH, int H, int W, float C1, float C2, const float* img1, const float* img2,

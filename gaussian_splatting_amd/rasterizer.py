@@ -5,6 +5,7 @@
 """
 from __future__ import annotations
 
+import threading
 from typing import NamedTuple
 
 import torch
@@ -44,6 +45,10 @@ def rasterize_gaussians(*args):
     raster_settings)`` (vendored, :24-46), or the 3DGS-accel form with ``dc`` before ``sh``."""
     if len(args) not in (9, 10):
         raise TypeError(f"rasterize_gaussians(): expected 9 or 10 arguments, got {len(args)}")
+    # (a render no backward can follow -- grad disabled, or no input requires grad -- skips the atomic backward's
+    # accumulator zeroing; autograd's needs_input_grad cannot tell, it ignores the grad mode)
+    _RasterizeGaussians._no_backward.value = not (torch.is_grad_enabled() and any(
+        isinstance(a, torch.Tensor) and a.requires_grad for a in args[:-1]))
     return _RasterizeGaussians.apply(*args)
 
 
@@ -58,6 +63,8 @@ class _RasterizeGaussians(torch.autograd.Function):
     its value is never read.
     """
 
+    _no_backward = threading.local()
+
     @staticmethod
     def forward(ctx, *args):
         if len(args) == 10:
@@ -69,7 +76,10 @@ class _RasterizeGaussians(torch.autograd.Function):
                 s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, s.image_height, s.image_width)
         tail = (s.sh_degree, s.campos, s.prefiltered, s.antialiasing, s.debug)
         sh_args = (sh,) if dc is None else (dc, sh)
-        num_rendered, color, radii, geom, binning, img, invdepths = _C.rasterize_gaussians(*head, *sh_args, *tail)
+        no_backward = getattr(_RasterizeGaussians._no_backward, "value", False)
+        _RasterizeGaussians._no_backward.value = False  # (set by rasterize_gaussians for this call only)
+        num_rendered, color, radii, geom, binning, img, invdepths = _C.rasterize_gaussians(
+            *head, *sh_args, *tail, no_backward=no_backward)
         ctx.raster_settings = s
         ctx.num_rendered = num_rendered
         ctx.separate_sh = dc is not None

@@ -353,6 +353,19 @@ int gsr_host_stats(double* values, int n, int reset);
  * unknown name or an out-of-range value.  Not synchronised against calls running on other threads. */
 int gsr_option_set(const char* name, int value);
 int gsr_option_get(const char* name);
+/* The same options for calls made on THIS thread only, over the process-wide values (e.g. a forward that no
+ * backward will follow: "bwd_atomic" 0 skips zeroing the atomic backward's accumulator rows -- a backward of
+ * it then takes the record path).  gsr_option_get reports the value in force on the calling thread.
+ * gsr_option_clear_thread(name) drops one override, (NULL) all of them.  Errors as gsr_option_set. */
+int gsr_option_set_thread(const char* name, int value);
+int gsr_option_clear_thread(const char* name);
+
+/* Forget what the library recorded about a geometry buffer's last forward (whether its accumulator rows were
+ * zeroed and its record inputs written).  A buffer the library did not write at that address -- a copy, one
+ * restored from a checkpoint -- must be forgotten before its backward, which then writes the record inputs
+ * and takes the deterministic record path.  (The Python layer calls it for any geometry tensor that is not
+ * the one its forward returned.)  Always GSR_OK. */
+int gsr_geom_forget(const void* geom_buffer);
 
 /* Message of the last error on this thread ("" if none). */
 const char* gsr_last_error(void);

@@ -171,3 +171,66 @@ def test_atomic_backward_repeats(case_name):
         for k, a, b in zip(C.GRAD_NAMES, o, base):
             scale = float(b.abs().max()) or 1.0
             assert float((a - b).abs().max()) <= 1e-5 * scale, (k, float((a - b).abs().max()), scale)
+
+
+def test_foreign_geometry_buffer_takes_record_path():
+    """A geometry tensor the forward did not return (here a view of it: the same address, another tensor) makes
+    the library forget that address's forward state (include/gsr.h gsr_geom_forget, _C._own_geometry): its
+    backward writes the record inputs and takes the deterministic record path -- bitwise the record path's
+    gradients -- instead of trusting the mark of the atomic forward that wrote the address."""
+    from gaussian_splatting_amd import _lib
+
+    case = next(c for c in C.SMALL_CASES if c.name == "sh3_scalerot")
+    inp = C.build(case)
+    gc, gd = C.unit_grads(case.H, case.W)
+    with _lib.options(bwd_atomic=0):
+        ref = C.run_gpu_backward(inp, C.run_gpu_forward(inp), gc, gd)
+    with _lib.options(bwd_atomic=1):
+        fwd = C.run_gpu_forward(inp)
+        nr, color, radii, geom, binning, img, invd = fwd
+        view = geom[:]
+        assert view.data_ptr() == geom.data_ptr() and view._cdata != geom._cdata
+        got = C.run_gpu_backward(inp, (nr, color, radii, view, binning, img, invd), gc, gd)
+        # the address is forgotten for the original tensor too: the record path again
+        again = C.run_gpu_backward(inp, fwd, gc, gd)
+    torch.cuda.synchronize()
+    for a, b, r in zip(got, again, ref):
+        assert torch.equal(a, r) and torch.equal(b, r)
+
+
+def test_no_backward_forward():
+    """_C.rasterize_gaussians(..., no_backward=True) (an eval render: rasterizer.py passes it when grad is off or
+    no input requires grad) skips zeroing the atomic backward's rows: the same image, and a backward of it anyway
+    takes the record path (bitwise the record path's gradients)."""
+    from gaussian_splatting_amd import _C, _lib
+    from gaussian_splatting_amd.rasterizer import GaussianRasterizationSettings, GaussianRasterizer
+
+    case = next(c for c in C.SMALL_CASES if c.name == "sh3_scalerot")
+    inp = C.build(case)
+    gc, gd = C.unit_grads(case.H, case.W)
+    dev = torch.device("cuda", 0)
+    d = lambda k: C._dev(inp[k], dev)  # noqa: E731
+    args = (d("bg"), d("means3D"), d("colors_precomp"), d("opacities"), d("scales"), d("rotations"), 1.0,
+            d("cov3D_precomp"), d("viewmatrix"), d("projmatrix"), inp["tanfovx"], inp["tanfovy"], inp["H"], inp["W"],
+            d("shs"), inp["sh_degree"], d("campos"), False, False, False)
+    with _lib.options(bwd_atomic=0):
+        ref_fwd = C.run_gpu_forward(inp)
+        ref = C.run_gpu_backward(inp, ref_fwd, gc, gd)
+    with _lib.options(bwd_atomic=1):
+        fwd = _C.rasterize_gaussians(*args, no_backward=True)
+        assert _lib.option_get("bwd_atomic") == 1  # (the override was this call's only)
+        got = C.run_gpu_backward(inp, fwd, gc, gd)
+    torch.cuda.synchronize()
+    assert fwd[0] == ref_fwd[0] and torch.equal(fwd[1], ref_fwd[1]) and torch.equal(fwd[6], ref_fwd[6])
+    for a, r in zip(got, ref):
+        assert torch.equal(a, r)
+    # the autograd module under no_grad renders the same image
+    s = GaussianRasterizationSettings(image_height=inp["H"], image_width=inp["W"], tanfovx=inp["tanfovx"],
+                                      tanfovy=inp["tanfovy"], bg=d("bg"), scale_modifier=1.0,
+                                      viewmatrix=d("viewmatrix"), projmatrix=d("projmatrix"), sh_degree=inp["sh_degree"],
+                                      campos=d("campos"), prefiltered=False, debug=False, antialiasing=False)
+    with torch.no_grad():
+        color, radii, invd = GaussianRasterizer(s)(means3D=d("means3D"), means2D=torch.zeros_like(d("means3D")),
+                                                   opacities=d("opacities"), shs=d("shs"), scales=d("scales"),
+                                                   rotations=d("rotations"))
+    assert torch.equal(color, ref_fwd[1])
