@@ -1,6 +1,7 @@
 #!/bin/bash
 # Interleaved A/B of library builds: bench.py under each library in turn, ROUNDS rounds, per config.
-# Usage: scripts/ab_libs.sh TAG ROUNDS "CONFIGS" LIB... (LIB: a path under gaussian_splatting_amd/lib, or "base")
+# Usage: scripts/ab_libs.sh TAG ROUNDS "CONFIGS" LIB... (LIB: a path under gaussian_splatting_amd/lib, "base",
+# or "env:NAME=VALUE[,NAME=VALUE...]" -- the default library under those environment settings, e.g. a GSR_ option)
 # Each run's JSON line goes to gpurun_out/TAG/<config>_<lib>_<round>.json; a summary (median ms/step and
 # render-stage times per library) is printed at the end.
 set -u
@@ -11,7 +12,9 @@ for cfg in $CONFIGS; do
   for r in $(seq 1 "$ROUNDS"); do
     for lib in "$@"; do
       name=$(basename "$lib" .so)
-      if [ "$lib" = base ]; then env_lib=""; else env_lib="GSR_LIBRARY=$ROOT/$lib"; fi
+      if [ "$lib" = base ]; then env_lib=""
+      elif [ "${lib#env:}" != "$lib" ]; then env_lib=$(echo "${lib#env:}" | tr ',' ' '); name=$(echo "${lib#env:}" | tr ',=' '-.')
+      else env_lib="GSR_LIBRARY=$ROOT/$lib"; fi
       env $env_lib timeout -k 10 300 python bench.py --config "$cfg" --no-cpu-baseline --no-census --steps 30 \
         > "$OUT/${cfg}_${name}_$r.json" 2> "$OUT/${cfg}_${name}_$r.err"; rc=$?
       echo "$cfg $name round $r rc=$rc"; [ $rc -eq 0 ] || exit $rc

@@ -81,8 +81,9 @@ def test_backward_without_invdepth_grad():
 
 @pytest.mark.record_path
 def test_deterministic_bitwise():
-    """No float atomics anywhere (the one atomic, an OR of a record's content bit, is order-free): two runs
-    give bit-identical images and gradients."""
+    """The record path (bwd_atomic=0, this module's default by the record_path marker) uses no float atomics --
+    its one atomic, an OR of a record's content bit, is order-free -- so two runs give bit-identical images and
+    gradients.  (The default atomic path adds in the hardware's order: tests/test_gpu_options.py.)"""
     case = C.SMALL_CASES[-1]
     inp = C.build(case)
     gc, gd = C.unit_grads(case.H, case.W)
