@@ -201,7 +201,7 @@ def build_id() -> str:
 
 # ---- runtime options (include/gsr.h gsr_option_set) ---------------------------------
 OPTIONS = ("fused_bin", "fwd_quads", "bwd_seg_ck", "host_total", "zero_fill", "live_list", "sort_prefix",
-           "count_wait", "bwd_grid", "bwd_atomic", "near_mass")
+           "count_wait", "bwd_grid", "bwd_atomic", "near_mass", "touched_run")
 
 
 def option_get(name: str) -> int:

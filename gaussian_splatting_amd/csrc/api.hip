@@ -286,7 +286,7 @@ constexpr uint32_t kFwdFillBlocks = 256;  // one-wave blocks zeroing the accumul
 static_assert(kFwdFillBlocks % 8 == 0, "the forward's fill blocks keep the tiles' XCD mapping");
 enum Opt {
     OPT_FUSED_BIN = 0, OPT_FWD_QUADS, OPT_BWD_SEG_CK, OPT_HOST_TOTAL, OPT_ZERO_FILL, OPT_LIVE_LIST, OPT_SORT_PREFIX,
-    OPT_COUNT_WAIT, OPT_BWD_GRID, OPT_BWD_ATOMIC, OPT_NEAR_MASS, OPT_COUNT
+    OPT_COUNT_WAIT, OPT_BWD_GRID, OPT_BWD_ATOMIC, OPT_NEAR_MASS, OPT_TOUCHED_RUN, OPT_COUNT
 };
 struct OptionSpec {
     const char* name;
@@ -305,6 +305,7 @@ const OptionSpec kOptions[OPT_COUNT] = {
     {"bwd_grid", "GSR_BWD_GRID", 0, 0, 2},
     {"bwd_atomic", "GSR_BWD_ATOMIC", 1, 0, 1},
     {"near_mass", "GSR_NEAR_MASS", 30, 0, 1 << 20},
+    {"touched_run", "GSR_TOUCHED_RUN", 0, 0, 32},
 };
 std::atomic<int> g_opt[OPT_COUNT];
 std::once_flag g_opt_once;
@@ -328,8 +329,8 @@ void options_init() {
 // Per-thread overrides (gsr_option_set_thread): kOptNone where the process-wide value applies.
 constexpr int kOptNone = INT_MIN;
 thread_local int t_opt[OPT_COUNT] = {kOptNone, kOptNone, kOptNone, kOptNone, kOptNone, kOptNone, kOptNone, kOptNone,
-                                     kOptNone, kOptNone, kOptNone};
-static_assert(OPT_COUNT == 11, "one kOptNone per option above");
+                                     kOptNone, kOptNone, kOptNone, kOptNone};
+static_assert(OPT_COUNT == 12, "one kOptNone per option above");
 
 int option(int id) {
     if (t_opt[id] != kOptNone) return t_opt[id];
@@ -355,22 +356,24 @@ int option_index(const char* name) {
 struct GeomMark {
     const void* buf;
     bool zeroed, recs;
+    bool long_lists;  // the frame's mean tile list is long (kLongMeanList): few of its Gaussians are touched
 };
 std::mutex g_mark_mu;
 std::vector<GeomMark> g_marks;
 constexpr size_t kGeomMarksMax = 4096;
 
-void geom_mark(const void* geom_buffer, bool zeroed, bool recs) {
+void geom_mark(const void* geom_buffer, bool zeroed, bool recs, bool long_lists) {
     std::lock_guard<std::mutex> lk(g_mark_mu);
     for (auto& m : g_marks)
         if (m.buf == geom_buffer) {
             m.zeroed = zeroed;
             m.recs = recs;
+            m.long_lists = long_lists;
             return;
         }
     if (!zeroed && !recs) return;  // (absent = neither)
     if (g_marks.size() >= kGeomMarksMax) g_marks.clear();
-    g_marks.push_back(GeomMark{geom_buffer, zeroed, recs});
+    g_marks.push_back(GeomMark{geom_buffer, zeroed, recs, long_lists});
 }
 
 void geom_forget(const void* geom_buffer) {
@@ -387,8 +390,12 @@ GeomMark geom_marked(const void* geom_buffer) {
     std::lock_guard<std::mutex> lk(g_mark_mu);
     for (const auto& m : g_marks)
         if (m.buf == geom_buffer) return m;
-    return GeomMark{geom_buffer, false, false};
+    return GeomMark{geom_buffer, false, false, false};
 }
+
+// A frame whose mean tile list holds at least this many entries is a "long-list" frame: near-first binning
+// applies (below) and the atomic backward lists its touched Gaussians over longer runs (few are touched).
+constexpr size_t kLongMeanList = 2048;
 
 // K2 folded into K3 in capacity mode.
 bool fused_binning_mode() { return option(OPT_FUSED_BIN) != 0; }
@@ -960,7 +967,7 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
     char* gbase = (char*)call_alloc(geom_alloc, geom_ctx, geom_bytes);
     if (!gbase) return fail(GSR_ERR_ALLOC, "rasterize_forward: geometry buffer allocation failed");
     GeomState geom = carve_geom(gbase, P, gx, gy, &geom_bytes);
-    geom_mark(gbase, false, false);  // (set below once the binning and the render's fill blocks are queued)
+    geom_mark(gbase, false, false, false);  // (set below once the binning and the render's fill blocks are queued)
     carve_image(nullptr, width, height, tiles, &img_bytes);
     char* ibase = (char*)call_alloc(image_alloc, image_ctx, img_bytes);
     if (!ibase) return fail(GSR_ERR_ALLOC, "rasterize_forward: image buffer allocation failed");
@@ -1005,7 +1012,7 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
     // regime): there the blend reaches a small part of each list and the cut pays; with short lists (1M@1080p:
     // 973) the frame's mass stays under the target anyway, and the redo chain's launches (far fill, whole
     // sort, redo render: ~6 us when empty) would only cost (r5d: 0.7305 -> 0.7372-0.7404 ms with no cut made)
-    constexpr size_t kNearMinMeanList = 2048;
+    constexpr size_t kNearMinMeanList = kLongMeanList;
     const unsigned long long near_target =
         fused && opt_near_mass > 0 && bin_near_ok(tiles) && C_hint >= kNearMinMeanList * (size_t)tiles
             ? (unsigned long long)opt_near_mass * (unsigned long long)kMassScale * (unsigned long long)width * height
@@ -1115,7 +1122,7 @@ int forward_impl(gsr_alloc_fn geom_alloc, void* geom_ctx, gsr_alloc_fn binning_a
                 ra.fill_blocks = kFwdFillBlocks;
             }
             HIP_TRY(launch_render_fwd(ra, stream, opt_quads), "render_fwd");
-            geom_mark(gbase, opt_atomic, k3_recs);
+            geom_mark(gbase, opt_atomic, k3_recs, (size_t)C >= kLongMeanList * (size_t)tiles);
             const bool near_now = fused_now && near_first;
             if ((prefix || near_now) && C > 0) {  // the tiles whose walk passed their sorted prefix (usually none)
                 if (near_now)  // their far instances first (none emitted by K3); their accumulator rows zeroed
@@ -1375,7 +1382,7 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
     // (also with R == 0: gauss_reduce still reads every Gaussian's record start)
     if (!atomic && !mark.recs) {  // a forward that left no record inputs (or a buffer never seen)
         HIP_TRY(launch_rec_prep(P, geom, bin, C, stream), "record prep");
-        geom_mark(geom_buffer, mark.zeroed, true);
+        geom_mark(geom_buffer, mark.zeroed, true, mark.long_lists);
     }
     if (R > 0) {
         StageScope sc(ST_RENDER_BWD, stream);
@@ -1444,6 +1451,11 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
         if (atomic) {  // the sums are the accumulator rows of the touched Gaussians (render_bwd ATOMIC)
             ga.touched = geom.touched;
             ga.acc = geom.acc;
+            // runs of 256 x N touched-bit positions per workgroup (backward.hip gauss_bwd_touched_kernel): N from
+            // the option, or by the frame -- 8 where the lists are long (few Gaussians touched: 5M@4K), else 1
+            const int opt_run = option(OPT_TOUCHED_RUN);
+            const uint32_t run = opt_run > 0 ? (uint32_t)opt_run : mark.long_lists ? 8u : 1u;
+            ga.touched_shift = 31u - (uint32_t)__builtin_clz(run);  // (a power of two at most, floor)
         }
         HIP_TRY(launch_gauss_bwd(ga, stream), "gauss_bwd");
     }

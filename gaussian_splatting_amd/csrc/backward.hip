@@ -784,38 +784,92 @@ __global__ void __launch_bounds__(64) gauss_bwd_kernel(GaussBwdArgs a) {
 }
 
 // The atomic backward's per-Gaussian pass (bwd_atomic): a workgroup of kTouchedWaves waves per run of
-// 64 x kTouchedWaves consecutive Gaussians reads the run's touched bits (render_bwd set them), lists the
-// touched Gaussians in LDS, clears the words, and wave w runs the live-list backward over list entries
-// [64 w, 64 w + 64) -- the waves past the list exit -- with the sums read from, and the rows then zeroed in,
-// the accumulator.  One kernel where a gauss_live pass listed the Gaussians into shards and moved their sums
-// to list order for the list kernel: 1M@1080p -6.8 us per step, 500k -9.3 (r7e, four interleaved rounds;
-// one wave per run of 256 serialising its passes: -7.0 / -3.4).
+// consecutive Gaussians reads the run's touched bits (render_bwd set them; cleared as read), lists the touched
+// Gaussians in LDS, and wave w runs the live-list backward over list entries [64 w, 64 w + 64) -- the waves
+// past the list skip -- with the sums read from, and the rows then zeroed in, the accumulator.  One kernel
+// where a gauss_live pass listed the Gaussians into shards and moved their sums to list order for the list
+// kernel (1M@1080p -6.8 us per step, 500k -9.3, r7e).
+//   RUNS = false: runs of 256, one list of at most 256, no loop (the 1080p frames: ~13% of a 1M view touched).
+//   RUNS = true: runs of 256 << touched_shift, sub-run by sub-run of 256 appended to a ring list and flushed
+// 256 at a time (and the rest at the end), so the waves stay full where few Gaussians are touched: 5M@4K
+// gauss_bwd 120 -> 56 us with runs of 2048 (r7g).  The loop around the row backward costs registers (153 ->
+// 197 VGPRs, combined SH layout) and 3-5 us at 1080p, hence two forms ("touched_run", api.hip).
 constexpr int kTouchedWaves = 4;
-template <int SH_MODE>
+constexpr int kTouchedSub = 64 * kTouchedWaves;  // Gaussians per sub-run (one bit per thread)
+constexpr uint32_t kTouchedShiftMax = 5;         // at most 32 sub-runs per workgroup: 256 words, one per thread
+constexpr uint32_t kTouchedRing = 2 * kTouchedSub;
+static_assert((kTouchedSub << kTouchedShiftMax) / 32 == kTouchedSub, "one touched word per thread at most");
+template <int SH_MODE, bool RUNS>
 __global__ void __launch_bounds__(64 * kTouchedWaves) gauss_bwd_touched_kernel(GaussBwdArgs a) {
     __shared__ __attribute__((aligned(16))) float s_sh[kTouchedWaves][SH_MODE != kShGlobal ? kGbShFloats : 4];
-    __shared__ uint32_t s_list[64 * kTouchedWaves];
+    __shared__ uint32_t s_list[RUNS ? kTouchedRing : kTouchedSub];
+    __shared__ uint32_t s_words[RUNS ? kTouchedSub : 1];
     __shared__ uint32_t s_cnt[kTouchedWaves];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t g = blockIdx.x * (64u * kTouchedWaves) + threadIdx.x;
-    const uint32_t w = g < (uint32_t)a.P ? a.touched[g >> 5] : 0u;  // (each word read by 32 lanes)
-    const unsigned long long m = __ballot((w >> (lane & 31)) & 1u);
-    if (lane == 0) s_cnt[wave] = (uint32_t)__popcll(m);
-    __syncthreads();
-    uint32_t base = 0, total = 0;
+    if constexpr (!RUNS) {
+        const uint32_t g = blockIdx.x * (uint32_t)kTouchedSub + threadIdx.x;
+        const uint32_t w = g < (uint32_t)a.P ? a.touched[g >> 5] : 0u;  // (each word read by 32 lanes)
+        const unsigned long long m = __ballot((w >> (lane & 31)) & 1u);
+        if (lane == 0) s_cnt[wave] = (uint32_t)__popcll(m);
+        __syncthreads();
+        uint32_t base = 0, total = 0;
 #pragma unroll
-    for (int k = 0; k < kTouchedWaves; k++) {
-        const uint32_t c = s_cnt[k];
-        base += k < wave ? c : 0u;
-        total += c;
+        for (int k = 0; k < kTouchedWaves; k++) {
+            const uint32_t c = s_cnt[k];
+            base += k < wave ? c : 0u;
+            total += c;
+        }
+        if ((m >> lane) & 1ull) s_list[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = g;
+        if ((lane & 31) == 0 && w) a.touched[g >> 5] = 0u;  // (after the ballot read it)
+        __syncthreads();
+        const uint32_t k0 = 64u * (uint32_t)wave;
+        if (k0 >= total) return;  // uniform per wave
+        const int idx = k0 + (uint32_t)lane < total ? (int)s_list[k0 + lane] : a.P;
+        gauss_bwd_rows<SH_MODE, true, true>(a, 0, idx, s_sh[wave]);
+    } else {
+        const int nsub = 1 << a.touched_shift;
+        const uint32_t run0 = blockIdx.x * ((uint32_t)kTouchedSub << a.touched_shift);
+        {
+            const uint32_t nwords = (uint32_t)(kTouchedSub / 32) << a.touched_shift;
+            const uint32_t wi = (run0 >> 5) + threadIdx.x;
+            uint32_t w = 0;
+            if (threadIdx.x < nwords && wi < ((uint32_t)a.P + 31u) >> 5) {
+                w = a.touched[wi];
+                if (w) a.touched[wi] = 0u;  // restored for the next backward of the same forward
+            }
+            s_words[threadIdx.x] = w;
+        }
+        __syncthreads();
+        uint32_t head = 0, tail = 0;  // the ring's listed entries [head, tail) (uniform)
+        for (int j = 0; j < nsub; j++) {
+            const uint32_t g = run0 + (uint32_t)(j * kTouchedSub) + threadIdx.x;
+            const uint32_t w = s_words[j * (kTouchedSub / 32) + (threadIdx.x >> 5)];
+            const unsigned long long m = __ballot((w >> (lane & 31)) & 1u);
+            if (lane == 0) s_cnt[wave] = (uint32_t)__popcll(m);
+            __syncthreads();  // (also: every wave's reads of the ring's last flush are done)
+            uint32_t base = 0, total = 0;
+#pragma unroll
+            for (int k = 0; k < kTouchedWaves; k++) {
+                const uint32_t c = s_cnt[k];
+                base += k < wave ? c : 0u;
+                total += c;
+            }
+            if ((m >> lane) & 1ull)
+                s_list[(tail + base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))) % kTouchedRing] = g;
+            tail += total;
+            __syncthreads();
+            // flush: 256 at a time, and at the last sub-run the rest (tail - head < 2 x 256 here)
+            while (tail - head >= (uint32_t)kTouchedSub || (j == nsub - 1 && tail > head)) {  // uniform
+                const uint32_t n = min(tail - head, (uint32_t)kTouchedSub);
+                const uint32_t k0 = 64u * (uint32_t)wave;
+                if (k0 < n) {  // uniform per wave
+                    const int idx = k0 + (uint32_t)lane < n ? (int)s_list[(head + k0 + lane) % kTouchedRing] : a.P;
+                    gauss_bwd_rows<SH_MODE, true, true>(a, 0, idx, s_sh[wave]);
+                }
+                head += n;
+            }
+        }
     }
-    if ((m >> lane) & 1ull) s_list[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = g;
-    if ((lane & 31) == 0 && w) a.touched[g >> 5] = 0u;  // (after the ballot read it)
-    __syncthreads();
-    const uint32_t k0 = 64u * (uint32_t)wave;
-    if (k0 >= total) return;  // uniform per wave
-    const int idx = k0 + (uint32_t)lane < total ? (int)s_list[k0 + lane] : a.P;
-    gauss_bwd_rows<SH_MODE, true, true>(a, 0, idx, s_sh[wave]);
 }
 
 // ---- 4. the same backward over several views' summed render gradients -----------
@@ -1347,14 +1401,18 @@ hipError_t launch_gauss_bwd(const GaussBwdArgs& a, hipStream_t stream) {
                         ((reinterpret_cast<uintptr_t>(a.shs) & 15) == 0) &&
                         ((reinterpret_cast<uintptr_t>(a.dL_dsh) & 15) == 0);
     if (a.touched) {  // the atomic backward: runs of touched Gaussians (outputs zero-filled)
-        const dim3 tgrid((uint32_t)(((size_t)a.P + 64 * kTouchedWaves - 1) / (64 * kTouchedWaves))),
-            tblock(64 * kTouchedWaves);
+        if (a.touched_shift > kTouchedShiftMax) return hipErrorInvalidValue;
+        const size_t run = (size_t)kTouchedSub << a.touched_shift;
+        const dim3 tgrid((uint32_t)(((size_t)a.P + run - 1) / run)), tblock(64 * kTouchedWaves);
+        const bool runs = a.touched_shift > 0;
+        void (*k)(GaussBwdArgs);
         if (lds_ok && a.dc)
-            hipLaunchKernelGGL((gauss_bwd_touched_kernel<kShLdsSplit>), tgrid, tblock, 0, stream, a);
+            k = runs ? gauss_bwd_touched_kernel<kShLdsSplit, true> : gauss_bwd_touched_kernel<kShLdsSplit, false>;
         else if (lds_ok)
-            hipLaunchKernelGGL((gauss_bwd_touched_kernel<kShLdsCombined>), tgrid, tblock, 0, stream, a);
+            k = runs ? gauss_bwd_touched_kernel<kShLdsCombined, true> : gauss_bwd_touched_kernel<kShLdsCombined, false>;
         else
-            hipLaunchKernelGGL((gauss_bwd_touched_kernel<kShGlobal>), tgrid, tblock, 0, stream, a);
+            k = runs ? gauss_bwd_touched_kernel<kShGlobal, true> : gauss_bwd_touched_kernel<kShGlobal, false>;
+        hipLaunchKernelGGL(k, tgrid, tblock, 0, stream, a);
         return hipGetLastError();
     }
     if (a.live && a.sparse) {  // the live list: kLiveShards x live_cap entries at most
