@@ -915,7 +915,8 @@ struct BucketLds {
     uint32_t start[NBMAX + 1];
     u64 red[2 * (T / 64)];
     uint32_t tmp[T / 64];
-    uint32_t m;  // entries sorted (prefix mode)
+    uint32_t m;   // entries sorted (prefix mode); a window's end (window modes)
+    uint32_t mb;  // the first bin past a window (bucket_sort_long)
 };
 
 template <int T>
@@ -1073,6 +1074,121 @@ __device__ bool bucket_sort_list(const u64* __restrict__ keys, uint32_t lo, uint
     return true;
 }
 
+// The same bucket sort for a list longer than the workgroup holds in registers (n > T x E): the keys stay in
+// global memory (a tile's list, L2-resident) and are read once for the range, once for the bin counts and
+// once per window of whole bins of at most NMAX keys (the WIN mode above, with the keys re-read instead of
+// held).  A key's slot in its bin comes from an LDS atomic on the bin's start, which leaves start[b] at the
+// next bin's start; so after a window's scatter bin b spans [start[b - 1], start[b]) (b > 0; [0, start[0])
+// for b = 0), since every bin before it is scattered or empty.  The rank inside the bin is its count of
+// smaller keys, as above.  Fails (uniformly; part of the list may be written, the caller's fallback rewrites
+// all of it) on skew or when one bin alone exceeds the buffer.
+template <int T, int NMAX, int NBMAX>
+__device__ bool bucket_sort_long(const u64* __restrict__ keys, uint32_t lo, uint32_t n,
+                                 uint32_t* __restrict__ gid_sorted, BucketLds<T, NMAX, NBMAX>& s) {
+    constexpr int U = 4;  // loads in flight per thread and pass
+    const uint32_t tid = threadIdx.x;
+    const u64* kl = keys + lo;
+    u64 mn = ~0ull, mx = 0ull;
+    for (uint32_t i0 = tid; i0 < n; i0 += U * T) {
+        u64 k[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) k[u] = i0 + u * T < n ? kl[i0 + u * T] : 0ull;
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            if (i0 + u * T < n) {
+                mn = k[u] < mn ? k[u] : mn;
+                mx = k[u] > mx ? k[u] : mx;
+            }
+    }
+    block_minmax_u64<T>(mn, mx, s.red);
+    uint32_t lg = 0;
+    while ((1u << lg) < (n >> kBinShift) && (1u << lg) < (uint32_t)NBMAX) lg++;
+    const u64 range = mx - mn;
+    const uint32_t bits = range ? 64u - (uint32_t)__clzll((long long)range) : 0u;
+    const uint32_t sh = bits > lg ? bits - lg : 0u;
+    const uint32_t nb = (uint32_t)(range >> sh) + 1u;  // <= 2^lg bins
+    const uint32_t per = (nb + T - 1) / T;
+    for (uint32_t i = tid; i < per * T + 1; i += T) s.start[i] = 0u;
+    __syncthreads();
+    for (uint32_t i0 = tid; i0 < n; i0 += U * T) {
+        u64 k[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) k[u] = i0 + u * T < n ? kl[i0 + u * T] : 0ull;
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            if (i0 + u * T < n) atomicAdd(&s.start[(uint32_t)((k[u] - mn) >> sh)], 1u);
+    }
+    __syncthreads();
+    uint32_t run = 0, sq = 0;
+    for (uint32_t c = 0; c < per; c++) {
+        const uint32_t v = s.start[tid * per + c];
+        run += v;
+        sq += v * v;
+    }
+    uint32_t all = 0;
+    uint32_t at = block_exclusive_scan(run, s.tmp, &all);
+    const uint32_t sumsq = block_sum(sq, s.tmp);  // (ends with a barrier: every count was read)
+    if (sumsq > kSkew * n) return false;  // uniform
+    for (uint32_t c = 0; c < per; c++) {
+        const uint32_t v = s.start[tid * per + c];
+        s.start[tid * per + c] = at;
+        at += v;
+    }
+    if (tid == 0) s.start[nb] = n;
+    __syncthreads();
+    // the window's bins are [bw0, bw1): the bins before bw0 are scattered (start[b] moved to the next bin's
+    // start, at most w0), so they never straddle a cut
+    uint32_t bw0 = 0;
+    for (uint32_t w0 = 0; w0 < n;) {  // uniform
+        const uint32_t cut = w0 + (uint32_t)NMAX;
+        if (tid == 0) {
+            s.m = cut < n ? cut : n;
+            s.mb = nb;
+        }
+        __syncthreads();
+        if (cut < n)
+            for (uint32_t c = 0; c < per; c++) {
+                const uint32_t b = tid * per + c;
+                if (b >= bw0 && b < nb && s.start[b] < cut && cut < s.start[b + 1]) atomicMin(&s.m, s.start[b]);
+            }
+        __syncthreads();
+        const uint32_t w1 = s.m;
+        if (w1 <= w0) return false;  // uniform: one bin holds more keys than the buffer
+        for (uint32_t c = 0; c < per; c++) {  // the first bin starting at or past w1
+            const uint32_t b = tid * per + c;
+            if (b >= bw0 && b < nb && s.start[b] >= w1) atomicMin(&s.mb, b);
+        }
+        __syncthreads();
+        const uint32_t bw1 = s.mb;
+        for (uint32_t i0 = tid; i0 < n; i0 += U * T) {
+            u64 k[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) k[u] = i0 + u * T < n ? kl[i0 + u * T] : 0ull;
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                if (i0 + u * T < n) {
+                    const uint32_t b = (uint32_t)((k[u] - mn) >> sh);
+                    if (b >= bw0 && b < bw1) s.buf[atomicAdd(&s.start[b], 1u) - w0] = k[u];
+                }
+            }
+        }
+        __syncthreads();
+        for (uint32_t j = tid; j < w1 - w0; j += T) {
+            const u64 kj = s.buf[j];
+            const uint32_t b = (uint32_t)((kj - mn) >> sh);
+            const uint32_t st = (b ? s.start[b - 1] : 0u) - w0, en = s.start[b] - w0;
+            uint32_t c = 0;
+#pragma unroll 4
+            for (uint32_t q = st; q < en; q++) c += s.buf[q] < kj ? 1u : 0u;
+            gid_sorted[lo + w0 + st + c] = (uint32_t)kj;
+        }
+        __syncthreads();  // the buffer, the starts and s.m / s.mb are reused by the next window
+        w0 = w1;
+        bw0 = bw1;
+    }
+    return true;
+}
+
 // Lists of up to kSortWaveMax keys: one workgroup (kSortT threads) per tile.  Short lists (<= kBucketMinN) are
 // sorted by a bitonic network in registers (no LDS, no barrier); longer ones by the bucket
 // sort, with the register network as its skew fallback.
@@ -1135,48 +1251,9 @@ __global__ void __launch_bounds__(kSortT) tile_sort_kernel(const uint2* __restri
     GSR_STAMP(g_st_sort, blockIdx.x, 1);
 }
 
-// Persistent: 256-thread workgroups walk one class list of long tiles (K2).  Class 0
-// (kSortWaveMax, kClass0Max]: tile_sort_window_kernel below.  Class 1 (> kClass0Max): bucket sort
-// up to kBucketMax keys, a 256 x 16 register network (its exchange buffer aliases the bucket
-// buffer) on skew up to 4096 keys, the global-memory network beyond.
+// Persistent: 256-thread workgroups walk the class lists of long tiles (K2).  Whole-list mode:
+// tile_sort_window_kernel below takes both classes.  Prefix mode: tile_sort_prefix_kernel, one launch per class.
 constexpr int kClassThreads = 256;
-
-// lim: sort only the reachable prefix of each list (the "sort_prefix" option; ~0u = whole lists):
-// the bucket sort then ranks the smallest lim (+ the rest of a bin) keys and leaves the tail
-// unwritten, and sorted_len records how many entries are in order.  The skew fallbacks sort the
-// whole list.
-__global__ void __launch_bounds__(kClassThreads) tile_sort_class1_kernel(const uint2* __restrict__ ranges,
-                                                                         u64* __restrict__ keys, u64 cap,
-                                                                         uint32_t* __restrict__ gid_sorted,
-                                                                         const uint32_t* __restrict__ list,
-                                                                         const uint32_t* __restrict__ count,
-                                                                         uint32_t lim,
-                                                                         uint32_t* __restrict__ sorted_len) {
-    constexpr int T = kClassThreads;
-    constexpr int NMAX = (int)kBucketMax;
-    constexpr int EF = 16;  // the fallback network's keys per thread
-    __shared__ BucketLds<T, NMAX, NMAX / 2> s;
-    static_assert(sizeof(s.buf) >= T * EF * sizeof(u64), "the fallback network's buffer");
-    const uint32_t nb = count[0];
-    for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
-        const uint32_t t = list[b];
-        const uint2 r = ranges[t];
-        const uint32_t n = tile_len(r, cap);  // may be shorter than its class when truncated by cap
-        if (n <= 1) {
-            if (n == 1 && threadIdx.x == 0) gid_sorted[r.x] = (uint32_t)keys[r.x];
-            if (threadIdx.x == 0) sorted_len[t] = n;
-        } else if (n > (uint32_t)NMAX || !bucket_sort_list<T, NMAX / T>(keys, r.x, n, gid_sorted, s, lim,
-                                                                          sorted_len + t)) {
-            __syncthreads();
-            if (n <= (uint32_t)T * EF)
-                sort_list<T, EF>(keys, r.x, n, gid_sorted, s.buf);
-            else
-                sort_list_global(keys, r.x, n, gid_sorted);
-            if (threadIdx.x == 0) sorted_len[t] = n;
-        }
-        __syncthreads();  // the LDS is reused by the next tile
-    }
-}
 
 // Prefix mode (the "sort_prefix" option in force): every long list -- both class lists -- sorted
 // to its reachable prefix by one kernel whose LDS holds only the prefix (kPrefixBuf keys and up to
@@ -1220,32 +1297,39 @@ tile_sort_prefix_kernel(const uint2* __restrict__ ranges,
     }
 }
 
-// Class 0 in whole-list mode: the prefix kernel's layout -- the keys in registers, an LDS buffer of
+// Whole-list mode, both classes: the prefix kernel's layout -- the keys in registers, an LDS buffer of
 // kPrefixBuf keys (24 KiB: five workgroups per CU, against three for the 41-KiB class-0 kernel) --
 // with the bins ranked in windows of at most kPrefixBuf keys; a skewed list or one bin over the
 // buffer takes the global-memory network.  tile_sort 57.5-57.9 -> 52.3-52.4 us at 1M@1080p (r3y6),
 // against a class-0 kernel with the whole 41-KiB list buffer in LDS.  Five waves (at four, no spill
-// but slower, r6e).
+// but slower, r6e).  Class-1 lists (> kClass0Max keys, more than the registers hold) are walked first
+// (the longest work first) and bucket-sorted with the keys re-read from memory (bucket_sort_long), so
+// no launch of their own is needed: a kernel queued behind another costs ~4.6 us however little it
+// does (tools/launch_floor.hip, r7n), which the 82-KiB class-1 kernel paid every step at 1080p with
+// nothing to sort.
 __global__ void __launch_bounds__(kClassThreads) __attribute__((amdgpu_waves_per_eu(kPrefixWaves)))
 tile_sort_window_kernel(const uint2* __restrict__ ranges, u64* __restrict__ keys, u64 cap,
-                        uint32_t* __restrict__ gid_sorted, const uint32_t* __restrict__ list,
-                        const uint32_t* __restrict__ count, uint32_t* __restrict__ sorted_len) {
+                        uint32_t* __restrict__ gid_sorted, const uint32_t* __restrict__ list0,
+                        const uint32_t* __restrict__ count0, const uint32_t* __restrict__ list1,
+                        const uint32_t* __restrict__ count1, uint32_t* __restrict__ sorted_len) {
     constexpr int T = kClassThreads, E = kClass0Max / kClassThreads;
     __shared__ BucketLds<T, kPrefixBuf, kPrefixBins> s;
-    const uint32_t nb = count[0];
+    const uint32_t n1 = count1[0], nb = n1 + count0[0];
     for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
-        const uint32_t t = list[b];
+        const uint32_t t = b < n1 ? list1[b] : list0[b - n1];
         const uint2 r = ranges[t];
-        const uint32_t n = tile_len(r, cap);
+        const uint32_t n = tile_len(r, cap);  // may be shorter than its class when truncated by cap
         if (n <= 1) {
             if (n == 1 && threadIdx.x == 0) gid_sorted[r.x] = (uint32_t)keys[r.x];
             if (threadIdx.x == 0) sorted_len[t] = n;
-        } else if (n > (uint32_t)(T * E) ||
-                   !bucket_sort_list<T, E, kPrefixBuf, kPrefixBins, true>(keys, r.x, n, gid_sorted, s, ~0u,
-                                                                         sorted_len + t)) {
+        } else if (n > (uint32_t)(T * E) ? !bucket_sort_long<T, kPrefixBuf, kPrefixBins>(keys, r.x, n, gid_sorted, s)
+                                         : !bucket_sort_list<T, E, kPrefixBuf, kPrefixBins, true>(
+                                               keys, r.x, n, gid_sorted, s, ~0u, sorted_len + t)) {
             __syncthreads();
             sort_list_global(keys, r.x, n, gid_sorted);
             if (threadIdx.x == 0) sorted_len[t] = n;
+        } else if (n > (uint32_t)(T * E) && threadIdx.x == 0) {
+            sorted_len[t] = n;
         }
         __syncthreads();  // the LDS is reused by the next tile
     }
@@ -1444,7 +1528,6 @@ hipError_t launch_rec_prep(int P, const GeomState& g, const BinningState& b, siz
     return hipGetLastError();
 }
 
-constexpr uint32_t kClass1GridSmall = 64;
 hipError_t launch_tile_sort(uint32_t tiles, const uint2* ranges, const GeomState& g, const BinningState& b,
                             size_t cap, hipStream_t stream, bool zero_counts, uint32_t cells, uint32_t prefix) {
     if (tiles == 0 || cap == 0) return hipSuccess;
@@ -1464,13 +1547,7 @@ hipError_t launch_tile_sort(uint32_t tiles, const uint2* ranges, const GeomState
         return hipGetLastError();
     }
     hipLaunchKernelGGL(tile_sort_window_kernel, grid(2048), dim3(kClassThreads), 0, stream, ranges, b.keys, c,
-                       b.gid_sorted, g.cls_list, g.cls_count, g.sorted_len);
-    // class 1 (lists > kClass0Max) is empty or nearly so while the mean list is short (1M@1080p: mean
-    // 973 keys): then a small persistent grid -- 512 workgroups of 82 KiB LDS cost 4.6 us to dispatch
-    // and retire with nothing to do (r4a trace)
-    const uint32_t c1_grid = cap / tiles <= kClass0Max / 2 ? kClass1GridSmall : 512u;
-    hipLaunchKernelGGL(tile_sort_class1_kernel, grid(c1_grid), dim3(kClassThreads), 0, stream, ranges, b.keys, c,
-                       b.gid_sorted, g.cls_list + tiles, g.cls_count + 1, lim, g.sorted_len);
+                       b.gid_sorted, g.cls_list, g.cls_count, g.cls_list + tiles, g.cls_count + 1, g.sorted_len);
     return hipGetLastError();
 }
 
