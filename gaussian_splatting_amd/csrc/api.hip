@@ -1451,10 +1451,10 @@ int backward_impl(int P, int D, int M, int R, const float* background, int width
         if (atomic) {  // the sums are the accumulator rows of the touched Gaussians (render_bwd ATOMIC)
             ga.touched = geom.touched;
             ga.acc = geom.acc;
-            // runs of 256 x N touched-bit positions per workgroup (backward.hip gauss_bwd_touched_kernel): N from
-            // the option, or by the frame -- 8 where the lists are long (few Gaussians touched: 5M@4K), else 1
+            // runs of 128 x N touched-bit positions per workgroup (backward.hip gauss_bwd_touched_kernel): N from
+            // the option, or by the frame -- 16 where the lists are long (few Gaussians touched: 5M@4K), else 1
             const int opt_run = option(OPT_TOUCHED_RUN);
-            const uint32_t run = opt_run > 0 ? (uint32_t)opt_run : mark.long_lists ? 8u : 1u;
+            const uint32_t run = opt_run > 0 ? (uint32_t)opt_run : mark.long_lists ? 16u : 1u;
             ga.touched_shift = 31u - (uint32_t)__builtin_clz(run);  // (a power of two at most, floor)
         }
         HIP_TRY(launch_gauss_bwd(ga, stream), "gauss_bwd");

@@ -788,15 +788,19 @@ __global__ void __launch_bounds__(64) gauss_bwd_kernel(GaussBwdArgs a) {
 // Gaussians in LDS, and wave w runs the live-list backward over list entries [64 w, 64 w + 64) -- the waves
 // past the list skip -- with the sums read from, and the rows then zeroed in, the accumulator.  One kernel
 // where a gauss_live pass listed the Gaussians into shards and moved their sums to list order for the list
-// kernel (1M@1080p -6.8 us per step, 500k -9.3, r7e).
-//   RUNS = false: runs of 256, one list of at most 256, no loop (the 1080p frames: ~13% of a 1M view touched).
-//   RUNS = true: runs of 256 << touched_shift, sub-run by sub-run of 256 appended to a ring list and flushed
-// 256 at a time (and the rest at the end), so the waves stay full where few Gaussians are touched: 5M@4K
-// gauss_bwd 120 -> 56 us with runs of 2048 (r7g).  The loop around the row backward costs registers (153 ->
-// 197 VGPRs, combined SH layout) and 3-5 us at 1080p, hence two forms ("touched_run", api.hip).
-constexpr int kTouchedWaves = 4;
+// kernel (1M@1080p -6.8 us per step, 500k -9.3, r7e).  Two waves per workgroup: at 1M@1080p a run of 128
+// holds ~17 touched Gaussians, so one wave works while the workgroup holds the LDS of its waves -- against
+// four waves per run of 256, gauss_bwd -1.8 / -2.0 us at 1M (r7r, r7s), equal at 500k; one wave per run of
+// 64: +6.5 us.
+//   RUNS = false: runs of 128, one list of at most 128, no loop (the 1080p frames: ~13% of a 1M view touched).
+//   RUNS = true: runs of 128 << touched_shift, sub-run by sub-run of 128 appended to a ring list and flushed
+// 128 at a time (and the rest at the end), so the waves stay full where few Gaussians are touched: 5M@4K
+// gauss_bwd 120 -> 56 us with runs of 2048 (r7g; 49 us with two waves, r7s).  The loop around the row
+// backward costs registers (153 -> 197 VGPRs, combined SH layout) and 3-5 us at 1080p, hence two forms
+// ("touched_run", api.hip).
+constexpr int kTouchedWaves = 2;
 constexpr int kTouchedSub = 64 * kTouchedWaves;  // Gaussians per sub-run (one bit per thread)
-constexpr uint32_t kTouchedShiftMax = 5;         // at most 32 sub-runs per workgroup: 256 words, one per thread
+constexpr uint32_t kTouchedShiftMax = 5;         // at most 32 sub-runs per workgroup: a touched word per thread
 constexpr uint32_t kTouchedRing = 2 * kTouchedSub;
 static_assert((kTouchedSub << kTouchedShiftMax) / 32 == kTouchedSub, "one touched word per thread at most");
 template <int SH_MODE, bool RUNS>

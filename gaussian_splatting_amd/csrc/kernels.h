@@ -147,7 +147,7 @@ struct GaussBwdArgs {
     uint32_t live_cap;           // entries per shard (live_list_cap)
     uint32_t* touched;           // atomic backward (sparse): the touched bits render_bwd set, or null; cleared here
     float4* acc;                 // with touched: the accumulator rows (the sums), zeroed after reading
-    uint32_t touched_shift;      // with touched: a workgroup lists 256 << touched_shift Gaussians ("touched_run")
+    uint32_t touched_shift;      // with touched: a workgroup lists 128 << touched_shift Gaussians ("touched_run")
 };
 
 hipError_t launch_zero_fill(const FillArgs& f, hipStream_t stream);

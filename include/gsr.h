@@ -348,8 +348,8 @@ int gsr_host_stats(double* values, int n, int reset);
  *                        whole list, so every output is the whole lists' (default M = 30; a pixel saturates
  *                        at 9.2) | every instance keyed and sorted
  *   "touched_run" 0|N   the atomic backward's per-Gaussian pass: one workgroup lists the touched Gaussians of
- *                        256 x N consecutive ones (N a power of two up to 32; others round down) and runs
- *                        their backward 256 at a time | 0: by the frame -- N = 8 where the mean tile list holds
+ *                        128 x N consecutive ones (N a power of two up to 32; others round down) and runs
+ *                        their backward 128 at a time | 0: by the frame -- N = 16 where the mean tile list holds
  *                        2048 entries or more (few Gaussians touched: 5M@4K), else 1 (default)
  * Every option is read once per forward / backward call, so a concurrent gsr_option_set never splits
  * one call's launches between two values.

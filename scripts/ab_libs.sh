@@ -13,7 +13,7 @@ for cfg in $CONFIGS; do
     for lib in "$@"; do
       name=$(basename "$lib" .so)
       if [ "$lib" = base ]; then env_lib=""
-      elif [ "${lib#env:}" != "$lib" ]; then env_lib=$(echo "${lib#env:}" | tr ',' ' '); name=$(echo "${lib#env:}" | tr ',=' '-.')
+      elif [ "${lib#env:}" != "$lib" ]; then env_lib=$(echo "${lib#env:}" | tr ',' ' '); name=$(echo "${lib#env:}" | sed 's#[^,]*/##g' | tr ',=' '-.')
       else env_lib="GSR_LIBRARY=$ROOT/$lib"; fi
       env $env_lib timeout -k 10 300 python bench.py --config "$cfg" --no-cpu-baseline --no-census --steps 30 \
         > "$OUT/${cfg}_${name}_$r.json" 2> "$OUT/${cfg}_${name}_$r.err"; rc=$?

@@ -45,7 +45,7 @@ VARIANTS = {
     "near_mass=0": dict(near_mass=0),         # no near-first binning: every instance keyed and sorted
     "near_mass=1": dict(near_mass=1),         # a very early depth cut: far fills and redos in dense tiles
     "bwd_atomic=1,near_mass=1": dict(bwd_atomic=1, near_mass=1),  # the far fill zeroes the far rows it files
-    # gauss_bwd over runs of 1024 / 8192 Gaussians: several flushes of 256 per workgroup, a ring list in LDS
+    # gauss_bwd over runs of 512 / 4096 Gaussians: several flushes of 128 per workgroup, a ring list in LDS
     "bwd_atomic=1,touched_run=4": dict(bwd_atomic=1, touched_run=4),
     "bwd_atomic=1,touched_run=32": dict(bwd_atomic=1, touched_run=32),
 }
@@ -145,7 +145,7 @@ def test_seg_ck_set_around_forward_only(seg_ck, case_name):
         np.testing.assert_allclose(_np(got), r[k], atol=1e-5, rtol=0, err_msg=k)
 
 
-@pytest.mark.parametrize("run", [1, 8], ids=["run256", "run2048"])
+@pytest.mark.parametrize("run", [1, 16], ids=["run128", "run2048"])
 @pytest.mark.parametrize("case_name", ["sh3_scalerot", "lists_4k_8k"])
 def test_atomic_backward_repeats(case_name, run):
     """bwd_atomic: the forward zeroes the accumulator rows and touched bits, and each backward restores
