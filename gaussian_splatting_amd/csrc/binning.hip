@@ -1082,9 +1082,12 @@ __device__ bool bucket_sort_list(const u64* __restrict__ keys, uint32_t lo, uint
 // for b = 0), since every bin before it is scattered or empty.  The rank inside the bin is its count of
 // smaller keys, as above.  Fails (uniformly; part of the list may be written, the caller's fallback rewrites
 // all of it) on skew or when one bin alone exceeds the buffer.
+// Prefix mode (lim < n): the windows stop once they cover lim keys; *sorted receives the keys in order (the
+// windows' end, >= lim), the rest is left unwritten -- the smallest *sorted keys of the list, as above.
 template <int T, int NMAX, int NBMAX>
 __device__ bool bucket_sort_long(const u64* __restrict__ keys, uint32_t lo, uint32_t n,
-                                 uint32_t* __restrict__ gid_sorted, BucketLds<T, NMAX, NBMAX>& s) {
+                                 uint32_t* __restrict__ gid_sorted, BucketLds<T, NMAX, NBMAX>& s,
+                                 uint32_t lim = ~0u, uint32_t* sorted = nullptr) {
     constexpr int U = 4;  // loads in flight per thread and pass
     const uint32_t tid = threadIdx.x;
     const u64* kl = keys + lo;
@@ -1138,8 +1141,8 @@ __device__ bool bucket_sort_long(const u64* __restrict__ keys, uint32_t lo, uint
     __syncthreads();
     // the window's bins are [bw0, bw1): the bins before bw0 are scattered (start[b] moved to the next bin's
     // start, at most w0), so they never straddle a cut
-    uint32_t bw0 = 0;
-    for (uint32_t w0 = 0; w0 < n;) {  // uniform
+    uint32_t bw0 = 0, w0 = 0;
+    while (w0 < n && w0 < lim) {  // uniform
         const uint32_t cut = w0 + (uint32_t)NMAX;
         if (tid == 0) {
             s.m = cut < n ? cut : n;
@@ -1186,6 +1189,7 @@ __device__ bool bucket_sort_long(const u64* __restrict__ keys, uint32_t lo, uint
         w0 = w1;
         bw0 = bw1;
     }
+    if (sorted && tid == 0) *sorted = w0;
     return true;
 }
 
@@ -1252,7 +1256,7 @@ __global__ void __launch_bounds__(kSortT) tile_sort_kernel(const uint2* __restri
 }
 
 // Persistent: 256-thread workgroups walk the class lists of long tiles (K2).  Whole-list mode:
-// tile_sort_window_kernel below takes both classes.  Prefix mode: tile_sort_prefix_kernel, one launch per class.
+// tile_sort_window_kernel below takes both classes.  Prefix mode: tile_sort_prefix_kernel, both classes too.
 constexpr int kClassThreads = 256;
 
 // Prefix mode (the "sort_prefix" option in force): every long list -- both class lists -- sorted
@@ -1264,31 +1268,30 @@ constexpr int kPrefixBuf = 2048;
 static_assert(kPrefixBuf >= 2 * (int)kSortPrefixMax, "a prefix plus the rest of its bucket fits the LDS buffer");
 constexpr int kPrefixBins = 2048;
 
-// T threads x E keys per thread: 256 x 16 for class 0's lists (<= 4096 keys), 256 x 32 for class 1's
-// (<= kBucketMax).  16 keys in at most 96 VGPRs: five workgroups per CU (the LDS would allow six;
-// 80 VGPRs spill): tile_sort 372-373 -> 357-360 us at 5M@4K against four; 512 x 8 measured 450
-// (six waves per SIMD) and 397 us (eight) (r3y3).
+// T threads x E keys per thread: 256 x 16 (<= 4096 keys: class 0's lists).  16 keys in at most 96 VGPRs: five
+// workgroups per CU (the LDS would allow six; 80 VGPRs spill): tile_sort 372-373 -> 357-360 us at 5M@4K against
+// four; 512 x 8 measured 450 (six waves per SIMD) and 397 us (eight) (r3y3).  Class 1's lists (longer) are
+// walked first by the same kernel, their keys re-read from memory (bucket_sort_long, prefix mode) -- no launch
+// of their own, and no length limit (a 256 x 32 register kernel took them up to 8192 keys before).
 constexpr int kPrefixWaves = 5;
 template <int T, int E>
-__global__ void __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(E <= 16 ? kPrefixWaves : 2)))
-tile_sort_prefix_kernel(const uint2* __restrict__ ranges,
-                                                                        u64* __restrict__ keys, u64 cap,
-                                                                        uint32_t* __restrict__ gid_sorted,
-                                                                        const uint32_t* __restrict__ list,
-                                                                        const uint32_t* __restrict__ count,
-                                                                        uint32_t lim,
-                                                                        uint32_t* __restrict__ sorted_len) {
+__global__ void __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(kPrefixWaves)))
+tile_sort_prefix_kernel(const uint2* __restrict__ ranges, u64* __restrict__ keys, u64 cap,
+                        uint32_t* __restrict__ gid_sorted, const uint32_t* __restrict__ list0,
+                        const uint32_t* __restrict__ count0, const uint32_t* __restrict__ list1,
+                        const uint32_t* __restrict__ count1, uint32_t lim, uint32_t* __restrict__ sorted_len) {
     __shared__ BucketLds<T, kPrefixBuf, kPrefixBins> s;
-    const uint32_t nb = count[0];
+    const uint32_t n1 = count1[0], nb = n1 + count0[0];
     for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
-        const uint32_t t = list[b];
+        const uint32_t t = b < n1 ? list1[b] : list0[b - n1];
         const uint2 r = ranges[t];
         const uint32_t n = tile_len(r, cap);
         if (n <= 1) {
             if (n == 1 && threadIdx.x == 0) gid_sorted[r.x] = (uint32_t)keys[r.x];
             if (threadIdx.x == 0) sorted_len[t] = n;
-        } else if (n > (uint32_t)(T * E) ||
-                   !bucket_sort_list<T, E>(keys, r.x, n, gid_sorted, s, lim, sorted_len + t)) {
+        } else if (n > (uint32_t)(T * E)
+                       ? !bucket_sort_long<T, kPrefixBuf, kPrefixBins>(keys, r.x, n, gid_sorted, s, lim, sorted_len + t)
+                       : !bucket_sort_list<T, E>(keys, r.x, n, gid_sorted, s, lim, sorted_len + t)) {
             __syncthreads();
             sort_list_global(keys, r.x, n, gid_sorted);
             if (threadIdx.x == 0) sorted_len[t] = n;
@@ -1539,11 +1542,9 @@ hipError_t launch_tile_sort(uint32_t tiles, const uint2* ranges, const GeomState
     // persistent class kernels: grids sized to fill the chip when their lists are long
     const auto grid = [&](uint32_t want) { return dim3(tiles < want ? tiles : want); };
     if (prefix) {
-        hipLaunchKernelGGL((tile_sort_prefix_kernel<kClassThreads, kClass0Max / kClassThreads>), grid(4096), dim3(kClassThreads), 0,
-                           stream, ranges, b.keys, c, b.gid_sorted, g.cls_list, g.cls_count, lim, g.sorted_len);
-        hipLaunchKernelGGL((tile_sort_prefix_kernel<kClassThreads, kBucketMax / kClassThreads>), grid(1024), dim3(kClassThreads), 0,
-                           stream, ranges, b.keys, c, b.gid_sorted, g.cls_list + tiles, g.cls_count + 1, lim,
-                           g.sorted_len);
+        hipLaunchKernelGGL((tile_sort_prefix_kernel<kClassThreads, kClass0Max / kClassThreads>), grid(4096),
+                           dim3(kClassThreads), 0, stream, ranges, b.keys, c, b.gid_sorted, g.cls_list, g.cls_count,
+                           g.cls_list + tiles, g.cls_count + 1, lim, g.sorted_len);
         return hipGetLastError();
     }
     hipLaunchKernelGGL(tile_sort_window_kernel, grid(2048), dim3(kClassThreads), 0, stream, ranges, b.keys, c,

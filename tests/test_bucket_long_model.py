@@ -17,8 +17,9 @@ K_BIN_SHIFT = 1
 K_SKEW = 48
 
 
-def bucket_sort_long_model(keys, nmax=2048, nbmax=2048, threads=256, rng=None):
-    """Returns the sorted list, or None where the kernel reports failure (skew, or one bin over the buffer)."""
+def bucket_sort_long_model(keys, nmax=2048, nbmax=2048, threads=256, rng=None, lim=None):
+    """Returns the sorted list -- in prefix mode (lim) (its first `sorted` entries, sorted) -- or None where the
+    kernel reports failure (skew, or one bin over the buffer)."""
     rng = rng or random.Random(0)
     n = len(keys)
     mn, mx = min(keys), max(keys)
@@ -43,7 +44,8 @@ def bucket_sort_long_model(keys, nmax=2048, nbmax=2048, threads=256, rng=None):
     start[nb] = n
     out = [None] * n
     bw0 = w0 = 0
-    while w0 < n:
+    lim = n if lim is None else lim
+    while w0 < n and w0 < lim:
         cut = w0 + nmax
         w1 = cut if cut < n else n
         if cut < n:
@@ -70,7 +72,7 @@ def bucket_sort_long_model(keys, nmax=2048, nbmax=2048, threads=256, rng=None):
             c = sum(1 for q in range(st, en) if buf[q] < kj)
             out[w0 + st + c] = kj
         w0, bw0 = w1, bw1
-    return out
+    return out if lim >= n else (out[:w0], w0)
 
 
 @pytest.mark.parametrize("seed", range(6))
@@ -90,6 +92,23 @@ def test_bucket_sort_long_model_sorts(seed):
         assert out == sorted(keys)
         sorted_ok += 1
     assert sorted_ok > 0
+
+
+@pytest.mark.parametrize("lim", [1024, 3000])
+def test_bucket_sort_long_model_prefix(lim):
+    """Prefix mode (the reachable-prefix sort): the windows stop once they cover lim keys; what they wrote is the
+    smallest `sorted` keys in order, sorted >= lim."""
+    rng = random.Random(lim)
+    for _ in range(8):
+        n = rng.choice([5000, 9000, 20000])
+        keys = [((rng.randint(0, 1 << 24)) << 20) | i for i in range(n)]
+        rng.shuffle(keys)
+        res = bucket_sort_long_model(keys, rng=rng, lim=lim)
+        if res is None:
+            continue
+        head, m = res
+        assert lim <= m <= n
+        assert head == sorted(keys)[:m]
 
 
 def test_bucket_sort_long_model_reports_skew():
