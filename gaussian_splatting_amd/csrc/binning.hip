@@ -508,6 +508,21 @@ __global__ void __launch_bounds__(kBinThreads) tile_count_kernel(int P, int chun
 // counts (independent loads), then one block scan per round.
 constexpr int kScanV = 8;
 
+// v = p[b, b + 8) (zero past n): two 16-byte loads where the run is whole and aligned.  K3's prologue loads
+// the per-tile words this way: the wave's lanes read consecutive 32-byte runs, and with one word per
+// instruction each load touched 16 cache lines for 256 bytes (8x the requests; stamps: ~5 us per load
+// at K3's start, 256 workgroups reading at once).
+__device__ __forceinline__ void load_run8(const uint32_t* __restrict__ p, uint32_t b, uint32_t n, uint32_t (&v)[kScanV]) {
+    static_assert(kScanV == 8, "two uint4 per run");
+    if (b + kScanV <= n && ((uintptr_t)(p + b) & 15u) == 0) {
+        const uint4 x = *reinterpret_cast<const uint4*>(p + b), y = *reinterpret_cast<const uint4*>(p + b + 4);
+        v[0] = x.x, v[1] = x.y, v[2] = x.z, v[3] = x.w, v[4] = y.x, v[5] = y.y, v[6] = y.z, v[7] = y.w;
+    } else {
+#pragma unroll
+        for (int i = 0; i < kScanV; i++) v[i] = b + i < n ? p[b + i] : 0u;
+    }
+}
+
 __global__ void __launch_bounds__(kBinThreads) tile_scan_kernel(uint32_t tiles, uint32_t* __restrict__ cnt,
                                                                 uint32_t n_counters, uint32_t* __restrict__ unit_cnt,
                                                                 unsigned long long* __restrict__ tile_join,
@@ -525,12 +540,10 @@ __global__ void __launch_bounds__(kBinThreads) tile_scan_kernel(uint32_t tiles, 
     for (uint32_t base = 0; base < tiles; base += T * kScanV) {
         const uint32_t b = base + threadIdx.x * kScanV;
         uint32_t v[kScanV];
+        load_run8(cnt, b, tiles, v);  // (as K3's prologue)
         u64 run = 0;
 #pragma unroll
-        for (int i = 0; i < kScanV; i++) {
-            v[i] = b + i < tiles ? cnt[b + i] : 0u;
-            run += v[i];
-        }
+        for (int i = 0; i < kScanV; i++) run += v[i];
         u64 all = 0;
         u64 at = carry + block_exclusive_scan(run, s_tmp, &all);
 #pragma unroll
@@ -622,21 +635,6 @@ __device__ __forceinline__ void rec_starts_chunk(int g0, int g1, u64 chunk_base,
         uint4* w = reinterpret_cast<uint4*>(rec_flag);
         for (u64 i = chunk_base / kPer + threadIdx.x; i < (e1 + kPer - 1) / kPer; i += blockDim.x)
             w[i] = make_uint4(0u, 0u, 0u, 0u);
-    }
-}
-
-// v = p[b, b + 8) (zero past n): two 16-byte loads where the run is whole and aligned.  K3's prologue loads
-// the per-tile words this way: the wave's lanes read consecutive 32-byte runs, and with one word per
-// instruction each load touched 16 cache lines for 256 bytes (8x the requests; stamps: ~5 us per load
-// at K3's start, 256 workgroups reading at once).
-__device__ __forceinline__ void load_run8(const uint32_t* __restrict__ p, uint32_t b, uint32_t n, uint32_t (&v)[kScanV]) {
-    static_assert(kScanV == 8, "two uint4 per run");
-    if (b + kScanV <= n && ((uintptr_t)(p + b) & 15u) == 0) {
-        const uint4 x = *reinterpret_cast<const uint4*>(p + b), y = *reinterpret_cast<const uint4*>(p + b + 4);
-        v[0] = x.x, v[1] = x.y, v[2] = x.z, v[3] = x.w, v[4] = y.x, v[5] = y.y, v[6] = y.z, v[7] = y.w;
-    } else {
-#pragma unroll
-        for (int i = 0; i < kScanV; i++) v[i] = b + i < n ? p[b + i] : 0u;
     }
 }
 
